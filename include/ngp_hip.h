@@ -1,0 +1,198 @@
+/*
+ * ngp_hip.h — C ABI of the MI355X (gfx950) instant-ngp hot path.
+ *
+ * One shared library (libngp_hip.so) exports every entry point below. The
+ * signatures take plain device pointers, sizes and a hipStream_t (passed as
+ * void*), never torch types, so any host language can bind them (ctypes,
+ * cgo, JNI, N-API). Each entry replaces one pybind11 function of the reference
+ * extension; the reference declaration it stands in for is cited per function
+ * (paths relative to the reference repository root).
+ *
+ * Conventions shared by every function:
+ *   - The caller allocates every output and scratch buffer; nothing here calls
+ *     hipMalloc/hipFree or synchronises, so each call can be captured into a
+ *     hipGraph. Work is enqueued on `stream` (NULL = the legacy null stream).
+ *   - Return value: NGP_OK (0) on success, a negative NGP_ERR_* code otherwise.
+ *     NGP_ERR_ARG / NGP_ERR_UNSUPPORTED mirror the reference's TORCH_CHECK /
+ *     std::runtime_error("... must be ...") failures; the Python shims raise
+ *     RuntimeError with the reference's wording.
+ *   - dtype codes: NGP_DTYPE_F32 = 0, NGP_DTYPE_F16 = 1, NGP_DTYPE_F64 = 2.
+ */
+#ifndef NGP_HIP_H
+#define NGP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NGP_OK 0
+#define NGP_ERR_ARG (-1)
+#define NGP_ERR_HIP (-2)
+#define NGP_ERR_UNSUPPORTED (-3)
+
+#define NGP_DTYPE_F32 0
+#define NGP_DTYPE_F16 1
+#define NGP_DTYPE_F64 2
+
+/* Library identification: ABI version (bumped on any signature change). */
+int ngp_abi_version(void);
+/* Human-readable message for the last NGP_ERR_* returned on this thread. */
+const char* ngp_last_error(void);
+
+/* ------------------------------------------------------------------------ */
+/* gridencoder                                                              */
+/* ------------------------------------------------------------------------ */
+
+/* Replaces grid_encode_forward, gridencoder/src/gridencoder.h:12 and
+ * gridencoder/src/gridencoder.cu:445-468.
+ *   inputs  f32 [B, D] in [0,1]; embeddings dtype [sum_T, C];
+ *   offsets i32 [L+1] (device); dy_dx dtype [B, L*D*C] or NULL.
+ *   out_layout 0: outputs [L, B, C] (the reference layout);
+ *   out_layout 1: outputs [B, L*C] (the layout the MLP consumes, no permute).
+ *   D in {2,3,4,5}, C in {1,2,4,8}, L <= 64. */
+int ngp_grid_encode_forward(const float* inputs, const void* embeddings, const int32_t* offsets,
+                            void* outputs, uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                            float S, uint32_t H, void* dy_dx, uint32_t gridtype,
+                            int32_t align_corners, uint32_t interp, int32_t dtype,
+                            int32_t out_layout, void* stream);
+
+/* Replaces grid_encode_backward, gridencoder/src/gridencoder.h:13 and
+ * gridencoder/src/gridencoder.cu:470-500. grad_embeddings must be zeroed by
+ * the caller (scatter-add target). grad_layout as out_layout above. */
+int ngp_grid_encode_backward(const void* grad, const float* inputs, const void* embeddings,
+                             const int32_t* offsets, void* grad_embeddings, uint32_t B, uint32_t D,
+                             uint32_t C, uint32_t L, float S, uint32_t H, const void* dy_dx,
+                             void* grad_inputs, uint32_t gridtype, int32_t align_corners,
+                             uint32_t interp, int32_t dtype, int32_t grad_layout, void* stream);
+
+/* Replaces grad_total_variation, gridencoder/src/gridencoder.h:15 and
+ * gridencoder/src/gridencoder.cu:636-642 (inputs are dtype, like the reference). */
+int ngp_grad_total_variation(const void* inputs, const void* embeddings, void* grad,
+                             const int32_t* offsets, float weight, uint32_t B, uint32_t D,
+                             uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                             int32_t align_corners, int32_t dtype, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* raymarching (all float32, like the reference wrappers' cast_inputs)      */
+/* ------------------------------------------------------------------------ */
+
+/* raymarching/src/raymarching.h:7, raymarching.cu:148-156 */
+int ngp_near_far_from_aabb(const float* rays_o, const float* rays_d, const float* aabb, uint32_t N,
+                           float min_near, float* nears, float* fars, void* stream);
+/* raymarching.h:8, raymarching.cu:201-209 */
+int ngp_sph_from_ray(const float* rays_o, const float* rays_d, float radius, uint32_t N,
+                     float* coords, void* stream);
+/* raymarching.h:9, raymarching.cu:229-232 */
+int ngp_morton3D(const int32_t* coords, uint32_t N, int32_t* indices, void* stream);
+/* raymarching.h:10, raymarching.cu:257-260 */
+int ngp_morton3D_invert(const int32_t* indices, uint32_t N, int32_t* coords, void* stream);
+/* raymarching.h:11, raymarching.cu:292-300 */
+int ngp_packbits(const float* grid, uint32_t N, float density_thresh, uint8_t* bitfield,
+                 void* stream);
+
+/* Replaces march_rays_train, raymarching.h:13 and raymarching.cu:311-492.
+ * Offsets are a deterministic exclusive prefix sum in ray order (a valid
+ * execution of the reference's atomicAdd ordering): rays[i] = (i, off_i, n_i).
+ * counter[0] += total samples, counter[1] += N (same as the reference).
+ * Samples of rays with off_i + n_i > M are dropped (reference :416); the
+ * caller zero-fills xyzs/dirs/deltas like the reference wrapper does. */
+int ngp_march_rays_train(const float* rays_o, const float* rays_d, const uint8_t* grid,
+                         float bound, float dt_gamma, uint32_t max_steps, uint32_t N, uint32_t C,
+                         uint32_t H, uint32_t M, const float* nears, const float* fars,
+                         float* xyzs, float* dirs, float* deltas, int32_t* rays, int32_t* counter,
+                         const float* noises, void* stream);
+
+/* raymarching.h:14, raymarching.cu:580-588 */
+int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs, const float* deltas,
+                                     const int32_t* rays, uint32_t M, uint32_t N, float T_thresh,
+                                     float* weights_sum, float* depth, float* image, void* stream);
+/* raymarching.h:15, raymarching.cu:694-702. grad_sigmas / grad_rgbs are
+ * zeroed by the caller (entries past a ray's early stop are not written). */
+int ngp_composite_rays_train_backward(const float* grad_weights_sum, const float* grad_depth,
+                                      const float* grad_image, const float* sigmas,
+                                      const float* rgbs, const float* deltas, const int32_t* rays,
+                                      const float* weights_sum, const float* depth,
+                                      const float* image, uint32_t M, uint32_t N, float T_thresh,
+                                      float* grad_sigmas, float* grad_rgbs, void* stream);
+/* raymarching.h:17, raymarching.cu:817-825 */
+int ngp_march_rays(uint32_t n_alive, uint32_t n_step, const int32_t* rays_alive,
+                   const float* rays_t, const float* rays_o, const float* rays_d, float bound,
+                   float dt_gamma, uint32_t max_steps, uint32_t C, uint32_t H, const uint8_t* grid,
+                   const float* nears, const float* fars, float* xyzs, float* dirs, float* deltas,
+                   const float* noises, void* stream);
+/* raymarching.h:18, raymarching.cu:917-923 (in place; rays_alive[n] = -1 on termination) */
+int ngp_composite_rays(uint32_t n_alive, uint32_t n_step, float T_thresh, int32_t* rays_alive,
+                       float* rays_t, const float* sigmas, const float* rgbs, const float* deltas,
+                       float* weights_sum, float* depth, float* image, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* shencoder                                                                */
+/* ------------------------------------------------------------------------ */
+
+/* shencoder/src/shencoder.h:9, shencoder.cu:420-439. dtype F32 or F64.
+ * C is the degree (1..8), outputs [B, C*C]; dy_dx [B, D*C*C] or NULL. */
+int ngp_sh_encode_forward(const void* inputs, void* outputs, uint32_t B, uint32_t D, uint32_t C,
+                          void* dy_dx, int32_t dtype, void* stream);
+/* shencoder.h:10, shencoder.cu:441-454. grad_inputs zeroed by the caller. */
+int ngp_sh_encode_backward(const void* grad, const void* inputs, uint32_t B, uint32_t D,
+                           uint32_t C, const void* dy_dx, void* grad_inputs, int32_t dtype,
+                           void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* ffmlp (fp16 storage, fp16 MFMA with fp32 accumulation)                   */
+/* ------------------------------------------------------------------------ */
+
+/* ffmlp/src/ffmlp.h:8, ffmlp.cu:635-671. inputs f16 [B, input_dim], weights
+ * f16 flat (per layer row-major [out, in], nn.Linear layout), outputs f16
+ * [B, output_dim]. forward_buffer f16 [num_layers, B, hidden] or NULL (the
+ * backward below recomputes activations and never reads it).
+ * hidden_dim in {16,32,64,128}, input_dim % 16 == 0, output_dim <= 16 (padded
+ * to 16 by the caller, like FFMLP does), B % 16 == 0. */
+int ngp_ffmlp_forward(const void* inputs, const void* weights, uint32_t B, uint32_t input_dim,
+                      uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,
+                      uint32_t activation, uint32_t output_activation, void* forward_buffer,
+                      void* outputs, void* stream);
+/* ffmlp.h:9, ffmlp.cu:673-709 */
+int ngp_ffmlp_inference(const void* inputs, const void* weights, uint32_t B, uint32_t input_dim,
+                        uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,
+                        uint32_t activation, uint32_t output_activation, void* inference_buffer,
+                        void* outputs, void* stream);
+/* Workspace (bytes) ngp_ffmlp_backward needs for its per-workgroup dW slabs. */
+size_t ngp_ffmlp_backward_workspace_bytes(uint32_t B, uint32_t input_dim, uint32_t output_dim,
+                                          uint32_t hidden_dim, uint32_t num_layers);
+/* ffmlp.h:11, ffmlp.cu:749-895. grad f16 [B, output_dim]; grad_inputs f16
+ * [B, input_dim] (written when calc_grad_inputs); grad_weights flat, dtype
+ * gw_dtype (F16 like the reference, or F32), overwritten (not accumulated).
+ * forward_buffer / backward_buffer may be NULL. */
+int ngp_ffmlp_backward(const void* grad, const void* inputs, const void* weights,
+                       const void* forward_buffer, uint32_t B, uint32_t input_dim,
+                       uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,
+                       uint32_t activation, uint32_t output_activation, int32_t calc_grad_inputs,
+                       void* backward_buffer, void* grad_inputs, void* grad_weights,
+                       int32_t gw_dtype, void* workspace, size_t workspace_bytes, void* stream);
+/* ffmlp.h:12-13, ffmlp.cu:711-740. The side-stream split-K pool of the
+ * reference is not needed (dW is reduced in-kernel); kept as no-ops so the
+ * FFMLP module's construction sequence is unchanged. */
+int ngp_ffmlp_allocate_splitk(size_t size);
+int ngp_ffmlp_free_splitk(void);
+
+/* ------------------------------------------------------------------------ */
+/* optimizer (next row of SURVEY §8f): fused Adam over a flat f32 param set */
+/* ------------------------------------------------------------------------ */
+
+/* torch.optim.Adam semantics (main_nerf.py:194; betas (0.9,0.99), eps 1e-15):
+ * m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g*g;
+ * p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps), g = grad (f32 or f16) * grad_scale.
+ * step is the 1-based step count after increment. */
+int ngp_adam_step(float* params, const void* grads, int32_t grad_dtype, float* exp_avg,
+                  float* exp_avg_sq, size_t n, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, int32_t step, float grad_scale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NGP_HIP_H */

@@ -1,0 +1,129 @@
+"""Loader for libngp_hip.so, the gfx950 C-ABI library behind every op package.
+
+The reference packages bind their CUDA sources through pybind11 (AOT
+`_gridencoder`/`_raymarching`/... or JIT `backend.py`, e.g.
+gridencoder/backend.py:31-38). Here a single prebuilt shared library exports
+the C functions declared in include/ngp_hip.h and each package's backend.py
+binds them with ctypes. There is deliberately NO fallback: if the library or
+a GPU is missing, every op raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must load libamdhip64 before the library below)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NGP_HIP_LIB", os.path.join(_HERE, "libngp_hip.so"))
+
+c_u32 = ctypes.c_uint32
+c_i32 = ctypes.c_int32
+c_f32 = ctypes.c_float
+c_vp = ctypes.c_void_p
+c_sz = ctypes.c_size_t
+
+# name -> argtypes (restype int unless listed in _RESTYPES). Mirrors ngp_hip.h.
+SIGNATURES = {
+    "ngp_abi_version": [],
+    "ngp_last_error": [],
+    "ngp_grid_encode_forward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_u32,
+                                c_vp, c_u32, c_i32, c_u32, c_i32, c_i32, c_vp],
+    "ngp_grid_encode_backward": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_f32,
+                                 c_u32, c_vp, c_vp, c_u32, c_i32, c_u32, c_i32, c_i32, c_vp],
+    "ngp_grad_total_variation": [c_vp, c_vp, c_vp, c_vp, c_f32, c_u32, c_u32, c_u32, c_u32, c_f32,
+                                 c_u32, c_u32, c_i32, c_i32, c_vp],
+    "ngp_near_far_from_aabb": [c_vp, c_vp, c_vp, c_u32, c_f32, c_vp, c_vp, c_vp],
+    "ngp_sph_from_ray": [c_vp, c_vp, c_f32, c_u32, c_vp, c_vp],
+    "ngp_morton3D": [c_vp, c_u32, c_vp, c_vp],
+    "ngp_morton3D_invert": [c_vp, c_u32, c_vp, c_vp],
+    "ngp_packbits": [c_vp, c_u32, c_f32, c_vp, c_vp],
+    "ngp_march_rays_train": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
+                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_composite_rays_train_forward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_vp, c_vp,
+                                         c_vp, c_vp],
+    "ngp_composite_rays_train_backward": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                          c_vp, c_u32, c_u32, c_f32, c_vp, c_vp, c_vp],
+    "ngp_march_rays": [c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32,
+                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_composite_rays": [c_u32, c_u32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                           c_vp],
+    "ngp_sh_encode_forward": [c_vp, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp],
+    "ngp_sh_encode_backward": [c_vp, c_vp, c_u32, c_u32, c_u32, c_vp, c_vp, c_i32, c_vp],
+    "ngp_ffmlp_forward": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp,
+                          c_vp],
+    "ngp_ffmlp_inference": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp,
+                            c_vp, c_vp],
+    "ngp_ffmlp_backward_workspace_bytes": [c_u32, c_u32, c_u32, c_u32, c_u32],
+    "ngp_ffmlp_backward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
+                           c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_sz, c_vp],
+    "ngp_ffmlp_allocate_splitk": [c_sz],
+    "ngp_ffmlp_free_splitk": [],
+    "ngp_adam_step": [c_vp, c_vp, c_i32, c_vp, c_vp, c_sz, c_f32, c_f32, c_f32, c_f32, c_f32,
+                      c_i32, c_f32, c_vp],
+}
+_RESTYPES = {
+    "ngp_last_error": ctypes.c_char_p,
+    "ngp_ffmlp_backward_workspace_bytes": c_sz,
+}
+
+DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the .so is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libngp_hip.so not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = handle
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().ngp_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (or NULL for None)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t):
+    """hipStream_t handle of the current torch stream on the tensor's device."""
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_cuda(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+
+
+def require_contiguous(t, name):
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be a contiguous tensor")
+
+
+def require_dtype(t, name, dtypes, what):
+    if t.dtype not in dtypes:
+        raise RuntimeError(f"{name} must be a {what} tensor")
+
+
+FLOATING = (torch.float32, torch.float16, torch.float64)
+
+
+def check_tensor(t, name, dtypes=FLOATING, what="floating", contiguous=True):
+    require_cuda(t, name)
+    if contiguous:
+        require_contiguous(t, name)
+    if dtypes is not None:
+        require_dtype(t, name, dtypes, what)

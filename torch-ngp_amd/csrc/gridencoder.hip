@@ -1,0 +1,571 @@
+// Multiresolution hash-grid encoder, forward / backward / TV-grad, for gfx950.
+//
+// Semantics follow the reference kernels line by line:
+//   fast_hash           gridencoder/src/gridencoder.cu:50-63
+//   get_grid_index      gridencoder.cu:66-84
+//   kernel_grid         gridencoder.cu:87-242   -> k_grid_fwd
+//   kernel_grid_backward gridencoder.cu:245-337 -> k_grid_bwd
+//   kernel_input_backward gridencoder.cu:340-366 -> k_grid_input_bwd
+//   kernel_grad_tv      gridencoder.cu:503-607  -> k_grid_tv
+//
+// MI355X design:
+//   * level-major scheduling: blockIdx.y = level, so the whole chip walks one
+//     level's table slice at a time. The largest hashed level is 2^19 entries =
+//     2 MiB in fp16, which fits one XCD's 4 MiB L2: the 8 random corner gathers
+//     per (point, level) are L2 hits instead of Infinity-Cache hits.
+//   * one lane per (point, level) handles all C channels of a corner with one
+//     vector access (C=2 fp16: one dword gather, one global_atomic_pk_add_f16).
+//   * out_layout 1 writes [B, L*C] directly (what the MLP consumes), removing
+//     the reference's permute copy (grid.py:69) and its grad permute (grid.py:87).
+//   * per-level scale/resolution are computed once on the host (exp2 in double,
+//     rounded to float) and passed as kernel arguments.
+//   * a hashed level's size is a power of two: the modulo becomes a mask.
+#include "ngp_common.h"
+
+#include <cmath>
+
+namespace {
+
+constexpr uint32_t kMaxLevels = 64;
+
+struct GridLevels {
+    float scale[kMaxLevels];
+    uint32_t res[kMaxLevels];
+};
+
+// reference semantics: scale = exp2f(level * S) * H - 1.0f;
+// resolution = (uint32_t)ceil(scale) + 1   (gridencoder.cu:138-139)
+static void make_levels(GridLevels& lv, uint32_t L, float S, uint32_t H) {
+    for (uint32_t l = 0; l < L; ++l) {
+        float ls = (float)l * S;
+        float e = (float)std::exp2((double)ls);
+        float scale = e * (float)H - 1.0f;
+        lv.scale[l] = scale;
+        lv.res[l] = (uint32_t)std::ceil(scale) + 1u;
+    }
+}
+
+template <uint32_t D>
+NGP_DEV uint32_t fast_hash(const uint32_t pos_grid[D]) {
+    constexpr uint32_t primes[7] = {1u, 2654435761u, 805459861u, 3674653429u,
+                                    2097192037u, 1434869437u, 2165219737u};
+    uint32_t result = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < D; ++i) result ^= pos_grid[i] * primes[i];
+    return result;
+}
+
+// Returns the entry index (not multiplied by C). `hs_mask` is hs-1 when hs is
+// a power of two, else 0 (then a true modulo is taken).
+template <uint32_t D>
+NGP_DEV uint32_t grid_index(uint32_t gridtype, bool align_corners, uint32_t hs, uint32_t hs_mask,
+                            uint32_t resolution, const uint32_t pos_grid[D]) {
+    uint32_t stride = 1;
+    uint32_t index = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < D && stride <= hs; d++) {
+        index += pos_grid[d] * stride;
+        stride *= align_corners ? resolution : (resolution + 1);
+    }
+    if (gridtype == 0 && stride > hs) index = fast_hash<D>(pos_grid);
+    return hs_mask ? (index & hs_mask) : (index % hs);
+}
+
+NGP_DEV float smoothstep(float v) { return v * v * (3.0f - 2.0f * v); }
+NGP_DEV float smoothstep_derivative(float v) { return 6 * v * (1.0f - v); }
+
+// Vector load/store of the C channels of one entry (entries are aligned to
+// C*sizeof(T) because offsets are multiples of 8 entries).
+template <typename T, uint32_t C>
+NGP_DEV void load_entry(const T* __restrict__ p, typename Acc<T>::F out[C]) {
+    struct alignas(sizeof(T) * C) V { T v[C]; };
+    V x = *reinterpret_cast<const V*>(p);
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) out[c] = (typename Acc<T>::F)x.v[c];
+}
+template <typename T, uint32_t C>
+NGP_DEV void store_entry(T* __restrict__ p, const T in[C]) {
+    struct alignas(sizeof(T) * C) V { T v[C]; };
+    V x;
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) x.v[c] = in[c];
+    *reinterpret_cast<V*>(p) = x;
+}
+
+template <typename T, uint32_t D, uint32_t C>
+__global__ void __launch_bounds__(256)
+k_grid_fwd(const float* __restrict__ inputs, const T* __restrict__ grid,
+           const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
+           GridLevels lv, T* __restrict__ dy_dx, uint32_t gridtype, bool align_corners,
+           uint32_t interp, int32_t out_layout) {
+    using A = Acc<T>;
+    using F = typename A::F;
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const uint32_t level = blockIdx.y;
+
+    T* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C
+                             : outputs + ((size_t)b * L + level) * C;
+
+    float x[D];
+    bool oob = false;
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        x[d] = inputs[(size_t)b * D + d];
+        if (x[d] < 0 || x[d] > 1) oob = true;
+    }
+    if (oob) {
+        T z[C];
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) z[c] = A::zero();
+        store_entry<T, C>(out, z);
+        if (dy_dx) {
+            T* g = dy_dx + (size_t)b * D * L * C + level * D * C;
+#pragma unroll
+            for (uint32_t i = 0; i < D * C; ++i) g[i] = A::zero();
+        }
+        return;
+    }
+
+    const uint32_t off0 = (uint32_t)offsets[level];
+    const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
+    const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
+    const T* __restrict__ g = grid + (size_t)off0 * C;
+    const float scale = lv.scale[level];
+    const uint32_t resolution = lv.res[level];
+
+    float pos[D], pos_deriv[D];
+    uint32_t pg[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        pos[d] = fmaf(x[d], scale, align_corners ? 0.0f : 0.5f);
+        pg[d] = (uint32_t)floorf(pos[d]);
+        pos[d] -= (float)pg[d];
+        pos_deriv[d] = 1.0f;  // reference bug at :143 zero-inits d >= 1; see DESIGN.md
+        if (interp == 1) {
+            pos_deriv[d] = smoothstep_derivative(pos[d]);
+            pos[d] = smoothstep(pos[d]);
+        }
+    }
+
+    typename A::S res[C];
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) res[c] = A::zero();
+
+#pragma unroll
+    for (uint32_t idx = 0; idx < (1u << D); idx++) {
+        float w = 1;
+        uint32_t pl[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; d++) {
+            if ((idx & (1u << d)) == 0) {
+                w *= 1 - pos[d];
+                pl[d] = pg[d];
+            } else {
+                w *= pos[d];
+                pl[d] = pg[d] + 1;
+            }
+        }
+        const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
+        F v[C];
+        load_entry<T, C>(g + (size_t)e * C, v);
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) res[c] = A::mac(res[c], (F)w, v[c]);
+    }
+    store_entry<T, C>(out, res);
+
+    if (dy_dx) {
+        T* dd = dy_dx + (size_t)b * D * L * C + level * D * C;
+#pragma unroll
+        for (uint32_t gd = 0; gd < D; gd++) {
+            typename A::S rg[C];
+#pragma unroll
+            for (uint32_t c = 0; c < C; ++c) rg[c] = A::zero();
+#pragma unroll
+            for (uint32_t idx = 0; idx < (1u << (D - 1)); idx++) {
+                float w = scale;
+                uint32_t pl[D];
+#pragma unroll
+                for (uint32_t nd = 0; nd < D - 1; nd++) {
+                    const uint32_t d = (nd >= gd) ? (nd + 1) : nd;
+                    if ((idx & (1u << nd)) == 0) {
+                        w *= 1 - pos[d];
+                        pl[d] = pg[d];
+                    } else {
+                        w *= pos[d];
+                        pl[d] = pg[d] + 1;
+                    }
+                }
+                pl[gd] = pg[gd];
+                const uint32_t il = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
+                pl[gd] = pg[gd] + 1;
+                const uint32_t ir = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
+                F vl[C], vr[C];
+                load_entry<T, C>(g + (size_t)il * C, vl);
+                load_entry<T, C>(g + (size_t)ir * C, vr);
+#pragma unroll
+                for (uint32_t c = 0; c < C; ++c)
+                    rg[c] = A::mac(rg[c], (F)w * (vr[c] - vl[c]), (F)pos_deriv[gd]);
+            }
+#pragma unroll
+            for (uint32_t c = 0; c < C; ++c) dd[gd * C + c] = rg[c];
+        }
+    }
+}
+
+// ---- scatter-add of one corner's C channels -------------------------------
+template <typename T, uint32_t C> struct Scatter;
+template <uint32_t C> struct Scatter<float, C> {
+    NGP_DEV static void add(float* p, float w, const float g[C]) {
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) atomicAdd(p + c, w * g[c]);
+    }
+};
+template <uint32_t C> struct Scatter<double, C> {
+    NGP_DEV static void add(double* p, float w, const double g[C]) {
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) atomicAdd(p + c, (double)w * g[c]);
+    }
+};
+template <uint32_t C> struct Scatter<ngp_half, C> {
+    NGP_DEV static void add(ngp_half* p, float w, const float g[C]) {
+        if constexpr (C % 2 == 0) {
+#pragma unroll
+            for (uint32_t c = 0; c < C; c += 2) {
+                ngp_half2 v = {(ngp_half)(w * g[c]), (ngp_half)(w * g[c + 1])};
+                __builtin_amdgcn_global_atomic_fadd_v2f16(reinterpret_cast<ngp_half2*>(p + c), v);
+            }
+        } else {
+            // C == 1: packed add of (v, 0) into the aligned dword holding the entry.
+            const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+            ngp_half2* base = reinterpret_cast<ngp_half2*>(a & ~uintptr_t(3));
+            const ngp_half hv = (ngp_half)(w * g[0]);
+            ngp_half2 v = (a & 2) ? ngp_half2{(ngp_half)0.0f, hv} : ngp_half2{hv, (ngp_half)0.0f};
+            __builtin_amdgcn_global_atomic_fadd_v2f16(base, v);
+        }
+    }
+};
+
+template <typename T, uint32_t D, uint32_t C>
+__global__ void __launch_bounds__(256)
+k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
+           const int32_t* __restrict__ offsets, T* __restrict__ grad_grid, uint32_t B, uint32_t L,
+           GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+           int32_t grad_layout) {
+    using A = Acc<T>;
+    using F = typename A::F;
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const uint32_t level = blockIdx.y;
+
+    float x[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        x[d] = inputs[(size_t)b * D + d];
+        if (x[d] < 0 || x[d] > 1) return;  // grad is zero-initialised
+    }
+
+    const uint32_t off0 = (uint32_t)offsets[level];
+    const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
+    const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
+    T* __restrict__ gg = grad_grid + (size_t)off0 * C;
+    const float scale = lv.scale[level];
+    const uint32_t resolution = lv.res[level];
+
+    float pos[D];
+    uint32_t pg[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        pos[d] = fmaf(x[d], scale, align_corners ? 0.0f : 0.5f);
+        pg[d] = (uint32_t)floorf(pos[d]);
+        pos[d] -= (float)pg[d];
+        if (interp == 1) pos[d] = smoothstep(pos[d]);
+    }
+
+    const T* gp = grad_layout == 0 ? grad + ((size_t)level * B + b) * C
+                                   : grad + ((size_t)b * L + level) * C;
+    F gcur[C];
+    load_entry<T, C>(gp, gcur);
+
+#pragma unroll
+    for (uint32_t idx = 0; idx < (1u << D); idx++) {
+        float w = 1;
+        uint32_t pl[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; d++) {
+            if ((idx & (1u << d)) == 0) {
+                w *= 1 - pos[d];
+                pl[d] = pg[d];
+            } else {
+                w *= pos[d];
+                pl[d] = pg[d] + 1;
+            }
+        }
+        const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
+        Scatter<T, C>::add(gg + (size_t)e * C, w, gcur);
+    }
+}
+
+template <typename T, uint32_t D, uint32_t C>
+__global__ void __launch_bounds__(256)
+k_grid_input_bwd(const T* __restrict__ grad, const T* __restrict__ dy_dx,
+                 T* __restrict__ grad_inputs, uint32_t B, uint32_t L, int32_t grad_layout) {
+    using A = Acc<T>;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * D) return;
+    const uint32_t b = t / D;
+    const uint32_t d = t - b * D;
+    const T* dd = dy_dx + (size_t)b * L * D * C;
+    typename A::S result = A::zero();
+    for (uint32_t l = 0; l < L; l++) {
+#pragma unroll
+        for (uint32_t ch = 0; ch < C; ch++) {
+            const size_t gi = grad_layout == 0 ? ((size_t)l * B + b) * C + ch
+                                               : ((size_t)b * L + l) * C + ch;
+            result = A::mac(result, A::load(grad + gi), A::load(dd + l * D * C + d * C + ch));
+        }
+    }
+    grad_inputs[t] = result;
+}
+
+// TV gradient (reference gridencoder.cu:503-607). float / double only: the
+// reference's half instantiation calls an empty at::Half atomicAdd stub
+// (gridencoder.cu:22-26) and so never writes anything.
+template <typename T, uint32_t D, uint32_t C>
+__global__ void __launch_bounds__(256)
+k_grid_tv(const T* __restrict__ inputs, const T* __restrict__ grid, T* __restrict__ grad,
+          const int32_t* __restrict__ offsets, float weight, uint32_t B, uint32_t L, GridLevels lv,
+          uint32_t gridtype, bool align_corners) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const uint32_t level = blockIdx.y;
+    T x[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        x[d] = inputs[(size_t)b * D + d];
+        if (x[d] < 0 || x[d] > 1) return;
+    }
+    const uint32_t off0 = (uint32_t)offsets[level];
+    const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
+    const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
+    const T* g = grid + (size_t)off0 * C;
+    T* gr = grad + (size_t)off0 * C;
+    const float scale = lv.scale[level];
+    const uint32_t resolution = lv.res[level];
+    uint32_t pg[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        float pos;
+        if constexpr (sizeof(T) == 8) pos = (float)fma(x[d], (double)scale, align_corners ? 0.0 : 0.5);
+        else pos = fmaf((float)x[d], scale, align_corners ? 0.0f : 0.5f);
+        pg[d] = (uint32_t)floorf(pos);
+    }
+    T results[C], idelta[C];
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) { results[c] = 0; idelta[c] = 0; }
+    const uint32_t index = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pg) * C;
+    const T w = (T)(weight / (2 * D));
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        const uint32_t cur_d = pg[d];
+        if (cur_d < resolution) {
+            pg[d] = cur_d + 1;
+            const uint32_t ir = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pg) * C;
+#pragma unroll
+            for (uint32_t c = 0; c < C; c++) {
+                const T gv = g[index + c] - g[ir + c];
+                results[c] += gv;
+                idelta[c] += gv * gv;
+            }
+        }
+        if (cur_d > 0) {
+            pg[d] = cur_d - 1;
+            const uint32_t il = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pg) * C;
+#pragma unroll
+            for (uint32_t c = 0; c < C; c++) {
+                const T gv = g[index + c] - g[il + c];
+                results[c] += gv;
+                idelta[c] += gv * gv;
+            }
+        }
+        pg[d] = cur_d;
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < C; c++)
+        atomicAdd(&gr[index + c], w * results[c] * (T)rsqrtf((float)(idelta[c] + (T)1e-9f)));
+}
+
+// ---- dispatch ---------------------------------------------------------------
+template <typename T, uint32_t D>
+int fwd_c(const float* inputs, const void* emb, const int32_t* offsets, void* out, uint32_t B,
+          uint32_t C, uint32_t L, const GridLevels& lv, void* dy_dx, uint32_t gridtype,
+          bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+    const dim3 grid(ngp_div_up(B, 256), L);
+    const T* e = (const T*)emb;
+    T* o = (T*)out;
+    T* dd = (T*)dy_dx;
+    switch (C) {
+        case 1: k_grid_fwd<T, D, 1><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout); break;
+        case 2: k_grid_fwd<T, D, 2><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout); break;
+        case 4: k_grid_fwd<T, D, 4><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout); break;
+        case 8: k_grid_fwd<T, D, 8><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout); break;
+        default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: C must be 1, 2, 4, or 8.");
+    }
+    return ngp_check_launch("grid_encode_forward");
+}
+
+template <typename T>
+int fwd_t(const float* inputs, const void* emb, const int32_t* offsets, void* out, uint32_t B,
+          uint32_t D, uint32_t C, uint32_t L, const GridLevels& lv, void* dy_dx,
+          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+    switch (D) {
+        case 2: return fwd_c<T, 2>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, st);
+        case 3: return fwd_c<T, 3>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, st);
+        case 4: return fwd_c<T, 4>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, st);
+        case 5: return fwd_c<T, 5>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, st);
+        default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: D must be 2, 3, 4, or 5.");
+    }
+}
+
+template <typename T, uint32_t D, uint32_t C>
+int bwd_one(const void* grad, const float* inputs, const int32_t* offsets, void* gemb,
+            uint32_t B, uint32_t L, const GridLevels& lv, const void* dy_dx, void* grad_inputs,
+            uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+    const dim3 grid(ngp_div_up(B, 256), L);
+    k_grid_bwd<T, D, C><<<grid, 256, 0, st>>>((const T*)grad, inputs, offsets, (T*)gemb, B, L, lv,
+                                               gridtype, ac, interp, layout);
+    if (dy_dx && grad_inputs) {
+        k_grid_input_bwd<T, D, C><<<ngp_div_up(B * D, 256), 256, 0, st>>>(
+            (const T*)grad, (const T*)dy_dx, (T*)grad_inputs, B, L, layout);
+    }
+    return ngp_check_launch("grid_encode_backward");
+}
+
+template <typename T, uint32_t D>
+int bwd_c(const void* grad, const float* inputs, const int32_t* offsets, void* gemb, uint32_t B,
+          uint32_t C, uint32_t L, const GridLevels& lv, const void* dy_dx, void* gi,
+          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+    switch (C) {
+        case 1: return bwd_one<T, D, 1>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        case 2: return bwd_one<T, D, 2>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        case 4: return bwd_one<T, D, 4>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        case 8: return bwd_one<T, D, 8>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: C must be 1, 2, 4, or 8.");
+    }
+}
+
+template <typename T>
+int bwd_t(const void* grad, const float* inputs, const int32_t* offsets, void* gemb, uint32_t B,
+          uint32_t D, uint32_t C, uint32_t L, const GridLevels& lv, const void* dy_dx, void* gi,
+          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+    switch (D) {
+        case 2: return bwd_c<T, 2>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        case 3: return bwd_c<T, 3>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        case 4: return bwd_c<T, 4>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        case 5: return bwd_c<T, 5>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: D must be 2, 3, 4, or 5.");
+    }
+}
+
+template <typename T, uint32_t D>
+int tv_c(const void* inputs, const void* emb, void* grad, const int32_t* offsets, float weight,
+         uint32_t B, uint32_t C, uint32_t L, const GridLevels& lv, uint32_t gridtype, bool ac,
+         hipStream_t st) {
+    const dim3 grid(ngp_div_up(B, 256), L);
+    const T* in = (const T*)inputs;
+    const T* e = (const T*)emb;
+    T* g = (T*)grad;
+    switch (C) {
+        case 1: k_grid_tv<T, D, 1><<<grid, 256, 0, st>>>(in, e, g, offsets, weight, B, L, lv, gridtype, ac); break;
+        case 2: k_grid_tv<T, D, 2><<<grid, 256, 0, st>>>(in, e, g, offsets, weight, B, L, lv, gridtype, ac); break;
+        case 4: k_grid_tv<T, D, 4><<<grid, 256, 0, st>>>(in, e, g, offsets, weight, B, L, lv, gridtype, ac); break;
+        case 8: k_grid_tv<T, D, 8><<<grid, 256, 0, st>>>(in, e, g, offsets, weight, B, L, lv, gridtype, ac); break;
+        default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: C must be 1, 2, 4, or 8.");
+    }
+    return ngp_check_launch("grad_total_variation");
+}
+
+template <typename T>
+int tv_t(const void* inputs, const void* emb, void* grad, const int32_t* offsets, float weight,
+         uint32_t B, uint32_t D, uint32_t C, uint32_t L, const GridLevels& lv, uint32_t gridtype,
+         bool ac, hipStream_t st) {
+    switch (D) {
+        case 2: return tv_c<T, 2>(inputs, emb, grad, offsets, weight, B, C, L, lv, gridtype, ac, st);
+        case 3: return tv_c<T, 3>(inputs, emb, grad, offsets, weight, B, C, L, lv, gridtype, ac, st);
+        case 4: return tv_c<T, 4>(inputs, emb, grad, offsets, weight, B, C, L, lv, gridtype, ac, st);
+        case 5: return tv_c<T, 5>(inputs, emb, grad, offsets, weight, B, C, L, lv, gridtype, ac, st);
+        default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: D must be 2, 3, 4, or 5.");
+    }
+}
+
+int check_common(uint32_t L, const void* a, const void* b, const void* c) {
+    NGP_REQUIRE(L >= 1 && L <= kMaxLevels, NGP_ERR_ARG, "GridEncoding: L must be in [1, %u], got %u", kMaxLevels, L);
+    NGP_REQUIRE(a && b && c, NGP_ERR_ARG, "GridEncoding: null tensor pointer");
+    return NGP_OK;
+}
+
+}  // namespace
+
+extern "C" int ngp_grid_encode_forward(const float* inputs, const void* embeddings,
+                                       const int32_t* offsets, void* outputs, uint32_t B,
+                                       uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                                       void* dy_dx, uint32_t gridtype, int32_t align_corners,
+                                       uint32_t interp, int32_t dtype, int32_t out_layout,
+                                       void* stream) {
+    if (int e = check_common(L, embeddings, offsets, outputs)) return e;
+    if (B == 0) return NGP_OK;
+    NGP_REQUIRE(inputs, NGP_ERR_ARG, "GridEncoding: null inputs");
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const bool ac = align_corners != 0;
+    hipStream_t st = ngp_stream(stream);
+    switch (dtype) {
+        case NGP_DTYPE_F32: return fwd_t<float>(inputs, embeddings, offsets, outputs, B, D, C, L, lv, dy_dx, gridtype, ac, interp, out_layout, st);
+        case NGP_DTYPE_F16: return fwd_t<ngp_half>(inputs, embeddings, offsets, outputs, B, D, C, L, lv, dy_dx, gridtype, ac, interp, out_layout, st);
+        case NGP_DTYPE_F64: return fwd_t<double>(inputs, embeddings, offsets, outputs, B, D, C, L, lv, dy_dx, gridtype, ac, interp, out_layout, st);
+        default: return ngp_set_error(NGP_ERR_ARG, "embeddings must be a floating tensor");
+    }
+}
+
+extern "C" int ngp_grid_encode_backward(const void* grad, const float* inputs,
+                                        const void* embeddings, const int32_t* offsets,
+                                        void* grad_embeddings, uint32_t B, uint32_t D, uint32_t C,
+                                        uint32_t L, float S, uint32_t H, const void* dy_dx,
+                                        void* grad_inputs, uint32_t gridtype,
+                                        int32_t align_corners, uint32_t interp, int32_t dtype,
+                                        int32_t grad_layout, void* stream) {
+    (void)embeddings;
+    if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
+    if (B == 0) return NGP_OK;
+    NGP_REQUIRE(inputs, NGP_ERR_ARG, "GridEncoding: null inputs");
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const bool ac = align_corners != 0;
+    hipStream_t st = ngp_stream(stream);
+    switch (dtype) {
+        case NGP_DTYPE_F32: return bwd_t<float>(grad, inputs, offsets, grad_embeddings, B, D, C, L, lv, dy_dx, grad_inputs, gridtype, ac, interp, grad_layout, st);
+        case NGP_DTYPE_F16: return bwd_t<ngp_half>(grad, inputs, offsets, grad_embeddings, B, D, C, L, lv, dy_dx, grad_inputs, gridtype, ac, interp, grad_layout, st);
+        case NGP_DTYPE_F64: return bwd_t<double>(grad, inputs, offsets, grad_embeddings, B, D, C, L, lv, dy_dx, grad_inputs, gridtype, ac, interp, grad_layout, st);
+        default: return ngp_set_error(NGP_ERR_ARG, "grad must be a floating tensor");
+    }
+}
+
+extern "C" int ngp_grad_total_variation(const void* inputs, const void* embeddings, void* grad,
+                                        const int32_t* offsets, float weight, uint32_t B,
+                                        uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                                        uint32_t gridtype, int32_t align_corners, int32_t dtype,
+                                        void* stream) {
+    if (int e = check_common(L, embeddings, offsets, grad)) return e;
+    if (B == 0) return NGP_OK;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const bool ac = align_corners != 0;
+    hipStream_t st = ngp_stream(stream);
+    switch (dtype) {
+        case NGP_DTYPE_F32: return tv_t<float>(inputs, embeddings, grad, offsets, weight, B, D, C, L, lv, gridtype, ac, st);
+        case NGP_DTYPE_F64: return tv_t<double>(inputs, embeddings, grad, offsets, weight, B, D, C, L, lv, gridtype, ac, st);
+        case NGP_DTYPE_F16:
+            return ngp_set_error(NGP_ERR_UNSUPPORTED, "grad_total_variation: half embeddings are not supported (call it outside autocast, as GridEncoder.grad_total_variation does)");
+        default: return ngp_set_error(NGP_ERR_ARG, "embeddings must be a floating tensor");
+    }
+}

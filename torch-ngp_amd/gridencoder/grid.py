@@ -1,0 +1,160 @@
+"""Multiresolution hash-grid encoder: autograd op + nn.Module.
+
+Mirrors the reference's hot-path half of gridencoder/grid.py (:21-105 and
+GridEncoder :754-843) with the same constructor arguments, parameter layout,
+state_dict keys (`embeddings`, `offsets`) and autocast behaviour (fp16 table
+under autocast when C is even, fp32 inputs always). The MinkowskiEngine
+encoders of the research fork (grid.py:108-751) are out of scope.
+
+Difference from the reference: the HIP kernel writes the [B, L*C] output
+directly and reads the [B, L*C] gradient directly, so the two permute copies
+of grid.py:69 and grid.py:87 are gone; `_backend.grid_encode_forward` itself
+keeps the reference's [L, B, C] contract for drop-in callers.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.autograd import Function
+
+from .backend import _backend
+
+_gridtype_to_id = {"hash": 0, "tiled": 1}
+_interp_to_id = {"linear": 0, "smoothstep": 1}
+
+
+class _grid_encode(Function):
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, inputs, embeddings, offsets, per_level_scale, base_resolution,
+                calc_grad_inputs=False, gridtype=0, align_corners=False, interpolation=0):
+        # inputs: [B, D] float in [0, 1]; embeddings: [sO, C]; offsets: [L + 1] int
+        inputs = inputs.contiguous()
+        B, D = inputs.shape
+        L = offsets.shape[0] - 1
+        C = embeddings.shape[1]
+        S = np.log2(per_level_scale)
+        H = base_resolution
+
+        # autocast: half table when C is even (grid.py:52-56); inputs stay float
+        if torch.is_autocast_enabled() and C % 2 == 0:
+            embeddings = embeddings.to(torch.half)
+
+        outputs = torch.empty(B, L * C, device=inputs.device, dtype=embeddings.dtype)
+        dy_dx = (torch.empty(B, L * D * C, device=inputs.device, dtype=embeddings.dtype)
+                 if calc_grad_inputs else None)
+
+        _backend.grid_encode_forward_bm(inputs, embeddings, offsets, outputs, B, D, C, L, S, H,
+                                        dy_dx, gridtype, align_corners, interpolation)
+
+        ctx.save_for_backward(inputs, embeddings, offsets, dy_dx)
+        ctx.dims = [B, D, C, L, S, H, gridtype, interpolation]
+        ctx.align_corners = align_corners
+        return outputs
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, grad):
+        inputs, embeddings, offsets, dy_dx = ctx.saved_tensors
+        B, D, C, L, S, H, gridtype, interpolation = ctx.dims
+        align_corners = ctx.align_corners
+
+        grad = grad.contiguous()
+        if grad.dtype != embeddings.dtype:
+            grad = grad.to(embeddings.dtype)
+        grad_embeddings = torch.zeros_like(embeddings)
+        grad_inputs = (torch.zeros_like(inputs, dtype=embeddings.dtype)
+                       if dy_dx is not None else None)
+
+        _backend.grid_encode_backward_bm(grad, inputs, embeddings, offsets, grad_embeddings, B, D,
+                                         C, L, S, H, dy_dx, grad_inputs, gridtype, align_corners,
+                                         interpolation)
+        if dy_dx is not None:
+            grad_inputs = grad_inputs.to(inputs.dtype)
+        return grad_inputs, grad_embeddings, None, None, None, None, None, None, None
+
+
+grid_encode = _grid_encode.apply
+
+
+class GridEncoder(nn.Module):
+    def __init__(self, input_dim=3, num_levels=16, level_dim=2, per_level_scale=2,
+                 base_resolution=16, log2_hashmap_size=19, desired_resolution=None,
+                 gridtype="hash", align_corners=False, interpolation="linear"):
+        super().__init__()
+        # the finest resolution overrides per_level_scale when given (grid.py:758-759)
+        if desired_resolution is not None:
+            per_level_scale = np.exp2(np.log2(desired_resolution / base_resolution) / (num_levels - 1))
+
+        self.input_dim = input_dim
+        self.num_levels = num_levels
+        self.level_dim = level_dim
+        self.per_level_scale = per_level_scale
+        self.log2_hashmap_size = log2_hashmap_size
+        self.base_resolution = base_resolution
+        self.output_dim = num_levels * level_dim
+        self.gridtype = gridtype
+        self.gridtype_id = _gridtype_to_id[gridtype]
+        self.interpolation = interpolation
+        self.interp_id = _interp_to_id[interpolation]
+        self.align_corners = align_corners
+
+        # level table layout (grid.py:776-789): entries per level capped at
+        # 2^log2T, rounded up to a multiple of 8
+        self.max_params = 2 ** log2_hashmap_size
+        offsets = []
+        offset = 0
+        for i in range(num_levels):
+            resolution = int(np.ceil(base_resolution * per_level_scale ** i))
+            params_in_level = min(self.max_params,
+                                  (resolution if align_corners else resolution + 1) ** input_dim)
+            params_in_level = int(np.ceil(params_in_level / 8) * 8)
+            offsets.append(offset)
+            offset += params_in_level
+        offsets.append(offset)
+        self.register_buffer("offsets", torch.from_numpy(np.array(offsets, dtype=np.int32)))
+        self.n_params = offsets[-1] * level_dim
+        self.embeddings = nn.Parameter(torch.empty(offset, level_dim))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        std = 1e-4
+        self.embeddings.data.uniform_(-std, std)
+
+    def __repr__(self):
+        return (f"GridEncoder: input_dim={self.input_dim} num_levels={self.num_levels} "
+                f"level_dim={self.level_dim} resolution={self.base_resolution} -> "
+                f"{int(round(self.base_resolution * self.per_level_scale ** (self.num_levels - 1)))} "
+                f"per_level_scale={self.per_level_scale:.4f} params={tuple(self.embeddings.shape)} "
+                f"gridtype={self.gridtype} align_corners={self.align_corners} "
+                f"interpolation={self.interpolation}")
+
+    def forward(self, inputs, bound=1):
+        # inputs: [..., input_dim] in [-bound, bound] -> [..., num_levels * level_dim]
+        inputs = (inputs + bound) / (2 * bound)
+        prefix_shape = list(inputs.shape[:-1])
+        inputs = inputs.view(-1, self.input_dim)
+        outputs = grid_encode(inputs, self.embeddings, self.offsets, self.per_level_scale,
+                              self.base_resolution, inputs.requires_grad, self.gridtype_id,
+                              self.align_corners, self.interp_id)
+        return outputs.view(prefix_shape + [self.output_dim])
+
+    @torch.amp.autocast("cuda", enabled=False)
+    def grad_total_variation(self, weight=1e-7, inputs=None, bound=1, B=1000000):
+        """Adds the TV-regulariser gradient into embeddings.grad (grid.py:821-843)."""
+        D = self.input_dim
+        C = self.embeddings.shape[1]
+        L = self.offsets.shape[0] - 1
+        S = np.log2(self.per_level_scale)
+        H = self.base_resolution
+        if inputs is None:
+            inputs = torch.rand(B, self.input_dim, device=self.embeddings.device)
+        else:
+            inputs = (inputs + bound) / (2 * bound)
+            inputs = inputs.view(-1, self.input_dim)
+            B = inputs.shape[0]
+        if self.embeddings.grad is None:
+            raise ValueError("grad is None, should be called after loss.backward() and before "
+                             "optimizer.step()!")
+        _backend.grad_total_variation(inputs.to(self.embeddings.dtype).contiguous(),
+                                      self.embeddings, self.embeddings.grad, self.offsets, weight,
+                                      B, D, C, L, S, H, self.gridtype_id, self.align_corners)

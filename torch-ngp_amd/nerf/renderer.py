@@ -1,0 +1,336 @@
+"""NeRF renderer: the hot-path caller (reference nerf/renderer.py:62-634).
+
+Restores the upstream torch-ngp behaviour the research fork broke (SURVEY
+§1.3): density grid updates work (update_extra_state), no Minkowski /
+frnn branches in run_cuda, no trimesh import. Public methods and buffers
+(`density_grid`, `density_bitfield`, `step_counter`, `mean_count`, ...) keep
+the reference names so checkpoints and trainers interoperate.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+import raymarching
+
+
+def custom_meshgrid(*args):
+    return torch.meshgrid(*args, indexing="ij")
+
+
+def sample_pdf(bins, weights, n_samples, det=False):
+    """Inverse-CDF sampling (reference renderer.py:12-46)."""
+    weights = weights + 1e-5
+    pdf = weights / torch.sum(weights, -1, keepdim=True)
+    cdf = torch.cumsum(pdf, -1)
+    cdf = torch.cat([torch.zeros_like(cdf[..., :1]), cdf], -1)
+    if det:
+        u = torch.linspace(0.5 / n_samples, 1.0 - 0.5 / n_samples, steps=n_samples, device=weights.device)
+        u = u.expand(list(cdf.shape[:-1]) + [n_samples])
+    else:
+        u = torch.rand(list(cdf.shape[:-1]) + [n_samples], device=weights.device)
+    u = u.contiguous()
+    inds = torch.searchsorted(cdf, u, right=True)
+    below = torch.clamp(inds - 1, min=0)
+    above = torch.clamp(inds, max=cdf.shape[-1] - 1)
+    inds_g = torch.stack([below, above], -1)
+    shape = [inds_g.shape[0], inds_g.shape[1], cdf.shape[-1]]
+    cdf_g = torch.gather(cdf.unsqueeze(1).expand(shape), 2, inds_g)
+    bins_g = torch.gather(bins.unsqueeze(1).expand(shape), 2, inds_g)
+    denom = cdf_g[..., 1] - cdf_g[..., 0]
+    denom = torch.where(denom < 1e-5, torch.ones_like(denom), denom)
+    t = (u - cdf_g[..., 0]) / denom
+    return bins_g[..., 0] + t * (bins_g[..., 1] - bins_g[..., 0])
+
+
+class NeRFRenderer(nn.Module):
+    def __init__(self, bound=1, cuda_ray=False, density_scale=1, min_near=0.2, density_thresh=0.01,
+                 bg_radius=-1, grid_size=128, **kwargs):
+        super().__init__()
+        self.bound = bound
+        self.cascade = 1 + math.ceil(math.log2(bound))
+        self.grid_size = grid_size
+        self.density_scale = density_scale
+        self.min_near = min_near
+        self.density_thresh = density_thresh
+        self.bg_radius = bg_radius
+
+        aabb_train = torch.FloatTensor([-bound, -bound, -bound, bound, bound, bound])
+        self.register_buffer("aabb_train", aabb_train)
+        self.register_buffer("aabb_infer", aabb_train.clone())
+
+        self.cuda_ray = cuda_ray
+        if cuda_ray:
+            self.register_buffer("density_grid", torch.zeros([self.cascade, grid_size ** 3]))
+            self.register_buffer("density_bitfield",
+                                 torch.zeros(self.cascade * grid_size ** 3 // 8, dtype=torch.uint8))
+            self.mean_density = 0
+            self.iter_density = 0
+            self.register_buffer("step_counter", torch.zeros(16, 2, dtype=torch.int32))
+            self.mean_count = 0
+            self.local_step = 0
+
+    def forward(self, x, d):
+        raise NotImplementedError()
+
+    def density(self, x):
+        raise NotImplementedError()
+
+    def color(self, x, d, mask=None, **kwargs):
+        raise NotImplementedError()
+
+    def background(self, x, d):
+        raise NotImplementedError()
+
+    def reset_extra_state(self):
+        if not self.cuda_ray:
+            return
+        self.density_grid.zero_()
+        self.mean_density = 0
+        self.iter_density = 0
+        self.step_counter.zero_()
+        self.mean_count = 0
+        self.local_step = 0
+
+    # ------------------------------------------------------------- torch path
+    def run(self, rays_o, rays_d, num_steps=128, upsample_steps=128, bg_color=None, perturb=False,
+            **kwargs):
+        """Uniform (+ importance) sampling without the density grid (renderer.py:126-254)."""
+        prefix = rays_o.shape[:-1]
+        rays_o = rays_o.contiguous().view(-1, 3)
+        rays_d = rays_d.contiguous().view(-1, 3)
+        N = rays_o.shape[0]
+        device = rays_o.device
+        aabb = self.aabb_train if self.training else self.aabb_infer
+        nears, fars = raymarching.near_far_from_aabb(rays_o, rays_d, aabb, self.min_near)
+        nears, fars = nears.unsqueeze(-1), fars.unsqueeze(-1)
+
+        z_vals = torch.linspace(0.0, 1.0, num_steps, device=device).unsqueeze(0).expand(N, num_steps)
+        z_vals = nears + (fars - nears) * z_vals
+        sample_dist = (fars - nears) / num_steps
+        if perturb:
+            z_vals = z_vals + (torch.rand(z_vals.shape, device=device) - 0.5) * sample_dist
+        xyzs = rays_o.unsqueeze(-2) + rays_d.unsqueeze(-2) * z_vals.unsqueeze(-1)
+        xyzs = torch.min(torch.max(xyzs, aabb[:3]), aabb[3:])
+        dens = {k: v.view(N, num_steps, -1) for k, v in self.density(xyzs.reshape(-1, 3)).items()}
+
+        if upsample_steps > 0:
+            with torch.no_grad():
+                deltas = z_vals[..., 1:] - z_vals[..., :-1]
+                deltas = torch.cat([deltas, sample_dist * torch.ones_like(deltas[..., :1])], dim=-1)
+                alphas = 1 - torch.exp(-deltas * self.density_scale * dens["sigma"].squeeze(-1))
+                alphas_shifted = torch.cat([torch.ones_like(alphas[..., :1]), 1 - alphas + 1e-15], dim=-1)
+                weights = alphas * torch.cumprod(alphas_shifted, dim=-1)[..., :-1]
+                z_mid = z_vals[..., :-1] + 0.5 * deltas[..., :-1]
+                new_z = sample_pdf(z_mid, weights[:, 1:-1], upsample_steps, det=not self.training).detach()
+                new_xyzs = rays_o.unsqueeze(-2) + rays_d.unsqueeze(-2) * new_z.unsqueeze(-1)
+                new_xyzs = torch.min(torch.max(new_xyzs, aabb[:3]), aabb[3:])
+            new_dens = {k: v.view(N, upsample_steps, -1)
+                        for k, v in self.density(new_xyzs.reshape(-1, 3)).items()}
+            z_vals, z_index = torch.sort(torch.cat([z_vals, new_z], dim=1), dim=1)
+            xyzs = torch.cat([xyzs, new_xyzs], dim=1)
+            xyzs = torch.gather(xyzs, 1, z_index.unsqueeze(-1).expand_as(xyzs))
+            for k in dens:
+                tmp = torch.cat([dens[k], new_dens[k]], dim=1)
+                dens[k] = torch.gather(tmp, 1, z_index.unsqueeze(-1).expand_as(tmp))
+
+        deltas = z_vals[..., 1:] - z_vals[..., :-1]
+        deltas = torch.cat([deltas, sample_dist * torch.ones_like(deltas[..., :1])], dim=-1)
+        alphas = 1 - torch.exp(-deltas * self.density_scale * dens["sigma"].squeeze(-1))
+        alphas_shifted = torch.cat([torch.ones_like(alphas[..., :1]), 1 - alphas + 1e-15], dim=-1)
+        weights = alphas * torch.cumprod(alphas_shifted, dim=-1)[..., :-1]
+        dirs = rays_d.view(-1, 1, 3).expand_as(xyzs)
+        dens = {k: v.reshape(-1, v.shape[-1]) for k, v in dens.items()}
+        mask = weights > 1e-4
+        rgbs = self.color(xyzs.reshape(-1, 3), dirs.reshape(-1, 3), mask=mask.reshape(-1), **dens)
+        rgbs = rgbs.view(N, -1, 3)
+        weights_sum = weights.sum(dim=-1)
+        ori_z = ((z_vals - nears) / (fars - nears)).clamp(0, 1)
+        depth = torch.sum(weights * ori_z, dim=-1)
+        image = torch.sum(weights.unsqueeze(-1) * rgbs, dim=-2)
+        if self.bg_radius > 0:
+            sph = raymarching.sph_from_ray(rays_o, rays_d, self.bg_radius)
+            bg_color = self.background(sph, rays_d.reshape(-1, 3))
+        elif bg_color is None:
+            bg_color = 1
+        image = image + (1 - weights_sum).unsqueeze(-1) * bg_color
+        return {"depth": depth.view(*prefix), "image": image.view(*prefix, 3),
+                "weights_sum": weights_sum}
+
+    # -------------------------------------------------------------- HIP path
+    def run_cuda(self, rays_o, rays_d, dt_gamma=0, bg_color=None, perturb=False,
+                 force_all_rays=False, max_steps=1024, T_thresh=1e-4, **kwargs):
+        """Density-grid ray marching (renderer.py:257-431, upstream semantics)."""
+        prefix = rays_o.shape[:-1]
+        rays_o = rays_o.contiguous().view(-1, 3)
+        rays_d = rays_d.contiguous().view(-1, 3)
+        N = rays_o.shape[0]
+        device = rays_o.device
+
+        nears, fars = raymarching.near_far_from_aabb(
+            rays_o, rays_d, self.aabb_train if self.training else self.aabb_infer, self.min_near)
+
+        if self.bg_radius > 0:
+            sph = raymarching.sph_from_ray(rays_o, rays_d, self.bg_radius)
+            bg_color = self.background(sph, rays_d)
+        elif bg_color is None:
+            bg_color = 1
+
+        results = {}
+        if self.training:
+            counter = self.step_counter[self.local_step % 16]
+            counter.zero_()
+            self.local_step += 1
+            xyzs, dirs, deltas, rays = raymarching.march_rays_train(
+                rays_o, rays_d, self.bound, self.density_bitfield, self.cascade, self.grid_size,
+                nears, fars, counter, self.mean_count, perturb, 128, force_all_rays, dt_gamma,
+                max_steps)
+            sigmas, rgbs = self(xyzs, dirs)
+            sigmas = self.density_scale * sigmas
+            weights_sum, depth, image = raymarching.composite_rays_train(sigmas, rgbs, deltas, rays,
+                                                                         T_thresh)
+            image = image + (1 - weights_sum).unsqueeze(-1) * bg_color
+            depth = torch.clamp(depth - nears, min=0) / (fars - nears)
+            results["weights_sum"] = weights_sum
+            image = image.view(*prefix, 3)
+            depth = depth.view(*prefix)
+        else:
+            dtype = torch.float32
+            weights_sum = torch.zeros(N, dtype=dtype, device=device)
+            depth = torch.zeros(N, dtype=dtype, device=device)
+            image = torch.zeros(N, 3, dtype=dtype, device=device)
+            rays_alive = torch.arange(N, dtype=torch.int32, device=device)
+            rays_t = nears.clone()
+            step = 0
+            while step < max_steps:
+                n_alive = rays_alive.shape[0]
+                if n_alive <= 0:
+                    break
+                n_step = max(min(N // n_alive, 8), 1)
+                xyzs, dirs, deltas = raymarching.march_rays(
+                    n_alive, n_step, rays_alive, rays_t, rays_o, rays_d, self.bound,
+                    self.density_bitfield, self.cascade, self.grid_size, nears, fars, 128,
+                    perturb if step == 0 else False, dt_gamma, max_steps)
+                sigmas, rgbs = self(xyzs, dirs)
+                sigmas = self.density_scale * sigmas
+                raymarching.composite_rays(n_alive, n_step, rays_alive, rays_t, sigmas, rgbs, deltas,
+                                           weights_sum, depth, image, T_thresh)
+                rays_alive = rays_alive[rays_alive >= 0]
+                step += n_step
+            image = image + (1 - weights_sum).unsqueeze(-1) * bg_color
+            depth = torch.clamp(depth - nears, min=0) / (fars - nears)
+            image = image.view(*prefix, 3)
+            depth = depth.view(*prefix)
+        results["depth"] = depth
+        results["image"] = image
+        return results
+
+    @torch.no_grad()
+    def mark_untrained_grid(self, poses, intrinsic, S=64):
+        """Mark cells no training camera sees as -1 (renderer.py:433-496)."""
+        if not self.cuda_ray:
+            return
+        if isinstance(poses, np.ndarray):
+            poses = torch.from_numpy(poses)
+        B = poses.shape[0]
+        fx, fy, cx, cy = intrinsic
+        dev = self.density_bitfield.device
+        X = torch.arange(self.grid_size, dtype=torch.int32, device=dev).split(S)
+        count = torch.zeros_like(self.density_grid)
+        poses = poses.to(dev)
+        for xs in X:
+            for ys in X:
+                for zs in X:
+                    xx, yy, zz = custom_meshgrid(xs, ys, zs)
+                    coords = torch.stack([xx.reshape(-1), yy.reshape(-1), zz.reshape(-1)], -1)
+                    indices = raymarching.morton3D(coords).long()
+                    world = (2 * coords.float() / (self.grid_size - 1) - 1).unsqueeze(0)
+                    for cas in range(self.cascade):
+                        bound = min(2 ** cas, self.bound)
+                        hgs = bound / self.grid_size
+                        cas_world = world * (bound - hgs)
+                        head = 0
+                        while head < B:
+                            tail = min(head + S, B)
+                            cam = cas_world - poses[head:tail, :3, 3].unsqueeze(1)
+                            cam = cam @ poses[head:tail, :3, :3]
+                            mz = cam[:, :, 2] > 0
+                            mx = torch.abs(cam[:, :, 0]) < cx / fx * cam[:, :, 2] + hgs * 2
+                            my = torch.abs(cam[:, :, 1]) < cy / fy * cam[:, :, 2] + hgs * 2
+                            count[cas, indices] += (mz & mx & my).sum(0).reshape(-1)
+                            head += S
+        self.density_grid[count == 0] = -1
+
+    @torch.no_grad()
+    def update_extra_state(self, decay=0.95, S=128):
+        """EMA density-grid update + packbits + mean_count (renderer.py:498-598,
+        upstream cadence: every update_extra_interval steps)."""
+        if not self.cuda_ray:
+            return
+        tmp_grid = -torch.ones_like(self.density_grid)
+        dev = self.density_bitfield.device
+        if self.iter_density < 16:
+            X = torch.arange(self.grid_size, dtype=torch.int32, device=dev).split(S)
+            for xs in X:
+                for ys in X:
+                    for zs in X:
+                        xx, yy, zz = custom_meshgrid(xs, ys, zs)
+                        coords = torch.stack([xx.reshape(-1), yy.reshape(-1), zz.reshape(-1)], -1)
+                        indices = raymarching.morton3D(coords).long()
+                        xyzs = 2 * coords.float() / (self.grid_size - 1) - 1
+                        for cas in range(self.cascade):
+                            bound = min(2 ** cas, self.bound)
+                            hgs = bound / self.grid_size
+                            cas_xyzs = xyzs * (bound - hgs)
+                            cas_xyzs += (torch.rand_like(cas_xyzs) * 2 - 1) * hgs
+                            sigmas = self.density(cas_xyzs)["sigma"].reshape(-1).detach()
+                            tmp_grid[cas, indices] = sigmas.float() * self.density_scale
+        else:
+            N = self.grid_size ** 3 // 4
+            for cas in range(self.cascade):
+                coords = torch.randint(0, self.grid_size, (N, 3), device=dev)
+                indices = raymarching.morton3D(coords).long()
+                occ = torch.nonzero(self.density_grid[cas] > 0).squeeze(-1)
+                rand_mask = torch.randint(0, max(occ.shape[0], 1), [N], dtype=torch.long, device=dev)
+                occ_indices = occ[rand_mask] if occ.shape[0] > 0 else indices
+                occ_coords = raymarching.morton3D_invert(occ_indices)
+                indices = torch.cat([indices, occ_indices], dim=0)
+                coords = torch.cat([coords.int(), occ_coords], dim=0)
+                xyzs = 2 * coords.float() / (self.grid_size - 1) - 1
+                bound = min(2 ** cas, self.bound)
+                hgs = bound / self.grid_size
+                cas_xyzs = xyzs * (bound - hgs)
+                cas_xyzs += (torch.rand_like(cas_xyzs) * 2 - 1) * hgs
+                sigmas = self.density(cas_xyzs)["sigma"].reshape(-1).detach()
+                tmp_grid[cas, indices] = sigmas.float() * self.density_scale
+        valid = (self.density_grid >= 0) & (tmp_grid >= 0)
+        self.density_grid[valid] = torch.maximum(self.density_grid[valid] * decay, tmp_grid[valid])
+        self.mean_density = torch.mean(self.density_grid.clamp(min=0)).item()
+        self.iter_density += 1
+        density_thresh = min(self.mean_density, self.density_thresh)
+        self.density_bitfield = raymarching.packbits(self.density_grid, density_thresh,
+                                                     self.density_bitfield)
+        total_step = min(16, self.local_step)
+        if total_step > 0:
+            self.mean_count = int(self.step_counter[:total_step, 0].sum().item() / total_step)
+        self.local_step = 0
+
+    def render(self, rays_o, rays_d, staged=False, max_ray_batch=4096, **kwargs):
+        """rays_o/rays_d [B, N, 3] -> {'image' [B, N, 3], 'depth' [B, N], ...}."""
+        _run = self.run_cuda if self.cuda_ray else self.run
+        B, N = rays_o.shape[:2]
+        device = rays_o.device
+        if staged and not self.cuda_ray:
+            depth = torch.empty((B, N), device=device)
+            image = torch.empty((B, N, 3), device=device)
+            for b in range(B):
+                head = 0
+                while head < N:
+                    tail = min(head + max_ray_batch, N)
+                    r = _run(rays_o[b:b + 1, head:tail], rays_d[b:b + 1, head:tail], **kwargs)
+                    depth[b:b + 1, head:tail] = r["depth"]
+                    image[b:b + 1, head:tail] = r["image"]
+                    head += max_ray_batch
+            return {"depth": depth, "image": image}
+        return _run(rays_o, rays_d, **kwargs)

@@ -1,0 +1,1 @@
+from .raymarching import *  # noqa: F401,F403
