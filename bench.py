@@ -1,0 +1,293 @@
+"""Train-step rays/s of the instant-ngp hot path on synthetic 800x800 Lego.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+
+One step = sample 4096 rays of a random training pose -> near/far ->
+march_rays_train -> hash-grid encode -> sigma FFMLP -> trunc_exp -> SH ->
+colour FFMLP -> composite -> MSE -> full backward -> Adam.
+The density bitfield is the analytic Lego-like fixture (density-grid update
+excluded from the timed step as SURVEY §8(d) defines it; its cost is reported
+separately as `density_update_ms`). Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "torch-ngp_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "train-step rays/sec (fwd+bwd) on 800×800 Lego; 1/2/4/8 MI355X"
+PUBLISHED_V100_RAYS_PER_S = 97 * 4096  # readme.md:211 via BASELINE.md (V100, torch -O)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+FP16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--num_rays", type=int, default=4096)
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--kernel-steps", type=int, default=10, help="instrumented steps for kernel timing")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu", dest="cpu", action="store_false")
+    return ap.parse_args()
+
+
+class KernelTimer:
+    """HIP-event timing of one _backend entry (one kernel launch per call) on
+    the stream it is launched on (torch's current stream)."""
+
+    def __init__(self, namespace, attr):
+        self.ns, self.attr = namespace, attr
+        self.fn = getattr(namespace, attr)
+        self.pairs = []
+        self.active = False
+
+    def __enter__(self):
+        def wrapped(*a, **k):
+            if not self.active:
+                return self.fn(*a, **k)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = self.fn(*a, **k)
+            e.record()
+            self.pairs.append((s, e))
+            return r
+        setattr(self.ns, self.attr, wrapped)
+        return self
+
+    def __exit__(self, *exc):
+        setattr(self.ns, self.attr, self.fn)
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        ts = [s.elapsed_time(e) for s, e in self.pairs]
+        return float(np.mean(ts)) if ts else float("nan")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(1234 + rank)
+    np.random.seed(rank)
+
+    import gridencoder.backend as gb
+    import ffmlp.backend as fb
+    import raymarching.backend as rb
+    from nerf.network_ff import NeRFNetwork
+    from nerf.provider import SyntheticLego, lego_bitfield
+    from nerf.train import Trainer
+
+    model = NeRFNetwork(bound=1, cuda_ray=True, density_thresh=10).to(dev)
+    if world > 1:  # identical initial parameters on every rank
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    bits = torch.from_numpy(lego_bitfield()).to(dev)
+    model.density_bitfield.copy_(bits)
+    data = SyntheticLego(dev, num_rays=args.num_rays)
+    trainer = Trainer(model, data, lr=1e-2, iters=30000, fp16=True, update_density=False,
+                      distributed=world > 1)
+
+    # warm-up: first step sizes the sample buffer with a D2H sync (mean_count = 0
+    # path of raymarching.py); afterwards mean_count is fixed from the measured
+    # counts, exactly what update_extra_state does upstream every 16 steps.
+    counts = []
+    n_first = max(2, min(args.warmup, 8))
+    for _ in range(n_first):
+        trainer.train_step()
+        counts.append(int(model.step_counter[(model.local_step - 1) % 16, 0].item()))
+    mean_count = int(np.mean(counts) * 1.25)
+    if world > 1:
+        t = torch.tensor([mean_count], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        mean_count = int(t.item())
+    model.mean_count = mean_count
+    for _ in range(max(0, args.warmup - n_first)):
+        trainer.train_step()
+    used_graph = False
+    if args.graph:
+        try:
+            trainer.capture()
+            for _ in range(3):
+                trainer.step()
+            used_graph = True
+        except Exception as e:  # eager steps are the same kernels; record why
+            print(f"[bench] graph capture failed, running eager: {e!r}", file=sys.stderr)
+            trainer.graph = None
+            trainer.static = None
+    torch.cuda.synchronize()
+
+    # ---------------- timed region ----------------
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    rays_total = args.num_rays * world * args.steps
+    value = rays_total / elapsed
+    samples = model.step_counter[:, 0].float()
+    samples_per_step = int(samples[samples > 0].mean().item()) if (samples > 0).any() else 0
+
+    # -------- per-kernel HIP-event timing (eager steps, same shapes) --------
+    trainer_graph, trainer_static = trainer.graph, trainer.static
+    trainer.graph, trainer.static = None, None
+    timers = {
+        "grid_encode_backward": KernelTimer(gb._backend, "grid_encode_backward_bm"),
+        "grid_encode_forward": KernelTimer(gb._backend, "grid_encode_forward_bm"),
+        "ffmlp_backward": KernelTimer(fb._backend, "ffmlp_backward"),
+        "ffmlp_forward": KernelTimer(fb._backend, "ffmlp_forward"),
+        "march_rays_train": KernelTimer(rb._backend, "march_rays_train"),
+        "composite_rays_train_forward": KernelTimer(rb._backend, "composite_rays_train_forward"),
+        "composite_rays_train_backward": KernelTimer(rb._backend, "composite_rays_train_backward"),
+    }
+    for tm in timers.values():
+        tm.__enter__()
+    for tm in timers.values():
+        tm.active = True
+    for _ in range(args.kernel_steps):
+        trainer.train_step()
+    kernel_ms = {k: tm.mean_ms() for k, tm in timers.items()}
+    for tm in timers.values():
+        tm.__exit__()
+    trainer.graph, trainer.static = trainer_graph, trainer_static
+    M_k = samples_per_step
+    # algorithmic bytes; fp16 table, D=3, L=16, C=2
+    grid_fwd_bytes = 588 * M_k
+    grid_bwd_bytes = 1100 * M_k
+    per_call_calls = {"grid_encode_forward": 1}
+    dominant = max(("grid_encode_backward", "grid_encode_forward"), key=lambda k: kernel_ms[k])
+    dom_bytes = grid_bwd_bytes if dominant == "grid_encode_backward" else grid_fwd_bytes
+    achieved = dom_bytes / (kernel_ms[dominant] * 1e-3) / 1e9
+    ffmlp_flops = 110592 * M_k
+    mlp_ms = kernel_ms["ffmlp_forward"] * 2 + kernel_ms["ffmlp_backward"] * 2
+    del per_call_calls
+
+    # density-grid update cost (reported, not in the timed step)
+    t = time.perf_counter()
+    with torch.autocast("cuda", dtype=torch.float16):
+        model.update_extra_state()
+    torch.cuda.synchronize()
+    density_update_ms = (time.perf_counter() - t) * 1e3
+    model.density_bitfield.copy_(bits)
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / PUBLISHED_V100_RAYS_PER_S, 3),
+        "dtype": "fp16",
+        "data": "synthetic",
+        "config": {
+            "workload": "lego_800x800_train_step (synthetic analytic Lego, bound 1, 1 cascade, "
+                        "128^3 bitfield fixture, hashgrid L16 C2 T2^19, FFMLP 64-wide)",
+            "num_rays_per_gpu": args.num_rays,
+            "global_batch_rays": args.num_rays * world,
+            "samples_per_step": samples_per_step,
+            "mean_count_M": mean_count,
+            "parallelism": f"dp{world}",
+            "hipgraph": used_graph,
+            "baseline_ref": "V100 97 it/s x 4096 rays (readme.md:211)",
+        },
+        "roofline": {
+            "kernel": dominant,
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "algorithmic_bytes_per_launch": int(dom_bytes),
+            "avg_launch_ms": round(kernel_ms[dominant], 5),
+        },
+        "kernels_ms": {k: round(v, 5) for k, v in kernel_ms.items()},
+        "ffmlp_mfma": {"flops_per_step": ffmlp_flops, "ms": round(mlp_ms, 5),
+                        "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
+                        "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
+        "density_update_ms": round(density_update_ms, 3),
+        "loss": float(loss.float().item()),
+    }
+
+    if rank == 0 and world == 1 and args.cpu:
+        result["cpu_baseline"] = cpu_baseline(model, data, args)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(model, data, args):
+    """The oracle's CPU restatement of the same train step (kind 'port'),
+    single-threaded, on a bounded sample of 4096-ray batches."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:  # pragma: no cover
+        threadpool_limits = None
+    import oracle
+    from oracle.pipeline import CPUNeRF, time_cpu_baseline
+
+    emb = model.encoder.embeddings.detach().float().cpu().numpy()
+    cpu = CPUNeRF(emb, model.encoder.offsets.cpu().numpy(), model.encoder.per_level_scale,
+                  model.sigma_net.weights.detach().float().cpu().numpy(),
+                  model.color_net.weights.detach().float().cpu().numpy(),
+                  model.density_bitfield.cpu().numpy())
+    oracle.build()
+    batches = []
+    for _ in range(16):
+        b = data.sample()
+        ro = b["rays_o"][0].cpu().numpy().astype(np.float32)
+        rd = b["rays_d"][0].cpu().numpy().astype(np.float32)
+        rgba = b["images"][0].cpu().numpy().astype(np.float32)
+        bg = np.random.rand(ro.shape[0], 3).astype(np.float32)
+        noises = np.random.rand(ro.shape[0]).astype(np.float32)
+        batches.append((ro, rd, rgba, bg, noises))
+    ctx = threadpool_limits(1) if threadpool_limits else None
+    if ctx:
+        ctx.__enter__()
+    try:
+        rps, steps, rays, secs, m = time_cpu_baseline(cpu, batches, args.cpu_budget)
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+    return {"value": round(rps, 2), "unit": "rays/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} train steps x {args.num_rays} rays (same synthetic Lego workload, "
+                      f"mean {int(m)} samples/step) in {secs:.1f}s, oracle/pipeline.py, 1 thread"}
+
+
+if __name__ == "__main__":
+    main()

@@ -68,7 +68,7 @@ class SyntheticLego:
     (scaled by `scale`, default 0.8 as in readme.md:139)."""
 
     def __init__(self, device, H=800, W=800, n_poses=100, scale=0.8, radius=4.0311,
-                 camera_angle_x=0.6911112, num_rays=4096, seed=0):
+                 camera_angle_x=0.6911112, num_rays=4096):
         self.device = device
         self.H, self.W = H, W
         self.num_rays = num_rays
@@ -87,8 +87,6 @@ class SyntheticLego:
             c2w[:3, 0], c2w[:3, 1], c2w[:3, 2], c2w[:3, 3] = right, up, back, c
             poses.append(nerf_matrix_to_ngp(c2w, scale=scale))
         self.poses = torch.from_numpy(np.stack(poses)).to(device)
-        self.gen = torch.Generator(device=device)
-        self.gen.manual_seed(seed)
         lo = torch.tensor([b[0] for b in LEGO_BOXES], device=device)
         hi = torch.tensor([b[1] for b in LEGO_BOXES], device=device)
         # the solid lives in ngp coordinates already (x, y, z of the bound box)
@@ -111,12 +109,14 @@ class SyntheticLego:
         return torch.cat([rgb, alpha[:, None]], -1).view(*rays_o.shape[:-1], 4)
 
     def sample(self, index=None):
-        """One training batch: rays of `num_rays` random pixels of one pose."""
+        """One training batch: rays of `num_rays` random pixels of one random
+        pose. Device-side RNG only (no host sync), so it can sit in a graph."""
         if index is None:
-            index = int(torch.randint(0, self.poses.shape[0], (1,), generator=self.gen,
-                                      device=self.device).item())
-        poses = self.poses[index:index + 1]
-        rays = get_rays(poses, self.intrinsics, self.H, self.W, self.num_rays, generator=self.gen)
+            index = torch.randint(0, self.poses.shape[0], (1,), device=self.device)
+        else:
+            index = torch.tensor([index], device=self.device)
+        poses = self.poses.index_select(0, index)
+        rays = get_rays(poses, self.intrinsics, self.H, self.W, self.num_rays)
         images = self.target(rays["rays_o"], rays["rays_d"])
         return {"H": self.H, "W": self.W, "rays_o": rays["rays_o"], "rays_d": rays["rays_d"],
                 "images": images}
