@@ -213,39 +213,52 @@ k_grid_fwd(const float* __restrict__ inputs, const T* __restrict__ grid,
     }
 }
 
-// ---- scatter-add of one corner's C channels -------------------------------
+// ---- scatter-add of one corner's C channels (values already weighted) -----
 template <typename T, uint32_t C> struct Scatter;
 template <uint32_t C> struct Scatter<float, C> {
-    NGP_DEV static void add(float* p, float w, const float g[C]) {
+    NGP_DEV static void add(float* p, const float v[C]) {
 #pragma unroll
-        for (uint32_t c = 0; c < C; ++c) atomicAdd(p + c, w * g[c]);
+        for (uint32_t c = 0; c < C; ++c) atomicAdd(p + c, v[c]);
     }
 };
 template <uint32_t C> struct Scatter<double, C> {
-    NGP_DEV static void add(double* p, float w, const double g[C]) {
+    NGP_DEV static void add(double* p, const double v[C]) {
 #pragma unroll
-        for (uint32_t c = 0; c < C; ++c) atomicAdd(p + c, (double)w * g[c]);
+        for (uint32_t c = 0; c < C; ++c) atomicAdd(p + c, v[c]);
     }
 };
 template <uint32_t C> struct Scatter<ngp_half, C> {
-    NGP_DEV static void add(ngp_half* p, float w, const float g[C]) {
+    NGP_DEV static void add(ngp_half* p, const float v[C]) {
         if constexpr (C % 2 == 0) {
 #pragma unroll
             for (uint32_t c = 0; c < C; c += 2) {
-                ngp_half2 v = {(ngp_half)(w * g[c]), (ngp_half)(w * g[c + 1])};
-                __builtin_amdgcn_global_atomic_fadd_v2f16(reinterpret_cast<ngp_half2*>(p + c), v);
+                ngp_half2 h = {(ngp_half)v[c], (ngp_half)v[c + 1]};
+                __builtin_amdgcn_global_atomic_fadd_v2f16(reinterpret_cast<ngp_half2*>(p + c), h);
             }
         } else {
             // C == 1: packed add of (v, 0) into the aligned dword holding the entry.
             const uintptr_t a = reinterpret_cast<uintptr_t>(p);
             ngp_half2* base = reinterpret_cast<ngp_half2*>(a & ~uintptr_t(3));
-            const ngp_half hv = (ngp_half)(w * g[0]);
-            ngp_half2 v = (a & 2) ? ngp_half2{(ngp_half)0.0f, hv} : ngp_half2{hv, (ngp_half)0.0f};
-            __builtin_amdgcn_global_atomic_fadd_v2f16(base, v);
+            const ngp_half hv = (ngp_half)v[0];
+            ngp_half2 h = (a & 2) ? ngp_half2{(ngp_half)0.0f, hv} : ngp_half2{hv, (ngp_half)0.0f};
+            __builtin_amdgcn_global_atomic_fadd_v2f16(base, h);
         }
     }
 };
 
+// Scatter-add with wave-level merging of identical targets.
+//
+// Samples arrive ordered along rays, so on the coarse levels many consecutive
+// lanes of a wave hit the same cell (level 0 cells hold ~40 consecutive
+// samples at Lego step sizes) and the reference's one-atomic-per-(point,
+// corner) serialises on the memory-side atomic unit. Per corner, lanes whose
+// target equals their left neighbour's form a run; a segmented inclusive scan
+// (shuffles) sums each run into its last lane, which issues ONE atomic for the
+// whole run. A ballot skips the scan when no two adjacent lanes collide (the
+// fine hashed levels), so those pay one shuffle + one ballot per corner.
+// For fp16 tables each run adds (half)(sum of w*g) instead of rounding every
+// term (the reference rounds each term, gridencoder.cu:325), i.e. the same
+// values with fewer roundings.
 template <typename T, uint32_t D, uint32_t C>
 __global__ void __launch_bounds__(256)
 k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
@@ -255,15 +268,17 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
     using A = Acc<T>;
     using F = typename A::F;
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
     const uint32_t level = blockIdx.y;
+    const int lane = (int)(threadIdx.x & 63);
 
+    bool valid = b < B;
     float x[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; d++) {
-        x[d] = inputs[(size_t)b * D + d];
-        if (x[d] < 0 || x[d] > 1) return;  // grad is zero-initialised
+        x[d] = valid ? inputs[(size_t)b * D + d] : 0.5f;
+        if (x[d] < 0 || x[d] > 1) valid = false;  // grad is zero-initialised
     }
+    if (__ballot(valid) == 0) return;  // whole wave idle (wave-uniform)
 
     const uint32_t off0 = (uint32_t)offsets[level];
     const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
@@ -282,10 +297,15 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
         if (interp == 1) pos[d] = smoothstep(pos[d]);
     }
 
-    const T* gp = grad_layout == 0 ? grad + ((size_t)level * B + b) * C
-                                   : grad + ((size_t)b * L + level) * C;
     F gcur[C];
-    load_entry<T, C>(gp, gcur);
+    if (valid) {
+        const T* gp = grad_layout == 0 ? grad + ((size_t)level * B + b) * C
+                                       : grad + ((size_t)b * L + level) * C;
+        load_entry<T, C>(gp, gcur);
+    } else {
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) gcur[c] = 0;
+    }
 
 #pragma unroll
     for (uint32_t idx = 0; idx < (1u << D); idx++) {
@@ -301,8 +321,36 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
                 pl[d] = pg[d] + 1;
             }
         }
-        const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
-        Scatter<T, C>::add(gg + (size_t)e * C, w, gcur);
+        const uint32_t key = valid ? grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl)
+                                   : 0xffffffffu;
+        F v[C];
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) v[c] = (F)w * gcur[c];
+
+        const uint32_t kprev = __shfl_up(key, 1, 64);
+        const bool same = lane > 0 && kprev == key;
+        if (__ballot(same) == 0) {
+            if (valid) Scatter<T, C>::add(gg + (size_t)key * C, v);
+            continue;
+        }
+        // run start = inclusive max-scan of head positions
+        int start = same ? 0 : lane;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(start, o, 64);
+            if (lane >= o) start = max(start, t);
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+            for (uint32_t c = 0; c < C; ++c) {
+                const F t = __shfl_up(v[c], o, 64);
+                if (lane - o >= start) v[c] += t;
+            }
+        }
+        const uint32_t knext = __shfl_down(key, 1, 64);
+        const bool tail = lane == 63 || knext != key;
+        if (valid && tail) Scatter<T, C>::add(gg + (size_t)key * C, v);
     }
 }
 
