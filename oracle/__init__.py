@@ -389,39 +389,44 @@ def mlp_layers(weights, input_dim, output_dim, hidden_dim, num_layers):
     return mats
 
 
-def mlp_forward(x, weights, input_dim, output_dim, hidden_dim, num_layers, act=0, out_act=6):
-    """fp16 storage between layers (like the fused kernel), float64 accumulation.
-    Returns (outputs fp16 [B, output_dim], list of hidden post-activations fp16)."""
-    mats = mlp_layers(np.asarray(weights, np.float16).astype(np.float64), input_dim, output_dim,
+def mlp_forward(x, weights, input_dim, output_dim, hidden_dim, num_layers, act=0, out_act=6,
+                fp16=True):
+    """fp16 storage between layers (like the fused kernel; fp16=False keeps
+    float64), float64 accumulation. Returns (outputs [B, output_dim], list of
+    hidden post-activations)."""
+    st = np.float16 if fp16 else np.float64
+    mats = mlp_layers(np.asarray(weights, st).astype(np.float64), input_dim, output_dim,
                       hidden_dim, num_layers)
-    h = np.asarray(x, np.float16)
+    h = np.asarray(x, st)
     hs = []
     for li, W in enumerate(mats):
         z = h.astype(np.float64) @ W.T
         if li < len(mats) - 1:
-            h = _act(act, z).astype(np.float16)
+            h = _act(act, z).astype(st)
             hs.append(h)
         else:
-            h = _act(out_act, z).astype(np.float16)
+            h = _act(out_act, z).astype(st)
     return h, hs
 
 
-def mlp_backward(grad, x, weights, input_dim, output_dim, hidden_dim, num_layers, act=0):
-    """float64 backward with fp16-rounded deltas (like the fused kernel).
-    Returns (grad_inputs fp16 [B, in], grad_weights float64 flat)."""
-    mats = mlp_layers(np.asarray(weights, np.float16).astype(np.float64), input_dim, output_dim,
+def mlp_backward(grad, x, weights, input_dim, output_dim, hidden_dim, num_layers, act=0,
+                 fp16=True):
+    """float64 backward with fp16-rounded deltas (like the fused kernel; fp16=False
+    keeps float64). Returns (grad_inputs [B, in], grad_weights float64 flat)."""
+    st = np.float16 if fp16 else np.float64
+    mats = mlp_layers(np.asarray(weights, st).astype(np.float64), input_dim, output_dim,
                       hidden_dim, num_layers)
-    _, hs = mlp_forward(x, weights, input_dim, output_dim, hidden_dim, num_layers, act)
-    ins = [np.asarray(x, np.float16).astype(np.float64)] + [h.astype(np.float64) for h in hs]
-    d = np.asarray(grad, np.float16).astype(np.float64)
+    _, hs = mlp_forward(x, weights, input_dim, output_dim, hidden_dim, num_layers, act, fp16=fp16)
+    ins = [np.asarray(x, st).astype(np.float64)] + [h.astype(np.float64) for h in hs]
+    d = np.asarray(grad, st).astype(np.float64)
     gws = [None] * len(mats)
     for li in range(len(mats) - 1, -1, -1):
         gws[li] = d.T @ ins[li]
         g_in = d @ mats[li]
         if li > 0:
-            d = _act_bwd(act, g_in, ins[li]).astype(np.float16).astype(np.float64)
+            d = _act_bwd(act, g_in, ins[li]).astype(st).astype(np.float64)
         else:
-            grad_inputs = g_in.astype(np.float16)
+            grad_inputs = g_in.astype(st)
     return grad_inputs, np.concatenate([g.reshape(-1) for g in gws])
 
 
