@@ -45,7 +45,7 @@ NGP_DEV f32x4 mfma(half8 a, half8 b, f32x4 c) {
 enum Act : uint32_t { kReLU = 0, kExp = 1, kSine = 2, kSigmoid = 3, kSquareplus = 4, kSoftplus = 5, kNone = 6 };
 constexpr float kKAct = 10.0f;
 
-NGP_DEV float act_fwd(uint32_t a, float x) {
+__device__ __attribute__((noinline)) float act_fwd(uint32_t a, float x) {
     switch (a) {
         case kReLU: return x > 0.0f ? x : 0.0f;
         case kExp: return expf(x);
@@ -57,7 +57,7 @@ NGP_DEV float act_fwd(uint32_t a, float x) {
     }
 }
 // derivative expressed through the post-activation value y (utils.h:536-580)
-NGP_DEV float act_bwd(uint32_t a, float g, float y) {
+__device__ __attribute__((noinline)) float act_bwd(uint32_t a, float g, float y) {
     switch (a) {
         case kReLU: return y > 0.0f ? g : 0.0f;
         case kExp: return g * y;
@@ -67,6 +67,25 @@ NGP_DEV float act_bwd(uint32_t a, float g, float y) {
         default: return g;  // None; Sine has no backward in the reference (utils.h:552-556)
     }
 }
+
+// Activation policies: the NeRF networks use ReLU hidden / no output
+// activation, which compile to inline VALU; any other enum value goes through
+// the out-of-line generic functions above (keeps the unrolled tile loops small:
+// inlining every activation into every element made the kernels ~45k
+// instructions and I-cache bound).
+struct ActReLU {
+    NGP_DEV float fwd(float x) const { return x > 0.0f ? x : 0.0f; }
+    NGP_DEV float bwd(float g, float y) const { return y > 0.0f ? g : 0.0f; }
+};
+struct ActNone {
+    NGP_DEV float fwd(float x) const { return x; }
+    NGP_DEV float bwd(float g, float) const { return g; }
+};
+struct ActAny {
+    uint32_t a;
+    NGP_DEV float fwd(float x) const { return act_fwd(a, x); }
+    NGP_DEV float bwd(float g, float y) const { return act_bwd(a, g, y); }
+};
 
 // K-slot permutation produced by packing two 16-row accumulator tiles into
 // one 32-deep B operand: slot (g, j) of K-step s holds unit 32s + perm(g, j).
@@ -84,23 +103,43 @@ struct MatDesc {
     bool kperm;              // K order of the B operand it multiplies is permuted
 };
 
+// One lane's 8-element slot of fragment f of matrix m.
+NGP_DEV half8 frag_slot(const ngp_half* __restrict__ w, const MatDesc& m, bool transposed,
+                        uint32_t f, uint32_t lane) {
+    const uint32_t mt = f / m.ks, s = f - mt * m.ks;
+    const int g = lane >> 4, c = lane & 15;
+    const uint32_t row = 16 * mt + c;  // M index
+    half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!transposed) {
+        // A[row=o][k=i] = W[o][i]: contiguous runs of the weight row -> vector loads
+        if (row >= m.out) return v;
+        const ngp_half* wr = w + m.off + row * m.in;
+        if (!m.kperm) {
+            const uint32_t i0 = 32 * s + 8 * g;  // 8 contiguous, all in or all out (in % 16 == 0)
+            if (i0 < m.in) v = *reinterpret_cast<const half8*>(wr + i0);
+        } else {
+            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+            const uint32_t i0 = 32 * s + 4 * g, i1 = 32 * s + 16 + 4 * g;
+            h4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+            if (i0 < m.in) a = *reinterpret_cast<const h4*>(wr + i0);
+            if (i1 < m.in) b = *reinterpret_cast<const h4*>(wr + i1);
+            v = half8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        }
+        return v;
+    }
+    // A[row=i][k=o] = W[o][i]: a column of W (strided gathers)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t o = 32 * s + (m.kperm ? perm_unit(g, j) : 8 * g + j);
+        v[j] = (o < m.out && row < m.in) ? w[m.off + o * m.in + row] : (ngp_half)0.0f;
+    }
+    return v;
+}
+
 NGP_DEV void build_frags(half8* lds, const ngp_half* __restrict__ w, const MatDesc& m, bool transposed) {
     const uint32_t n = m.mt * m.ks * 64;  // lanes to fill
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
-        const uint32_t lane = t & 63, f = t >> 6;
-        const uint32_t mt = f / m.ks, s = f - mt * m.ks;
-        const int g = lane >> 4, c = lane & 15;
-        half8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t row = 16 * mt + c;                                  // M index
-            const uint32_t k = 32 * s + (m.kperm ? perm_unit(g, j) : 8 * g + j);  // K index
-            // forward: A[row=o][k=i] = W[o][i]; transposed: A[row=i][k=o] = W[o][i]
-            const uint32_t o = transposed ? k : row, i = transposed ? row : k;
-            v[j] = (o < m.out && i < m.in) ? w[m.off + o * m.in + i] : (ngp_half)0.0f;
-        }
-        lds[(m.frag0 + f) * 64 + lane] = v;
-    }
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
+        lds[m.frag0 * 64 + t] = frag_slot(w, m, transposed, t >> 6, t & 63);
 }
 
 // Network geometry (all compile-time except in_dim, which only changes
@@ -170,8 +209,8 @@ NGP_DEV void dense(const half8* __restrict__ lds, uint32_t frag0, const half8 (&
 }
 
 // accumulator tiles -> activation -> permuted B operand of the next product
-template <int MT, int KS>
-NGP_DEV void pack_act(const f32x4 (&acc)[kNB][MT], uint32_t act, half8 (&out)[kNB][KS]) {
+template <int MT, int KS, typename ACT>
+NGP_DEV void pack_act(const f32x4 (&acc)[kNB][MT], ACT act, half8 (&out)[kNB][KS]) {
 #pragma unroll
     for (int nb = 0; nb < kNB; ++nb)
 #pragma unroll
@@ -180,7 +219,7 @@ NGP_DEV void pack_act(const f32x4 (&acc)[kNB][MT], uint32_t act, half8 (&out)[kN
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int mt = 2 * s + (j >> 2);
-                v[j] = mt < MT ? (ngp_half)act_fwd(act, acc[nb][mt][j & 3]) : (ngp_half)0.0f;
+                v[j] = mt < MT ? (ngp_half)act.fwd(acc[nb][mt][j & 3]) : (ngp_half)0.0f;
             }
             out[nb][s] = v;
         }
@@ -205,9 +244,9 @@ NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_
 }
 
 // store accumulator tiles (optionally activated) as fp16 rows [row][16 mt + 4g .. +3]
-template <int MT>
+template <int MT, typename ACT>
 NGP_DEV void store_tiles(ngp_half* __restrict__ dst, uint32_t width, uint32_t row0, uint32_t B,
-                         const f32x4 (&acc)[kNB][MT], uint32_t act) {
+                         const f32x4 (&acc)[kNB][MT], ACT act) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
     for (int nb = 0; nb < kNB; ++nb) {
@@ -219,18 +258,18 @@ NGP_DEV void store_tiles(ngp_half* __restrict__ dst, uint32_t width, uint32_t ro
             if (col >= width) continue;
             half4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = (ngp_half)act_fwd(act, acc[nb][mt][r]);
+            for (int r = 0; r < 4; ++r) v[r] = (ngp_half)act.fwd(acc[nb][mt][r]);
             *reinterpret_cast<half4*>(dst + (size_t)row * width + col) = v;
         }
     }
 }
 
 // ---- forward ----------------------------------------------------------------
-template <int W, int IN_KS, int NH>
+template <int W, int IN_KS, int NH, typename FA, typename FO>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weights,
           ngp_half* __restrict__ outputs, ngp_half* __restrict__ fwd_buf, uint32_t B,
-          uint32_t in_dim, uint32_t act, uint32_t out_act) {
+          uint32_t in_dim, FA act, FO out_act) {
     using N = Net<W, IN_KS, NH>;
     extern __shared__ half8 lds[];
     for (int q = 0; q < N::NMAT; ++q) build_frags(lds, weights, fwd_desc<W, IN_KS, NH>(q, in_dim), false);
@@ -293,8 +332,8 @@ NGP_DEV void dw_accum(const ngp_half* __restrict__ dT, const ngp_half* __restric
 }
 
 // delta (C layout, MT tiles) * act'(post-activation h, permuted B form) -> permuted B form
-template <int MT, int KS>
-NGP_DEV void pack_delta(const f32x4 (&acc)[kNB][MT], const half8 (&h)[kNB][KS], uint32_t act,
+template <int MT, int KS, typename ACT>
+NGP_DEV void pack_delta(const f32x4 (&acc)[kNB][MT], const half8 (&h)[kNB][KS], ACT act,
                         half8 (&out)[kNB][KS]) {
 #pragma unroll
     for (int nb = 0; nb < kNB; ++nb)
@@ -304,21 +343,26 @@ NGP_DEV void pack_delta(const f32x4 (&acc)[kNB][MT], const half8 (&h)[kNB][KS], 
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int mt = 2 * s + (j >> 2);
-                v[j] = mt < MT ? (ngp_half)act_bwd(act, acc[nb][mt][j & 3], (float)h[nb][s][j]) : (ngp_half)0.0f;
+                v[j] = mt < MT ? (ngp_half)act.bwd(acc[nb][mt][j & 3], (float)h[nb][s][j]) : (ngp_half)0.0f;
             }
             out[nb][s] = v;
         }
 }
 
-// Sum the workgroup's per-wave dW tiles (LDS fp32 atomics) and publish one slab row.
+// Add one wave's dW tile sums (C layout) into the workgroup's fp32 accumulator.
+#ifndef NGP_MLP_ABLATE
+#define NGP_MLP_ABLATE 0
+#endif
 template <int MO, int MI>
-NGP_DEV void flush_dw(const f32x4 (&acc)[MO][MI], float* __restrict__ red, uint32_t in_w,
-                      uint32_t out_w, float* __restrict__ slab_row) {
+NGP_DEV void add_dw(const f32x4 (&t)[MO][MI], float* __restrict__ acc, uint32_t in_w, uint32_t out_w) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    const uint32_t n = out_w * in_w;
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) red[t] = 0.0f;
-    __syncthreads();
+    if constexpr (NGP_MLP_ABLATE == 1) {
+#pragma unroll
+        for (int m = 0; m < MO; ++m)
+#pragma unroll
+            for (int k = 0; k < MI; ++k) asm volatile("" ::"v"(t[m][k]));
+        return;
+    }
 #pragma unroll
     for (int m = 0; m < MO; ++m)
 #pragma unroll
@@ -326,10 +370,16 @@ NGP_DEV void flush_dw(const f32x4 (&acc)[MO][MI], float* __restrict__ red, uint3
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint32_t o = 16 * m + 4 * g + r, i = 16 * k + c;
-                if (o < out_w && i < in_w) atomicAdd(&red[o * in_w + i], acc[m][k][r]);
+                if (o < out_w && i < in_w) atomicAdd(&acc[o * in_w + i], t[m][k][r]);
             }
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) slab_row[t] = red[t];
+}
+
+template <int MO, int MI>
+NGP_DEV void zero_tiles(f32x4 (&t)[MO][MI]) {
+#pragma unroll
+    for (int m = 0; m < MO; ++m)
+#pragma unroll
+        for (int k = 0; k < MI; ++k) t[m][k] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
 template <int W, int IN_KS, int NH>
@@ -339,134 +389,136 @@ struct BwdLds {
     static constexpr int TILE_ROWS = (W > 32 * IN_KS ? W : 32 * IN_KS);
     static constexpr size_t frag_bytes = (size_t)FRAGS * 64 * 16;
     static constexpr size_t tile_bytes = (size_t)kWaves * 2 * TILE_ROWS * kScratchLd * 2;
-    static constexpr size_t red_bytes = (size_t)W * (W > 32 * IN_KS ? W : 32 * IN_KS) * 4;
-    static constexpr size_t scratch_bytes = tile_bytes > red_bytes ? tile_bytes : red_bytes;
-    static constexpr size_t total = frag_bytes + scratch_bytes;
+    static constexpr size_t nparams_max = (size_t)W * (32 * IN_KS) + (size_t)NH * W * W + (size_t)kOut * W;
+    static constexpr size_t acc_bytes = nparams_max * 4;
+    // dW accumulator in LDS when it fits next to the fragments and tiles, else
+    // in the workgroup's own slab row (global fp32 atomics, no inter-WG sharing)
+    static constexpr bool lds_acc = frag_bytes + tile_bytes + acc_bytes <= 160 * 1024;
+    static constexpr size_t total = frag_bytes + tile_bytes + (lds_acc ? acc_bytes : 0);
 };
 
-// Shared state of one backward launch.
-struct BwdCtx {
-    const ngp_half* grad;
-    const ngp_half* inputs;
-    ngp_half* grad_inputs;
-    const half8* fr;
-    ngp_half* dT;
-    ngp_half* hT;
-    float* red;
-    float* slab_row;
-    uint32_t B, in_dim, act, nchunks;
-};
-
-// One pass for matmul P (compile-time): recompute the forward, propagate the
-// deltas down to matmul P, accumulate dW_P over every chunk this wave owns,
-// then publish the workgroup's dW_P. Recurses to P-1.
-template <int W, int IN_KS, int NH, int P>
-NGP_DEV void bwd_pass(const BwdCtx& cx) {
-    using N = Net<W, IN_KS, NH>;
-    constexpr int LAST = N::NMAT - 1;
-    constexpr int MO = P == LAST ? 1 : N::MTW;    // 16-row tiles over matmul P's outputs
-    constexpr int MI = P == 0 ? N::IN_MT : N::MTW; // 16-col tiles over matmul P's inputs
-    const uint32_t wave = threadIdx.x >> 6;
-
-    f32x4 dw[MO][MI];
-#pragma unroll
-    for (int m = 0; m < MO; ++m)
-#pragma unroll
-        for (int k = 0; k < MI; ++k) dw[m][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (uint32_t chunk = blockIdx.x * kWaves + wave; chunk < cx.nchunks; chunk += gridDim.x * kWaves) {
-        const uint32_t row0 = chunk * 16 * kNB;
-        half8 x[kNB][IN_KS];
-        load_rows<IN_KS>(cx.inputs, cx.in_dim, row0, cx.B, x);
-        // recompute the post-activations of every hidden layer
-        half8 h[NH + 1][kNB][N::KSW];
-        f32x4 acc[kNB][N::MTW];
-        dense<N::MTW, IN_KS>(cx.fr, fwd_desc<W, IN_KS, NH>(0, cx.in_dim).frag0, x, acc);
-        pack_act<N::MTW, N::KSW>(acc, cx.act, h[0]);
-#pragma unroll
-        for (int q = 1; q <= NH; ++q) {
-            dense<N::MTW, N::KSW>(cx.fr, fwd_desc<W, IN_KS, NH>(q, cx.in_dim).frag0, h[q - 1], acc);
-            pack_act<N::MTW, N::KSW>(acc, cx.act, h[q]);
-        }
-        // output gradient (output activation ignored, ffmlp.cu:783): natural K order
-        half8 dout[kNB][1];
-        load_rows<1>(cx.grad, kOut, row0, cx.B, dout);
-
-        if constexpr (P == LAST) {
-            write_transposed<1, false>(cx.dT, dout, kOut);
-            write_transposed<N::KSW, true>(cx.hT, h[NH], W);
-            dw_accum<MO, MI>(cx.dT, cx.hT, dw);
-        } else {
-            half8 d[kNB][N::KSW];  // delta of a matmul's (pre-activation) output, permuted B form
-            dense<N::MTW, 1>(cx.fr, bwd_desc<W, IN_KS, NH>(LAST, cx.in_dim).frag0 + N::FWD_FRAGS, dout, acc);
-            pack_delta<N::MTW, N::KSW>(acc, h[NH], cx.act, d);
-#pragma unroll
-            for (int q = NH; q > P; --q) {
-                dense<N::MTW, N::KSW>(cx.fr, bwd_desc<W, IN_KS, NH>(q, cx.in_dim).frag0 + N::FWD_FRAGS, d, acc);
-                pack_delta<N::MTW, N::KSW>(acc, h[q - 1], cx.act, d);
-            }
-            write_transposed<N::KSW, true>(cx.dT, d, W);
-            if constexpr (P == 0) write_transposed<IN_KS, false>(cx.hT, x, 32 * IN_KS);
-            else write_transposed<N::KSW, true>(cx.hT, h[P - 1], W);
-            dw_accum<MO, MI>(cx.dT, cx.hT, dw);
-            if constexpr (P == 0) {
-                if (cx.grad_inputs) {
-                    f32x4 gi[kNB][N::IN_MT];
-                    dense<N::IN_MT, N::KSW>(cx.fr, bwd_desc<W, IN_KS, NH>(0, cx.in_dim).frag0 + N::FWD_FRAGS, d, gi);
-                    store_tiles<N::IN_MT>(cx.grad_inputs, cx.in_dim, row0, cx.B, gi, kNone);
-                }
-            }
-        }
-    }
-    const MatDesc mf = fwd_desc<W, IN_KS, NH>(P, cx.in_dim);
-    flush_dw<MO, MI>(dw, cx.red, mf.in, mf.out, cx.slab_row + mf.off);
-    __syncthreads();
-    if constexpr (P > 0) bwd_pass<W, IN_KS, NH, P - 1>(cx);
-}
-
+// Writes the permuted forward and transposed-backward fragment images of
+// every matmul once per call (workspace), so each backward workgroup fills
+// its LDS with straight 16-byte copies. One block per (matmul, direction).
 template <int W, int IN_KS, int NH>
-__global__ void __launch_bounds__(kThreads)
-k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
-          const ngp_half* __restrict__ weights, ngp_half* __restrict__ grad_inputs,
-          float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, uint32_t act) {
+__global__ void __launch_bounds__(256)
+k_mlp_pack(const ngp_half* __restrict__ weights, uint32_t in_dim, half8* __restrict__ image) {
     using N = Net<W, IN_KS, NH>;
-    using L = BwdLds<W, IN_KS, NH>;
-    extern __shared__ half8 lds[];
-    ngp_half* scratch = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
-
-    for (int q = 0; q < N::NMAT; ++q) {
-        build_frags(lds, weights, fwd_desc<W, IN_KS, NH>(q, in_dim), false);
+    const int q = blockIdx.x >> 1;
+    if (blockIdx.x & 1) {
         MatDesc mb = bwd_desc<W, IN_KS, NH>(q, in_dim);
         mb.frag0 += N::FWD_FRAGS;
-        build_frags(lds, weights, mb, true);
+        build_frags(image, weights, mb, true);
+    } else {
+        build_frags(image, weights, fwd_desc<W, IN_KS, NH>(q, in_dim), false);
     }
+}
+
+// Single-pass fused backward: per 32-sample chunk a wave recomputes the
+// forward (activations stay in registers), walks the deltas down through
+// W^T fragments, and for every matmul forms dW = delta^T . input over the
+// chunk with MFMAs whose K is the sample index, summing into the workgroup
+// accumulator. Each workgroup finally publishes its dW row to the slab.
+template <int W, int IN_KS, int NH, typename FA>
+__global__ void __launch_bounds__(kThreads)
+k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
+          const half8* __restrict__ image, ngp_half* __restrict__ grad_inputs,
+          float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, FA act) {
+    using N = Net<W, IN_KS, NH>;
+    using L = BwdLds<W, IN_KS, NH>;
+    constexpr int LAST = N::NMAT - 1;
+    extern __shared__ half8 lds[];
+    const half8* fr = lds;
+    ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
+    float* slab_row = slab + (size_t)blockIdx.x * nparams;
+    float* acc = L::lds_acc ? reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + L::frag_bytes + L::tile_bytes)
+                            : slab_row;
+
+    if constexpr (NGP_MLP_ABLATE != 3)
+        for (uint32_t t = threadIdx.x; t < (uint32_t)L::FRAGS * 64; t += blockDim.x) lds[t] = image[t];
+    for (uint32_t t = threadIdx.x; t < nparams; t += blockDim.x) acc[t] = 0.0f;
     __syncthreads();
 
     const uint32_t wave = threadIdx.x >> 6;
-    BwdCtx cx;
-    cx.grad = grad;
-    cx.inputs = inputs;
-    cx.grad_inputs = grad_inputs;
-    cx.fr = lds;
-    cx.dT = scratch + (size_t)wave * 2 * L::TILE_ROWS * kScratchLd;
-    cx.hT = cx.dT + (size_t)L::TILE_ROWS * kScratchLd;
-    cx.red = reinterpret_cast<float*>(scratch);
-    cx.slab_row = slab + (size_t)blockIdx.x * nparams;
-    cx.B = B;
-    cx.in_dim = in_dim;
-    cx.act = act;
-    cx.nchunks = ngp_div_up(B, 16 * kNB);
-    bwd_pass<W, IN_KS, NH, N::NMAT - 1>(cx);
+    ngp_half* dT = tiles + (size_t)wave * 2 * L::TILE_ROWS * kScratchLd;
+    ngp_half* hT = dT + (size_t)L::TILE_ROWS * kScratchLd;
+    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
+    const uint32_t off_last = fwd_desc<W, IN_KS, NH>(LAST, in_dim).off;
+
+    for (uint32_t chunk = blockIdx.x * kWaves + wave; chunk < nchunks; chunk += gridDim.x * kWaves) {
+        const uint32_t row0 = chunk * 16 * kNB;
+        half8 x[kNB][IN_KS];
+        load_rows<IN_KS>(inputs, in_dim, row0, B, x);
+        half8 dout[kNB][1];
+        load_rows<1>(grad, kOut, row0, B, dout);  // output activation ignored (ffmlp.cu:783)
+        // recompute the post-activations of every hidden layer
+        half8 h[NH + 1][kNB][N::KSW];
+        f32x4 a[kNB][N::MTW];
+        dense<N::MTW, IN_KS>(fr, fwd_desc<W, IN_KS, NH>(0, in_dim).frag0, x, a);
+        pack_act<N::MTW, N::KSW>(a, act, h[0]);
+#pragma unroll
+        for (int q = 1; q <= NH; ++q) {
+            dense<N::MTW, N::KSW>(fr, fwd_desc<W, IN_KS, NH>(q, in_dim).frag0, h[q - 1], a);
+            pack_act<N::MTW, N::KSW>(a, act, h[q]);
+        }
+        // last matmul: dW = dout^T . h[NH]
+        {
+            write_transposed<1, false>(dT, dout, kOut);
+            write_transposed<N::KSW, true>(hT, h[NH], W);
+            f32x4 t[1][N::MTW];
+            zero_tiles(t);
+            dw_accum<1, N::MTW>(dT, hT, t);
+            add_dw(t, acc + off_last, W, kOut);
+        }
+        half8 d[kNB][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
+        dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
+        pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
+#pragma unroll
+        for (int q = NH; q >= 1; --q) {
+            write_transposed<N::KSW, true>(dT, d, W);
+            write_transposed<N::KSW, true>(hT, h[q - 1], W);
+            f32x4 t[N::MTW][N::MTW];
+            zero_tiles(t);
+            dw_accum<N::MTW, N::MTW>(dT, hT, t);
+            add_dw(t, acc + fwd_desc<W, IN_KS, NH>(q, in_dim).off, W, W);
+            dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
+            pack_delta<N::MTW, N::KSW>(a, h[q - 1], act, d);
+        }
+        // first matmul: dW = d^T . x, and grad_inputs = W_0^T d
+        write_transposed<N::KSW, true>(dT, d, W);
+        write_transposed<IN_KS, false>(hT, x, 32 * IN_KS);
+        {
+            f32x4 t[N::MTW][N::IN_MT];
+            zero_tiles(t);
+            dw_accum<N::MTW, N::IN_MT>(dT, hT, t);
+            add_dw(t, acc, in_dim, W);
+        }
+        if (grad_inputs) {
+            f32x4 gi[kNB][N::IN_MT];
+            dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
+            store_tiles<N::IN_MT>(grad_inputs, in_dim, row0, B, gi, ActNone{});
+        }
+    }
+    if constexpr (L::lds_acc) {
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < nparams; t += blockDim.x) slab_row[t] = acc[t];
+    }
 }
 
+// grad_weights[p] = sum over workgroup rows of the slab, in fixed row order
+// (deterministic). 64 parameters x 4 row phases per block.
 template <typename OUT>
 __global__ void __launch_bounds__(256)
 k_slab_reduce(const float* __restrict__ slab, uint32_t rows, uint32_t n, OUT* __restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    __shared__ float part[4][64];
+    const uint32_t lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const uint32_t p = blockIdx.x * 64 + lane;
     float s = 0.0f;
-    for (uint32_t r = 0; r < rows; ++r) s += slab[(size_t)r * n + i];
-    out[i] = (OUT)s;
+    if (p < n)
+        for (uint32_t r = ph; r < rows; r += 4) s += slab[(size_t)r * n + p];
+    part[ph][lane] = s;
+    __syncthreads();
+    if (ph == 0 && p < n) out[p] = (OUT)((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
 }
 
 // ---- host dispatch ----------------------------------------------------------
@@ -492,37 +544,70 @@ int check_shape(uint32_t B, uint32_t in_dim, uint32_t out_dim, uint32_t hidden, 
     return NGP_OK;
 }
 
+template <int W, int IN_KS, int NH, typename FA, typename FO>
+int launch_fwd_t(const void* in, const void* w, uint32_t B, uint32_t in_dim, FA act, FO out_act,
+                 void* fwd_buf, void* out, hipStream_t st);
+
 template <int W, int IN_KS, int NH>
 int launch_fwd(const void* in, const void* w, uint32_t B, uint32_t in_dim, uint32_t act,
                uint32_t out_act, void* fwd_buf, void* out, hipStream_t st) {
+    if (act == kReLU && out_act == kNone)
+        return launch_fwd_t<W, IN_KS, NH>(in, w, B, in_dim, ActReLU{}, ActNone{}, fwd_buf, out, st);
+    return launch_fwd_t<W, IN_KS, NH>(in, w, B, in_dim, ActAny{act}, ActAny{out_act}, fwd_buf, out, st);
+}
+
+template <int W, int IN_KS, int NH, typename FA, typename FO>
+int launch_fwd_t(const void* in, const void* w, uint32_t B, uint32_t in_dim, FA act, FO out_act,
+                 void* fwd_buf, void* out, hipStream_t st) {
     using N = Net<W, IN_KS, NH>;
     const size_t lds = (size_t)N::FWD_FRAGS * 64 * 16;
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
     uint32_t blocks = ngp_div_up(nchunks, kWaves);
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) return NGP_OK;
-    hipLaunchKernelGGL((k_mlp_fwd<W, IN_KS, NH>), dim3(blocks), dim3(kThreads), lds, st,
+    hipLaunchKernelGGL((k_mlp_fwd<W, IN_KS, NH, FA, FO>), dim3(blocks), dim3(kThreads), lds, st,
                        (const ngp_half*)in, (const ngp_half*)w, (ngp_half*)out, (ngp_half*)fwd_buf,
                        B, in_dim, act, out_act);
     return ngp_check_launch("ffmlp_forward");
 }
 
+constexpr size_t kImageBytes = 128 * 1024;  // fragment image slot at the head of the workspace
+
+template <int W, int IN_KS, int NH, typename FA>
+int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
+                 FA act, void* grad_in, void* gw, int32_t gw_dtype, void* ws, hipStream_t st);
+
 template <int W, int IN_KS, int NH>
 int launch_bwd(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
-               uint32_t act, void* grad_in, void* gw, int32_t gw_dtype, float* slab,
+               uint32_t act, void* grad_in, void* gw, int32_t gw_dtype, void* ws,
                hipStream_t st) {
+    if (act == kReLU)
+        return launch_bwd_t<W, IN_KS, NH>(grad, in, w, B, in_dim, ActReLU{}, grad_in, gw, gw_dtype, ws, st);
+    return launch_bwd_t<W, IN_KS, NH>(grad, in, w, B, in_dim, ActAny{act}, grad_in, gw, gw_dtype, ws, st);
+}
+
+template <int W, int IN_KS, int NH, typename FA>
+int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
+                 FA act, void* grad_in, void* gw, int32_t gw_dtype, void* ws, hipStream_t st) {
+    using N = Net<W, IN_KS, NH>;
     using L = BwdLds<W, IN_KS, NH>;
+    static_assert(L::frag_bytes <= kImageBytes, "fragment image exceeds its workspace slot");
+    static_assert(L::total <= 160 * 1024, "backward LDS budget exceeded");
     const uint32_t blocks = bwd_blocks(B);
     const uint32_t np = num_params(in_dim, W, NH + 1);
     if (blocks == 0) return NGP_OK;
-    hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH>), dim3(blocks), dim3(kThreads), L::total, st,
-                       (const ngp_half*)grad, (const ngp_half*)in, (const ngp_half*)w,
+    half8* image = reinterpret_cast<half8*>(ws);
+    float* slab = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kImageBytes);
+    hipLaunchKernelGGL((k_mlp_pack<W, IN_KS, NH>), dim3(2 * N::NMAT), dim3(256), 0, st,
+                       (const ngp_half*)w, in_dim, image);
+    hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH, FA>), dim3(blocks), dim3(kThreads), L::total, st,
+                       (const ngp_half*)grad, (const ngp_half*)in, (const half8*)image,
                        (ngp_half*)grad_in, slab, np, B, in_dim, act);
     if (gw_dtype == NGP_DTYPE_F16) {
-        hipLaunchKernelGGL((k_slab_reduce<ngp_half>), dim3(ngp_div_up(np, 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL((k_slab_reduce<ngp_half>), dim3(ngp_div_up(np, 64)), dim3(256), 0, st,
                            (const float*)slab, blocks, np, (ngp_half*)gw);
     } else {
-        hipLaunchKernelGGL((k_slab_reduce<float>), dim3(ngp_div_up(np, 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL((k_slab_reduce<float>), dim3(ngp_div_up(np, 64)), dim3(256), 0, st,
                            (const float*)slab, blocks, np, (float*)gw);
     }
     return ngp_check_launch("ffmlp_backward");
@@ -571,7 +656,7 @@ extern "C" size_t ngp_ffmlp_backward_workspace_bytes(uint32_t B, uint32_t input_
                                                      uint32_t output_dim, uint32_t hidden_dim,
                                                      uint32_t num_layers) {
     (void)output_dim;
-    return (size_t)bwd_blocks(B) * num_params(input_dim, hidden_dim, num_layers) * sizeof(float);
+    return kImageBytes + (size_t)bwd_blocks(B) * num_params(input_dim, hidden_dim, num_layers) * sizeof(float);
 }
 
 extern "C" int ngp_ffmlp_backward(const void* grad, const void* inputs, const void* weights,
@@ -594,7 +679,7 @@ extern "C" int ngp_ffmlp_backward(const void* grad, const void* inputs, const vo
     hipStream_t st = ngp_stream(stream);
     void* gi = calc_grad_inputs ? grad_inputs : nullptr;
     NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, B, in_dim, activation, gi, grad_weights,
-                     gw_dtype, (float*)workspace, st);
+                     gw_dtype, workspace, st);
 }
 
 extern "C" int ngp_ffmlp_allocate_splitk(size_t size) { (void)size; return NGP_OK; }
