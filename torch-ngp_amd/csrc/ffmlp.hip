@@ -30,7 +30,7 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kWaves = 4;
+constexpr int kWaves = 4;  // the backward epilogue folds waves pairwise (0+2, 1+3)
 constexpr int kThreads = kWaves * 64;
 constexpr int kNB = 2;          // 16-sample column blocks per wave step (32 samples)
 constexpr int kOut = 16;        // padded output width (FFMLP pads to 16)
@@ -349,20 +349,12 @@ NGP_DEV void pack_delta(const f32x4 (&acc)[kNB][MT], const half8 (&h)[kNB][KS], 
         }
 }
 
-// Add one wave's dW tile sums (C layout) into the workgroup's fp32 accumulator.
-#ifndef NGP_MLP_ABLATE
-#define NGP_MLP_ABLATE 0
-#endif
-template <int MO, int MI>
+// Add (FIRST: store) one wave's dW tile sums (C layout) into the workgroup's
+// fp32 dW image in LDS. Waves take turns (see k_mlp_bwd), so the summation
+// order is fixed and the result reproducible.
+template <bool FIRST, int MO, int MI>
 NGP_DEV void add_dw(const f32x4 (&t)[MO][MI], float* __restrict__ acc, uint32_t in_w, uint32_t out_w) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    if constexpr (NGP_MLP_ABLATE == 1) {
-#pragma unroll
-        for (int m = 0; m < MO; ++m)
-#pragma unroll
-            for (int k = 0; k < MI; ++k) asm volatile("" ::"v"(t[m][k]));
-        return;
-    }
 #pragma unroll
     for (int m = 0; m < MO; ++m)
 #pragma unroll
@@ -370,7 +362,10 @@ NGP_DEV void add_dw(const f32x4 (&t)[MO][MI], float* __restrict__ acc, uint32_t 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint32_t o = 16 * m + 4 * g + r, i = 16 * k + c;
-                if (o < out_w && i < in_w) atomicAdd(&acc[o * in_w + i], t[m][k][r]);
+                if (o < out_w && i < in_w) {
+                    float* p = &acc[o * in_w + i];
+                    *p = FIRST ? t[m][k][r] : *p + t[m][k][r];
+                }
             }
 }
 
@@ -391,10 +386,10 @@ struct BwdLds {
     static constexpr size_t tile_bytes = (size_t)kWaves * 2 * TILE_ROWS * kScratchLd * 2;
     static constexpr size_t nparams_max = (size_t)W * (32 * IN_KS) + (size_t)NH * W * W + (size_t)kOut * W;
     static constexpr size_t acc_bytes = nparams_max * 4;
-    // dW accumulator in LDS when it fits next to the fragments and tiles, else
-    // in the workgroup's own slab row (global fp32 atomics, no inter-WG sharing)
-    static constexpr bool lds_acc = frag_bytes + tile_bytes + acc_bytes <= 160 * 1024;
-    static constexpr size_t total = frag_bytes + tile_bytes + (lds_acc ? acc_bytes : 0);
+    // the two dW images of the epilogue reuse the fragment + tile space once
+    // the chunk loop is done
+    static constexpr size_t total =
+        frag_bytes + tile_bytes > 2 * acc_bytes ? frag_bytes + tile_bytes : 2 * acc_bytes;
 };
 
 // Writes the permuted forward and transposed-backward fragment images of
@@ -416,9 +411,11 @@ k_mlp_pack(const ngp_half* __restrict__ weights, uint32_t in_dim, half8* __restr
 
 // Single-pass fused backward: per 32-sample chunk a wave recomputes the
 // forward (activations stay in registers), walks the deltas down through
-// W^T fragments, and for every matmul forms dW = delta^T . input over the
-// chunk with MFMAs whose K is the sample index, summing into the workgroup
-// accumulator. Each workgroup finally publishes its dW row to the slab.
+// W^T fragments, and for every matmul forms dW += delta^T . input over the
+// chunk with MFMAs whose K is the sample index. The dW tiles live in the
+// wave's registers (accumulation VGPRs) for the whole chunk loop; only at the
+// end do the waves fold them, in fixed order, into an LDS image of dW that
+// the workgroup publishes as its slab row.
 template <int W, int IN_KS, int NH, typename FA>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
@@ -430,27 +427,39 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     extern __shared__ half8 lds[];
     const half8* fr = lds;
     ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
-    float* slab_row = slab + (size_t)blockIdx.x * nparams;
-    float* acc = L::lds_acc ? reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + L::frag_bytes + L::tile_bytes)
-                            : slab_row;
 
-    if constexpr (NGP_MLP_ABLATE != 3)
-        for (uint32_t t = threadIdx.x; t < (uint32_t)L::FRAGS * 64; t += blockDim.x) lds[t] = image[t];
-    for (uint32_t t = threadIdx.x; t < nparams; t += blockDim.x) acc[t] = 0.0f;
+    for (uint32_t t = threadIdx.x; t < (uint32_t)L::FRAGS * 64; t += blockDim.x) lds[t] = image[t];
     __syncthreads();
 
     const uint32_t wave = threadIdx.x >> 6;
     ngp_half* dT = tiles + (size_t)wave * 2 * L::TILE_ROWS * kScratchLd;
     ngp_half* hT = dT + (size_t)L::TILE_ROWS * kScratchLd;
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
-    const uint32_t off_last = fwd_desc<W, IN_KS, NH>(LAST, in_dim).off;
 
-    for (uint32_t chunk = blockIdx.x * kWaves + wave; chunk < nchunks; chunk += gridDim.x * kWaves) {
+    f32x4 dw_last[1][N::MTW], dw_hid[NH][N::MTW][N::MTW], dw_first[N::MTW][N::IN_MT];
+    zero_tiles(dw_last);
+#pragma unroll
+    for (int q = 0; q < NH; ++q) zero_tiles(dw_hid[q]);
+    zero_tiles(dw_first);
+
+    // inputs and output gradients of the next chunk are prefetched while the
+    // current one computes (one wave per SIMD: nothing else hides the latency)
+    const uint32_t stride = gridDim.x * kWaves;
+    uint32_t chunk = blockIdx.x * kWaves + wave;
+    half8 xn[kNB][IN_KS], dn[kNB][1];
+    load_rows<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
+    load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn);  // output activation ignored (ffmlp.cu:783)
+    for (; chunk < nchunks; chunk += stride) {
         const uint32_t row0 = chunk * 16 * kNB;
-        half8 x[kNB][IN_KS];
-        load_rows<IN_KS>(inputs, in_dim, row0, B, x);
-        half8 dout[kNB][1];
-        load_rows<1>(grad, kOut, row0, B, dout);  // output activation ignored (ffmlp.cu:783)
+        half8 x[kNB][IN_KS], dout[kNB][1];
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+#pragma unroll
+            for (int s = 0; s < IN_KS; ++s) x[nb][s] = xn[nb][s];
+            dout[nb][0] = dn[nb][0];
+        }
+        load_rows<IN_KS>(inputs, in_dim, row0 + stride * 16 * kNB, B, xn);
+        load_rows<1>(grad, kOut, row0 + stride * 16 * kNB, B, dn);
         // recompute the post-activations of every hidden layer
         half8 h[NH + 1][kNB][N::KSW];
         f32x4 a[kNB][N::MTW];
@@ -461,15 +470,10 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
             dense<N::MTW, N::KSW>(fr, fwd_desc<W, IN_KS, NH>(q, in_dim).frag0, h[q - 1], a);
             pack_act<N::MTW, N::KSW>(a, act, h[q]);
         }
-        // last matmul: dW = dout^T . h[NH]
-        {
-            write_transposed<1, false>(dT, dout, kOut);
-            write_transposed<N::KSW, true>(hT, h[NH], W);
-            f32x4 t[1][N::MTW];
-            zero_tiles(t);
-            dw_accum<1, N::MTW>(dT, hT, t);
-            add_dw(t, acc + off_last, W, kOut);
-        }
+        // last matmul: dW += dout^T . h[NH]
+        write_transposed<1, false>(dT, dout, kOut);
+        write_transposed<N::KSW, true>(hT, h[NH], W);
+        dw_accum<1, N::MTW>(dT, hT, dw_last);
         half8 d[kNB][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
         dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
         pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
@@ -477,48 +481,75 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
         for (int q = NH; q >= 1; --q) {
             write_transposed<N::KSW, true>(dT, d, W);
             write_transposed<N::KSW, true>(hT, h[q - 1], W);
-            f32x4 t[N::MTW][N::MTW];
-            zero_tiles(t);
-            dw_accum<N::MTW, N::MTW>(dT, hT, t);
-            add_dw(t, acc + fwd_desc<W, IN_KS, NH>(q, in_dim).off, W, W);
+            dw_accum<N::MTW, N::MTW>(dT, hT, dw_hid[q - 1]);
             dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
             pack_delta<N::MTW, N::KSW>(a, h[q - 1], act, d);
         }
-        // first matmul: dW = d^T . x, and grad_inputs = W_0^T d
+        // first matmul: dW += d^T . x, and grad_inputs = W_0^T d
         write_transposed<N::KSW, true>(dT, d, W);
         write_transposed<IN_KS, false>(hT, x, 32 * IN_KS);
-        {
-            f32x4 t[N::MTW][N::IN_MT];
-            zero_tiles(t);
-            dw_accum<N::MTW, N::IN_MT>(dT, hT, t);
-            add_dw(t, acc, in_dim, W);
-        }
+        dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
         if (grad_inputs) {
             f32x4 gi[kNB][N::IN_MT];
             dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
             store_tiles<N::IN_MT>(grad_inputs, in_dim, row0, B, gi, ActNone{});
         }
     }
-    if constexpr (L::lds_acc) {
-        __syncthreads();
-        for (uint32_t t = threadIdx.x; t < nparams; t += blockDim.x) slab_row[t] = acc[t];
+
+    // fold the waves' register tiles into two LDS dW images (waves 0/1 store,
+    // then waves 2/3 add), then publish image0 + image1 as the slab row: a
+    // fixed summation order, so dW is bit-reproducible
+    float* img = reinterpret_cast<float*>(lds) + (size_t)(wave & 1) * nparams;
+    __syncthreads();  // fragments and tiles are dead from here on
+    if (wave < 2) {
+        add_dw<true>(dw_first, img, in_dim, W);
+#pragma unroll
+        for (int q = 1; q <= NH; ++q) add_dw<true>(dw_hid[q - 1], img + fwd_desc<W, IN_KS, NH>(q, in_dim).off, W, W);
+        add_dw<true>(dw_last, img + fwd_desc<W, IN_KS, NH>(LAST, in_dim).off, W, kOut);
     }
+    __syncthreads();
+    if (wave >= 2) {
+        add_dw<false>(dw_first, img, in_dim, W);
+#pragma unroll
+        for (int q = 1; q <= NH; ++q) add_dw<false>(dw_hid[q - 1], img + fwd_desc<W, IN_KS, NH>(q, in_dim).off, W, W);
+        add_dw<false>(dw_last, img + fwd_desc<W, IN_KS, NH>(LAST, in_dim).off, W, kOut);
+    }
+    __syncthreads();
+    const float* img0 = reinterpret_cast<const float*>(lds);
+    float* slab_row = slab + (size_t)blockIdx.x * nparams;
+    for (uint32_t t = threadIdx.x; t < nparams; t += blockDim.x) slab_row[t] = img0[t] + img0[nparams + t];
 }
 
-// grad_weights[p] = sum over workgroup rows of the slab, in fixed row order
-// (deterministic). 64 parameters x 4 row phases per block.
+// grad_weights[p] = sum over workgroup rows of the slab, in a fixed order
+// (deterministic). Block = 64 parameters (one 256 B row segment per wave) x
+// kReducePhases row phases; each thread keeps 4 independent partial sums so
+// its loads stay in flight.
+constexpr int kReducePhases = 16;
 template <typename OUT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64 * kReducePhases)
 k_slab_reduce(const float* __restrict__ slab, uint32_t rows, uint32_t n, OUT* __restrict__ out) {
-    __shared__ float part[4][64];
+    __shared__ float part[kReducePhases][64];
     const uint32_t lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
     const uint32_t p = blockIdx.x * 64 + lane;
-    float s = 0.0f;
-    if (p < n)
-        for (uint32_t r = ph; r < rows; r += 4) s += slab[(size_t)r * n + p];
-    part[ph][lane] = s;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+    if (p < n) {
+        uint32_t r = ph;
+        for (; r + 3 * kReducePhases < rows; r += 4 * kReducePhases) {
+            s0 += slab[(size_t)r * n + p];
+            s1 += slab[(size_t)(r + kReducePhases) * n + p];
+            s2 += slab[(size_t)(r + 2 * kReducePhases) * n + p];
+            s3 += slab[(size_t)(r + 3 * kReducePhases) * n + p];
+        }
+        for (; r < rows; r += kReducePhases) s0 += slab[(size_t)r * n + p];
+    }
+    part[ph][lane] = (s0 + s1) + (s2 + s3);
     __syncthreads();
-    if (ph == 0 && p < n) out[p] = (OUT)((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
+    if (ph == 0 && p < n) {
+        float t = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kReducePhases; ++k) t += part[k][lane];
+        out[p] = (OUT)t;
+    }
 }
 
 // ---- host dispatch ----------------------------------------------------------
@@ -604,10 +635,10 @@ int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, ui
                        (const ngp_half*)grad, (const ngp_half*)in, (const half8*)image,
                        (ngp_half*)grad_in, slab, np, B, in_dim, act);
     if (gw_dtype == NGP_DTYPE_F16) {
-        hipLaunchKernelGGL((k_slab_reduce<ngp_half>), dim3(ngp_div_up(np, 64)), dim3(256), 0, st,
+        hipLaunchKernelGGL((k_slab_reduce<ngp_half>), dim3(ngp_div_up(np, 64)), dim3(64 * kReducePhases), 0, st,
                            (const float*)slab, blocks, np, (ngp_half*)gw);
     } else {
-        hipLaunchKernelGGL((k_slab_reduce<float>), dim3(ngp_div_up(np, 64)), dim3(256), 0, st,
+        hipLaunchKernelGGL((k_slab_reduce<float>), dim3(ngp_div_up(np, 64)), dim3(64 * kReducePhases), 0, st,
                            (const float*)slab, blocks, np, (float*)gw);
     }
     return ngp_check_launch("ffmlp_backward");
