@@ -98,12 +98,18 @@ int ngp_packbits(const float* grid, uint32_t N, float density_thresh, uint8_t* b
  * execution of the reference's atomicAdd ordering): rays[i] = (i, off_i, n_i).
  * counter[0] += total samples, counter[1] += N (same as the reference).
  * Samples of rays with off_i + n_i > M are dropped (reference :416); the
- * caller zero-fills xyzs/dirs/deltas like the reference wrapper does. */
+ * caller zero-fills xyzs/dirs/deltas like the reference wrapper does.
+ * workspace: 16-byte aligned device scratch of at least
+ * ngp_march_rays_train_workspace_bytes (one float per possible sample,
+ * N * max_steps, plus an occupancy image of ~C * H^3 / 6 bytes), e.g. from
+ * the caller's caching allocator. */
+size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_steps, uint32_t C, uint32_t H);
 int ngp_march_rays_train(const float* rays_o, const float* rays_d, const uint8_t* grid,
                          float bound, float dt_gamma, uint32_t max_steps, uint32_t N, uint32_t C,
                          uint32_t H, uint32_t M, const float* nears, const float* fars,
                          float* xyzs, float* dirs, float* deltas, int32_t* rays, int32_t* counter,
-                         const float* noises, void* stream);
+                         const float* noises, void* workspace, size_t workspace_bytes,
+                         void* stream);
 
 /* raymarching.h:14, raymarching.cu:580-588 */
 int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs, const float* deltas,

@@ -156,17 +156,19 @@ def _rays(N, seed, dev):
     return ro, rd
 
 
-def _march_case(cuda, N, C=1, bound=1.0, dt_gamma=0.0, M=None, perturb_seed=0, max_steps=1024):
+def _march_case(cuda, N, C=1, bound=1.0, dt_gamma=0.0, M=None, perturb_seed=0, max_steps=1024,
+                bits=None, H=128):
     import raymarching.backend as rb
     ro, rd = lego_rays(N, seed=perturb_seed)
     if bound > 1:
         ro = ro * (bound / 2.0)
     aabb = np.array([-bound] * 3 + [bound] * 3, np.float32)
     nears, fars = oracle.near_far_from_aabb(ro, rd, aabb, 0.2)
-    bits = box_bitfield(lego_boxes(), cascade=C, bound=bound)
+    if bits is None:
+        bits = box_bitfield(lego_boxes(), cascade=C, bound=bound, H=H)
     noises = np.random.default_rng(perturb_seed + 100).random(N, dtype=np.float32)
     Mr = M if M is not None else N * max_steps
-    ref = oracle.march_rays_train(ro, rd, bound, bits, C, 128, nears, fars, noises, M=Mr,
+    ref = oracle.march_rays_train(ro, rd, bound, bits, C, H, nears, fars, noises, M=Mr,
                                   dt_gamma=dt_gamma, max_steps=max_steps)
     xyzs = torch.zeros(Mr, 3, device=cuda); dirs = torch.zeros(Mr, 3, device=cuda)
     deltas = torch.zeros(Mr, 2, device=cuda)
@@ -176,13 +178,11 @@ def _march_case(cuda, N, C=1, bound=1.0, dt_gamma=0.0, M=None, perturb_seed=0, m
     rb._backend.near_far_from_aabb(t(ro, cuda), t(rd, cuda), t(aabb, cuda), N, 0.2, tn, tf)
     assert np.array_equal(tn.cpu().numpy(), nears) and np.array_equal(tf.cpu().numpy(), fars)
     rb._backend.march_rays_train(t(ro, cuda), t(rd, cuda), t(bits, cuda), bound, dt_gamma, max_steps,
-                                 N, C, 128, Mr, tn, tf, xyzs, dirs, deltas, rays, counter, t(noises, cuda))
+                                 N, C, H, Mr, tn, tf, xyzs, dirs, deltas, rays, counter, t(noises, cuda))
     return ref, (xyzs, dirs, deltas, rays, counter)
 
 
-@pytest.mark.parametrize("N,C,bound,dt_gamma", [(4096, 1, 1.0, 0.0), (1000, 2, 2.0, 1 / 128), (77, 1, 1.0, 0.0)])
-def test_march_rays_train_bit_exact(cuda, N, C, bound, dt_gamma):
-    ref, got = _march_case(cuda, N, C, bound, dt_gamma)
+def _assert_march_equal(ref, got):
     rx, rdirs, rdel, rrays, rcnt = ref
     xyzs, dirs, deltas, rays, counter = [a.cpu().numpy() for a in got]
     assert np.array_equal(rays, rrays)
@@ -192,6 +192,32 @@ def test_march_rays_train_bit_exact(cuda, N, C, bound, dt_gamma):
     assert np.array_equal(xyzs[:m].view(np.uint32), rx[:m].view(np.uint32))
     assert np.array_equal(dirs[:m].view(np.uint32), rdirs[:m].view(np.uint32))
     assert np.array_equal(deltas[:m].view(np.uint32), rdel[:m].view(np.uint32))
+
+
+@pytest.mark.parametrize("N,C,bound,dt_gamma", [(4096, 1, 1.0, 0.0), (1000, 2, 2.0, 1 / 128), (77, 1, 1.0, 0.0),
+                                                (1000, 2, 2.0, 0.0), (600, 3, 4.0, 0.0)])
+def test_march_rays_train_bit_exact(cuda, N, C, bound, dt_gamma):
+    # dt_gamma == 0: one wave per ray, 64 speculative segments stitched
+    # (multi-level cascades skip across whole segments); dt_gamma > 0: serial
+    _assert_march_equal(*_march_case(cuda, N, C, bound, dt_gamma))
+
+
+@pytest.mark.parametrize("density", [0.02, 0.3, 1.0])
+def test_march_rays_train_random_bitfields(cuda, density):
+    """Irregular occupancy exercises the segment stitching (re-walks) and, at
+    density 1, rays that sample every chain index."""
+    rng = np.random.default_rng(int(density * 100))
+    bits = np.packbits(rng.random(128 ** 3) < density, bitorder="little")
+    _assert_march_equal(*_march_case(cuda, 700, bits=bits, perturb_seed=5))
+
+
+@pytest.mark.parametrize("max_steps", [1, 7, 64])
+def test_march_rays_train_max_steps(cuda, max_steps):
+    _assert_march_equal(*_march_case(cuda, 500, max_steps=max_steps, perturb_seed=2))
+
+
+def test_march_rays_train_grid64(cuda):
+    _assert_march_equal(*_march_case(cuda, 800, H=64, perturb_seed=3))
 
 
 def test_march_rays_train_overflow_drops_tail_rays(cuda):

@@ -36,8 +36,9 @@ SIGNATURES = {
     "ngp_morton3D": [c_vp, c_u32, c_vp, c_vp],
     "ngp_morton3D_invert": [c_vp, c_u32, c_vp, c_vp],
     "ngp_packbits": [c_vp, c_u32, c_f32, c_vp, c_vp],
+    "ngp_march_rays_train_workspace_bytes": [c_u32, c_u32, c_u32, c_u32],
     "ngp_march_rays_train": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
-                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_composite_rays_train_forward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_vp, c_vp,
                                          c_vp, c_vp],
     "ngp_composite_rays_train_backward": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -63,6 +64,7 @@ SIGNATURES = {
 _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
+    "ngp_march_rays_train_workspace_bytes": c_sz,
 }
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}

@@ -10,21 +10,23 @@
 //   kernel_composite_rays_train_forward / backward    :500-577 / :601-691
 //   kernel_march_rays / kernel_composite_rays         :709-814 / :827-914
 //
-// MI355X design: the reference orders samples
-// with two atomicAdd counters (:405-406), so its row order changes run to run.
-// Here the per-ray sample counts are turned into offsets by a deterministic
-// exclusive prefix sum in ray order: pass 1 counts (and reduces per
-// workgroup), a one-workgroup scan turns the workgroup sums into bases, and
-// pass 2 re-marches and writes at base + in-workgroup prefix (wave ballot +
-// LDS scan). Output is a valid execution of the reference and is identical on
-// every run, so parity can compare rows directly.
+// MI355X design:
+//   * the reference orders samples with two atomicAdd counters (:405-406), so
+//     its row order changes run to run. Here offsets are a deterministic
+//     exclusive prefix sum in ray order; the output is a valid execution of the
+//     reference and identical on every run, so parity compares rows directly;
+//   * each ray is marched ONCE (the reference marches twice): the t of every
+//     occupied sample goes to a workspace row, and a flat per-sample pass
+//     writes xyzs/dirs/deltas at the scanned offsets;
+//   * occupancy lookups hit an LDS rank/select image of the bitfield (OccLds)
+//     instead of L2: marching is a serial dependency chain per ray, so the
+//     lookup latency is the step time.
 #include "ngp_common.h"
 
 #include <cfloat>
 
 namespace {
 
-constexpr uint32_t kMarchBlock = 128;
 constexpr float kSQRT3 = 1.7320508075688772f;
 constexpr float kRPI = 0.3183098861837907f;
 
@@ -59,7 +61,7 @@ NGP_DEV uint32_t morton3D_invert(uint32_t x) {
 }
 
 struct MarchConst {
-    float bound, dt_gamma, dt_min, dt_max, rH, H3;
+    float bound, rbound, dt_gamma, dt_min, dt_max, rH, H3;
     uint32_t max_steps, C, H;
 };
 
@@ -67,6 +69,7 @@ static MarchConst make_march_const(float bound, float dt_gamma, uint32_t max_ste
                                    uint32_t H) {
     MarchConst k;
     k.bound = bound;
+    k.rbound = 1 / bound;  // IEEE division, as the device's 1 / mip_bound
     k.dt_gamma = dt_gamma;
     k.dt_min = 2 * kSQRT3 / (float)max_steps;
     k.dt_max = 2 * kSQRT3 * (float)(1u << (C - 1)) / (float)H;
@@ -90,40 +93,84 @@ NGP_DEV Ray load_ray(const float* __restrict__ rays_o, const float* __restrict__
     return r;
 }
 
-// One marching step decision, shared by the count pass, the write pass and
-// inference marching (raymarching.cu:359-400). Returns true if the sample at
-// the current t is occupied; otherwise advances t past the empty cell.
+// ---- occupancy lookups ----------------------------------------------------------
+// Bit `index` of the cascaded bitfield, straight from HBM/L2.
+struct OccGlobal {
+    const uint8_t* __restrict__ grid;
+    NGP_DEV bool operator()(uint32_t index) const { return (grid[index >> 3] >> (index & 7)) & 1u; }
+};
+
+// LDS-resident rank/select image of the bitfield (built per workgroup by
+// k_occ_build, copied in by load_occ_index). Because Morton order interleaves the coordinate bits,
+// bitfield byte b holds exactly the 2x2x2 cells of coarse cell b, so:
+//   sum[w]   bit i  = (grid byte 32w+i != 0)          (coarse occupancy, 1 bit/byte)
+//   pre[g]          = non-zero bytes before word 4g   (rank directory)
+//   bytes[]         = the non-zero grid bytes, in order
+// A lookup in empty space costs one ds_read_b128; an occupied coarse cell one
+// more LDS read. The marching loop never waits on L2 (~10x the latency).
+struct OccLds {
+    const uint32_t* sum;
+    const uint32_t* pre;
+    const uint8_t* bytes;
+    NGP_DEV bool operator()(uint32_t index) const {
+        const uint32_t byte = index >> 3, w = byte >> 5, g = w >> 2, j = w & 3, bit = byte & 31;
+        const uint4 q = reinterpret_cast<const uint4*>(sum)[g];
+        const uint32_t m = j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w;
+        if (!((m >> bit) & 1u)) return false;
+        uint32_t pos = pre[g] + __popc(m & ((1u << bit) - 1u));
+        if (j > 0) pos += __popc(q.x);
+        if (j > 1) pos += __popc(q.y);
+        if (j > 2) pos += __popc(q.z);
+        return (bytes[pos] >> (index & 7)) & 1u;
+    }
+};
+
+// One marching step decision, shared by training and inference marching
+// (raymarching.cu:359-400). Returns true if the sample at the current t is
+// occupied; otherwise advances t past the empty cell.
 struct Sample {
     float x, y, z, dt;
 };
 
-NGP_DEV bool march_step(const Ray& r, const MarchConst& k, const uint8_t* __restrict__ grid,
-                        float& t, Sample& s) {
+// ONE_LEVEL: C == 1, where both mip levels clamp to 0 (every Lego config).
+// mip_rbound = 1 / min(2^level, bound) without a division: 2^-level is exact
+// when 2^level <= bound, otherwise it is the host's IEEE 1 / bound.
+// probe: the occupancy decision at t and the DDA skip target tt of its cell.
+template <bool ONE_LEVEL, typename OCC>
+NGP_DEV bool probe(const Ray& r, const MarchConst& k, const OCC& occupied, float t, Sample& s, float& tt) {
     s.x = clampf(fmaf(t, r.dx, r.ox), -k.bound, k.bound);
     s.y = clampf(fmaf(t, r.dy, r.oy), -k.bound, k.bound);
     s.z = clampf(fmaf(t, r.dz, r.oz), -k.bound, k.bound);
     s.dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
 
-    const int maxl = (int)k.C - 1;
-    const float mxp = fmaxf(fabsf(s.x), fmaxf(fabsf(s.y), fabsf(s.z)));
-    const float mxd = s.dt * (float)k.H * 0.5f;
-    const int level = max(frexp_level(mxp, maxl), frexp_level(mxd, maxl));
-
-    const float mip_bound = fminf(scalbnf(1.0f, level), k.bound);
-    const float mip_rbound = 1 / mip_bound;
+    int level = 0;
+    if (!ONE_LEVEL) {
+        const int maxl = (int)k.C - 1;
+        const float mxp = fmaxf(fabsf(s.x), fmaxf(fabsf(s.y), fabsf(s.z)));
+        const float mxd = s.dt * (float)k.H * 0.5f;
+        level = max(frexp_level(mxp, maxl), frexp_level(mxd, maxl));
+    }
+    const float p2 = scalbnf(1.0f, level);
+    const float mip_bound = fminf(p2, k.bound);
+    const float mip_rbound = p2 <= k.bound ? scalbnf(1.0f, -level) : k.rbound;
     const float Hm1 = (float)(k.H - 1);
     const int nx = (int)clampf(0.5f * fmaf(s.x, mip_rbound, 1.0f) * (float)k.H, 0.0f, Hm1);
     const int ny = (int)clampf(0.5f * fmaf(s.y, mip_rbound, 1.0f) * (float)k.H, 0.0f, Hm1);
     const int nz = (int)clampf(0.5f * fmaf(s.z, mip_rbound, 1.0f) * (float)k.H, 0.0f, Hm1);
 
     const uint32_t index = (uint32_t)((float)level * k.H3 + (float)morton3D(nx, ny, nz));
-    const bool occ = grid[index / 8] & (1u << (index % 8));
-    if (occ) return true;
-
+    // the skip target does not depend on the lookup: computed in its shadow
     const float tx = ((((float)nx + 0.5f + 0.5f * signf(r.dx)) * k.rH * 2 - 1) * mip_bound - s.x) * r.rdx;
     const float ty = ((((float)ny + 0.5f + 0.5f * signf(r.dy)) * k.rH * 2 - 1) * mip_bound - s.y) * r.rdy;
     const float tz = ((((float)nz + 0.5f + 0.5f * signf(r.dz)) * k.rH * 2 - 1) * mip_bound - s.z) * r.rdz;
-    const float tt = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+    tt = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+    return occupied(index);
+}
+
+template <bool ONE_LEVEL, typename OCC>
+NGP_DEV bool march_step(const Ray& r, const MarchConst& k, const OCC& occupied, float& t, Sample& s) {
+    float tt;
+    if (probe<ONE_LEVEL>(r, k, occupied, t, s, tt)) return true;
     do {
         t += clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
     } while (t < tt);
@@ -214,8 +261,10 @@ __global__ void k_packbits(const float* __restrict__ grid, uint32_t N, float thr
     bitfield[n] = (uint8_t)bits;
 }
 
-// Workgroup-wide exclusive scan of one uint32 per thread (kMarchBlock threads):
-// wave-level scan with DPP-free shuffles, then the two wave totals via LDS.
+// Workgroup-wide exclusive scan of one uint32 per thread (BLOCK threads):
+// wave-level shuffle scan, then the wave totals via LDS. Ends with a barrier,
+// so lds_waves can be reused right away.
+template <uint32_t BLOCK>
 NGP_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds_waves, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
@@ -229,68 +278,344 @@ NGP_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds_waves, uint32_t&
     __syncthreads();
     uint32_t wave_base = 0;
     total = 0;
-    for (uint32_t w = 0; w < kMarchBlock / 64; ++w) {
+#pragma unroll
+    for (uint32_t w = 0; w < BLOCK / 64; ++w) {
         const uint32_t s = lds_waves[w];
         if (w < wave) wave_base += s;
         total += s;
     }
+    __syncthreads();
     return wave_base + incl - v;
 }
 
-// Pass 1: count samples per ray; rays[n] = (n, -, count). The workgroup's sum is
-// parked in the offset column of its first ray (rays[first*3+1]).
-__global__ void __launch_bounds__(kMarchBlock)
-k_march_count(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
-              const uint8_t* __restrict__ grid, MarchConst k, uint32_t N,
-              const float* __restrict__ nears, const float* __restrict__ fars,
-              const float* __restrict__ noises, int32_t* __restrict__ rays) {
-    __shared__ uint32_t lds_waves[kMarchBlock / 64];
-    const uint32_t n = blockIdx.x * kMarchBlock + threadIdx.x;
-    uint32_t num_steps = 0;
-    if (n < N) {
-        const Ray r = load_ray(rays_o, rays_d, n);
-        const float far = fars[n];
-        float t = ray_t0(nears[n], noises[n], k);
-        Sample s;
-        while (t < far && num_steps < k.max_steps) {
-            if (march_step(r, k, grid, t, s)) {
-                num_steps++;
-                t += s.dt;
-            }
-        }
-        rays[n * 3 + 0] = (int32_t)n;
-        rays[n * 3 + 2] = (int32_t)num_steps;
+// ---- march_rays_train ------------------------------------------------------------
+// Three kernels, all deterministic:
+//   k_march_train  one WAVE per ray (below): the t of every occupied sample goes
+//                  to the workspace row ts[n][0..count), rays[n] = (n, -, count)
+//   k_march_scan   one workgroup: exclusive scan of the counts in ray order ->
+//                  rays[n].offset, counter
+//   k_march_emit   per SAMPLE (flat, balanced): xyzs/dirs/deltas recomputed
+//                  from the recorded t with the reference's exact float ops
+//
+// Why one wave per ray. Marching is a serial recurrence on t: ~150-500 probes
+// per Lego ray, ~130 dependent VALU each. One lane per ray gives 64 waves for
+// 4096 rays — 1/16 of the SIMDs, each a pure latency chain. But the state of
+// the recurrence is only t, and t only ever moves along ONE chain:
+//     t_0 = near + noise * dt0,   t_{k+1} = t_k + clamp(t_k * dt_gamma, ...)
+// (an occupied step and every iteration of the DDA skip loop apply the same
+// update). A probe at chain index k goes to k+1 (occupied) or to the first j
+// with t_j >= tt(t_k) (empty). So with dt_gamma == 0, where t_k has a closed
+// form per binade (advance0), the chain splits into 64 index segments: lane s
+// walks segment s speculatively from its first index, then the true walk is
+// stitched across segments (a walk that reaches an index the speculative walk
+// visited continues identically from there). Exact for every ray; rays the
+// closed form does not cover (dt_gamma > 0, > 64 x 64 chain steps) are
+// marched serially by lane 0 (the reference loop).
+constexpr uint32_t kMarchThreads = 256;   // rays per k_march_emit group
+constexpr uint32_t kSegWaves = 16;        // rays (waves) per march workgroup
+constexpr uint32_t kSegThreads = kSegWaves * 64;
+constexpr uint32_t kMaxMarchBlocks = 256;
+constexpr size_t kMarchLdsBytes = 156 * 1024;
+constexpr uint32_t kEmitSplit = 8;        // workgroups per ray group in k_march_emit
+constexpr uint32_t kInf = 0xffffffffu;
+
+struct OccLayout {
+    uint32_t nbytes, nwords, ngroups, cap;  // cap = LDS bytes left for the compacted bytes
+};
+
+// Global occupancy image (workspace), laid out exactly as OccLds in LDS:
+//   [total (16 B)] [sum: 4 words / group] [pre: 1 word / group] [bytes]
+NGP_DEV uint32_t* occ_sum(uint8_t* img) { return reinterpret_cast<uint32_t*>(img + 16); }
+
+// 32 bitfield bytes starting at 32w as 8 dwords (vector loads when in range).
+NGP_DEV void load_word32(const uint8_t* __restrict__ grid, uint32_t w, uint32_t nbytes, uint32_t (&d)[8]) {
+    if (32 * w + 32 <= nbytes) {
+        const uint4* g = reinterpret_cast<const uint4*>(grid + 32 * (size_t)w);
+        const uint4 a = g[0], b = g[1];
+        d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+        return;
     }
-    uint32_t total;
-    block_exclusive_scan(num_steps, lds_waves, total);
-    if (threadIdx.x == 0) rays[(size_t)blockIdx.x * kMarchBlock * 3 + 1] = (int32_t)total;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = 0;
+    for (uint32_t i = 0; i < 32 && 32 * w + i < nbytes; ++i) d[i >> 2] |= (uint32_t)grid[32 * w + i] << (8 * (i & 3));
 }
 
-// One workgroup: exclusive scan over the per-workgroup sums (in place), then
-// counter[0] += total, counter[1] += N.
-__global__ void __launch_bounds__(1024)
-k_march_scan(int32_t* __restrict__ rays, uint32_t num_blocks, uint32_t N, int32_t* counter) {
-    __shared__ uint32_t lds[1024];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = (uint32_t)counter[0];
-    __syncthreads();
-    for (uint32_t base = 0; base < num_blocks; base += 1024) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < num_blocks ? (uint32_t)rays[(size_t)i * kMarchBlock * 3 + 1] : 0u;
-        lds[threadIdx.x] = v;
-        __syncthreads();
-        // Hillis-Steele inclusive scan in LDS (num_blocks is small: N / 128).
-        for (uint32_t o = 1; o < 1024; o <<= 1) {
-            const uint32_t u = threadIdx.x >= o ? lds[threadIdx.x - o] : 0u;
-            __syncthreads();
-            lds[threadIdx.x] += u;
-            __syncthreads();
+NGP_DEV uint32_t nonzero_bytes(const uint32_t (&d)[8]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m |= ((d[i] >> (8 * j)) & 0xffu) ? (1u << (4 * i + j)) : 0u;
+    return m;
+}
+
+// One workgroup of 1024: summary words, rank directory and compacted
+// non-zero bytes of the bitfield, in rounds of 2 groups (256 B) per thread
+// with every load of a round in flight together.
+constexpr uint32_t kBuildThreads = 1024;
+constexpr uint32_t kBuildGroups = 2;
+__global__ void __launch_bounds__(kBuildThreads)
+k_occ_build(const uint8_t* __restrict__ grid, OccLayout L, uint8_t* __restrict__ img) {
+    __shared__ uint32_t lds_waves[kBuildThreads / 64];
+    uint32_t* sum = occ_sum(img);
+    uint32_t* pre = sum + 4 * L.ngroups;
+    uint8_t* bytes = reinterpret_cast<uint8_t*>(pre + L.ngroups);
+    uint32_t carry = 0;
+    for (uint32_t gb = 0; gb < L.ngroups; gb += kBuildThreads * kBuildGroups) {
+        const uint32_t g0 = gb + threadIdx.x * kBuildGroups;
+        uint32_t d[kBuildGroups * 4][8];
+        uint32_t m[kBuildGroups * 4];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kBuildGroups * 4; ++i) {
+            if (4 * g0 + i < 4 * L.ngroups) {
+                load_word32(grid, 4 * g0 + i, L.nbytes, d[i]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d[i][j] = 0;
+            }
         }
-        const uint32_t excl = carry + lds[threadIdx.x] - v;
-        if (i < num_blocks) rays[(size_t)i * kMarchBlock * 3 + 1] = (int32_t)excl;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += lds[1023];
-        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < kBuildGroups * 4; ++i) {
+            m[i] = nonzero_bytes(d[i]);
+            if (4 * g0 + i < 4 * L.ngroups) sum[4 * g0 + i] = m[i];
+            cnt += __popc(m[i]);
+        }
+        uint32_t total;
+        uint32_t pos = carry + block_exclusive_scan<kBuildThreads>(cnt, lds_waves, total);
+#pragma unroll
+        for (uint32_t i = 0; i < kBuildGroups * 4; ++i) {
+            if (i % 4 == 0 && g0 + i / 4 < L.ngroups) pre[g0 + i / 4] = pos;
+            uint32_t mm = m[i];
+            while (mm) {
+                const uint32_t b = __ffs(mm) - 1;
+                bytes[pos++] = (uint8_t)(d[i][b >> 2] >> (8 * (b & 3)));
+                mm &= mm - 1;
+            }
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(img)[0] = carry;
+}
+
+// Copies the global image into this workgroup's LDS when its bytes fit.
+// Returns false (workgroup-uniform) otherwise: lookups then go to HBM/L2.
+NGP_DEV bool load_occ_index(const uint8_t* __restrict__ img, const OccLayout& L, uint4* lds) {
+    const uint32_t total = reinterpret_cast<const uint32_t*>(img)[0];
+    if (total > L.cap) return false;
+    const uint32_t n16 = (20 * L.ngroups + total + 15) / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(img + 16);
+#pragma unroll 8
+    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) lds[i] = src[i];
+    __syncthreads();
+    return true;
+}
+
+template <bool ONE_LEVEL, typename OCC>
+NGP_DEV uint32_t march_ray_train(const Ray& r, const MarchConst& k, const OCC& occ, float t, float far,
+                                 float* __restrict__ ts) {
+    uint32_t num_steps = 0;
+    Sample s;
+    while (t < far && num_steps < k.max_steps) {
+        if (march_step<ONE_LEVEL>(r, k, occ, t, s)) {
+            ts[num_steps++] = t;
+            t += s.dt;
+        }
+    }
+    return num_steps;
+}
+
+// Exact f^m(t) for f(t) = t + delta in float (round to nearest even): inside a
+// binade [2^e, 2^(e+1)) every step adds the same multiple of the ulp unless
+// delta / ulp ends in exactly .5 (a tie), so whole runs of steps are one
+// exact multiply-add; ties and binade crossings are stepped one by one.
+NGP_DEV float advance0(float t, uint32_t m, float delta) {
+    const uint32_t db = __float_as_uint(delta);
+    const int ed = (int)((db >> 23) & 0xffu);
+    const uint32_t md = (db & 0x7fffffu) | 0x800000u;
+    while (m > 0) {
+        const float t1 = t + delta;
+        const int e = (int)((__float_as_uint(t) >> 23) & 0xffu);
+        const int sh = e - ed;
+        const bool tie = sh >= 1 && sh <= 24 && (md & ((1u << sh) - 1u)) == (1u << (sh - 1));
+        if (e == 0 || e >= 254 || tie || !(t1 > t)) {
+            t = t1;
+            --m;
+            continue;
+        }
+        const float step = t1 - t;  // exact: t, t1 are multiples of ulp(t) in [t, 2t]
+        const float top = __uint_as_float((uint32_t)(e + 1) << 23);
+        const double room = ((double)top - (double)delta - (double)t) / (double)step;
+        uint32_t j = room > 2.0 ? (uint32_t)fmin(room - 2.0, 4.0e9) : 0u;
+        if (j > m) j = m;
+        if (j == 0) {
+            t = t1;
+            --m;
+            continue;
+        }
+        t = t + (float)j * step;  // exact: j * step < 2^e and a multiple of ulp(t)
+        m -= j;
+    }
+    return t;
+}
+
+// One ray, one wave (dt_gamma == 0 path). Returns the sample count (all lanes).
+template <bool ONE_LEVEL, typename OCC>
+NGP_DEV uint32_t march_ray_segmented(const Ray& r, const MarchConst& k, const OCC& occ, float t0,
+                                     float far, float delta, uint32_t L, float* __restrict__ ts) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t a = lane * L, b = a + L;
+    const float ta = advance0(t0, a, delta);
+    // speculative walk of segment [a, b) from a
+    uint64_t vis = 0, occm = 0;
+    uint32_t kk = a;
+    float t = ta;
+    Sample s;
+    auto walk = [&](uint32_t from, float tf) {
+        vis = 0;
+        occm = 0;
+        kk = from;
+        t = tf;
+        while (t < far && kk < b) {
+            const uint64_t bit = 1ull << (kk - a);
+            vis |= bit;
+            float tt;
+            if (probe<ONE_LEVEL>(r, k, occ, t, s, tt)) {
+                occm |= bit;
+                t += delta;
+                ++kk;
+            } else {
+                do {
+                    t += delta;
+                    ++kk;
+                } while (t < tt);
+            }
+        }
+    };
+    walk(a, ta);
+    // exit index of the segment's walk; kInf once t >= far (the ray ends there)
+    uint32_t X = t < far ? kk : kInf;
+    uint32_t kend = kk;
+    bool ended = !(t < far);
+
+    uint32_t in = kInf;
+    for (;;) {
+        // stitch: in_s = first index >= a_s the true walk visits
+        uint32_t cur = 0;
+        for (uint32_t sg = 0; sg < 64; ++sg) {
+            if (lane == sg) in = cur;
+            const uint32_t Xs = __shfl(X, sg, 64);
+            if (cur < (sg + 1) * L) cur = Xs;
+        }
+        const bool inside = in < b && !(ended && in >= kend);
+        const bool merged = !inside || ((vis >> (in - a)) & 1ull);
+        const uint64_t bad = __ballot(!merged);
+        if (!bad) break;
+        if (lane == (uint32_t)__ffsll((unsigned long long)bad) - 1) {  // re-walk from the true entry
+            walk(in, advance0(t0, in, delta));
+            X = t < far ? kk : kInf;
+            kend = kk;
+            ended = !(t < far);
+        }
+    }
+    const bool inside = in < b && !(ended && in >= kend);
+    const uint64_t mine = inside ? occm & ~((1ull << (in - a)) - 1ull) : 0ull;
+    const uint32_t cnt = __popcll(mine);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    uint32_t off = incl - cnt;
+    if (mine && off < k.max_steps) {
+        float tj = ta;
+        uint64_t m = mine;
+        for (uint32_t j = 0; m && off < k.max_steps; ++j, tj += delta) {
+            if ((m >> j) & 1ull) {
+                ts[off++] = tj;
+                m &= m - 1;
+            }
+        }
+    }
+    return total < k.max_steps ? total : k.max_steps;
+}
+
+template <bool ONE_LEVEL, typename OCC>
+NGP_DEV uint32_t march_ray_wave(const Ray& r, const MarchConst& k, const OCC& occ, float t0, float far,
+                                float* __restrict__ ts) {
+    if (!(t0 < far)) return 0;
+    const float delta = clampf(0.0f, k.dt_min, k.dt_max);  // the update when dt_gamma == 0
+    if (k.dt_gamma == 0.0f) {
+        // every chain step is >= delta - ulp(far); chain length to far bounds
+        const float ulp_far = __uint_as_float(((__float_as_uint(far) >> 23) & 0xffu) << 23) * 1.1920929e-7f;
+        const double smin = (double)delta - (double)ulp_far;
+        if (smin > 0.0) {
+            const double kest = ceil(((double)far - (double)t0) / smin) + 2.0;
+            const uint32_t L = (uint32_t)ceil(kest / 64.0);
+            if (L <= 64) return march_ray_segmented<ONE_LEVEL>(r, k, occ, t0, far, delta, L, ts);
+        }
+    }
+    uint32_t n = 0;
+    if ((threadIdx.x & 63) == 0) n = march_ray_train<ONE_LEVEL>(r, k, occ, t0, far, ts);
+    return __shfl(n, 0, 64);
+}
+
+__global__ void __launch_bounds__(kSegThreads)
+k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+              const uint8_t* __restrict__ grid, const uint8_t* __restrict__ img, OccLayout L,
+              MarchConst k, uint32_t N, const float* __restrict__ nears, const float* __restrict__ fars,
+              const float* __restrict__ noises, int32_t* __restrict__ rays, float* __restrict__ ts) {
+    extern __shared__ uint4 dyn[];
+    uint32_t* sum = reinterpret_cast<uint32_t*>(dyn);
+    uint32_t* pre = sum + 4 * L.ngroups;
+    const bool lds = L.ngroups > 0 && load_occ_index(img, L, dyn);
+    const OccLds occ_lds{sum, pre, reinterpret_cast<const uint8_t*>(pre + L.ngroups)};
+    const OccGlobal occ_glb{grid};
+    const uint32_t wave = threadIdx.x >> 6;
+    for (uint32_t n = blockIdx.x * kSegWaves + wave; n < N; n += gridDim.x * kSegWaves) {
+        const Ray r = load_ray(rays_o, rays_d, n);
+        const float t0 = ray_t0(nears[n], noises[n], k);
+        const float far = fars[n];
+        float* row = ts + (size_t)n * k.max_steps;
+        uint32_t cnt;
+        if (lds) {
+            cnt = k.C == 1 ? march_ray_wave<true>(r, k, occ_lds, t0, far, row)
+                           : march_ray_wave<false>(r, k, occ_lds, t0, far, row);
+        } else {
+            cnt = k.C == 1 ? march_ray_wave<true>(r, k, occ_glb, t0, far, row)
+                           : march_ray_wave<false>(r, k, occ_glb, t0, far, row);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            rays[n * 3 + 0] = (int32_t)n;
+            rays[n * 3 + 2] = (int32_t)cnt;
+        }
+    }
+}
+
+// One workgroup: exclusive scan of the per-ray counts in ray order (4 rays per
+// thread per round), then counter[0] += total, counter[1] += N.
+__global__ void __launch_bounds__(1024)
+k_march_scan(int32_t* __restrict__ rays, uint32_t N, int32_t* counter) {
+    __shared__ uint32_t lds_waves[1024 / 64];
+    uint32_t carry = (uint32_t)counter[0];
+    for (uint32_t base = 0; base < N; base += 4096) {
+        const uint32_t i0 = base + 4 * threadIdx.x;
+        uint32_t v[4], local = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            v[j] = i0 + j < N ? (uint32_t)rays[(size_t)(i0 + j) * 3 + 2] : 0u;
+            local += v[j];
+        }
+        uint32_t total;
+        uint32_t run = carry + block_exclusive_scan<1024>(local, lds_waves, total);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            if (i0 + j < N) rays[(size_t)(i0 + j) * 3 + 1] = (int32_t)run;
+            run += v[j];
+        }
+        carry += total;
     }
     if (threadIdx.x == 0) {
         counter[0] = (int32_t)carry;
@@ -298,46 +623,79 @@ k_march_scan(int32_t* __restrict__ rays, uint32_t num_blocks, uint32_t N, int32_
     }
 }
 
-// Pass 2: offsets = workgroup base + in-workgroup prefix; re-march and write.
-__global__ void __launch_bounds__(kMarchBlock)
-k_march_write(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
-              const uint8_t* __restrict__ grid, MarchConst k, uint32_t N, uint32_t M,
-              const float* __restrict__ nears, const float* __restrict__ fars,
-              const float* __restrict__ noises, float* __restrict__ xyzs,
-              float* __restrict__ dirs, float* __restrict__ deltas, int32_t* __restrict__ rays) {
-    __shared__ uint32_t lds_waves[kMarchBlock / 64];
-    const uint32_t n = blockIdx.x * kMarchBlock + threadIdx.x;
-    const uint32_t block_base = (uint32_t)rays[(size_t)blockIdx.x * kMarchBlock * 3 + 1];
-    const uint32_t num_steps = n < N ? (uint32_t)rays[n * 3 + 2] : 0u;
-    __syncthreads();  // every lane has read the parked base before lane 0 overwrites it
-    uint32_t total;
-    const uint32_t point_index = block_base + block_exclusive_scan(num_steps, lds_waves, total);
-    if (n >= N) return;
-    rays[n * 3 + 1] = (int32_t)point_index;
-    if (num_steps == 0) return;
-    if (point_index + num_steps > M) return;
+// Grid (ray groups of 256, kEmitSplit): each workgroup loads its group's
+// offsets and writes its 1/kEmitSplit slice of the group's samples. Outputs
+// of rays with offset + count > M are skipped (reference :416).
+__global__ void __launch_bounds__(kMarchThreads)
+k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d, MarchConst k,
+             uint32_t N, uint32_t M, const float* __restrict__ nears, const float* __restrict__ noises,
+             const float* __restrict__ ts, float* __restrict__ xyzs, float* __restrict__ dirs,
+             float* __restrict__ deltas, const int32_t* __restrict__ rays) {
+    __shared__ uint32_t off[kMarchThreads + 1];
+    const uint32_t n0 = blockIdx.x * kMarchThreads;
+    const uint32_t nlast = min(N, n0 + kMarchThreads) - 1;
+    const uint32_t base = (uint32_t)rays[(size_t)n0 * 3 + 1];
+    const uint32_t end = (uint32_t)rays[(size_t)nlast * 3 + 1] + (uint32_t)rays[(size_t)nlast * 3 + 2];
+    const uint32_t n = n0 + threadIdx.x;
+    off[threadIdx.x] = n < N ? (uint32_t)rays[(size_t)n * 3 + 1] - base : end - base;
+    if (threadIdx.x == 0) off[kMarchThreads] = end - base;
+    __syncthreads();
 
-    const Ray r = load_ray(rays_o, rays_d, n);
-    const float far = fars[n];
-    float t = ray_t0(nears[n], noises[n], k);
-    float last_t = t;
-    float* xyz = xyzs + (size_t)point_index * 3;
-    float* dir = dirs + (size_t)point_index * 3;
-    float* dlt = deltas + (size_t)point_index * 2;
-    uint32_t step = 0;
-    Sample s;
-    while (t < far && step < num_steps) {
-        if (march_step(r, k, grid, t, s)) {
-            xyz[0] = s.x; xyz[1] = s.y; xyz[2] = s.z;
-            dir[0] = r.dx; dir[1] = r.dy; dir[2] = r.dz;
-            t += s.dt;
-            dlt[0] = s.dt;
-            dlt[1] = t - last_t;
-            last_t = t;
-            xyz += 3; dir += 3; dlt += 2;
-            step++;
+    const uint32_t total = end - base;
+    const uint32_t chunk = ngp_div_up(total, kEmitSplit);
+    const uint32_t j0 = blockIdx.y * chunk, j1 = min(total, j0 + chunk);
+    for (uint32_t j = j0 + threadIdx.x; j < j1; j += kMarchThreads) {
+        uint32_t lo = 0, hi = kMarchThreads;  // largest ray r with off[r] <= j
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (off[mid] <= j) lo = mid; else hi = mid;
         }
+        const uint32_t rn = n0 + lo, kk = j - off[lo];
+        if (base + off[lo + 1] > M) continue;  // whole ray dropped, like the reference
+        const float* row = ts + (size_t)rn * k.max_steps;
+        const float t = row[kk];
+        float prev;
+        if (kk == 0) {
+            prev = ray_t0(nears[rn], noises[rn], k);
+        } else {
+            const float tp = row[kk - 1];
+            prev = tp + clampf(tp * k.dt_gamma, k.dt_min, k.dt_max);
+        }
+        const float ox = rays_o[rn * 3], oy = rays_o[rn * 3 + 1], oz = rays_o[rn * 3 + 2];
+        const float dx = rays_d[rn * 3], dy = rays_d[rn * 3 + 1], dz = rays_d[rn * 3 + 2];
+        const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
+        const size_t p = (size_t)base + j;
+        xyzs[p * 3 + 0] = clampf(fmaf(t, dx, ox), -k.bound, k.bound);
+        xyzs[p * 3 + 1] = clampf(fmaf(t, dy, oy), -k.bound, k.bound);
+        xyzs[p * 3 + 2] = clampf(fmaf(t, dz, oz), -k.bound, k.bound);
+        dirs[p * 3 + 0] = dx;
+        dirs[p * 3 + 1] = dy;
+        dirs[p * 3 + 2] = dz;
+        deltas[p * 2 + 0] = dt;
+        deltas[p * 2 + 1] = (t + dt) - prev;
     }
+}
+
+OccLayout occ_layout(const uint8_t* grid, uint32_t C, uint32_t H) {
+    OccLayout L{};
+    const size_t nbytes = (size_t)C * H * H * H / 8;
+    L.nbytes = (uint32_t)nbytes;
+    L.nwords = (uint32_t)((nbytes + 31) / 32);
+    L.ngroups = (L.nwords + 3) / 4;
+    const size_t dir_bytes = (size_t)L.ngroups * 20;
+    // LDS image only when the directory leaves room for bytes and the bitfield
+    // can be read with 16-byte loads; otherwise every lookup goes to HBM/L2.
+    if ((reinterpret_cast<uintptr_t>(grid) & 15) != 0 || dir_bytes + 4096 > kMarchLdsBytes) {
+        L.ngroups = 0;
+        return L;
+    }
+    L.cap = (uint32_t)(kMarchLdsBytes - dir_bytes);
+    return L;
+}
+
+// bytes of the global occupancy image (0 when the LDS path is off)
+size_t occ_image_bytes(const OccLayout& L) {
+    return L.ngroups ? ((16 + (size_t)L.ngroups * 20 + L.nbytes + 15) / 16) * 16 : 0;
 }
 
 __global__ void __launch_bounds__(128)
@@ -451,8 +809,9 @@ k_march_rays(uint32_t n_alive, uint32_t n_step, const int32_t* __restrict__ rays
     float last_t = t;
     uint32_t step = 0;
     Sample s;
+    const OccGlobal occ{grid};
     while (t < far && step < n_step) {
-        if (march_step(r, k, grid, t, s)) {
+        if (march_step<false>(r, k, occ, t, s)) {
             xyz[0] = s.x; xyz[1] = s.y; xyz[2] = s.z;
             dir[0] = r.dx; dir[1] = r.dy; dir[2] = r.dz;
             t += s.dt;
@@ -548,22 +907,46 @@ extern "C" int ngp_packbits(const float* grid, uint32_t N, float density_thresh,
     return ngp_check_launch("packbits");
 }
 
+// workspace = [t scratch: N * max_steps floats][occupancy image]
+static size_t march_ts_bytes(uint32_t N, uint32_t max_steps) {
+    return ((size_t)N * max_steps * sizeof(float) + 255) / 256 * 256;
+}
+
+extern "C" size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_steps, uint32_t C,
+                                                        uint32_t H) {
+    // the image size does not depend on the grid pointer's alignment
+    OccLayout L = occ_layout(nullptr, C, H);
+    return march_ts_bytes(N, max_steps) + occ_image_bytes(L);
+}
+
 extern "C" int ngp_march_rays_train(const float* rays_o, const float* rays_d, const uint8_t* grid,
                                     float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
                                     uint32_t C, uint32_t H, uint32_t M, const float* nears,
                                     const float* fars, float* xyzs, float* dirs, float* deltas,
                                     int32_t* rays, int32_t* counter, const float* noises,
-                                    void* stream) {
+                                    void* workspace, size_t workspace_bytes, void* stream) {
     if (int e = check_cascade(C, H, max_steps)) return e;
     NGP_REQUIRE(rays && counter, NGP_ERR_ARG, "march_rays_train: null rays/counter");
     if (N == 0) return NGP_OK;
+    const size_t need = ngp_march_rays_train_workspace_bytes(N, max_steps, C, H);
+    NGP_REQUIRE(workspace && workspace_bytes >= need, NGP_ERR_ARG,
+                "march_rays_train: workspace of %zu bytes required, got %zu", need, workspace_bytes);
+    NGP_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, NGP_ERR_ARG,
+                "march_rays_train: workspace must be 16-byte aligned");
     const MarchConst k = make_march_const(bound, dt_gamma, max_steps, C, H);
+    const OccLayout L = occ_layout(grid, C, H);
     hipStream_t st = ngp_stream(stream);
-    const uint32_t nb = ngp_div_up(N, kMarchBlock);
-    k_march_count<<<nb, kMarchBlock, 0, st>>>(rays_o, rays_d, grid, k, N, nears, fars, noises, rays);
-    k_march_scan<<<1, 1024, 0, st>>>(rays, nb, N, counter);
-    k_march_write<<<nb, kMarchBlock, 0, st>>>(rays_o, rays_d, grid, k, N, M, nears, fars, noises,
-                                              xyzs, dirs, deltas, rays);
+    const uint32_t groups = ngp_div_up(N, kMarchThreads);
+    const uint32_t wgs = ngp_div_up(N, kSegWaves);
+    const uint32_t blocks = wgs < kMaxMarchBlocks ? wgs : kMaxMarchBlocks;
+    float* ts = static_cast<float*>(workspace);
+    uint8_t* img = static_cast<uint8_t*>(workspace) + march_ts_bytes(N, max_steps);
+    if (L.ngroups) k_occ_build<<<1, kBuildThreads, 0, st>>>(grid, L, img);
+    k_march_train<<<blocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
+        rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts);
+    k_march_scan<<<1, 1024, 0, st>>>(rays, N, counter);
+    k_march_emit<<<dim3(groups, kEmitSplit), kMarchThreads, 0, st>>>(rays_o, rays_d, k, N, M, nears, noises,
+                                                                    ts, xyzs, dirs, deltas, rays);
     return ngp_check_launch("march_rays_train");
 }
 

@@ -66,10 +66,15 @@ def march_rays_train(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, 
     nat.check_tensor(grid, "grid", _U8, "uint8")
     _i(rays, "rays")
     _i(counter, "counter")
+    # per-sample t scratch of the single marching pass (caching allocator:
+    # reused across steps and hipGraph-capture safe)
+    ws_bytes = nat.lib().ngp_march_rays_train_workspace_bytes(N, max_steps, C, H)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=rays_o.device)
     nat.check(nat.lib().ngp_march_rays_train(
         nat.ptr(rays_o), nat.ptr(rays_d), nat.ptr(grid), float(bound), float(dt_gamma), max_steps,
         N, C, H, M, nat.ptr(nears), nat.ptr(fars), nat.ptr(xyzs), nat.ptr(dirs), nat.ptr(deltas),
-        nat.ptr(rays), nat.ptr(counter), nat.ptr(noises), nat.stream_of(rays_o)), "march_rays_train")
+        nat.ptr(rays), nat.ptr(counter), nat.ptr(noises), nat.ptr(ws), ws.numel(),
+        nat.stream_of(rays_o)), "march_rays_train")
 
 
 def composite_rays_train_forward(sigmas, rgbs, deltas, rays, M, N, T_thresh, weights_sum, depth, image):
