@@ -101,7 +101,7 @@ struct OccGlobal {
 };
 
 // LDS-resident rank/select image of the bitfield (built per workgroup by
-// k_occ_build, copied in by load_occ_index). Because Morton order interleaves the coordinate bits,
+// k_occ_count/k_occ_compact, copied in by load_occ_index). Because Morton order interleaves the coordinate bits,
 // bitfield byte b holds exactly the 2x2x2 cells of coarse cell b, so:
 //   sum[w]   bit i  = (grid byte 32w+i != 0)          (coarse occupancy, 1 bit/byte)
 //   pre[g]          = non-zero bytes before word 4g   (rank directory)
@@ -349,53 +349,64 @@ NGP_DEV uint32_t nonzero_bytes(const uint32_t (&d)[8]) {
     return m;
 }
 
-// One workgroup of 1024: summary words, rank directory and compacted
-// non-zero bytes of the bitfield, in rounds of 2 groups (256 B) per thread
-// with every load of a round in flight together.
-constexpr uint32_t kBuildThreads = 1024;
-constexpr uint32_t kBuildGroups = 2;
+// Two kernels build the image, 256 groups (32 KB of bitfield) per workgroup:
+//   k_occ_count    summary words + per-group counts (count scratch after the image)
+//   k_occ_compact  base = counts of all earlier groups (each workgroup sums
+//                  them itself: a few thousand L2 reads), in-workgroup scan ->
+//                  rank directory, then the non-zero bytes written in order
+constexpr uint32_t kBuildThreads = 256;
 __global__ void __launch_bounds__(kBuildThreads)
-k_occ_build(const uint8_t* __restrict__ grid, OccLayout L, uint8_t* __restrict__ img) {
+k_occ_count(const uint8_t* __restrict__ grid, OccLayout L, uint8_t* __restrict__ img,
+            uint32_t* __restrict__ cnt) {
+    const uint32_t g = blockIdx.x * kBuildThreads + threadIdx.x;
+    if (g >= L.ngroups) return;
+    uint32_t d[4][8];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) load_word32(grid, 4 * g + i, L.nbytes, d[i]);
+    uint32_t c = 0;
+    uint4 m;
+    m.x = nonzero_bytes(d[0]);
+    m.y = nonzero_bytes(d[1]);
+    m.z = nonzero_bytes(d[2]);
+    m.w = nonzero_bytes(d[3]);
+    reinterpret_cast<uint4*>(occ_sum(img))[g] = m;
+    c = __popc(m.x) + __popc(m.y) + __popc(m.z) + __popc(m.w);
+    cnt[g] = c;
+}
+
+__global__ void __launch_bounds__(kBuildThreads)
+k_occ_compact(const uint8_t* __restrict__ grid, OccLayout L, uint8_t* __restrict__ img,
+              const uint32_t* __restrict__ cnt) {
     __shared__ uint32_t lds_waves[kBuildThreads / 64];
-    uint32_t* sum = occ_sum(img);
-    uint32_t* pre = sum + 4 * L.ngroups;
+    const uint32_t g0 = blockIdx.x * kBuildThreads;
+    uint32_t part = 0;
+    for (uint32_t g = threadIdx.x; g < g0; g += kBuildThreads) part += cnt[g];
+    uint32_t base;
+    block_exclusive_scan<kBuildThreads>(part, lds_waves, base);  // base = sum of all earlier groups
+    const uint32_t g = g0 + threadIdx.x;
+    const uint32_t c = g < L.ngroups ? cnt[g] : 0u;
+    uint32_t total;
+    uint32_t pos = base + block_exclusive_scan<kBuildThreads>(c, lds_waves, total);
+    uint32_t* pre = occ_sum(img) + 4 * L.ngroups;
     uint8_t* bytes = reinterpret_cast<uint8_t*>(pre + L.ngroups);
-    uint32_t carry = 0;
-    for (uint32_t gb = 0; gb < L.ngroups; gb += kBuildThreads * kBuildGroups) {
-        const uint32_t g0 = gb + threadIdx.x * kBuildGroups;
-        uint32_t d[kBuildGroups * 4][8];
-        uint32_t m[kBuildGroups * 4];
-        uint32_t cnt = 0;
+    if (g < L.ngroups) {
+        pre[g] = pos;
+        if (c) {
 #pragma unroll
-        for (uint32_t i = 0; i < kBuildGroups * 4; ++i) {
-            if (4 * g0 + i < 4 * L.ngroups) {
-                load_word32(grid, 4 * g0 + i, L.nbytes, d[i]);
-            } else {
+            for (uint32_t i = 0; i < 4; ++i) {
+                uint32_t d[8];
+                load_word32(grid, 4 * g + i, L.nbytes, d);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) d[i][j] = 0;
+                for (int q = 0; q < 8; ++q)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t v = (d[q] >> (8 * j)) & 0xffu;
+                        if (v) bytes[pos++] = (uint8_t)v;
+                    }
             }
         }
-#pragma unroll
-        for (uint32_t i = 0; i < kBuildGroups * 4; ++i) {
-            m[i] = nonzero_bytes(d[i]);
-            if (4 * g0 + i < 4 * L.ngroups) sum[4 * g0 + i] = m[i];
-            cnt += __popc(m[i]);
-        }
-        uint32_t total;
-        uint32_t pos = carry + block_exclusive_scan<kBuildThreads>(cnt, lds_waves, total);
-#pragma unroll
-        for (uint32_t i = 0; i < kBuildGroups * 4; ++i) {
-            if (i % 4 == 0 && g0 + i / 4 < L.ngroups) pre[g0 + i / 4] = pos;
-            uint32_t mm = m[i];
-            while (mm) {
-                const uint32_t b = __ffs(mm) - 1;
-                bytes[pos++] = (uint8_t)(d[i][b >> 2] >> (8 * (b & 3)));
-                mm &= mm - 1;
-            }
-        }
-        carry += total;
     }
-    if (threadIdx.x == 0) reinterpret_cast<uint32_t*>(img)[0] = carry;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) reinterpret_cast<uint32_t*>(img)[0] = base + total;
 }
 
 // Copies the global image into this workgroup's LDS when its bytes fit.
@@ -697,6 +708,8 @@ OccLayout occ_layout(const uint8_t* grid, uint32_t C, uint32_t H) {
 size_t occ_image_bytes(const OccLayout& L) {
     return L.ngroups ? ((16 + (size_t)L.ngroups * 20 + L.nbytes + 15) / 16) * 16 : 0;
 }
+// per-group count scratch of the build, after the image
+size_t occ_scratch_bytes(const OccLayout& L) { return (size_t)L.ngroups * 4; }
 
 __global__ void __launch_bounds__(128)
 k_composite_train_fwd(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
@@ -916,7 +929,7 @@ extern "C" size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_
                                                         uint32_t H) {
     // the image size does not depend on the grid pointer's alignment
     OccLayout L = occ_layout(nullptr, C, H);
-    return march_ts_bytes(N, max_steps) + occ_image_bytes(L);
+    return march_ts_bytes(N, max_steps) + occ_image_bytes(L) + occ_scratch_bytes(L);
 }
 
 extern "C" int ngp_march_rays_train(const float* rays_o, const float* rays_d, const uint8_t* grid,
@@ -941,7 +954,12 @@ extern "C" int ngp_march_rays_train(const float* rays_o, const float* rays_d, co
     const uint32_t blocks = wgs < kMaxMarchBlocks ? wgs : kMaxMarchBlocks;
     float* ts = static_cast<float*>(workspace);
     uint8_t* img = static_cast<uint8_t*>(workspace) + march_ts_bytes(N, max_steps);
-    if (L.ngroups) k_occ_build<<<1, kBuildThreads, 0, st>>>(grid, L, img);
+    if (L.ngroups) {
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(img + occ_image_bytes(L));
+        const uint32_t wg = ngp_div_up(L.ngroups, kBuildThreads);
+        k_occ_count<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
+        k_occ_compact<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
+    }
     k_march_train<<<blocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
         rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts);
     k_march_scan<<<1, 1024, 0, st>>>(rays, N, counter);
