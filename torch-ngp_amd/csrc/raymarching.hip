@@ -711,56 +711,82 @@ size_t occ_image_bytes(const OccLayout& L) {
 // per-group count scratch of the build, after the image
 size_t occ_scratch_bytes(const OccLayout& L) { return (size_t)L.ngroups * 4; }
 
-__global__ void __launch_bounds__(128)
+// ---- composite_rays_train (one WAVE per ray) ------------------------------------
+// The compositing recurrence (T, rgb, depth, weight sum) is sequential per ray
+// and must stay in sample order to match the reference bit for bit. One lane
+// per ray left 64 waves for 4096 rays, each stalling on every sample's loads.
+// Here a wave owns a ray: lanes load 64 samples at once (coalesced) and
+// compute their alphas in parallel; the recurrence then runs wave-uniform over
+// readlane'd operands, and (backward) each lane keeps the running state of
+// "its" sample so the per-sample gradients are computed and stored in parallel.
+constexpr uint32_t kCompWaves = 4;
+
+NGP_DEV float lanef(float v, uint32_t j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)j));
+}
+
+__global__ void __launch_bounds__(kCompWaves * 64)
 k_composite_train_fwd(const float* __restrict__ sigmas, const float* __restrict__ rgbs,
                       const float* __restrict__ deltas, const int32_t* __restrict__ rays,
                       uint32_t M, uint32_t N, float T_thresh, float* weights_sum, float* depth,
                       float* image) {
-    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t n = blockIdx.x * kCompWaves + (threadIdx.x >> 6);
     if (n >= N) return;
     const uint32_t index = (uint32_t)rays[n * 3];
     const uint32_t offset = (uint32_t)rays[n * 3 + 1];
     const uint32_t num_steps = (uint32_t)rays[n * 3 + 2];
-    if (num_steps == 0 || offset + num_steps > M) {
-        weights_sum[index] = 0;
-        depth[index] = 0;
-        image[index * 3] = 0;
-        image[index * 3 + 1] = 0;
-        image[index * 3 + 2] = 0;
-        return;
-    }
-    const float* sg = sigmas + offset;
-    const float* cl = rgbs + (size_t)offset * 3;
-    const float* dl = deltas + (size_t)offset * 2;
     float T = 1.0f;
     float r = 0, g = 0, b = 0, ws = 0, t = 0, d = 0;
-    for (uint32_t step = 0; step < num_steps; ++step) {
-        const float alpha = 1.0f - expf(-sg[step] * dl[step * 2]);
-        const float weight = alpha * T;
-        r = fmaf(weight, cl[step * 3 + 0], r);
-        g = fmaf(weight, cl[step * 3 + 1], g);
-        b = fmaf(weight, cl[step * 3 + 2], b);
-        t += dl[step * 2 + 1];
-        d = fmaf(weight, t, d);
-        ws += weight;
-        T *= 1.0f - alpha;
-        if (T < T_thresh) break;
+    if (num_steps != 0 && offset + num_steps <= M) {
+        for (uint32_t base = 0; base < num_steps; base += 64) {
+            const uint32_t i = offset + base + lane;
+            const bool valid = base + lane < num_steps;
+            const float sg = valid ? sigmas[i] : 0.0f;
+            const float d0 = valid ? deltas[(size_t)i * 2] : 0.0f;
+            const float d1 = valid ? deltas[(size_t)i * 2 + 1] : 0.0f;
+            const float c0 = valid ? rgbs[(size_t)i * 3 + 0] : 0.0f;
+            const float c1 = valid ? rgbs[(size_t)i * 3 + 1] : 0.0f;
+            const float c2 = valid ? rgbs[(size_t)i * 3 + 2] : 0.0f;
+            const float alpha = 1.0f - expf(-sg * d0);
+            const uint32_t cnt = min(64u, num_steps - base);
+            bool stop = false;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const float a = lanef(alpha, j);
+                const float weight = a * T;
+                r = fmaf(weight, lanef(c0, j), r);
+                g = fmaf(weight, lanef(c1, j), g);
+                b = fmaf(weight, lanef(c2, j), b);
+                t += lanef(d1, j);
+                d = fmaf(weight, t, d);
+                ws += weight;
+                T *= 1.0f - a;
+                if (T < T_thresh) {
+                    stop = true;
+                    break;
+                }
+            }
+            if (stop) break;
+        }
     }
-    weights_sum[index] = ws;
-    depth[index] = d;
-    image[index * 3] = r;
-    image[index * 3 + 1] = g;
-    image[index * 3 + 2] = b;
+    if (lane == 0) {
+        weights_sum[index] = ws;
+        depth[index] = d;
+        image[index * 3] = r;
+        image[index * 3 + 1] = g;
+        image[index * 3 + 2] = b;
+    }
 }
 
-__global__ void __launch_bounds__(128)
+__global__ void __launch_bounds__(kCompWaves * 64)
 k_composite_train_bwd(const float* __restrict__ grad_weights_sum, const float* __restrict__ grad_depth,
                       const float* __restrict__ grad_image, const float* __restrict__ sigmas,
                       const float* __restrict__ rgbs, const float* __restrict__ deltas,
                       const int32_t* __restrict__ rays, const float* __restrict__ weights_sum,
                       const float* __restrict__ depth, const float* __restrict__ image, uint32_t M,
                       uint32_t N, float T_thresh, float* grad_sigmas, float* grad_rgbs) {
-    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t n = blockIdx.x * kCompWaves + (threadIdx.x >> 6);
     if (n >= N) return;
     const uint32_t index = (uint32_t)rays[n * 3];
     const uint32_t offset = (uint32_t)rays[n * 3 + 1];
@@ -771,34 +797,51 @@ k_composite_train_bwd(const float* __restrict__ grad_weights_sum, const float* _
     const float gr = grad_image[index * 3], gg = grad_image[index * 3 + 1], gb = grad_image[index * 3 + 2];
     const float r_final = image[index * 3], g_final = image[index * 3 + 1], b_final = image[index * 3 + 2];
     const float ws_final = weights_sum[index], d_final = depth[index];
-    const float* sg = sigmas + offset;
-    const float* cl = rgbs + (size_t)offset * 3;
-    const float* dl = deltas + (size_t)offset * 2;
-    float* gs = grad_sigmas + offset;
-    float* gc = grad_rgbs + (size_t)offset * 3;
 
     float T = 1.0f;
     float r = 0, g = 0, b = 0, t = 0, d = 0;
-    for (uint32_t step = 0; step < num_steps; ++step) {
-        const float c0 = cl[step * 3 + 0], c1 = cl[step * 3 + 1], c2 = cl[step * 3 + 2];
-        const float d0 = dl[step * 2];
-        const float alpha = 1.0f - expf(-sg[step] * d0);
-        const float weight = alpha * T;
-        r = fmaf(weight, c0, r);
-        g = fmaf(weight, c1, g);
-        b = fmaf(weight, c2, b);
-        t += dl[step * 2 + 1];
-        d = fmaf(weight, t, d);
-        T *= 1.0f - alpha;
-        gc[step * 3 + 0] = gr * weight;
-        gc[step * 3 + 1] = gg * weight;
-        gc[step * 3 + 2] = gb * weight;
-        gs[step] = d0 * (gr * (T * c0 - (r_final - r)) +
-                         gg * (T * c1 - (g_final - g)) +
-                         gb * (T * c2 - (b_final - b)) +
-                         gd * (T * t - (d_final - d)) +
-                         gws * (1 - ws_final));
-        if (T < T_thresh) break;
+    for (uint32_t base = 0; base < num_steps; base += 64) {
+        const uint32_t i = offset + base + lane;
+        const bool valid = base + lane < num_steps;
+        const float sg = valid ? sigmas[i] : 0.0f;
+        const float d0 = valid ? deltas[(size_t)i * 2] : 0.0f;
+        const float d1 = valid ? deltas[(size_t)i * 2 + 1] : 0.0f;
+        const float c0 = valid ? rgbs[(size_t)i * 3 + 0] : 0.0f;
+        const float c1 = valid ? rgbs[(size_t)i * 3 + 1] : 0.0f;
+        const float c2 = valid ? rgbs[(size_t)i * 3 + 2] : 0.0f;
+        const float alpha = 1.0f - expf(-sg * d0);
+        const uint32_t cnt = min(64u, num_steps - base);
+        // running state after this lane's sample
+        float mw = 0, mT = 0, mr = 0, mg = 0, mb = 0, mt = 0, md = 0;
+        uint32_t done = cnt;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const float a = lanef(alpha, j);
+            const float weight = a * T;
+            r = fmaf(weight, lanef(c0, j), r);
+            g = fmaf(weight, lanef(c1, j), g);
+            b = fmaf(weight, lanef(c2, j), b);
+            t += lanef(d1, j);
+            d = fmaf(weight, t, d);
+            T *= 1.0f - a;
+            if (lane == j) {
+                mw = weight; mT = T; mr = r; mg = g; mb = b; mt = t; md = d;
+            }
+            if (T < T_thresh) {
+                done = j + 1;
+                break;
+            }
+        }
+        if (lane < done) {
+            grad_rgbs[(size_t)i * 3 + 0] = gr * mw;
+            grad_rgbs[(size_t)i * 3 + 1] = gg * mw;
+            grad_rgbs[(size_t)i * 3 + 2] = gb * mw;
+            grad_sigmas[i] = d0 * (gr * (mT * c0 - (r_final - mr)) +
+                                   gg * (mT * c1 - (g_final - mg)) +
+                                   gb * (mT * c2 - (b_final - mb)) +
+                                   gd * (mT * mt - (d_final - md)) +
+                                   gws * (1 - ws_final));
+        }
+        if (done < cnt || T < T_thresh) break;
     }
 }
 
@@ -974,7 +1017,7 @@ extern "C" int ngp_composite_rays_train_forward(const float* sigmas, const float
                                                 float* weights_sum, float* depth, float* image,
                                                 void* stream) {
     if (N == 0) return NGP_OK;
-    k_composite_train_fwd<<<ngp_div_up(N, 128), 128, 0, ngp_stream(stream)>>>(
+    k_composite_train_fwd<<<ngp_div_up(N, kCompWaves), kCompWaves * 64, 0, ngp_stream(stream)>>>(
         sigmas, rgbs, deltas, rays, M, N, T_thresh, weights_sum, depth, image);
     return ngp_check_launch("composite_rays_train_forward");
 }
@@ -988,7 +1031,7 @@ extern "C" int ngp_composite_rays_train_backward(const float* grad_weights_sum,
                                                  float T_thresh, float* grad_sigmas,
                                                  float* grad_rgbs, void* stream) {
     if (N == 0) return NGP_OK;
-    k_composite_train_bwd<<<ngp_div_up(N, 128), 128, 0, ngp_stream(stream)>>>(
+    k_composite_train_bwd<<<ngp_div_up(N, kCompWaves), kCompWaves * 64, 0, ngp_stream(stream)>>>(
         grad_weights_sum, grad_depth, grad_image, sigmas, rgbs, deltas, rays, weights_sum, depth,
         image, M, N, T_thresh, grad_sigmas, grad_rgbs);
     return ngp_check_launch("composite_rays_train_backward");
