@@ -6,6 +6,9 @@
 One step = sample 4096 rays of a random training pose -> near/far ->
 march_rays_train -> hash-grid encode -> sigma FFMLP -> trunc_exp -> SH ->
 colour FFMLP -> composite -> MSE -> full backward -> Adam.
+--engine fused (default): nerf/fused.py, the step as ~22 fused launches in
+one hipGraph; --engine autograd: nerf/train.py, the same step through the
+reference-API autograd Functions (torch glue ops between them).
 The density bitfield is the analytic Lego-like fixture (density-grid update
 excluded from the timed step as SURVEY §8(d) defines it; its cost is reported
 separately as `density_update_ms`). Rank 0 prints ONE JSON line.
@@ -42,6 +45,8 @@ def parse():
     ap.add_argument("--kernel-steps", type=int, default=10, help="instrumented steps for kernel timing")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
+    ap.add_argument("--engine", choices=["fused", "autograd"], default="fused")
+    ap.add_argument("--profile-reps", type=int, default=20, help="back-to-back launches per kernel timing")
     return ap.parse_args()
 
 
@@ -90,12 +95,8 @@ def main():
     torch.manual_seed(1234 + rank)
     np.random.seed(rank)
 
-    import gridencoder.backend as gb
-    import ffmlp.backend as fb
-    import raymarching.backend as rb
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield
-    from nerf.train import Trainer
 
     model = NeRFNetwork(bound=1, cuda_ray=True, density_thresh=10).to(dev)
     if world > 1:  # identical initial parameters on every rank
@@ -104,6 +105,27 @@ def main():
     bits = torch.from_numpy(lego_bitfield()).to(dev)
     model.density_bitfield.copy_(bits)
     data = SyntheticLego(dev, num_rays=args.num_rays)
+    if args.engine == "fused":
+        result = run_fused(args, model, data, bits, world, dev)
+    else:
+        result = run_autograd(args, model, data, bits, world, dev)
+
+    if rank == 0 and world == 1 and args.cpu:
+        result["cpu_baseline"] = cpu_baseline(model, data, args)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_autograd(args, model, data, bits, world, dev):
+    """The step through the reference-API autograd Functions (nerf/train.py)."""
+    import gridencoder.backend as gb
+    import ffmlp.backend as fb
+    import raymarching.backend as rb
+    from nerf.train import Trainer
+
     trainer = Trainer(model, data, lr=1e-2, iters=30000, fp16=True, update_density=False,
                       distributed=world > 1)
 
@@ -242,13 +264,174 @@ def main():
         "loss": float(loss.float().item()),
     }
 
-    if rank == 0 and world == 1 and args.cpu:
-        result["cpu_baseline"] = cpu_baseline(model, data, args)
+    result["config"]["engine"] = "autograd"
+    return result
 
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+
+def kernel_profile(ft, reps):
+    """Average device time per launch of the fused step's main kernels: each
+    is launched `reps` times back to back between two HIP events on the
+    stream it runs on, with the buffers of the last step (the launch queue
+    stays ahead of the GPU, so host gaps do not count)."""
+    import _ngp_native as nat
+    lib, P = nat.lib(), nat.ptr
+    m, e = ft.model, ft.enc
+    s = nat.stream_of(ft.rays_o)
+    M, N, cnt = ft.M, ft.N, P(ft.counter)
+    ga = (e.input_dim, e.level_dim, e.num_levels, ft.S, e.base_resolution, e.gridtype_id,
+          int(e.align_corners), e.interp_id, s)
+    sn, cn = ft.sig_net, ft.col_net
+    calls = {
+        "grid_encode_backward": lambda: lib.ngp_grid_encode_backward_fused(
+            P(ft.g_enc), P(ft.xyzs), float(m.bound), P(e.offsets), P(ft.grads[0]), M, cnt, *ga),
+        "grid_encode_forward": lambda: lib.ngp_grid_encode_forward_fused(
+            P(ft.xyzs), float(m.bound), P(e.embeddings), P(e.offsets), P(ft.enc_out), M, cnt, *ga),
+        "march_rays_train": lambda: lib.ngp_march_rays_train(
+            P(ft.rays_o), P(ft.rays_d), P(m.density_bitfield), float(m.bound), ft.dt_gamma, ft.max_steps, N,
+            m.cascade, m.grid_size, M, P(ft.nears), P(ft.fars), P(ft.xyzs), P(ft.dirs), P(ft.deltas),
+            P(ft.rays), P(ft.march_cnt_scratch), P(ft.noises), P(ft.march_ws), ft.march_ws.numel(), s),
+        "ffmlp_forward_sigma": lambda: lib.ngp_ffmlp_forward_rows(
+            P(ft.enc_out), P(ft.w_half[1]), M, cnt, 32, 16, sn.hidden_dim, sn.num_layers, 0, 6, P(ft.h_sigma), s),
+        "ffmlp_forward_color": lambda: lib.ngp_ffmlp_forward_rows(
+            P(ft.color_in), P(ft.w_half[2]), M, cnt, 32, 16, cn.hidden_dim, cn.num_layers, 0, 6, P(ft.color_out), s),
+        "ffmlp_backward_sigma": lambda: lib.ngp_ffmlp_backward_rows(
+            P(ft.g_h), P(ft.enc_out), P(ft.w_half[1]), M, cnt, 32, 16, sn.hidden_dim, sn.num_layers, 0,
+            P(ft.g_enc), P(ft.grads[1]), 1, P(ft.mlp_ws[0]), ft.mlp_ws[0].numel(), s),
+        "ffmlp_backward_color": lambda: lib.ngp_ffmlp_backward_rows(
+            P(ft.g_color_out), P(ft.color_in), P(ft.w_half[2]), M, cnt, 32, 16, cn.hidden_dim, cn.num_layers,
+            0, P(ft.g_color_in), P(ft.grads[2]), 1, P(ft.mlp_ws[1]), ft.mlp_ws[1].numel(), s),
+        "composite_loss": lambda: lib.ngp_nerf_composite_loss(
+            P(ft.sigma), P(ft.color_out), P(ft.h_sigma), P(ft.deltas), P(ft.rays), M, N, ft.T_thresh,
+            float(m.density_scale), P(ft.rgba), 4, P(ft.bg), P(ft.scratch_state), P(ft.g_color_out),
+            P(ft.g_h), None, None, s),
+    }
+    out = {}
+    for name, fn in calls.items():
+        nat.check(fn(), name)
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(reps):
+            fn()
+        end.record()
+        end.synchronize()
+        out[name] = start.elapsed_time(end) / reps
+    return out
+
+
+def run_fused(args, model, data, bits, world, dev):
+    from nerf.fused import FusedTrainer
+
+    # sample-buffer size: measured counts x 1.25 (mean_count, update_extra_state)
+    probe = FusedTrainer(model, data, M=args.num_rays * 64, distributed=world > 1)
+    counts = []
+    for _ in range(4):
+        probe.step()
+        counts.append(probe.sample_count())
+    mean_count = int(np.mean(counts) * 1.25)
     if world > 1:
-        dist.destroy_process_group()
+        t = torch.tensor([mean_count], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        mean_count = int(t.item())
+    del probe
+    torch.cuda.empty_cache()
+    ft = FusedTrainer(model, data, M=mean_count, distributed=world > 1)
+    for _ in range(max(1, args.warmup)):
+        ft.step()
+    used_graph = False
+    if args.graph:
+        try:
+            ft.capture()
+            for _ in range(3):
+                ft.step()
+            used_graph = True
+        except Exception as e:  # eager launches are the same kernels; record why
+            print(f"[bench] graph capture failed, running eager: {e!r}", file=sys.stderr)
+            ft.graph = ft.graph_opt = None
+    torch.cuda.synchronize()
+
+    # ---------------- timed region ----------------
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ft.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = args.num_rays * world * args.steps / elapsed
+    samples = model.step_counter[:, 0].float()
+    samples_per_step = int(samples[samples > 0].mean().item()) if (samples > 0).any() else 0
+    loss = ft.last_loss
+
+    # ---------------- per-kernel device time (roofline) ----------------
+    ft.march_cnt_scratch = torch.zeros(2, dtype=torch.int32, device=dev)
+    ft.scratch_state = ft.state.clone()
+    kernel_ms = kernel_profile(ft, args.profile_reps)
+    rows = min(ft.sample_count(), ft.M)
+    grid_fwd_bytes, grid_bwd_bytes = 588 * rows, 1100 * rows  # SURVEY §8(d), per sample
+    dominant = max(("grid_encode_backward", "grid_encode_forward"), key=lambda k: kernel_ms[k])
+    dom_bytes = grid_bwd_bytes if dominant == "grid_encode_backward" else grid_fwd_bytes
+    achieved = dom_bytes / (kernel_ms[dominant] * 1e-3) / 1e9
+    mlp_ms = sum(v for k, v in kernel_ms.items() if k.startswith("ffmlp"))
+    ffmlp_flops = 110592 * rows
+
+    t = time.perf_counter()
+    with torch.autocast("cuda", dtype=torch.float16):
+        model.update_extra_state()
+    torch.cuda.synchronize()
+    density_update_ms = (time.perf_counter() - t) * 1e3
+    model.density_bitfield.copy_(bits)
+
+    return {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / PUBLISHED_V100_RAYS_PER_S, 3),
+        "dtype": "fp16",
+        "data": "synthetic",
+        "config": {
+            "workload": "lego_800x800_train_step (synthetic analytic Lego, bound 1, 1 cascade, "
+                        "128^3 bitfield fixture, hashgrid L16 C2 T2^19, FFMLP 64-wide)",
+            "num_rays_per_gpu": args.num_rays,
+            "global_batch_rays": args.num_rays * world,
+            "samples_per_step": samples_per_step,
+            "mean_count_M": mean_count,
+            "parallelism": f"dp{world}",
+            "hipgraph": used_graph,
+            "engine": "fused",
+            "baseline_ref": "V100 97 it/s x 4096 rays (readme.md:211)",
+        },
+        "roofline": {
+            "kernel": dominant,
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "algorithmic_bytes_per_launch": int(dom_bytes),
+            "avg_launch_ms": round(kernel_ms[dominant], 5),
+        },
+        "kernels_ms": {k: round(v, 5) for k, v in kernel_ms.items()},
+        "ffmlp_mfma": {"flops_per_step": ffmlp_flops, "ms": round(mlp_ms, 5),
+                        "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
+                        "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
+        "density_update_ms": round(density_update_ms, 3),
+        "loss": loss,
+    }
 
 
 def cpu_baseline(model, data, args):

@@ -197,6 +197,67 @@ int ngp_adam_step(float* params, const void* grads, int32_t grad_dtype, float* e
                   float* exp_avg_sq, size_t n, float lr, float beta1, float beta2, float eps,
                   float weight_decay, int32_t step, float grad_scale, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Fused train step (DESIGN.md "fused step"). No reference counterpart as C
+ * functions: together they replace the elementwise torch glue of one
+ * reference training iteration (nerf/utils.py train_step :453-497 with
+ * GradScaler/Adam :194-217, renderer.run_cuda :257-375, network_ff.forward
+ * :69-105, gridencoder/grid.py:61-89 casts) with fused kernels. `count`
+ * arguments are device pointers to the marcher's sample count: rows at or
+ * past it are not computed. `state` is a device StepState
+ * (ngp_fused_state_bytes). */
+int ngp_grid_encode_forward_fused(const float* xyz, float bound, const float* embeddings,
+                                  const int32_t* offsets, void* outputs, uint32_t B,
+                                  const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
+                                  uint32_t H, uint32_t gridtype, int32_t align_corners,
+                                  uint32_t interp, void* stream);
+int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
+                                   const int32_t* offsets, void* grad_embeddings, uint32_t B,
+                                   const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
+                                   uint32_t H, uint32_t gridtype, int32_t align_corners,
+                                   uint32_t interp, void* stream);
+int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, uint32_t B, const int32_t* count,
+                           uint32_t in_dim, uint32_t output_dim, uint32_t hidden_dim,
+                           uint32_t num_layers, uint32_t activation, uint32_t output_activation,
+                           void* outputs, void* stream);
+int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* weights, uint32_t B,
+                            const int32_t* count, uint32_t in_dim, uint32_t output_dim,
+                            uint32_t hidden_dim, uint32_t num_layers, uint32_t activation,
+                            void* grad_inputs, void* grad_weights, int32_t gw_dtype,
+                            void* workspace, size_t workspace_bytes, void* stream);
+size_t ngp_fused_state_bytes(void);
+int ngp_fused_state_init(void* state, float init_scale, void* stream);
+/* Synthetic Lego batch (nerf/provider.py SyntheticLego): boxes = nboxes x
+ * (lo[3], hi[3], rgb[3]); poses [n_poses, 4, 4]; intrinsics (fx, fy, cx, cy).
+ * Also zeroes counter[0..1] for the marcher. */
+int ngp_lego_rays(const float* poses, uint32_t n_poses, const float* intrinsics4, uint32_t H,
+                  uint32_t W, uint32_t N, const float* boxes, int32_t nboxes, const float* aabb6,
+                  float min_near, uint32_t seed, void* state, float* rays_o, float* rays_d,
+                  float* rgba, float* bg, float* nears, float* fars, float* noises,
+                  int32_t* counter, void* stream);
+int ngp_nerf_glue_forward(const void* h_sigma, const float* dirs, float density_scale, float* sigma,
+                          void* color_in, uint32_t B, const int32_t* count, void* stream);
+int ngp_nerf_glue_backward(const void* grad_color_in, void* grad_h_sigma, uint32_t B,
+                           const int32_t* count, void* stream);
+int ngp_nerf_composite_loss(const float* sigma, const void* color_out, const void* h_sigma,
+                            const float* deltas, const int32_t* rays, uint32_t M, uint32_t N,
+                            float T_thresh, float density_scale, const float* gt,
+                            uint32_t gt_channels, const float* bg, void* state,
+                            void* grad_color_out, void* grad_h_sigma, float* out_image,
+                            float* out_ws, void* stream);
+/* Adam (+ GradScaler inf check/unscale/update, LambdaLR 0.1^(epoch/iters))
+ * over n_tensors fp32 params with fp16 grads; half_params[k] (nullable) is
+ * refreshed with half(p) after the update; grads are zeroed when zero_grads;
+ * grads are multiplied by grad_mult as well as unscaled (data-parallel mean). */
+int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* const* grads,
+                             float* const* exp_avg, float* const* exp_avg_sq,
+                             void* const* half_params, const uint64_t* sizes, float lr, float beta1,
+                             float beta2, float eps, int32_t iters, int32_t zero_grads,
+                             float grad_mult, float growth_factor, float backoff_factor,
+                             int32_t growth_interval,
+                             int32_t scaler_enabled, uint32_t num_rays, const int32_t* counter,
+                             int32_t* step_counter, void* state, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

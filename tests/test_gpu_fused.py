@@ -1,0 +1,153 @@
+"""GPU: the fused train step (nerf/fused.py) against the autograd step.
+
+The autograd path (NeRFNetwork.render through the reference-API autograd
+Functions, torch loss, GradScaler, torch Adam) is the anchor. Both are fed the
+same batch (the fused sampler's rays / target / background, zero march noise),
+then compared stage by stage: sample counts (bit-exact), loss, gradients of
+all three parameter tensors, and the Adam update from identical gradients.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(cuda, num_rays=1024, mean_count=30000):
+    from nerf.fused import FusedTrainer
+    from nerf.network_ff import NeRFNetwork
+    from nerf.provider import SyntheticLego, lego_bitfield
+    torch.manual_seed(0)
+    model = NeRFNetwork(bound=1, cuda_ray=True, density_thresh=10).to(cuda)
+    with torch.no_grad():  # a non-trivial field: larger table values than the 1e-4 init
+        model.encoder.embeddings.normal_(0, 0.05)
+    model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(cuda))
+    ref = copy.deepcopy(model)
+    data = SyntheticLego(cuda, num_rays=num_rays)
+    M = mean_count + 128 - mean_count % 128  # what run_cuda's align=128 makes of mean_count
+    ref.mean_count = mean_count
+    ft = FusedTrainer(model, data, M=M, seed=3)
+    return model, ref, data, ft
+
+
+def _ref_forward_backward(ref, ft, scale):
+    rays_o, rays_d = ft.rays_o.clone(), ft.rays_d.clone()
+    rgba, bg = ft.rgba.clone(), ft.bg.clone()
+    ref.train()
+    with torch.autocast("cuda", dtype=torch.float16):
+        out = ref.render(rays_o[None], rays_d[None], staged=False, bg_color=bg[None], perturb=False,
+                         force_all_rays=False, dt_gamma=0.0, max_steps=1024)
+        pred = out["image"][0]
+        gt = rgba[:, :3] * rgba[:, 3:] + bg * (1 - rgba[:, 3:])
+        loss = ((pred - gt) ** 2).mean(-1).mean()
+    (loss * scale).backward()
+    return loss
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+def test_lego_sampler(cuda):
+    import raymarching
+    model, ref, data, ft = _setup(cuda)
+    ft._sample()
+    torch.cuda.synchronize()
+    n = ft.rays_d.norm(dim=-1)
+    assert torch.allclose(n, torch.ones_like(n), atol=1e-5)
+    poses_t = data.poses[:, :3, 3]
+    assert ((ft.rays_o[:1] - poses_t).abs().sum(-1) == 0).any()        # origin = a pose centre
+    assert torch.equal(ft.rays_o, ft.rays_o[:1].expand_as(ft.rays_o))  # one pose per step
+    tgt = data.target(ft.rays_o, ft.rays_d)
+    assert torch.allclose(tgt, ft.rgba, atol=1e-6)
+    assert 0.05 < float(ft.rgba[:, 3].mean()) < 0.95
+    nears, fars = raymarching.near_far_from_aabb(ft.rays_o, ft.rays_d, model.aabb_train, model.min_near)
+    assert torch.equal(nears, ft.nears) and torch.equal(fars, ft.fars)
+    assert 0.0 <= float(ft.bg.min()) and float(ft.bg.max()) < 1.0
+    assert int(ft.counter.abs().sum()) == 0
+    # a new step draws a new batch
+    r0 = ft.rays_d.clone()
+    ft._state_i()[8] += 1
+    ft._sample()
+    assert not torch.equal(r0, ft.rays_d)
+
+
+def test_fused_forward_backward_matches_autograd(cuda):
+    model, ref, data, ft = _setup(cuda)
+    ft._sample()
+    ft.noises.zero_()  # the autograd call below marches with perturb=False
+    ft._forward_backward()
+    torch.cuda.synchronize()
+    scale = ft.scale
+    loss = _ref_forward_backward(ref, ft, scale)
+    torch.cuda.synchronize()
+    # identical march (same rays, near/far, noise): same sample count
+    assert int(ft.counter[0]) == int(ref.step_counter[0, 0]) > 0
+    fused_loss = float(ft._state_f()[1].item()) / ft.N
+    lv = float(loss.detach())
+    assert abs(fused_loss - lv) <= 2e-3 * abs(lv) + 1e-7
+    names = ["embeddings", "sigma_net", "color_net"]
+    refs = [ref.encoder.embeddings.grad, ref.sigma_net.weights.grad, ref.color_net.weights.grad]
+    for name, g, r in zip(names, ft.grads, refs):
+        assert torch.isfinite(g.float()).all(), name
+        assert r.abs().max() > 0, name
+        assert _rel(g, r) < 2e-2, (name, _rel(g, r))
+
+
+def test_fused_optimizer_matches_torch_adam_and_scaler(cuda):
+    model, ref, data, ft = _setup(cuda)
+    ft._sample()
+    ft._forward_backward()
+    torch.cuda.synchronize()
+    scale = ft.scale
+    params_ref = [p.detach().clone() for p in ft.params]
+    grads16 = [g.clone() for g in ft.grads]
+    ft._optimizer()
+    torch.cuda.synchronize()
+    # torch: GradScaler(unscale) + Adam(0.9, 0.99, eps 1e-15) + LambdaLR on fp32 grads
+    ps = [torch.nn.Parameter(p.clone()) for p in params_ref]
+    for p, g in zip(ps, grads16):
+        p.grad = g.float()
+    opt = torch.optim.Adam(ps, lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+    scaler = torch.amp.GradScaler("cuda", init_scale=scale)
+    scaler.scale(torch.ones((), device=cuda))  # initialises the scaler's scale tensor
+    scaler.step(opt)
+    scaler.update()
+    for name, a, b, p0 in zip(["emb", "sigma", "color"], ft.params, ps, params_ref):
+        assert torch.allclose(a.detach(), b.detach(), rtol=1e-5, atol=1e-7), name
+        assert not torch.equal(a.detach(), p0), name  # the step moved the parameter
+    assert all(int(g.abs().sum()) == 0 for g in ft.grads)   # grads zeroed for the next step
+    assert ft.optimizer_steps == 1
+    # MLP fp16 forward copies refreshed from the fp32 masters
+    assert torch.equal(ft.w_half[1], ft.params[1].detach().half())
+    assert torch.equal(ft.w_half[2], ft.params[2].detach().half())
+
+
+def test_fused_optimizer_skips_on_inf(cuda):
+    model, ref, data, ft = _setup(cuda)
+    before = [p.detach().clone() for p in ft.params]
+    ft.grads[1][3] = float("inf")
+    s0 = ft.scale
+    ft._optimizer()
+    torch.cuda.synchronize()
+    for a, b in zip(ft.params, before):
+        assert torch.equal(a.detach(), b)
+    assert ft.scale == s0 * 0.5 and ft.optimizer_steps == 0
+    assert all(int(torch.isinf(g.float()).sum()) == 0 for g in ft.grads)
+
+
+def test_fused_training_reduces_loss_and_captures(cuda):
+    model, ref, data, ft = _setup(cuda, num_rays=4096, mean_count=100000)
+    losses = []
+    for _ in range(4):
+        ft.step()
+        losses.append(ft.last_loss)
+    ft.capture()
+    for _ in range(60):
+        ft.step()
+    torch.cuda.synchronize()
+    late = ft.last_loss
+    assert np.isfinite(late) and late < losses[0], (losses, late)
+    assert ft.optimizer_steps >= 60

@@ -60,11 +60,31 @@ SIGNATURES = {
     "ngp_ffmlp_free_splitk": [],
     "ngp_adam_step": [c_vp, c_vp, c_i32, c_vp, c_vp, c_sz, c_f32, c_f32, c_f32, c_f32, c_f32,
                       c_i32, c_f32, c_vp],
+    "ngp_grid_encode_forward_fused": [c_vp, c_f32, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
+                                      c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp],
+    "ngp_grid_encode_backward_fused": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
+                                       c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp],
+    "ngp_ffmlp_forward_rows": [c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
+                               c_vp, c_vp],
+    "ngp_ffmlp_backward_rows": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32,
+                                c_vp, c_vp, c_i32, c_vp, c_sz, c_vp],
+    "ngp_fused_state_bytes": [],
+    "ngp_fused_state_init": [c_vp, c_f32, c_vp],
+    "ngp_lego_rays": [c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32,
+                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_nerf_glue_forward": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_vp],
+    "ngp_nerf_glue_backward": [c_vp, c_vp, c_u32, c_vp, c_vp],
+    "ngp_nerf_composite_loss": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
+                                c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_fused_optimizer_step": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
+                                 c_i32, c_i32, c_f32, c_f32, c_f32, c_i32, c_i32, c_u32, c_vp, c_vp,
+                                 c_vp, c_vp],
 }
 _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
     "ngp_march_rays_train_workspace_bytes": c_sz,
+    "ngp_fused_state_bytes": c_sz,
 }
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}

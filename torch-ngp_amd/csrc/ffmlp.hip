@@ -269,8 +269,9 @@ template <int W, int IN_KS, int NH, typename FA, typename FO>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weights,
           ngp_half* __restrict__ outputs, ngp_half* __restrict__ fwd_buf, uint32_t B,
-          uint32_t in_dim, FA act, FO out_act) {
+          uint32_t in_dim, FA act, FO out_act, const int32_t* __restrict__ count) {
     using N = Net<W, IN_KS, NH>;
+    if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);  // rows past the sample count
     extern __shared__ half8 lds[];
     for (int q = 0; q < N::NMAT; ++q) build_frags(lds, weights, fwd_desc<W, IN_KS, NH>(q, in_dim), false);
     __syncthreads();
@@ -420,9 +421,11 @@ template <int W, int IN_KS, int NH, typename FA>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
           const half8* __restrict__ image, ngp_half* __restrict__ grad_inputs,
-          float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, FA act) {
+          float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, FA act,
+          const int32_t* __restrict__ count) {
     using N = Net<W, IN_KS, NH>;
     using L = BwdLds<W, IN_KS, NH>;
+    if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);  // rows past the sample count
     constexpr int LAST = N::NMAT - 1;
     extern __shared__ half8 lds[];
     const half8* fr = lds;
@@ -577,19 +580,19 @@ int check_shape(uint32_t B, uint32_t in_dim, uint32_t out_dim, uint32_t hidden, 
 
 template <int W, int IN_KS, int NH, typename FA, typename FO>
 int launch_fwd_t(const void* in, const void* w, uint32_t B, uint32_t in_dim, FA act, FO out_act,
-                 void* fwd_buf, void* out, hipStream_t st);
+                 void* fwd_buf, void* out, const int32_t* count, hipStream_t st);
 
 template <int W, int IN_KS, int NH>
 int launch_fwd(const void* in, const void* w, uint32_t B, uint32_t in_dim, uint32_t act,
-               uint32_t out_act, void* fwd_buf, void* out, hipStream_t st) {
+               uint32_t out_act, void* fwd_buf, void* out, const int32_t* count, hipStream_t st) {
     if (act == kReLU && out_act == kNone)
-        return launch_fwd_t<W, IN_KS, NH>(in, w, B, in_dim, ActReLU{}, ActNone{}, fwd_buf, out, st);
-    return launch_fwd_t<W, IN_KS, NH>(in, w, B, in_dim, ActAny{act}, ActAny{out_act}, fwd_buf, out, st);
+        return launch_fwd_t<W, IN_KS, NH>(in, w, B, in_dim, ActReLU{}, ActNone{}, fwd_buf, out, count, st);
+    return launch_fwd_t<W, IN_KS, NH>(in, w, B, in_dim, ActAny{act}, ActAny{out_act}, fwd_buf, out, count, st);
 }
 
 template <int W, int IN_KS, int NH, typename FA, typename FO>
 int launch_fwd_t(const void* in, const void* w, uint32_t B, uint32_t in_dim, FA act, FO out_act,
-                 void* fwd_buf, void* out, hipStream_t st) {
+                 void* fwd_buf, void* out, const int32_t* count, hipStream_t st) {
     using N = Net<W, IN_KS, NH>;
     const size_t lds = (size_t)N::FWD_FRAGS * 64 * 16;
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
@@ -598,7 +601,7 @@ int launch_fwd_t(const void* in, const void* w, uint32_t B, uint32_t in_dim, FA 
     if (blocks == 0) return NGP_OK;
     hipLaunchKernelGGL((k_mlp_fwd<W, IN_KS, NH, FA, FO>), dim3(blocks), dim3(kThreads), lds, st,
                        (const ngp_half*)in, (const ngp_half*)w, (ngp_half*)out, (ngp_half*)fwd_buf,
-                       B, in_dim, act, out_act);
+                       B, in_dim, act, out_act, count);
     return ngp_check_launch("ffmlp_forward");
 }
 
@@ -606,20 +609,22 @@ constexpr size_t kImageBytes = 128 * 1024;  // fragment image slot at the head o
 
 template <int W, int IN_KS, int NH, typename FA>
 int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
-                 FA act, void* grad_in, void* gw, int32_t gw_dtype, void* ws, hipStream_t st);
+                 FA act, void* grad_in, void* gw, int32_t gw_dtype, void* ws, const int32_t* count,
+                 hipStream_t st);
 
 template <int W, int IN_KS, int NH>
 int launch_bwd(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
                uint32_t act, void* grad_in, void* gw, int32_t gw_dtype, void* ws,
-               hipStream_t st) {
+               const int32_t* count, hipStream_t st) {
     if (act == kReLU)
-        return launch_bwd_t<W, IN_KS, NH>(grad, in, w, B, in_dim, ActReLU{}, grad_in, gw, gw_dtype, ws, st);
-    return launch_bwd_t<W, IN_KS, NH>(grad, in, w, B, in_dim, ActAny{act}, grad_in, gw, gw_dtype, ws, st);
+        return launch_bwd_t<W, IN_KS, NH>(grad, in, w, B, in_dim, ActReLU{}, grad_in, gw, gw_dtype, ws, count, st);
+    return launch_bwd_t<W, IN_KS, NH>(grad, in, w, B, in_dim, ActAny{act}, grad_in, gw, gw_dtype, ws, count, st);
 }
 
 template <int W, int IN_KS, int NH, typename FA>
 int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
-                 FA act, void* grad_in, void* gw, int32_t gw_dtype, void* ws, hipStream_t st) {
+                 FA act, void* grad_in, void* gw, int32_t gw_dtype, void* ws, const int32_t* count,
+                 hipStream_t st) {
     using N = Net<W, IN_KS, NH>;
     using L = BwdLds<W, IN_KS, NH>;
     static_assert(L::frag_bytes <= kImageBytes, "fragment image exceeds its workspace slot");
@@ -633,7 +638,7 @@ int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, ui
                        (const ngp_half*)w, in_dim, image);
     hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH, FA>), dim3(blocks), dim3(kThreads), L::total, st,
                        (const ngp_half*)grad, (const ngp_half*)in, (const half8*)image,
-                       (ngp_half*)grad_in, slab, np, B, in_dim, act);
+                       (ngp_half*)grad_in, slab, np, B, in_dim, act, count);
     if (gw_dtype == NGP_DTYPE_F16) {
         hipLaunchKernelGGL((k_slab_reduce<ngp_half>), dim3(ngp_div_up(np, 64)), dim3(64 * kReducePhases), 0, st,
                            (const float*)slab, blocks, np, (ngp_half*)gw);
@@ -670,7 +675,20 @@ extern "C" int ngp_ffmlp_forward(const void* inputs, const void* weights, uint32
     if (B == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
     NGP_MLP_DISPATCH(launch_fwd, inputs, weights, B, in_dim, activation, output_activation,
-                     forward_buffer, outputs, st);
+                     forward_buffer, outputs, nullptr, st);
+}
+
+/* Fused-step variant: rows at or past *count are not computed (count may be
+ * null). */
+extern "C" int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, uint32_t B,
+                                      const int32_t* count, uint32_t in_dim, uint32_t output_dim,
+                                      uint32_t hidden_dim, uint32_t num_layers, uint32_t activation,
+                                      uint32_t output_activation, void* outputs, void* stream) {
+    if (int e = check_shape(B, in_dim, output_dim, hidden_dim, num_layers)) return e;
+    if (B == 0) return NGP_OK;
+    hipStream_t st = ngp_stream(stream);
+    NGP_MLP_DISPATCH(launch_fwd, inputs, weights, B, in_dim, activation, output_activation,
+                     nullptr, outputs, count, st);
 }
 
 extern "C" int ngp_ffmlp_inference(const void* inputs, const void* weights, uint32_t B,
@@ -710,7 +728,27 @@ extern "C" int ngp_ffmlp_backward(const void* grad, const void* inputs, const vo
     hipStream_t st = ngp_stream(stream);
     void* gi = calc_grad_inputs ? grad_inputs : nullptr;
     NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, B, in_dim, activation, gi, grad_weights,
-                     gw_dtype, workspace, st);
+                     gw_dtype, workspace, nullptr, st);
+}
+
+/* Fused-step variant: rows at or past *count contribute nothing (their
+ * grad_inputs are not written). */
+extern "C" int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* weights,
+                                       uint32_t B, const int32_t* count, uint32_t in_dim,
+                                       uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,
+                                       uint32_t activation, void* grad_inputs, void* grad_weights,
+                                       int32_t gw_dtype, void* workspace, size_t workspace_bytes,
+                                       void* stream) {
+    if (int e = check_shape(B, in_dim, output_dim, hidden_dim, num_layers)) return e;
+    NGP_REQUIRE(gw_dtype == NGP_DTYPE_F16 || gw_dtype == NGP_DTYPE_F32, NGP_ERR_ARG,
+                "grad_weights must be float16 or float32");
+    if (B == 0) return NGP_OK;
+    const size_t need = ngp_ffmlp_backward_workspace_bytes(B, in_dim, output_dim, hidden_dim, num_layers);
+    NGP_REQUIRE(workspace && workspace_bytes >= need, NGP_ERR_ARG,
+                "ffmlp_backward: workspace of %zu bytes required, got %zu", need, workspace_bytes);
+    hipStream_t st = ngp_stream(stream);
+    NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, B, in_dim, activation, grad_inputs, grad_weights,
+                     gw_dtype, workspace, count, st);
 }
 
 extern "C" int ngp_ffmlp_allocate_splitk(size_t size) { (void)size; return NGP_OK; }

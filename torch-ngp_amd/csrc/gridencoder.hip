@@ -83,6 +83,30 @@ NGP_DEV void load_entry(const T* __restrict__ p, typename Acc<T>::F out[C]) {
 #pragma unroll
     for (uint32_t c = 0; c < C; ++c) out[c] = (typename Acc<T>::F)x.v[c];
 }
+// Entry stored as E, computed as T: (F)(T)e, i.e. the reference's
+// embeddings.half() applied on the fly to an fp32 table.
+template <typename T, typename E, uint32_t C>
+NGP_DEV void load_entry_as(const E* __restrict__ p, typename Acc<T>::F out[C]) {
+    struct alignas(sizeof(E) * C) V { E v[C]; };
+    V x = *reinterpret_cast<const V*>(p);
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) out[c] = (typename Acc<T>::F)(T)x.v[c];
+}
+
+// Optional input mapping of the fused train step: x = (raw + shift) * scale
+// (GridEncoder.forward's (inputs + bound) / (2 * bound), which torch evaluates
+// as a multiply by the fp32 reciprocal), and a device-side row count that
+// clips B (rows past the marcher's sample count are not touched).
+struct InMap {
+    float shift, scale;  // scale == 0: inputs are used as given
+    const int32_t* count;
+};
+NGP_DEV uint32_t rows_of(uint32_t B, const InMap& m) {
+    if (!m.count) return B;
+    const int32_t c = *m.count;
+    return c <= 0 ? 0u : min(B, (uint32_t)c);
+}
+
 template <typename T, uint32_t C>
 NGP_DEV void store_entry(T* __restrict__ p, const T in[C]) {
     struct alignas(sizeof(T) * C) V { T v[C]; };
@@ -92,16 +116,16 @@ NGP_DEV void store_entry(T* __restrict__ p, const T in[C]) {
     *reinterpret_cast<V*>(p) = x;
 }
 
-template <typename T, uint32_t D, uint32_t C>
+template <typename T, typename E, uint32_t D, uint32_t C>
 __global__ void __launch_bounds__(256)
-k_grid_fwd(const float* __restrict__ inputs, const T* __restrict__ grid,
+k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
            const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
            GridLevels lv, T* __restrict__ dy_dx, uint32_t gridtype, bool align_corners,
-           uint32_t interp, int32_t out_layout) {
+           uint32_t interp, int32_t out_layout, InMap im) {
     using A = Acc<T>;
     using F = typename A::F;
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+    if (b >= rows_of(B, im)) return;
     const uint32_t level = blockIdx.y;
 
     T* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C
@@ -112,6 +136,7 @@ k_grid_fwd(const float* __restrict__ inputs, const T* __restrict__ grid,
 #pragma unroll
     for (uint32_t d = 0; d < D; d++) {
         x[d] = inputs[(size_t)b * D + d];
+        if (im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
         if (x[d] < 0 || x[d] > 1) oob = true;
     }
     if (oob) {
@@ -130,7 +155,7 @@ k_grid_fwd(const float* __restrict__ inputs, const T* __restrict__ grid,
     const uint32_t off0 = (uint32_t)offsets[level];
     const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
     const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
-    const T* __restrict__ g = grid + (size_t)off0 * C;
+    const E* __restrict__ g = grid + (size_t)off0 * C;
     const float scale = lv.scale[level];
     const uint32_t resolution = lv.res[level];
 
@@ -168,7 +193,7 @@ k_grid_fwd(const float* __restrict__ inputs, const T* __restrict__ grid,
         }
         const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
         F v[C];
-        load_entry<T, C>(g + (size_t)e * C, v);
+        load_entry_as<T, E, C>(g + (size_t)e * C, v);
 #pragma unroll
         for (uint32_t c = 0; c < C; ++c) res[c] = A::mac(res[c], (F)w, v[c]);
     }
@@ -201,8 +226,8 @@ k_grid_fwd(const float* __restrict__ inputs, const T* __restrict__ grid,
                 pl[gd] = pg[gd] + 1;
                 const uint32_t ir = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
                 F vl[C], vr[C];
-                load_entry<T, C>(g + (size_t)il * C, vl);
-                load_entry<T, C>(g + (size_t)ir * C, vr);
+                load_entry_as<T, E, C>(g + (size_t)il * C, vl);
+                load_entry_as<T, E, C>(g + (size_t)ir * C, vr);
 #pragma unroll
                 for (uint32_t c = 0; c < C; ++c)
                     rg[c] = A::mac(rg[c], (F)w * (vr[c] - vl[c]), (F)pos_deriv[gd]);
@@ -264,18 +289,19 @@ __global__ void __launch_bounds__(256)
 k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
            const int32_t* __restrict__ offsets, T* __restrict__ grad_grid, uint32_t B, uint32_t L,
            GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
-           int32_t grad_layout) {
+           int32_t grad_layout, InMap im) {
     using A = Acc<T>;
     using F = typename A::F;
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t level = blockIdx.y;
     const int lane = (int)(threadIdx.x & 63);
 
-    bool valid = b < B;
+    bool valid = b < rows_of(B, im);
     float x[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; d++) {
         x[d] = valid ? inputs[(size_t)b * D + d] : 0.5f;
+        if (valid && im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
         if (x[d] < 0 || x[d] > 1) valid = false;  // grad is zero-initialised
     }
     if (__ballot(valid) == 0) return;  // whole wave idle (wave-uniform)
@@ -444,33 +470,34 @@ k_grid_tv(const T* __restrict__ inputs, const T* __restrict__ grid, T* __restric
 }
 
 // ---- dispatch ---------------------------------------------------------------
-template <typename T, uint32_t D>
+template <typename T, typename E, uint32_t D>
 int fwd_c(const float* inputs, const void* emb, const int32_t* offsets, void* out, uint32_t B,
           uint32_t C, uint32_t L, const GridLevels& lv, void* dy_dx, uint32_t gridtype,
-          bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+          bool ac, uint32_t interp, int32_t layout, const InMap& im, hipStream_t st) {
     const dim3 grid(ngp_div_up(B, 256), L);
-    const T* e = (const T*)emb;
+    const E* e = (const E*)emb;
     T* o = (T*)out;
     T* dd = (T*)dy_dx;
     switch (C) {
-        case 1: k_grid_fwd<T, D, 1><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout); break;
-        case 2: k_grid_fwd<T, D, 2><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout); break;
-        case 4: k_grid_fwd<T, D, 4><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout); break;
-        case 8: k_grid_fwd<T, D, 8><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout); break;
+        case 1: k_grid_fwd<T, E, D, 1><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout, im); break;
+        case 2: k_grid_fwd<T, E, D, 2><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout, im); break;
+        case 4: k_grid_fwd<T, E, D, 4><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout, im); break;
+        case 8: k_grid_fwd<T, E, D, 8><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout, im); break;
         default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: C must be 1, 2, 4, or 8.");
     }
     return ngp_check_launch("grid_encode_forward");
 }
 
-template <typename T>
+template <typename T, typename E = T>
 int fwd_t(const float* inputs, const void* emb, const int32_t* offsets, void* out, uint32_t B,
           uint32_t D, uint32_t C, uint32_t L, const GridLevels& lv, void* dy_dx,
-          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st,
+          const InMap& im = InMap{0.0f, 0.0f, nullptr}) {
     switch (D) {
-        case 2: return fwd_c<T, 2>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, st);
-        case 3: return fwd_c<T, 3>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, st);
-        case 4: return fwd_c<T, 4>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, st);
-        case 5: return fwd_c<T, 5>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, st);
+        case 2: return fwd_c<T, E, 2>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, im, st);
+        case 3: return fwd_c<T, E, 3>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, im, st);
+        case 4: return fwd_c<T, E, 4>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, im, st);
+        case 5: return fwd_c<T, E, 5>(inputs, emb, offsets, out, B, C, L, lv, dy_dx, gridtype, ac, interp, layout, im, st);
         default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: D must be 2, 3, 4, or 5.");
     }
 }
@@ -478,10 +505,11 @@ int fwd_t(const float* inputs, const void* emb, const int32_t* offsets, void* ou
 template <typename T, uint32_t D, uint32_t C>
 int bwd_one(const void* grad, const float* inputs, const int32_t* offsets, void* gemb,
             uint32_t B, uint32_t L, const GridLevels& lv, const void* dy_dx, void* grad_inputs,
-            uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+            uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st,
+            const InMap& im) {
     const dim3 grid(ngp_div_up(B, 256), L);
     k_grid_bwd<T, D, C><<<grid, 256, 0, st>>>((const T*)grad, inputs, offsets, (T*)gemb, B, L, lv,
-                                               gridtype, ac, interp, layout);
+                                               gridtype, ac, interp, layout, im);
     if (dy_dx && grad_inputs) {
         k_grid_input_bwd<T, D, C><<<ngp_div_up(B * D, 256), 256, 0, st>>>(
             (const T*)grad, (const T*)dy_dx, (T*)grad_inputs, B, L, layout);
@@ -492,12 +520,13 @@ int bwd_one(const void* grad, const float* inputs, const int32_t* offsets, void*
 template <typename T, uint32_t D>
 int bwd_c(const void* grad, const float* inputs, const int32_t* offsets, void* gemb, uint32_t B,
           uint32_t C, uint32_t L, const GridLevels& lv, const void* dy_dx, void* gi,
-          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st,
+          const InMap& im) {
     switch (C) {
-        case 1: return bwd_one<T, D, 1>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
-        case 2: return bwd_one<T, D, 2>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
-        case 4: return bwd_one<T, D, 4>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
-        case 8: return bwd_one<T, D, 8>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        case 1: return bwd_one<T, D, 1>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st, im);
+        case 2: return bwd_one<T, D, 2>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st, im);
+        case 4: return bwd_one<T, D, 4>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st, im);
+        case 8: return bwd_one<T, D, 8>(grad, inputs, offsets, gemb, B, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st, im);
         default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: C must be 1, 2, 4, or 8.");
     }
 }
@@ -505,12 +534,13 @@ int bwd_c(const void* grad, const float* inputs, const int32_t* offsets, void* g
 template <typename T>
 int bwd_t(const void* grad, const float* inputs, const int32_t* offsets, void* gemb, uint32_t B,
           uint32_t D, uint32_t C, uint32_t L, const GridLevels& lv, const void* dy_dx, void* gi,
-          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st) {
+          uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st,
+          const InMap& im = InMap{0.0f, 0.0f, nullptr}) {
     switch (D) {
-        case 2: return bwd_c<T, 2>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
-        case 3: return bwd_c<T, 3>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
-        case 4: return bwd_c<T, 4>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
-        case 5: return bwd_c<T, 5>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st);
+        case 2: return bwd_c<T, 2>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st, im);
+        case 3: return bwd_c<T, 3>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st, im);
+        case 4: return bwd_c<T, 4>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st, im);
+        case 5: return bwd_c<T, 5>(grad, inputs, offsets, gemb, B, C, L, lv, dy_dx, gi, gridtype, ac, interp, layout, st, im);
         default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: D must be 2, 3, 4, or 5.");
     }
 }
@@ -616,4 +646,39 @@ extern "C" int ngp_grad_total_variation(const void* inputs, const void* embeddin
             return ngp_set_error(NGP_ERR_UNSUPPORTED, "grad_total_variation: half embeddings are not supported (call it outside autocast, as GridEncoder.grad_total_variation does)");
         default: return ngp_set_error(NGP_ERR_ARG, "embeddings must be a floating tensor");
     }
+}
+
+/* Fused train-step entry points (DESIGN.md "fused step"): world-space inputs
+ * normalised in-kernel exactly as GridEncoder.forward does, an fp32 table
+ * read as half (the reference's embeddings.half()), fp16 [B, L*C] outputs /
+ * output grads, fp16 grad table, rows clipped at *count. */
+extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, const float* embeddings,
+                                             const int32_t* offsets, void* outputs, uint32_t B,
+                                             const int32_t* count, uint32_t D, uint32_t C, uint32_t L,
+                                             float S, uint32_t H, uint32_t gridtype,
+                                             int32_t align_corners, uint32_t interp, void* stream) {
+    if (int e = check_common(L, embeddings, offsets, outputs)) return e;
+    NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_forward_fused: null xyz or bound <= 0");
+    if (B == 0) return NGP_OK;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const InMap im{bound, 1.0f / (2.0f * bound), count};
+    return fwd_t<ngp_half, float>(xyz, embeddings, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
+                                  align_corners != 0, interp, 1, ngp_stream(stream), im);
+}
+
+extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
+                                              const int32_t* offsets, void* grad_embeddings,
+                                              uint32_t B, const int32_t* count, uint32_t D,
+                                              uint32_t C, uint32_t L, float S, uint32_t H,
+                                              uint32_t gridtype, int32_t align_corners,
+                                              uint32_t interp, void* stream) {
+    if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
+    NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_backward_fused: null xyz or bound <= 0");
+    if (B == 0) return NGP_OK;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const InMap im{bound, 1.0f / (2.0f * bound), count};
+    return bwd_t<ngp_half>(grad, xyz, offsets, grad_embeddings, B, D, C, L, lv, nullptr, nullptr,
+                           gridtype, align_corners != 0, interp, 1, ngp_stream(stream), im);
 }

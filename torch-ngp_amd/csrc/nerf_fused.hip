@@ -1,0 +1,628 @@
+// Fused NeRF train step (DESIGN.md "fused step"): the elementwise glue of the
+// reference step (nerf/utils.py train_step :453-497, renderer.run_cuda
+// :257-375, network_ff.forward :69-105, GradScaler + Adam) folded into a
+// handful of kernels around the hot-path ops, so the whole step is ~22
+// launches instead of ~150. Each kernel reproduces the reference's float
+// operations (including torch's scalar-division-as-reciprocal-multiply and
+// autocast casts) so the fused step and the autograd step agree to fp16/fp32
+// rounding (tests/test_gpu_fused.py).
+//
+//   k_lego_rays       synthetic Lego batch: pose + pixels (counter-based RNG),
+//                     rays (get_rays :52-136), analytic RGBA target, random
+//                     background, march noise, near/far (raymarching.cu:91-145)
+//   k_glue_fwd        sigma = ds * exp(h0); color_in = [half(SH4(d)) | h1..15 | 0]
+//   k_composite_loss  per ray (one wave): composite forward, background blend,
+//                     MSE, d loss / d image (AMP-scaled), composite backward,
+//                     cast/sigmoid/trunc_exp backward -> fp16 MLP-output grads
+//   k_glue_bwd        geo-feature grads (color MLP grad_inputs 16..30) -> h1..15
+//   k_nonfinite       GradScaler's inf/nan check over the fp16 grads
+//   k_adam_multi      Adam over all parameter tensors, unscaled fp16 grads,
+//                     skip on inf, device-side lr schedule; zeroes the grads
+//   k_step_end        GradScaler.update, counters, loss
+#include "ngp_common.h"
+#include "sh_basis.h"
+
+#include <cfloat>
+
+namespace {
+
+constexpr int kMaxBoxes = 8;
+constexpr int kMaxTensors = 8;
+
+NGP_DEV uint32_t clip_rows(uint32_t B, const int32_t* count) {
+    if (!count) return B;
+    const int32_t c = *count;
+    return c <= 0 ? 0u : min(B, (uint32_t)c);
+}
+
+// ---- device step state ------------------------------------------------------
+struct StepState {
+    float scale;           // GradScaler scale
+    float loss_sum;        // sum over rays of the per-ray MSE (this step)
+    float last_loss;       // mean loss of the last finished step
+    float pad;
+    int32_t growth_tracker;
+    int32_t found_inf;
+    int32_t adam_step;     // optimizer steps taken (skipped steps excluded)
+    int32_t epoch;         // LambdaLR epoch (every step)
+    int32_t iter;          // sampler counter
+    int32_t pad2[3];
+};
+
+// counter-based RNG (no state, graph-safe): 32-bit mix of (seed, a, b, c)
+NGP_DEV uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du;
+    x ^= x >> 15; x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+NGP_DEV uint32_t rng_u32(uint32_t seed, uint32_t a, uint32_t b, uint32_t c) {
+    return mix32(seed ^ mix32(a + 0x9e3779b9u * mix32(b ^ mix32(c + 0x85ebca6bu))));
+}
+NGP_DEV float rng_unit(uint32_t seed, uint32_t a, uint32_t b, uint32_t c) {
+    return (float)(rng_u32(seed, a, b, c) >> 8) * (1.0f / 16777216.0f);
+}
+
+struct LegoScene {
+    float lo[kMaxBoxes][3], hi[kMaxBoxes][3], rgb[kMaxBoxes][3];
+    int nboxes;
+    float fx, fy, cx, cy;
+    uint32_t H, W, n_poses;
+    float aabb[6];
+    float min_near;
+    uint32_t seed;
+};
+
+// near/far against the aabb, reference raymarching.cu:91-145 (same as
+// k_near_far in raymarching.hip)
+NGP_DEV void near_far(const float o[3], const float d[3], const float aabb[6], float min_near,
+                      float& near, float& far) {
+    const float rdx = 1 / d[0], rdy = 1 / d[1], rdz = 1 / d[2];
+    near = (aabb[0] - o[0]) * rdx;
+    far = (aabb[3] - o[0]) * rdx;
+    if (near > far) { float c = near; near = far; far = c; }
+    float ny = (aabb[1] - o[1]) * rdy, fy = (aabb[4] - o[1]) * rdy;
+    if (ny > fy) { float c = ny; ny = fy; fy = c; }
+    if (near > fy || ny > far) { near = far = FLT_MAX; return; }
+    if (ny > near) near = ny;
+    if (fy < far) far = fy;
+    float nz = (aabb[2] - o[2]) * rdz, fz = (aabb[5] - o[2]) * rdz;
+    if (nz > fz) { float c = nz; nz = fz; fz = c; }
+    if (near > fz || nz > far) { near = far = FLT_MAX; return; }
+    if (nz > near) near = nz;
+    if (fz < far) far = fz;
+    if (near < min_near) near = min_near;
+}
+
+__global__ void __launch_bounds__(256)
+k_lego_rays(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState* __restrict__ st,
+            float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ rgba,
+            float* __restrict__ bg, float* __restrict__ nears, float* __restrict__ fars,
+            float* __restrict__ noises, int32_t* __restrict__ counter) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t it = (uint32_t)st->iter;
+    if (n == 0) { counter[0] = 0; counter[1] = 0; }
+    if (n >= N) return;
+    const uint32_t pose = rng_u32(sc.seed, it, 0xffffffffu, 0) % sc.n_poses;
+    const float* P = poses + (size_t)pose * 16;
+    const uint32_t pix = rng_u32(sc.seed, it, n, 1) % (sc.H * sc.W);
+    // get_rays (utils.py:52-136): pixel centre, camera direction, normalise, rotate
+    const float i = (float)(pix % sc.W) + 0.5f;
+    const float j = (float)(pix / sc.W) + 0.5f;
+    float xs = (i - sc.cx) / sc.fx, ys = (j - sc.cy) / sc.fy, zs = 1.0f;
+    const float nrm = sqrtf(xs * xs + ys * ys + zs * zs);
+    xs /= nrm; ys /= nrm; zs /= nrm;
+    float o[3], d[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        d[k] = fmaf(zs, P[k * 4 + 2], fmaf(ys, P[k * 4 + 1], xs * P[k * 4 + 0]));
+        o[k] = P[k * 4 + 3];
+        rays_o[n * 3 + k] = o[k];
+        rays_d[n * 3 + k] = d[k];
+    }
+    // analytic RGBA: colour of the nearest box hit (SyntheticLego.target)
+    float best = INFINITY;
+    int arg = -1;
+    for (int b = 0; b < sc.nboxes; ++b) {
+        float tn = -INFINITY, tf = INFINITY;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float inv = 1.0f / d[k];
+            const float t0 = (sc.lo[b][k] - o[k]) * inv, t1 = (sc.hi[b][k] - o[k]) * inv;
+            tn = fmaxf(tn, fminf(t0, t1));
+            tf = fminf(tf, fmaxf(t0, t1));
+        }
+        if (tf >= tn && tf > 0 && tn < best) { best = tn; arg = b; }
+    }
+    rgba[n * 4 + 0] = arg >= 0 ? sc.rgb[arg][0] : 0.0f;
+    rgba[n * 4 + 1] = arg >= 0 ? sc.rgb[arg][1] : 0.0f;
+    rgba[n * 4 + 2] = arg >= 0 ? sc.rgb[arg][2] : 0.0f;
+    rgba[n * 4 + 3] = arg >= 0 ? 1.0f : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bg[n * 3 + k] = rng_unit(sc.seed, it, n, 2 + k);
+    noises[n] = rng_unit(sc.seed, it, n, 5);
+    float nr, fr;
+    near_far(o, d, sc.aabb, sc.min_near, nr, fr);
+    nears[n] = nr;
+    fars[n] = fr;
+}
+
+// ---- network glue -------------------------------------------------------------
+// h: sigma-MLP output [B, 16] fp16 (col 0 = log density, 1..15 = geo features)
+__global__ void __launch_bounds__(256)
+k_glue_fwd(const ngp_half* __restrict__ h, const float* __restrict__ dirs, float density_scale,
+           float* __restrict__ sigma, ngp_half* __restrict__ color_in, uint32_t B,
+           const int32_t* __restrict__ count) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= clip_rows(B, count)) return;
+    typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+    const half8* hr = reinterpret_cast<const half8*>(h + (size_t)b * 16);
+    const half8 h0 = hr[0], h1 = hr[1];
+    // trunc_exp forward (activation.py: exp of the fp32-cast input), * density_scale
+    sigma[b] = density_scale * expf((float)h0[0]);
+    // SH degree 4 of the (unnormalised, size 1) direction, fp32 -> half
+    float sh[16];
+    ngp_sh::sh_basis<float>(dirs[b * 3], dirs[b * 3 + 1], dirs[b * 3 + 2], 4u,
+                            [&](uint32_t k, float v) { sh[k] = v; });
+    half8 o0, o1, o2, o3;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { o0[k] = (ngp_half)sh[k]; o1[k] = (ngp_half)sh[8 + k]; }
+    // geo features h[1..15], then the zero pad column
+#pragma unroll
+    for (int k = 0; k < 7; ++k) o2[k] = h0[k + 1];
+    o2[7] = h1[0];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) o3[k] = h1[k + 1];
+    o3[7] = (ngp_half)0.0f;
+    half8* out = reinterpret_cast<half8*>(color_in + (size_t)b * 32);
+    out[0] = o0; out[1] = o1; out[2] = o2; out[3] = o3;
+}
+
+// geo-feature grads: grad_h[b, 1..15] = grad_color_in[b, 16..30] (col 0 was
+// written by k_composite_loss)
+__global__ void __launch_bounds__(256)
+k_glue_bwd(const ngp_half* __restrict__ grad_color_in, ngp_half* __restrict__ grad_h, uint32_t B,
+           const int32_t* __restrict__ count) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= clip_rows(B, count)) return;
+    const ngp_half* src = grad_color_in + (size_t)b * 32 + 16;
+    ngp_half* dst = grad_h + (size_t)b * 16;
+#pragma unroll
+    for (int k = 1; k < 16; ++k) dst[k] = src[k - 1];
+}
+
+// ---- composite + loss + backward (one wave per ray) ---------------------------
+constexpr uint32_t kLossWaves = 4;
+
+NGP_DEV float lanef(float v, uint32_t j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)j));
+}
+// torch.sigmoid on a half tensor: fp32 math, half result
+NGP_DEV float sigmoid_h(ngp_half x) { return (float)(ngp_half)(1.0f / (1.0f + expf(-(float)x))); }
+
+struct LossArgs {
+    float T_thresh, density_scale, inv_n, inv_c;  // inv_n = 1/N, inv_c = 1/3 (torch mean backward)
+    uint32_t gt_channels;                         // 4: RGBA with random background, 3: RGB on white
+};
+
+__global__ void __launch_bounds__(kLossWaves * 64)
+k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ color_out,
+                 const ngp_half* __restrict__ h_sigma, const float* __restrict__ deltas,
+                 const int32_t* __restrict__ rays, uint32_t M, uint32_t N,
+                 const float* __restrict__ gt, const float* __restrict__ bg, LossArgs la,
+                 StepState* __restrict__ st, ngp_half* __restrict__ grad_color_out,
+                 ngp_half* __restrict__ grad_h, float* __restrict__ out_image,
+                 float* __restrict__ out_ws) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t n = blockIdx.x * kLossWaves + (threadIdx.x >> 6);
+    if (n >= N) return;
+    const uint32_t index = (uint32_t)rays[n * 3];
+    const uint32_t offset = (uint32_t)rays[n * 3 + 1];
+    const uint32_t num_steps = (uint32_t)rays[n * 3 + 2];
+    const bool valid = num_steps != 0 && offset + num_steps <= M;
+
+    // ---- forward recurrence (composite_rays_train_forward)
+    float T = 1.0f, r = 0, g = 0, b = 0, ws = 0, t = 0, d = 0;
+    if (valid) {
+        for (uint32_t base = 0; base < num_steps; base += 64) {
+            const uint32_t i = offset + base + lane;
+            const bool ok = base + lane < num_steps;
+            const float sg = ok ? sigma[i] : 0.0f;
+            const float d0 = ok ? deltas[(size_t)i * 2] : 0.0f;
+            const float d1 = ok ? deltas[(size_t)i * 2 + 1] : 0.0f;
+            float c0 = 0, c1 = 0, c2 = 0;
+            if (ok) {
+                c0 = sigmoid_h(color_out[(size_t)i * 16 + 0]);
+                c1 = sigmoid_h(color_out[(size_t)i * 16 + 1]);
+                c2 = sigmoid_h(color_out[(size_t)i * 16 + 2]);
+            }
+            const float alpha = 1.0f - expf(-sg * d0);
+            const uint32_t cnt = min(64u, num_steps - base);
+            bool stop = false;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const float a = lanef(alpha, j);
+                const float weight = a * T;
+                r = fmaf(weight, lanef(c0, j), r);
+                g = fmaf(weight, lanef(c1, j), g);
+                b = fmaf(weight, lanef(c2, j), b);
+                t += lanef(d1, j);
+                d = fmaf(weight, t, d);
+                ws += weight;
+                T *= 1.0f - a;
+                if (T < la.T_thresh) { stop = true; break; }
+            }
+            if (stop) break;
+        }
+    }
+    // ---- background blend + MSE (utils.py train_step) and its gradient
+    const float bg0 = bg[index * 3], bg1 = bg[index * 3 + 1], bg2 = bg[index * 3 + 2];
+    const float one_m_ws = 1.0f - ws;
+    const float p0 = r + one_m_ws * bg0, p1 = g + one_m_ws * bg1, p2 = b + one_m_ws * bg2;
+    float q0, q1, q2;
+    if (la.gt_channels == 4) {
+        const float* gp = gt + (size_t)index * 4;
+        const float a = gp[3], om = 1.0f - a;
+        q0 = gp[0] * a + bg0 * om;
+        q1 = gp[1] * a + bg1 * om;
+        q2 = gp[2] * a + bg2 * om;
+    } else {
+        const float* gp = gt + (size_t)index * 3;
+        q0 = gp[0]; q1 = gp[1]; q2 = gp[2];
+    }
+    const float e0 = p0 - q0, e1 = p1 - q1, e2 = p2 - q2;
+    if (lane == 0) {
+        atomicAdd(&st->loss_sum, ((e0 * e0 + e1 * e1) + e2 * e2) * la.inv_c);
+        if (out_image) {
+            out_image[index * 3] = p0; out_image[index * 3 + 1] = p1; out_image[index * 3 + 2] = p2;
+        }
+        if (out_ws) out_ws[index] = ws;
+    }
+    // (loss * scale).backward(): mean -> mean(-1) -> pow(2) -> sub
+    const float G = (st->scale * la.inv_n) * la.inv_c;
+    const float gr = G * (2.0f * e0), gg = G * (2.0f * e1), gb = G * (2.0f * e2);
+    const float gws = -((gr * bg0 + gg * bg1) + gb * bg2);  // d/dws of image + (1 - ws) * bg
+    const float gd = 0.0f;                                  // depth is not in the loss
+    const float r_final = r, g_final = g, b_final = b, ws_final = ws, d_final = d;
+
+    // ---- backward recurrence (composite_rays_train_backward) + activation backward
+    if (!valid) {
+        // a ray dropped for overflowing M still owns rows [offset, M): zero their grads
+        for (uint32_t k = offset + lane; k < min(offset + num_steps, M); k += 64) {
+            typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+            const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+            reinterpret_cast<half8*>(grad_color_out + (size_t)k * 16)[0] = z;
+            reinterpret_cast<half8*>(grad_color_out + (size_t)k * 16)[1] = z;
+            grad_h[(size_t)k * 16] = (ngp_half)0.0f;
+        }
+        return;
+    }
+    T = 1.0f; r = 0; g = 0; b = 0; t = 0; d = 0;
+    bool stopped = false;
+    for (uint32_t base = 0; base < num_steps; base += 64) {
+        const uint32_t i = offset + base + lane;
+        const bool ok = base + lane < num_steps;
+        const float sg = ok ? sigma[i] : 0.0f;
+        const float d0 = ok ? deltas[(size_t)i * 2] : 0.0f;
+        const float d1 = ok ? deltas[(size_t)i * 2 + 1] : 0.0f;
+        float c0 = 0, c1 = 0, c2 = 0;
+        if (ok) {
+            c0 = sigmoid_h(color_out[(size_t)i * 16 + 0]);
+            c1 = sigmoid_h(color_out[(size_t)i * 16 + 1]);
+            c2 = sigmoid_h(color_out[(size_t)i * 16 + 2]);
+        }
+        const float alpha = 1.0f - expf(-sg * d0);
+        const uint32_t cnt = min(64u, num_steps - base);
+        float mw = 0, mT = 0, mr = 0, mg = 0, mb = 0, mt = 0, md = 0;
+        uint32_t done = stopped ? 0u : cnt;
+        if (!stopped) {
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const float a = lanef(alpha, j);
+                const float weight = a * T;
+                r = fmaf(weight, lanef(c0, j), r);
+                g = fmaf(weight, lanef(c1, j), g);
+                b = fmaf(weight, lanef(c2, j), b);
+                t += lanef(d1, j);
+                d = fmaf(weight, t, d);
+                T *= 1.0f - a;
+                if (lane == j) { mw = weight; mT = T; mr = r; mg = g; mb = b; mt = t; md = d; }
+                if (T < la.T_thresh) { done = j + 1; stopped = true; break; }
+            }
+        }
+        if (!ok) continue;
+        float gc0 = 0, gc1 = 0, gc2 = 0, gs = 0;
+        if (lane < done) {
+            gc0 = gr * mw; gc1 = gg * mw; gc2 = gb * mw;
+            gs = d0 * (gr * (mT * c0 - (r_final - mr)) + gg * (mT * c1 - (g_final - mg)) +
+                       gb * (mT * c2 - (b_final - mb)) + gd * (mT * mt - (d_final - md)) +
+                       gws * (1 - ws_final));
+        }
+        // rgbs.float() <- half, then sigmoid_backward(grad, y) = grad * (1 - y) * y (fp32 math)
+        typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+        half8 o0 = {0, 0, 0, 0, 0, 0, 0, 0}, o1 = {0, 0, 0, 0, 0, 0, 0, 0};
+        o0[0] = (ngp_half)((float)(ngp_half)gc0 * (1.0f - c0) * c0);
+        o0[1] = (ngp_half)((float)(ngp_half)gc1 * (1.0f - c1) * c1);
+        o0[2] = (ngp_half)((float)(ngp_half)gc2 * (1.0f - c2) * c2);
+        half8* go = reinterpret_cast<half8*>(grad_color_out + (size_t)i * 16);
+        go[0] = o0;
+        go[1] = o1;
+        // sigmas = ds * trunc_exp(h0): grad_h0 = (gs * ds) * exp(clamp(h0, -15, 15)), -> half
+        const float h0 = (float)h_sigma[(size_t)i * 16];
+        grad_h[(size_t)i * 16] = (ngp_half)((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
+    }
+}
+
+// ---- optimizer ------------------------------------------------------------------
+struct TensorList {
+    int n;
+    float* p[kMaxTensors];
+    ngp_half* g[kMaxTensors];
+    float* m[kMaxTensors];
+    float* v[kMaxTensors];
+    ngp_half* ph[kMaxTensors];        // optional fp16 shadow of p (the MLPs' forward weights)
+    uint64_t size[kMaxTensors];
+    uint64_t start[kMaxTensors + 1];  // flat index space; each tensor starts 8-aligned
+};
+
+NGP_DEV int find_tensor(const TensorList& tl, uint64_t i) {
+    int k = 0;
+    while (k + 1 < tl.n && i >= tl.start[k + 1]) ++k;
+    return k;
+}
+
+// GradScaler._unscale_grads_ inf/nan check over every grad (8 halves / lane)
+__global__ void __launch_bounds__(256)
+k_nonfinite(TensorList tl, StepState* __restrict__ st) {
+    const uint64_t total = tl.start[tl.n];
+    bool bad = false;
+    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i0 < total;
+         i0 += (uint64_t)gridDim.x * blockDim.x * 8) {
+        const int k = find_tensor(tl, i0);
+        const uint64_t off = i0 - tl.start[k];
+        const ngp_half* g = tl.g[k] + off;
+        if (off + 8 <= tl.size[k] && ((reinterpret_cast<uintptr_t>(g) & 15) == 0)) {
+            typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+            const half8 v = *reinterpret_cast<const half8*>(g);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bad |= !__builtin_isfinite((float)v[j]);
+        } else {
+            for (uint64_t j = 0; j < 8 && off + j < tl.size[k]; ++j) bad |= !__builtin_isfinite((float)g[j]);
+        }
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&st->found_inf, 1);
+}
+
+struct AdamArgs {
+    float base_lr, beta1, beta2, eps;
+    int32_t iters;   // LambdaLR: lr = base_lr * 0.1 ** min(epoch / iters, 1)
+    int32_t zero_grads;
+    float grad_mult; // e.g. 1 / world_size after a data-parallel all-reduce (sum)
+};
+
+// torch.optim.Adam (weight_decay 0) on p, with g = half_grad * (1 / scale);
+// skipped (state untouched) when the check found an inf/nan, like
+// GradScaler.step. Grads are zeroed afterwards either way.
+__global__ void __launch_bounds__(256)
+k_adam_multi(TensorList tl, const StepState* __restrict__ st, AdamArgs aa) {
+    const bool skip = st->found_inf != 0;
+    const int32_t step = st->adam_step + 1;
+    const double lr = (double)aa.base_lr * pow(0.1, fmin((double)st->epoch / (double)aa.iters, 1.0));
+    const double bc1 = 1.0 - pow((double)aa.beta1, step);
+    const double bc2 = 1.0 - pow((double)aa.beta2, step);
+    const float step_size = (float)(lr / bc1);
+    const float inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
+    const float inv_scale = (float)(1.0 / (double)st->scale) * aa.grad_mult;
+    const uint64_t total = tl.start[tl.n];
+    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < total;
+         i0 += (uint64_t)gridDim.x * blockDim.x * 4) {
+        const int k = find_tensor(tl, i0);
+        const uint64_t off = i0 - tl.start[k];
+        if (off >= tl.size[k]) continue;  // alignment padding between tensors
+        float* p = tl.p[k] + off;
+        float* m = tl.m[k] + off;
+        float* v = tl.v[k] + off;
+        ngp_half* g = tl.g[k] + off;
+        ngp_half* ph = tl.ph[k] ? tl.ph[k] + off : nullptr;
+        const uint64_t n4 = min((uint64_t)4, tl.size[k] - off);
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+        if (n4 == 4) {
+            float4 pv = *reinterpret_cast<float4*>(p);
+            float4 mv = *reinterpret_cast<float4*>(m);
+            float4 vv = *reinterpret_cast<float4*>(v);
+            const half4 gh = *reinterpret_cast<const half4*>(g);
+            if (!skip) {
+                float* pp = &pv.x; float* mm = &mv.x; float* vq = &vv.x;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float gk = (float)gh[j] * inv_scale;
+                    mm[j] = mm[j] + (1.0f - aa.beta1) * (gk - mm[j]);
+                    vq[j] = vq[j] * aa.beta2 + (1.0f - aa.beta2) * gk * gk;
+                    const float denom = sqrtf(vq[j]) * inv_bc2_sqrt + aa.eps;
+                    pp[j] = pp[j] - step_size * (mm[j] / denom);
+                }
+                *reinterpret_cast<float4*>(p) = pv;
+                *reinterpret_cast<float4*>(m) = mv;
+                *reinterpret_cast<float4*>(v) = vv;
+                if (ph) *reinterpret_cast<half4*>(ph) = half4{(ngp_half)pv.x, (ngp_half)pv.y, (ngp_half)pv.z, (ngp_half)pv.w};
+            }
+            if (aa.zero_grads) *reinterpret_cast<half4*>(g) = half4{0, 0, 0, 0};
+        } else {
+            for (uint64_t j = 0; j < n4; ++j) {
+                if (!skip) {
+                    const float gk = (float)g[j] * inv_scale;
+                    m[j] = m[j] + (1.0f - aa.beta1) * (gk - m[j]);
+                    v[j] = v[j] * aa.beta2 + (1.0f - aa.beta2) * gk * gk;
+                    const float denom = sqrtf(v[j]) * inv_bc2_sqrt + aa.eps;
+                    p[j] = p[j] - step_size * (m[j] / denom);
+                    if (ph) ph[j] = (ngp_half)p[j];
+                }
+                if (aa.zero_grads) g[j] = (ngp_half)0.0f;
+            }
+        }
+    }
+}
+
+struct ScalerArgs {
+    float growth_factor, backoff_factor;
+    int32_t growth_interval, enabled;
+    float inv_n;
+};
+
+// GradScaler.update, LambdaLR epoch, Adam step count, loss bookkeeping;
+// also records this step's sample count into step_counter[iter % 16]
+__global__ void k_step_end(StepState* __restrict__ st, ScalerArgs sa, const int32_t* __restrict__ counter,
+                           int32_t* __restrict__ step_counter) {
+    if (threadIdx.x != 0) return;
+    const bool inf = st->found_inf != 0;
+    if (sa.enabled) {
+        if (inf) {
+            st->scale *= sa.backoff_factor;
+            st->growth_tracker = 0;
+        } else if (++st->growth_tracker == sa.growth_interval) {
+            st->scale *= sa.growth_factor;
+            st->growth_tracker = 0;
+        }
+    }
+    if (!inf) st->adam_step += 1;
+    st->epoch += 1;
+    if (step_counter) {
+        const int slot = st->iter % 16;
+        step_counter[slot * 2] = counter[0];
+        step_counter[slot * 2 + 1] = counter[1];
+    }
+    st->iter += 1;
+    st->last_loss = st->loss_sum * sa.inv_n;
+    st->loss_sum = 0.0f;
+    st->found_inf = 0;
+}
+
+TensorList make_list(int n, float* const* p, void* const* g, float* const* m, float* const* v,
+                     void* const* ph, const uint64_t* sizes) {
+    TensorList tl{};
+    tl.n = n;
+    tl.start[0] = 0;
+    for (int k = 0; k < n; ++k) {
+        tl.p[k] = p ? p[k] : nullptr;
+        tl.g[k] = static_cast<ngp_half*>(g[k]);
+        tl.m[k] = m ? m[k] : nullptr;
+        tl.v[k] = v ? v[k] : nullptr;
+        tl.ph[k] = ph ? static_cast<ngp_half*>(ph[k]) : nullptr;
+        tl.size[k] = sizes[k];
+        tl.start[k + 1] = tl.start[k] + (sizes[k] + 7) / 8 * 8;
+    }
+    return tl;
+}
+
+uint32_t sweep_blocks(uint64_t total, uint32_t per_thread) {
+    uint64_t b = (total / per_thread + 255) / 256;
+    if (b > 8192) b = 8192;
+    return b ? (uint32_t)b : 1u;
+}
+
+}  // namespace
+
+extern "C" size_t ngp_fused_state_bytes(void) { return sizeof(StepState); }
+
+extern "C" int ngp_fused_state_init(void* state, float init_scale, void* stream) {
+    NGP_REQUIRE(state, NGP_ERR_ARG, "fused_state_init: null state");
+    StepState s{};
+    s.scale = init_scale;
+    return hipMemcpyAsync(state, &s, sizeof(s), hipMemcpyHostToDevice, ngp_stream(stream)) == hipSuccess
+               ? NGP_OK
+               : ngp_set_error(NGP_ERR_HIP, "fused_state_init: copy failed");
+}
+
+extern "C" int ngp_lego_rays(const float* poses, uint32_t n_poses, const float* intrinsics4,
+                             uint32_t H, uint32_t W, uint32_t N, const float* boxes, int32_t nboxes,
+                             const float* aabb6, float min_near, uint32_t seed, void* state,
+                             float* rays_o, float* rays_d, float* rgba, float* bg, float* nears,
+                             float* fars, float* noises, int32_t* counter, void* stream) {
+    NGP_REQUIRE(nboxes >= 0 && nboxes <= kMaxBoxes, NGP_ERR_ARG, "lego_rays: at most %d boxes", kMaxBoxes);
+    NGP_REQUIRE(n_poses > 0 && H > 0 && W > 0, NGP_ERR_ARG, "lego_rays: empty pose set or image");
+    if (N == 0) return NGP_OK;
+    LegoScene sc{};
+    for (int b = 0; b < nboxes; ++b)
+        for (int k = 0; k < 3; ++k) {
+            sc.lo[b][k] = boxes[b * 9 + k];
+            sc.hi[b][k] = boxes[b * 9 + 3 + k];
+            sc.rgb[b][k] = boxes[b * 9 + 6 + k];
+        }
+    sc.nboxes = nboxes;
+    sc.fx = intrinsics4[0]; sc.fy = intrinsics4[1]; sc.cx = intrinsics4[2]; sc.cy = intrinsics4[3];
+    sc.H = H; sc.W = W; sc.n_poses = n_poses;
+    for (int k = 0; k < 6; ++k) sc.aabb[k] = aabb6[k];
+    sc.min_near = min_near;
+    sc.seed = seed;
+    k_lego_rays<<<ngp_div_up(N, 256), 256, 0, ngp_stream(stream)>>>(
+        poses, sc, N, static_cast<StepState*>(state), rays_o, rays_d, rgba, bg, nears, fars, noises, counter);
+    return ngp_check_launch("lego_rays");
+}
+
+extern "C" int ngp_nerf_glue_forward(const void* h_sigma, const float* dirs, float density_scale,
+                                     float* sigma, void* color_in, uint32_t B, const int32_t* count,
+                                     void* stream) {
+    if (B == 0) return NGP_OK;
+    k_glue_fwd<<<ngp_div_up(B, 256), 256, 0, ngp_stream(stream)>>>(
+        (const ngp_half*)h_sigma, dirs, density_scale, sigma, (ngp_half*)color_in, B, count);
+    return ngp_check_launch("nerf_glue_forward");
+}
+
+extern "C" int ngp_nerf_glue_backward(const void* grad_color_in, void* grad_h_sigma, uint32_t B,
+                                      const int32_t* count, void* stream) {
+    if (B == 0) return NGP_OK;
+    k_glue_bwd<<<ngp_div_up(B, 256), 256, 0, ngp_stream(stream)>>>(
+        (const ngp_half*)grad_color_in, (ngp_half*)grad_h_sigma, B, count);
+    return ngp_check_launch("nerf_glue_backward");
+}
+
+extern "C" int ngp_nerf_composite_loss(const float* sigma, const void* color_out, const void* h_sigma,
+                                       const float* deltas, const int32_t* rays, uint32_t M,
+                                       uint32_t N, float T_thresh, float density_scale,
+                                       const float* gt, uint32_t gt_channels, const float* bg,
+                                       void* state, void* grad_color_out, void* grad_h_sigma,
+                                       float* out_image, float* out_ws, void* stream) {
+    NGP_REQUIRE(gt_channels == 3 || gt_channels == 4, NGP_ERR_ARG, "composite_loss: gt must be RGB or RGBA");
+    if (N == 0) return NGP_OK;
+    LossArgs la;
+    la.T_thresh = T_thresh;
+    la.density_scale = density_scale;
+    la.inv_n = 1.0f / (float)N;
+    la.inv_c = 1.0f / 3.0f;
+    la.gt_channels = gt_channels;
+    k_composite_loss<<<ngp_div_up(N, kLossWaves), kLossWaves * 64, 0, ngp_stream(stream)>>>(
+        sigma, (const ngp_half*)color_out, (const ngp_half*)h_sigma, deltas, rays, M, N, gt, bg, la,
+        static_cast<StepState*>(state), (ngp_half*)grad_color_out, (ngp_half*)grad_h_sigma, out_image,
+        out_ws);
+    return ngp_check_launch("nerf_composite_loss");
+}
+
+extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* const* grads,
+                                        float* const* exp_avg, float* const* exp_avg_sq,
+                                        void* const* half_params, const uint64_t* sizes, float lr,
+                                        float beta1, float beta2, float eps, int32_t iters,
+                                        int32_t zero_grads, float grad_mult,
+                                        float growth_factor, float backoff_factor,
+                                        int32_t growth_interval, int32_t scaler_enabled,
+                                        uint32_t num_rays, const int32_t* counter,
+                                        int32_t* step_counter, void* state, void* stream) {
+    NGP_REQUIRE(n_tensors >= 1 && n_tensors <= kMaxTensors, NGP_ERR_ARG,
+                "fused_optimizer_step: 1..%d tensors", kMaxTensors);
+    for (int k = 0; k < n_tensors; ++k)
+        NGP_REQUIRE(((reinterpret_cast<uintptr_t>(params[k]) | reinterpret_cast<uintptr_t>(exp_avg[k]) |
+                      reinterpret_cast<uintptr_t>(exp_avg_sq[k])) & 15) == 0 &&
+                        (reinterpret_cast<uintptr_t>(grads[k]) & 7) == 0,
+                    NGP_ERR_ARG, "fused_optimizer_step: tensor %d misaligned", k);
+    hipStream_t s = ngp_stream(stream);
+    StepState* st = static_cast<StepState*>(state);
+    for (int k = 0; k < n_tensors; ++k)
+        NGP_REQUIRE(!half_params || !half_params[k] || (reinterpret_cast<uintptr_t>(half_params[k]) & 7) == 0,
+                    NGP_ERR_ARG, "fused_optimizer_step: half shadow %d misaligned", k);
+    const TensorList tl = make_list(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes);
+    const uint64_t total = tl.start[n_tensors];
+    if (scaler_enabled) k_nonfinite<<<sweep_blocks(total, 8), 256, 0, s>>>(tl, st);
+    AdamArgs aa{lr, beta1, beta2, eps, iters, zero_grads, grad_mult};
+    k_adam_multi<<<sweep_blocks(total, 4), 256, 0, s>>>(tl, st, aa);
+    ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled,
+                  num_rays ? 1.0f / (float)num_rays : 0.0f};
+    k_step_end<<<1, 64, 0, s>>>(st, sa, counter, step_counter);
+    return ngp_check_launch("fused_optimizer_step");
+}

@@ -1,0 +1,237 @@
+"""Fused instant-ngp train step: one training iteration of the reference
+(nerf/utils.py Trainer.train_step :453-497 + optimizer/scaler/scheduler
+:194-217, 574-609) as ~22 kernel launches through the C ABI, no autograd.
+
+The autograd path (nerf.train.Trainer + the gridencoder/raymarching/
+shencoder/ffmlp Functions) is the reference's op-level API and stays the
+parity anchor; this engine computes the same iteration with the elementwise
+glue fused into the hot-path kernels (DESIGN.md "fused step"):
+
+    lego_rays -> march_rays_train -> grid_encode(fused) -> sigma FFMLP
+    -> glue(trunc_exp, SH, cat) -> color FFMLP -> composite+loss+backward
+    -> color FFMLP backward -> glue backward -> sigma FFMLP backward
+    -> grid_encode backward(fused) -> GradScaler check + Adam + update
+
+Static shapes: N rays per step, M = the sample buffer (mean_count); rows past
+the marcher's sample count are skipped on the device, so a fixed M costs
+nothing beyond its memory. Every launch goes to the current stream, so the
+whole step captures into one hipGraph (`capture`).
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+import _ngp_native as nat
+
+from .provider import LEGO_BOXES, LEGO_COLORS
+
+_F16 = nat.DTYPE_CODE[torch.float16]
+_RELU, _NONE = 0, 6
+
+
+def _vp_array(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+class FusedTrainer:
+    def __init__(self, model, dataset, M, lr=1e-2, iters=30000, max_steps=1024, T_thresh=1e-4,
+                 dt_gamma=0.0, seed=0, betas=(0.9, 0.99), eps=1e-15, init_scale=65536.0,
+                 growth_interval=2000, distributed=False):
+        """distributed: ray-sharded data parallelism over the initialised
+        torch.distributed group (each rank draws its own rays; the flat fp16
+        gradient is summed with one RCCL all-reduce, the optimizer averages)."""
+        assert model.cuda_ray, "the fused step marches the density bitfield (cuda_ray=True)"
+        enc = model.encoder
+        assert enc.level_dim == 2 and enc.num_levels * enc.level_dim == 32 and enc.input_dim == 3
+        assert model.sigma_net.input_dim == 32 and model.color_net.input_dim == 32
+        self.model, self.data = model, dataset
+        dev = model.density_bitfield.device
+        self.dev = dev
+        self.N = N = int(dataset.num_rays)
+        self.M = M = int(M)
+        self.max_steps, self.T_thresh, self.dt_gamma = int(max_steps), float(T_thresh), float(dt_gamma)
+        self.lr, self.iters, self.betas, self.eps = float(lr), int(iters), betas, float(eps)
+        self.growth_interval, self.seed = int(growth_interval), int(seed)
+        self.world = dist.get_world_size() if distributed and dist.is_initialized() else 1
+        if self.world > 1:
+            self.seed += 7919 * dist.get_rank()
+        self.enc = enc
+        self.S = float(np.log2(enc.per_level_scale))
+        self.sig_net, self.col_net = model.sigma_net, model.color_net
+
+        def z(*shape, dtype=torch.float32):
+            return torch.zeros(*shape, dtype=dtype, device=dev)
+
+        # per-ray and per-sample buffers
+        self.rays_o, self.rays_d = z(N, 3), z(N, 3)
+        self.rgba, self.bg = z(N, 4), z(N, 3)
+        self.nears, self.fars, self.noises = z(N), z(N), z(N)
+        self.counter = z(2, dtype=torch.int32)
+        self.rays = z(N, 3, dtype=torch.int32)
+        self.xyzs, self.dirs, self.deltas = z(M, 3), z(M, 3), z(M, 2)
+        ws = nat.lib().ngp_march_rays_train_workspace_bytes(N, self.max_steps, model.cascade, model.grid_size)
+        self.march_ws = z(ws, dtype=torch.uint8)
+        h = torch.float16
+        self.enc_out, self.h_sigma = z(M, 32, dtype=h), z(M, 16, dtype=h)
+        self.sigma, self.color_in, self.color_out = z(M), z(M, 32, dtype=h), z(M, 16, dtype=h)
+        self.g_color_out, self.g_h = z(M, 16, dtype=h), z(M, 16, dtype=h)
+        self.g_color_in, self.g_enc = z(M, 32, dtype=h), z(M, 32, dtype=h)
+        # parameters: fp32 masters, fp16 grads, fp16 forward copies of the MLPs
+        self.params = [enc.embeddings, self.sig_net.weights, self.col_net.weights]
+        # one flat fp16 gradient (one all-reduce in data-parallel mode), 8-aligned views
+        sizes = [p.numel() for p in self.params]
+        starts = np.cumsum([0] + [(n + 7) // 8 * 8 for n in sizes])
+        self.flat_grad = z(int(starts[-1]), dtype=h)
+        self.grads = [self.flat_grad[int(a):int(a) + n].view(p.shape)
+                      for a, n, p in zip(starts[:-1], sizes, self.params)]
+        self.exp_avg = [torch.zeros_like(p) for p in self.params]
+        self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
+        self.w_half = [None] + [p.detach().half() for p in self.params[1:]]
+        self.mlp_ws = []
+        for net in (self.sig_net, self.col_net):
+            b = nat.lib().ngp_ffmlp_backward_workspace_bytes(M, net.input_dim, net.padded_output_dim,
+                                                             net.hidden_dim, net.num_layers)
+            self.mlp_ws.append(z(b, dtype=torch.uint8))
+        self.state = z(nat.lib().ngp_fused_state_bytes(), dtype=torch.uint8)
+        nat.check(nat.lib().ngp_fused_state_init(nat.ptr(self.state), float(init_scale),
+                                                 nat.stream_of(self.state)), "fused_state_init")
+        # host-side constants of the synthetic scene
+        boxes = [v for (lo, hi), rgb in zip(LEGO_BOXES, LEGO_COLORS) for v in (*lo, *hi, *rgb)]
+        self._boxes = (ctypes.c_float * len(boxes))(*boxes)
+        self._nboxes = len(LEGO_BOXES)
+        self._intr = (ctypes.c_float * 4)(*[float(v) for v in dataset.intrinsics])
+        self._aabb = (ctypes.c_float * 6)(*model.aabb_train.detach().cpu().tolist())
+        self._opt = dict(
+            params=_vp_array([nat.ptr(p) for p in self.params]),
+            grads=_vp_array([nat.ptr(g) for g in self.grads]),
+            m=_vp_array([nat.ptr(t) for t in self.exp_avg]),
+            v=_vp_array([nat.ptr(t) for t in self.exp_avg_sq]),
+            half=_vp_array([None] + [nat.ptr(t) for t in self.w_half[1:]]),
+            sizes=(ctypes.c_uint64 * 3)(*[p.numel() for p in self.params]))
+        self.graph = None
+        self.graph_opt = None
+
+    # ------------------------------------------------------------------ step
+    def _launch(self):
+        self._sample()
+        self._forward_backward()
+        self._allreduce()
+        self._optimizer()
+
+    def _allreduce(self):
+        if self.world > 1:
+            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+
+    def _sample(self):
+        """Batch of N rays: rays, RGBA target, background, march noise, near/far."""
+        lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
+        m, d = self.model, self.data
+        nat.check(lib.ngp_lego_rays(P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N,
+                                    self._boxes, self._nboxes, self._aabb, float(m.min_near), self.seed,
+                                    P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
+                                    P(self.nears), P(self.fars), P(self.noises), P(self.counter), s),
+                  "lego_rays")
+
+    def _forward_backward(self):
+        """march -> network -> composite + MSE -> full backward into the fp16 grads."""
+        lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
+        m, e = self.model, self.enc
+        M, N, cnt = self.M, self.N, P(self.counter)
+        chk = nat.check
+        chk(lib.ngp_march_rays_train(P(self.rays_o), P(self.rays_d), P(m.density_bitfield),
+                                     float(m.bound), self.dt_gamma, self.max_steps, N, m.cascade,
+                                     m.grid_size, M, P(self.nears), P(self.fars), P(self.xyzs),
+                                     P(self.dirs), P(self.deltas), P(self.rays), cnt, P(self.noises),
+                                     P(self.march_ws), self.march_ws.numel(), s), "march_rays_train")
+        grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
+                     int(e.align_corners), e.interp_id, s)
+        chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(e.embeddings), P(e.offsets),
+                                              P(self.enc_out), M, cnt, *grid_args), "grid_encode_fused")
+        sn, cn = self.sig_net, self.col_net
+        chk(lib.ngp_ffmlp_forward_rows(P(self.enc_out), P(self.w_half[1]), M, cnt, 32, 16, sn.hidden_dim,
+                                       sn.num_layers, _RELU, _NONE, P(self.h_sigma), s), "sigma_mlp")
+        chk(lib.ngp_nerf_glue_forward(P(self.h_sigma), P(self.dirs), float(m.density_scale), P(self.sigma),
+                                      P(self.color_in), M, cnt, s), "glue_forward")
+        chk(lib.ngp_ffmlp_forward_rows(P(self.color_in), P(self.w_half[2]), M, cnt, 32, 16, cn.hidden_dim,
+                                       cn.num_layers, _RELU, _NONE, P(self.color_out), s), "color_mlp")
+        chk(lib.ngp_nerf_composite_loss(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
+                                        P(self.rays), M, N, self.T_thresh, float(m.density_scale),
+                                        P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
+                                        P(self.g_h), None, None, s), "composite_loss")
+        chk(lib.ngp_ffmlp_backward_rows(P(self.g_color_out), P(self.color_in), P(self.w_half[2]), M, cnt,
+                                        32, 16, cn.hidden_dim, cn.num_layers, _RELU, P(self.g_color_in),
+                                        P(self.grads[2]), _F16, P(self.mlp_ws[1]), self.mlp_ws[1].numel(),
+                                        s), "color_mlp_backward")
+        chk(lib.ngp_nerf_glue_backward(P(self.g_color_in), P(self.g_h), M, cnt, s), "glue_backward")
+        chk(lib.ngp_ffmlp_backward_rows(P(self.g_h), P(self.enc_out), P(self.w_half[1]), M, cnt, 32, 16,
+                                        sn.hidden_dim, sn.num_layers, _RELU, P(self.g_enc),
+                                        P(self.grads[1]), _F16, P(self.mlp_ws[0]), self.mlp_ws[0].numel(),
+                                        s), "sigma_mlp_backward")
+        chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
+                                               P(self.grads[0]), M, cnt, *grid_args), "grid_backward_fused")
+
+    def _optimizer(self):
+        """GradScaler inf check + Adam (unscaled fp16 grads, LambdaLR) + scaler update."""
+        lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
+        o, chk, N, cnt, m = self._opt, nat.check, self.N, P(self.counter), self.model
+        chk(lib.ngp_fused_optimizer_step(3, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"],
+                                         self.lr, self.betas[0], self.betas[1], self.eps, self.iters, 1,
+                                         1.0 / self.world, 2.0, 0.5, self.growth_interval, 1, N, cnt,
+                                         P(m.step_counter),
+                                         P(self.state), s), "fused_optimizer_step")
+
+    def step(self):
+        if self.graph is None:
+            self._launch()
+        elif self.graph_opt is None:
+            self.graph.replay()
+        else:  # data parallel: graph, RCCL all-reduce (eager), optimizer graph
+            self.graph.replay()
+            self._allreduce()
+            self.graph_opt.replay()
+        self.model.local_step += 1
+
+    def capture(self, warmup=2):
+        """One hipGraph for the whole step (two around the all-reduce when
+        data parallel)."""
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._launch()
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        if self.world == 1:
+            with torch.cuda.graph(self.graph):
+                self._launch()
+            return
+        with torch.cuda.graph(self.graph):
+            self._sample()
+            self._forward_backward()
+        self.graph_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_opt):
+            self._optimizer()
+
+    # ----------------------------------------------------------- read-outs
+    def _state_f(self):
+        return self.state.view(torch.float32)
+
+    def _state_i(self):
+        return self.state.view(torch.int32)
+
+    @property
+    def last_loss(self):
+        return float(self._state_f()[2].item())
+
+    @property
+    def scale(self):
+        return float(self._state_f()[0].item())
+
+    @property
+    def optimizer_steps(self):
+        return int(self._state_i()[6].item())
+
+    def sample_count(self):
+        return int(self.counter[0].item())
