@@ -286,7 +286,7 @@ def kernel_profile(ft, reps):
             P(ft.g_enc), P(ft.xyzs), float(m.bound), P(e.offsets), P(ft.grads[0]), M, cnt, *ga),
         "grid_encode_forward": lambda: lib.ngp_grid_encode_forward_fused(
             P(ft.xyzs), float(m.bound), P(e.embeddings), P(e.offsets), P(ft.enc_out), M, cnt, *ga),
-        "march_rays_train": lambda: lib.ngp_march_rays_train(
+        "march_rays_train": lambda: lib.ngp_march_rays_train_prebuilt(
             P(ft.rays_o), P(ft.rays_d), P(m.density_bitfield), float(m.bound), ft.dt_gamma, ft.max_steps, N,
             m.cascade, m.grid_size, M, P(ft.nears), P(ft.fars), P(ft.xyzs), P(ft.dirs), P(ft.deltas),
             P(ft.rays), P(ft.march_cnt_scratch), P(ft.noises), P(ft.march_ws), ft.march_ws.numel(), s),
@@ -303,7 +303,7 @@ def kernel_profile(ft, reps):
         "composite_loss": lambda: lib.ngp_nerf_composite_loss(
             P(ft.sigma), P(ft.color_out), P(ft.h_sigma), P(ft.deltas), P(ft.rays), M, N, ft.T_thresh,
             float(m.density_scale), P(ft.rgba), 4, P(ft.bg), P(ft.scratch_state), P(ft.g_color_out),
-            P(ft.g_h), None, None, s),
+            P(ft.g_h), None, None, P(ft.loss_ray), s),
     }
     out = {}
     for name, fn in calls.items():

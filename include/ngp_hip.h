@@ -111,6 +111,20 @@ int ngp_march_rays_train(const float* rays_o, const float* rays_d, const uint8_t
                          const float* noises, void* workspace, size_t workspace_bytes,
                          void* stream);
 
+/* The occupancy image march_rays_train builds from `grid` on every call can be
+ * built once per bitfield change instead: ngp_march_occupancy_build into the
+ * workspace, then ngp_march_rays_train_prebuilt (same arguments) as long as
+ * grid's contents are unchanged. */
+int ngp_march_occupancy_build(const uint8_t* grid, uint32_t C, uint32_t H, uint32_t N,
+                              uint32_t max_steps, void* workspace, size_t workspace_bytes,
+                              void* stream);
+int ngp_march_rays_train_prebuilt(const float* rays_o, const float* rays_d, const uint8_t* grid,
+                                  float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
+                                  uint32_t C, uint32_t H, uint32_t M, const float* nears,
+                                  const float* fars, float* xyzs, float* dirs, float* deltas,
+                                  int32_t* rays, int32_t* counter, const float* noises,
+                                  void* workspace, size_t workspace_bytes, void* stream);
+
 /* raymarching.h:14, raymarching.cu:580-588 */
 int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs, const float* deltas,
                                      const int32_t* rays, uint32_t M, uint32_t N, float T_thresh,
@@ -244,7 +258,7 @@ int ngp_nerf_composite_loss(const float* sigma, const void* color_out, const voi
                             float T_thresh, float density_scale, const float* gt,
                             uint32_t gt_channels, const float* bg, void* state,
                             void* grad_color_out, void* grad_h_sigma, float* out_image,
-                            float* out_ws, void* stream);
+                            float* out_ws, float* loss_ray, void* stream);
 /* Adam (+ GradScaler inf check/unscale/update, LambdaLR 0.1^(epoch/iters))
  * over n_tensors fp32 params with fp16 grads; half_params[k] (nullable) is
  * refreshed with half(p) after the update; grads are zeroed when zero_grads;
@@ -256,7 +270,8 @@ int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* cons
                              float grad_mult, float growth_factor, float backoff_factor,
                              int32_t growth_interval,
                              int32_t scaler_enabled, uint32_t num_rays, const int32_t* counter,
-                             int32_t* step_counter, void* state, void* stream);
+                             int32_t* step_counter, const float* loss_ray, void* state,
+                             void* stream);
 
 #ifdef __cplusplus
 }

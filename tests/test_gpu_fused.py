@@ -85,7 +85,7 @@ def test_fused_forward_backward_matches_autograd(cuda):
     torch.cuda.synchronize()
     # identical march (same rays, near/far, noise): same sample count
     assert int(ft.counter[0]) == int(ref.step_counter[0, 0]) > 0
-    fused_loss = float(ft._state_f()[1].item()) / ft.N
+    fused_loss = float(ft.loss_ray.double().sum()) / ft.N
     lv = float(loss.detach())
     assert abs(fused_loss - lv) <= 2e-3 * abs(lv) + 1e-7
     names = ["embeddings", "sigma_net", "color_net"]

@@ -37,6 +37,9 @@ SIGNATURES = {
     "ngp_morton3D_invert": [c_vp, c_u32, c_vp, c_vp],
     "ngp_packbits": [c_vp, c_u32, c_f32, c_vp, c_vp],
     "ngp_march_rays_train_workspace_bytes": [c_u32, c_u32, c_u32, c_u32],
+    "ngp_march_occupancy_build": [c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_sz, c_vp],
+    "ngp_march_rays_train_prebuilt": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_march_rays_train": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_composite_rays_train_forward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_vp, c_vp,
@@ -75,10 +78,10 @@ SIGNATURES = {
     "ngp_nerf_glue_forward": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_vp],
     "ngp_nerf_glue_backward": [c_vp, c_vp, c_u32, c_vp, c_vp],
     "ngp_nerf_composite_loss": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
-                                c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+                                c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_fused_optimizer_step": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
                                  c_i32, c_i32, c_f32, c_f32, c_f32, c_i32, c_i32, c_u32, c_vp, c_vp,
-                                 c_vp, c_vp],
+                                 c_vp, c_vp, c_vp],
 }
 _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,

@@ -238,6 +238,94 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
     }
 }
 
+// Forward without dy_dx: two lanes per (point, level). The lane with x bit b
+// gathers the 2^(D-1) corners whose x offset is b, which neighbour its
+// partner's (x prime 1 / dense stride 1): each gather instruction touches one
+// cache line per lane PAIR. The partner's values arrive by one shuffle and
+// both lanes accumulate all 2^D corners in the reference's order, so the
+// result is bit-identical to k_grid_fwd; the even lane stores it.
+template <typename T, typename E, uint32_t D, uint32_t C>
+__global__ void __launch_bounds__(256)
+k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
+                const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
+                GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+                int32_t out_layout, InMap im) {
+    using A = Acc<T>;
+    using F = typename A::F;
+    const uint32_t b = blockIdx.x * (blockDim.x / 2) + (threadIdx.x >> 1);
+    const uint32_t xbit = threadIdx.x & 1;
+    const uint32_t level = blockIdx.y;
+    const bool live = b < rows_of(B, im);
+    if (__ballot(live) == 0) return;  // wave-uniform exit; pairs stay together below
+
+    float x[D];
+    bool oob = !live;
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        x[d] = live ? inputs[(size_t)b * D + d] : 0.5f;
+        if (im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
+        if (x[d] < 0 || x[d] > 1) oob = true;
+    }
+    T* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C
+                             : outputs + ((size_t)b * L + level) * C;
+
+    const uint32_t off0 = (uint32_t)offsets[level];
+    const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
+    const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
+    const E* __restrict__ g = grid + (size_t)off0 * C;
+    const float scale = lv.scale[level];
+    const uint32_t resolution = lv.res[level];
+
+    float pos[D];
+    uint32_t pg[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        pos[d] = fmaf(x[d], scale, align_corners ? 0.0f : 0.5f);
+        pg[d] = (uint32_t)floorf(pos[d]);
+        pos[d] -= (float)pg[d];
+        if (interp == 1) pos[d] = smoothstep(pos[d]);
+    }
+    // this lane's corners: idx = (rest << 1) | xbit
+    F mine[1u << (D - 1)][C];
+#pragma unroll
+    for (uint32_t rest = 0; rest < (1u << (D - 1)); rest++) {
+        const uint32_t idx = (rest << 1) | xbit;
+        uint32_t pl[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; d++) pl[d] = (idx & (1u << d)) ? pg[d] + 1 : pg[d];
+        if (!oob) {
+            const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
+            load_entry_as<T, E, C>(g + (size_t)e * C, mine[rest]);
+        } else {
+#pragma unroll
+            for (uint32_t c = 0; c < C; ++c) mine[rest][c] = 0;
+        }
+    }
+    typename A::S res[C];
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) res[c] = A::zero();
+#pragma unroll
+    for (uint32_t idx = 0; idx < (1u << D); idx++) {
+        float w = 1;
+#pragma unroll
+        for (uint32_t d = 0; d < D; d++) w *= (idx & (1u << d)) ? pos[d] : 1 - pos[d];
+        const uint32_t rest = idx >> 1;
+#pragma unroll
+        for (uint32_t c = 0; c < C; ++c) {
+            const F other = (F)__shfl_xor((float)mine[rest][c], 1, 64);
+            const F v = ((idx & 1u) == xbit) ? mine[rest][c] : other;
+            res[c] = A::mac(res[c], (F)w, v);
+        }
+    }
+    if (live && xbit == 0) {
+        if (oob) {
+#pragma unroll
+            for (uint32_t c = 0; c < C; ++c) res[c] = A::zero();
+        }
+        store_entry<T, C>(out, res);
+    }
+}
+
 // ---- scatter-add of one corner's C channels (values already weighted) -----
 template <typename T, uint32_t C> struct Scatter;
 template <uint32_t C> struct Scatter<float, C> {
@@ -271,19 +359,25 @@ template <uint32_t C> struct Scatter<ngp_half, C> {
     }
 };
 
-// Scatter-add with wave-level merging of identical targets.
+// Scatter-add with corner pairing and wave-level merging of identical targets.
 //
-// Samples arrive ordered along rays, so on the coarse levels many consecutive
-// lanes of a wave hit the same cell (level 0 cells hold ~40 consecutive
-// samples at Lego step sizes) and the reference's one-atomic-per-(point,
-// corner) serialises on the memory-side atomic unit. Per corner, lanes whose
-// target equals their left neighbour's form a run; a segmented inclusive scan
-// (shuffles) sums each run into its last lane, which issues ONE atomic for the
-// whole run. A ballot skips the scan when no two adjacent lanes collide (the
-// fine hashed levels), so those pay one shuffle + one ballot per corner.
-// For fp16 tables each run adds (half)(sum of w*g) instead of rounding every
-// term (the reference rounds each term, gridencoder.cu:325), i.e. the same
-// values with fewer roundings.
+// Float atomics execute at the memory side, one 64-B request per distinct
+// 64-B segment a wave instruction touches (MI355X_MICROARCH.md "Global float
+// atomics"), so the request count, not the add count, sets the time. Two
+// lanes per (point, level): lane pair (2s, 2s+1) handles the corners with
+// x = floor and x = floor + 1 of point s, which are neighbouring entries on
+// dense levels and on hashed ones (the x prime of the hash is 1), i.e. one
+// request per pair instead of two. Each lane then walks the 2^(D-1) corners
+// of the remaining dimensions.
+//
+// Samples arrive ordered along rays, so on the coarse levels consecutive
+// points hit the same cell: per corner, lanes whose target equals that of the
+// lane two to the left (same x parity) form a run; a segmented inclusive scan
+// (stride-2 shuffles) sums each run into its last lane, which issues ONE
+// atomic for the whole run. A ballot skips the scan when nothing collides
+// (the fine hashed levels). For fp16 tables each run adds (half)(sum of w*g)
+// instead of rounding every term (the reference rounds each term,
+// gridencoder.cu:325), i.e. the same values with fewer roundings.
 template <typename T, uint32_t D, uint32_t C>
 __global__ void __launch_bounds__(256)
 k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
@@ -292,7 +386,8 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
            int32_t grad_layout, InMap im) {
     using A = Acc<T>;
     using F = typename A::F;
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = blockIdx.x * (blockDim.x / 2) + (threadIdx.x >> 1);
+    const uint32_t xbit = threadIdx.x & 1;
     const uint32_t level = blockIdx.y;
     const int lane = (int)(threadIdx.x & 63);
 
@@ -334,7 +429,8 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
     }
 
 #pragma unroll
-    for (uint32_t idx = 0; idx < (1u << D); idx++) {
+    for (uint32_t rest = 0; rest < (1u << (D - 1)); rest++) {
+        const uint32_t idx = (rest << 1) | xbit;  // corner bits, dimension 0 = x from the lane
         float w = 1;
         uint32_t pl[D];
 #pragma unroll
@@ -353,29 +449,29 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #pragma unroll
         for (uint32_t c = 0; c < C; ++c) v[c] = (F)w * gcur[c];
 
-        const uint32_t kprev = __shfl_up(key, 1, 64);
-        const bool same = lane > 0 && kprev == key;
+        const uint32_t kprev = __shfl_up(key, 2, 64);
+        const bool same = lane > 1 && kprev == key;
         if (__ballot(same) == 0) {
             if (valid) Scatter<T, C>::add(gg + (size_t)key * C, v);
             continue;
         }
-        // run start = inclusive max-scan of head positions
+        // run start (same parity) = inclusive max-scan of head positions
         int start = same ? 0 : lane;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
+        for (int o = 2; o < 64; o <<= 1) {
             const int t = __shfl_up(start, o, 64);
             if (lane >= o) start = max(start, t);
         }
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
+        for (int o = 2; o < 64; o <<= 1) {
 #pragma unroll
             for (uint32_t c = 0; c < C; ++c) {
                 const F t = __shfl_up(v[c], o, 64);
                 if (lane - o >= start) v[c] += t;
             }
         }
-        const uint32_t knext = __shfl_down(key, 1, 64);
-        const bool tail = lane == 63 || knext != key;
+        const uint32_t knext = __shfl_down(key, 2, 64);
+        const bool tail = lane >= 62 || knext != key;
         if (valid && tail) Scatter<T, C>::add(gg + (size_t)key * C, v);
     }
 }
@@ -478,6 +574,17 @@ int fwd_c(const float* inputs, const void* emb, const int32_t* offsets, void* ou
     const E* e = (const E*)emb;
     T* o = (T*)out;
     T* dd = (T*)dy_dx;
+    if (!dd && (sizeof(T) <= 4)) {
+        const dim3 gp(ngp_div_up(B, 128), L);
+        switch (C) {
+            case 1: k_grid_fwd_pair<T, E, D, 1><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
+            case 2: k_grid_fwd_pair<T, E, D, 2><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
+            case 4: k_grid_fwd_pair<T, E, D, 4><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
+            case 8: k_grid_fwd_pair<T, E, D, 8><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
+            default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: C must be 1, 2, 4, or 8.");
+        }
+        return ngp_check_launch("grid_encode_forward");
+    }
     switch (C) {
         case 1: k_grid_fwd<T, E, D, 1><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout, im); break;
         case 2: k_grid_fwd<T, E, D, 2><<<grid, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, dd, gridtype, ac, interp, layout, im); break;
@@ -507,7 +614,7 @@ int bwd_one(const void* grad, const float* inputs, const int32_t* offsets, void*
             uint32_t B, uint32_t L, const GridLevels& lv, const void* dy_dx, void* grad_inputs,
             uint32_t gridtype, bool ac, uint32_t interp, int32_t layout, hipStream_t st,
             const InMap& im) {
-    const dim3 grid(ngp_div_up(B, 256), L);
+    const dim3 grid(ngp_div_up(B, 128), L);  // two lanes per point (corner pairs)
     k_grid_bwd<T, D, C><<<grid, 256, 0, st>>>((const T*)grad, inputs, offsets, (T*)gemb, B, L, lv,
                                                gridtype, ac, interp, layout, im);
     if (dy_dx && grad_inputs) {

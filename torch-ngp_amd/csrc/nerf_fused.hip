@@ -212,7 +212,7 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
                  const float* __restrict__ gt, const float* __restrict__ bg, LossArgs la,
                  StepState* __restrict__ st, ngp_half* __restrict__ grad_color_out,
                  ngp_half* __restrict__ grad_h, float* __restrict__ out_image,
-                 float* __restrict__ out_ws) {
+                 float* __restrict__ out_ws, float* __restrict__ loss_ray) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t n = blockIdx.x * kLossWaves + (threadIdx.x >> 6);
     if (n >= N) return;
@@ -271,7 +271,8 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     }
     const float e0 = p0 - q0, e1 = p1 - q1, e2 = p2 - q2;
     if (lane == 0) {
-        atomicAdd(&st->loss_sum, ((e0 * e0 + e1 * e1) + e2 * e2) * la.inv_c);
+        // per-ray loss; summed by k_step_end (one reduction, no contended atomics)
+        loss_ray[n] = ((e0 * e0 + e1 * e1) + e2 * e2) * la.inv_c;
         if (out_image) {
             out_image[index * 3] = p0; out_image[index * 3 + 1] = p1; out_image[index * 3 + 2] = p2;
         }
@@ -467,11 +468,24 @@ struct ScalerArgs {
     float inv_n;
 };
 
-// GradScaler.update, LambdaLR epoch, Adam step count, loss bookkeeping;
-// also records this step's sample count into step_counter[iter % 16]
-__global__ void k_step_end(StepState* __restrict__ st, ScalerArgs sa, const int32_t* __restrict__ counter,
-                           int32_t* __restrict__ step_counter) {
+// GradScaler.update, LambdaLR epoch, Adam step count, loss bookkeeping (mean
+// of the per-ray losses, fixed-order tree sum); also records this step's
+// sample count into step_counter[iter % 16]
+__global__ void __launch_bounds__(256)
+k_step_end(StepState* __restrict__ st, ScalerArgs sa, const int32_t* __restrict__ counter,
+           int32_t* __restrict__ step_counter, const float* __restrict__ loss_ray, uint32_t n_rays) {
+    __shared__ float part[256];
+    float acc = 0.0f;
+    if (loss_ray)
+        for (uint32_t i = threadIdx.x; i < n_rays; i += 256) acc += loss_ray[i];
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+        __syncthreads();
+    }
     if (threadIdx.x != 0) return;
+    if (loss_ray) st->loss_sum = part[0];
     const bool inf = st->found_inf != 0;
     if (sa.enabled) {
         if (inf) {
@@ -579,7 +593,9 @@ extern "C" int ngp_nerf_composite_loss(const float* sigma, const void* color_out
                                        uint32_t N, float T_thresh, float density_scale,
                                        const float* gt, uint32_t gt_channels, const float* bg,
                                        void* state, void* grad_color_out, void* grad_h_sigma,
-                                       float* out_image, float* out_ws, void* stream) {
+                                       float* out_image, float* out_ws, float* loss_ray,
+                                       void* stream) {
+    NGP_REQUIRE(loss_ray, NGP_ERR_ARG, "composite_loss: loss_ray [N] buffer required");
     NGP_REQUIRE(gt_channels == 3 || gt_channels == 4, NGP_ERR_ARG, "composite_loss: gt must be RGB or RGBA");
     if (N == 0) return NGP_OK;
     LossArgs la;
@@ -591,7 +607,7 @@ extern "C" int ngp_nerf_composite_loss(const float* sigma, const void* color_out
     k_composite_loss<<<ngp_div_up(N, kLossWaves), kLossWaves * 64, 0, ngp_stream(stream)>>>(
         sigma, (const ngp_half*)color_out, (const ngp_half*)h_sigma, deltas, rays, M, N, gt, bg, la,
         static_cast<StepState*>(state), (ngp_half*)grad_color_out, (ngp_half*)grad_h_sigma, out_image,
-        out_ws);
+        out_ws, loss_ray);
     return ngp_check_launch("nerf_composite_loss");
 }
 
@@ -603,7 +619,8 @@ extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params,
                                         float growth_factor, float backoff_factor,
                                         int32_t growth_interval, int32_t scaler_enabled,
                                         uint32_t num_rays, const int32_t* counter,
-                                        int32_t* step_counter, void* state, void* stream) {
+                                        int32_t* step_counter, const float* loss_ray, void* state,
+                                        void* stream) {
     NGP_REQUIRE(n_tensors >= 1 && n_tensors <= kMaxTensors, NGP_ERR_ARG,
                 "fused_optimizer_step: 1..%d tensors", kMaxTensors);
     for (int k = 0; k < n_tensors; ++k)
@@ -623,6 +640,6 @@ extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params,
     k_adam_multi<<<sweep_blocks(total, 4), 256, 0, s>>>(tl, st, aa);
     ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled,
                   num_rays ? 1.0f / (float)num_rays : 0.0f};
-    k_step_end<<<1, 64, 0, s>>>(st, sa, counter, step_counter);
+    k_step_end<<<1, 256, 0, s>>>(st, sa, counter, step_counter, loss_ray, num_rays);
     return ngp_check_launch("fused_optimizer_step");
 }

@@ -975,12 +975,12 @@ extern "C" size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_
     return march_ts_bytes(N, max_steps) + occ_image_bytes(L) + occ_scratch_bytes(L);
 }
 
-extern "C" int ngp_march_rays_train(const float* rays_o, const float* rays_d, const uint8_t* grid,
-                                    float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
-                                    uint32_t C, uint32_t H, uint32_t M, const float* nears,
-                                    const float* fars, float* xyzs, float* dirs, float* deltas,
-                                    int32_t* rays, int32_t* counter, const float* noises,
-                                    void* workspace, size_t workspace_bytes, void* stream) {
+static int march_train_impl(const float* rays_o, const float* rays_d, const uint8_t* grid,
+                             float bound, float dt_gamma, uint32_t max_steps, uint32_t N, uint32_t C,
+                             uint32_t H, uint32_t M, const float* nears, const float* fars,
+                             float* xyzs, float* dirs, float* deltas, int32_t* rays, int32_t* counter,
+                             const float* noises, void* workspace, size_t workspace_bytes,
+                             bool build_image, void* stream) {
     if (int e = check_cascade(C, H, max_steps)) return e;
     NGP_REQUIRE(rays && counter, NGP_ERR_ARG, "march_rays_train: null rays/counter");
     if (N == 0) return NGP_OK;
@@ -997,7 +997,7 @@ extern "C" int ngp_march_rays_train(const float* rays_o, const float* rays_d, co
     const uint32_t blocks = wgs < kMaxMarchBlocks ? wgs : kMaxMarchBlocks;
     float* ts = static_cast<float*>(workspace);
     uint8_t* img = static_cast<uint8_t*>(workspace) + march_ts_bytes(N, max_steps);
-    if (L.ngroups) {
+    if (L.ngroups && build_image) {
         uint32_t* cnt = reinterpret_cast<uint32_t*>(img + occ_image_bytes(L));
         const uint32_t wg = ngp_div_up(L.ngroups, kBuildThreads);
         k_occ_count<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
@@ -1009,6 +1009,47 @@ extern "C" int ngp_march_rays_train(const float* rays_o, const float* rays_d, co
     k_march_emit<<<dim3(groups, kEmitSplit), kMarchThreads, 0, st>>>(rays_o, rays_d, k, N, M, nears, noises,
                                                                     ts, xyzs, dirs, deltas, rays);
     return ngp_check_launch("march_rays_train");
+}
+
+extern "C" int ngp_march_rays_train(const float* rays_o, const float* rays_d, const uint8_t* grid,
+                                    float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
+                                    uint32_t C, uint32_t H, uint32_t M, const float* nears,
+                                    const float* fars, float* xyzs, float* dirs, float* deltas,
+                                    int32_t* rays, int32_t* counter, const float* noises,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+    return march_train_impl(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, M, nears, fars,
+                            xyzs, dirs, deltas, rays, counter, noises, workspace, workspace_bytes, true,
+                            stream);
+}
+
+extern "C" int ngp_march_occupancy_build(const uint8_t* grid, uint32_t C, uint32_t H, uint32_t N,
+                                         uint32_t max_steps, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+    if (int e = check_cascade(C, H, max_steps)) return e;
+    const size_t need = ngp_march_rays_train_workspace_bytes(N, max_steps, C, H);
+    NGP_REQUIRE(workspace && workspace_bytes >= need, NGP_ERR_ARG,
+                "march_occupancy_build: workspace of %zu bytes required, got %zu", need, workspace_bytes);
+    const OccLayout L = occ_layout(grid, C, H);
+    if (!L.ngroups) return NGP_OK;
+    hipStream_t st = ngp_stream(stream);
+    uint8_t* img = static_cast<uint8_t*>(workspace) + march_ts_bytes(N, max_steps);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(img + occ_image_bytes(L));
+    const uint32_t wg = ngp_div_up(L.ngroups, kBuildThreads);
+    k_occ_count<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
+    k_occ_compact<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
+    return ngp_check_launch("march_occupancy_build");
+}
+
+extern "C" int ngp_march_rays_train_prebuilt(const float* rays_o, const float* rays_d,
+                                             const uint8_t* grid, float bound, float dt_gamma,
+                                             uint32_t max_steps, uint32_t N, uint32_t C, uint32_t H,
+                                             uint32_t M, const float* nears, const float* fars,
+                                             float* xyzs, float* dirs, float* deltas, int32_t* rays,
+                                             int32_t* counter, const float* noises, void* workspace,
+                                             size_t workspace_bytes, void* stream) {
+    return march_train_impl(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, M, nears, fars,
+                            xyzs, dirs, deltas, rays, counter, noises, workspace, workspace_bytes, false,
+                            stream);
 }
 
 extern "C" int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs,

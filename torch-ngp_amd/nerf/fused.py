@@ -68,11 +68,13 @@ class FusedTrainer:
         self.rays_o, self.rays_d = z(N, 3), z(N, 3)
         self.rgba, self.bg = z(N, 4), z(N, 3)
         self.nears, self.fars, self.noises = z(N), z(N), z(N)
+        self.loss_ray = z(N)
         self.counter = z(2, dtype=torch.int32)
         self.rays = z(N, 3, dtype=torch.int32)
         self.xyzs, self.dirs, self.deltas = z(M, 3), z(M, 3), z(M, 2)
         ws = nat.lib().ngp_march_rays_train_workspace_bytes(N, self.max_steps, model.cascade, model.grid_size)
         self.march_ws = z(ws, dtype=torch.uint8)
+        self.refresh_occupancy()
         h = torch.float16
         self.enc_out, self.h_sigma = z(M, 32, dtype=h), z(M, 16, dtype=h)
         self.sigma, self.color_in, self.color_out = z(M), z(M, 32, dtype=h), z(M, 16, dtype=h)
@@ -113,6 +115,15 @@ class FusedTrainer:
         self.graph = None
         self.graph_opt = None
 
+    def refresh_occupancy(self):
+        """Rebuild the marcher's occupancy image after density_bitfield changed
+        (model.update_extra_state); the captured step reuses it."""
+        m = self.model
+        nat.check(nat.lib().ngp_march_occupancy_build(
+            nat.ptr(m.density_bitfield), m.cascade, m.grid_size, self.N, self.max_steps,
+            nat.ptr(self.march_ws), self.march_ws.numel(), nat.stream_of(self.march_ws)),
+            "march_occupancy_build")
+
     # ------------------------------------------------------------------ step
     def _launch(self):
         self._sample()
@@ -140,7 +151,7 @@ class FusedTrainer:
         m, e = self.model, self.enc
         M, N, cnt = self.M, self.N, P(self.counter)
         chk = nat.check
-        chk(lib.ngp_march_rays_train(P(self.rays_o), P(self.rays_d), P(m.density_bitfield),
+        chk(lib.ngp_march_rays_train_prebuilt(P(self.rays_o), P(self.rays_d), P(m.density_bitfield),
                                      float(m.bound), self.dt_gamma, self.max_steps, N, m.cascade,
                                      m.grid_size, M, P(self.nears), P(self.fars), P(self.xyzs),
                                      P(self.dirs), P(self.deltas), P(self.rays), cnt, P(self.noises),
@@ -159,7 +170,7 @@ class FusedTrainer:
         chk(lib.ngp_nerf_composite_loss(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
                                         P(self.rays), M, N, self.T_thresh, float(m.density_scale),
                                         P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
-                                        P(self.g_h), None, None, s), "composite_loss")
+                                        P(self.g_h), None, None, P(self.loss_ray), s), "composite_loss")
         chk(lib.ngp_ffmlp_backward_rows(P(self.g_color_out), P(self.color_in), P(self.w_half[2]), M, cnt,
                                         32, 16, cn.hidden_dim, cn.num_layers, _RELU, P(self.g_color_in),
                                         P(self.grads[2]), _F16, P(self.mlp_ws[1]), self.mlp_ws[1].numel(),
@@ -179,7 +190,7 @@ class FusedTrainer:
         chk(lib.ngp_fused_optimizer_step(3, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"],
                                          self.lr, self.betas[0], self.betas[1], self.eps, self.iters, 1,
                                          1.0 / self.world, 2.0, 0.5, self.growth_interval, 1, N, cnt,
-                                         P(m.step_counter),
+                                         P(m.step_counter), P(self.loss_ray),
                                          P(self.state), s), "fused_optimizer_step")
 
     def step(self):
