@@ -283,7 +283,8 @@ def kernel_profile(ft, reps):
     sn, cn = ft.sig_net, ft.col_net
     calls = {
         "grid_encode_backward": lambda: lib.ngp_grid_encode_backward_fused(
-            P(ft.g_enc), P(ft.xyzs), float(m.bound), P(e.offsets), P(ft.grads[0]), M, cnt, *ga),
+            P(ft.g_enc), P(ft.xyzs), float(m.bound), P(e.offsets), P(ft.grads[0]), M, cnt, *ga[:-1],
+            ft._offsets_host, P(ft.grid_ws), ft.grid_ws.numel(), s),
         "grid_encode_forward": lambda: lib.ngp_grid_encode_forward_fused(
             P(ft.xyzs), float(m.bound), P(e.embeddings), P(e.offsets), P(ft.enc_out), M, cnt, *ga),
         "march_rays_train": lambda: lib.ngp_march_rays_train_prebuilt(

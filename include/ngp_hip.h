@@ -225,11 +225,19 @@ int ngp_grid_encode_forward_fused(const float* xyz, float bound, const float* em
                                   const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
                                   uint32_t H, uint32_t gridtype, int32_t align_corners,
                                   uint32_t interp, void* stream);
+/* Binned backward (hashed levels without scattered atomics) when workspace is
+ * given: offsets_host is a host copy of offsets; the workspace (size from
+ * ngp_grid_encode_backward_fused_workspace_bytes, 0 if nothing is binned) must
+ * be zero-filled before its first use and is left ready for the next call. */
+size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                                      float S, uint32_t H, int32_t align_corners,
+                                                      const int32_t* offsets_host);
 int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
                                    const int32_t* offsets, void* grad_embeddings, uint32_t B,
                                    const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
                                    uint32_t H, uint32_t gridtype, int32_t align_corners,
-                                   uint32_t interp, void* stream);
+                                   uint32_t interp, const int32_t* offsets_host, void* workspace,
+                                   size_t workspace_bytes, void* stream);
 int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, uint32_t B, const int32_t* count,
                            uint32_t in_dim, uint32_t output_dim, uint32_t hidden_dim,
                            uint32_t num_layers, uint32_t activation, uint32_t output_activation,

@@ -383,12 +383,12 @@ __global__ void __launch_bounds__(256)
 k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
            const int32_t* __restrict__ offsets, T* __restrict__ grad_grid, uint32_t B, uint32_t L,
            GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
-           int32_t grad_layout, InMap im) {
+           int32_t grad_layout, InMap im, uint32_t level0) {
     using A = Acc<T>;
     using F = typename A::F;
     const uint32_t b = blockIdx.x * (blockDim.x / 2) + (threadIdx.x >> 1);
     const uint32_t xbit = threadIdx.x & 1;
-    const uint32_t level = blockIdx.y;
+    const uint32_t level = level0 + blockIdx.y;
     const int lane = (int)(threadIdx.x & 63);
 
     bool valid = b < rows_of(B, im);
@@ -474,6 +474,224 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
         const bool tail = lane >= 62 || knext != key;
         if (valid && tail) Scatter<T, C>::add(gg + (size_t)key * C, v);
     }
+}
+
+// ---- binned backward for the hashed levels (fused train step) ----------------
+// Scattered atomics on the hashed levels cost one memory-side request per
+// (point, corner pair) whatever is done (no reuse between points at those
+// resolutions), ~180 us per Lego step. Instead, the corner contributions of a
+// hashed level are sorted into bins of 2^13 table entries: each workgroup
+// (256 points of one level) ranks its 2048 contributions per bin in LDS,
+// reserves space per bin with one atomic, and writes each bin's run
+// contiguously; then one workgroup per bin sums its contributions in an LDS
+// fp32 image of the bin's entries and adds that image to the fp16 table with
+// plain loads/stores (every entry has one owner). Contributions are rounded
+// to half per term, like the reference's Half += float (gridencoder.cu:325),
+// and summed in fp32. Bins that overflow their capacity fall back to atomics.
+constexpr uint32_t kBinShift = 13;
+constexpr uint32_t kBinEntries = 1u << kBinShift;
+constexpr uint32_t kMaxBinsPerLevel = 256;
+
+struct BinPlan {
+    uint32_t first_level;            // levels [first_level, L) are binned
+    uint32_t total_bins;
+    uint32_t cap;                    // contributions per bin
+    uint32_t nbins[kMaxLevels];
+    uint32_t bin0[kMaxLevels];
+};
+
+struct BinItem {
+    uint32_t e;                      // entry within the bin (| bin << 16 while staged)
+    ngp_half2 v;
+};
+
+template <uint32_t D>
+__global__ void __launch_bounds__(256)
+k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
+               const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
+               uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+               InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items) {
+    constexpr uint32_t C = 2, NC = 1u << D;
+    __shared__ uint32_t cnt[kMaxBinsPerLevel], base[kMaxBinsPerLevel], soff[kMaxBinsPerLevel + 1];
+    __shared__ BinItem stage[256 * NC];
+    const uint32_t level = bp.first_level + blockIdx.y;
+    const uint32_t nb = bp.nbins[level];
+    for (uint32_t t = threadIdx.x; t < nb; t += 256) cnt[t] = 0;
+    __syncthreads();
+
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    bool valid = b < rows_of(B, im);
+    float x[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        x[d] = valid ? inputs[(size_t)b * D + d] : 0.5f;
+        if (valid && im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
+        if (x[d] < 0 || x[d] > 1) valid = false;
+    }
+    const uint32_t off0 = (uint32_t)offsets[level];
+    const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
+    const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
+    const float scale = lv.scale[level];
+    const uint32_t resolution = lv.res[level];
+    float pos[D];
+    uint32_t pg[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; d++) {
+        pos[d] = fmaf(x[d], scale, align_corners ? 0.0f : 0.5f);
+        pg[d] = (uint32_t)floorf(pos[d]);
+        pos[d] -= (float)pg[d];
+        if (interp == 1) pos[d] = smoothstep(pos[d]);
+    }
+    float g0 = 0.0f, g1 = 0.0f;
+    if (valid) {
+        const ngp_half2 gv = *reinterpret_cast<const ngp_half2*>(grad + ((size_t)b * L + level) * C);
+        g0 = (float)gv[0];
+        g1 = (float)gv[1];
+    }
+    if (g0 == 0.0f && g1 == 0.0f) valid = false;  // nothing to add (e.g. samples past the early stop)
+
+    uint32_t key[NC], rank[NC];
+    ngp_half2 val[NC];
+#pragma unroll
+    for (uint32_t idx = 0; idx < NC; idx++) {
+        float w = 1;
+        uint32_t pl[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; d++) {
+            if ((idx & (1u << d)) == 0) {
+                w *= 1 - pos[d];
+                pl[d] = pg[d];
+            } else {
+                w *= pos[d];
+                pl[d] = pg[d] + 1;
+            }
+        }
+        key[idx] = valid ? grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl) : 0u;
+        val[idx] = ngp_half2{(ngp_half)(w * g0), (ngp_half)(w * g1)};
+        rank[idx] = valid ? atomicAdd(&cnt[key[idx] >> kBinShift], 1u) : 0u;
+    }
+    __syncthreads();
+    // reserve each bin's run; exclusive scan of the counts for the staging layout
+    for (uint32_t t = threadIdx.x; t < nb; t += 256) {
+        const uint32_t c = cnt[t];
+        uint32_t bs = 0;
+        if (c) {
+            bs = atomicAdd(&cursor[bp.bin0[level] + t], c);
+            if (bs + c > bp.cap) bs = 0xffffffffu;  // overflow: this block's items of bin t go atomic
+        }
+        base[t] = bs;
+    }
+    {   // block-wide exclusive scan of cnt[0..nb) (nb <= 256 = blockDim)
+        __shared__ uint32_t wsum[4];
+        const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+        const uint32_t v = t < nb ? cnt[t] : 0u;
+        uint32_t incl = v;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 4; ++w) {
+            before += w < wv ? wsum[w] : 0u;
+            all += wsum[w];
+        }
+        if (t < nb) soff[t] = before + incl - v;
+        if (t == 0) soff[nb] = all;
+    }
+    __syncthreads();
+    if (valid) {
+        ngp_half* gg = grad_grid + (size_t)off0 * C;
+#pragma unroll
+        for (uint32_t idx = 0; idx < NC; idx++) {
+            const uint32_t bin = key[idx] >> kBinShift;
+            if (base[bin] == 0xffffffffu) {
+                __builtin_amdgcn_global_atomic_fadd_v2f16(reinterpret_cast<ngp_half2*>(gg + (size_t)key[idx] * C),
+                                                          val[idx]);
+            } else {
+                stage[soff[bin] + rank[idx]] = BinItem{(key[idx] & (kBinEntries - 1)) | (bin << 16), val[idx]};
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t total = soff[nb];
+    for (uint32_t k = threadIdx.x; k < total; k += 256) {
+        const BinItem it = stage[k];
+        const uint32_t bin = it.e >> 16;
+        if (base[bin] == 0xffffffffu) continue;
+        BinItem* dst = items + (size_t)(bp.bin0[level] + bin) * bp.cap + base[bin] + (k - soff[bin]);
+        *dst = BinItem{it.e & 0xffffu, it.v};
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t L,
+                 BinPlan bp, uint32_t* __restrict__ cursor, const BinItem* __restrict__ items) {
+    constexpr uint32_t C = 2;
+    __shared__ float acc[kBinEntries * C];
+    const uint32_t g = blockIdx.x;
+    uint32_t level = bp.first_level;
+    while (level + 1 < L && g >= bp.bin0[level + 1]) ++level;
+    const uint32_t lbin = g - bp.bin0[level];
+    for (uint32_t t = threadIdx.x; t < kBinEntries * C; t += 256) acc[t] = 0.0f;
+    __syncthreads();
+    const uint32_t n = min(cursor[g], bp.cap);
+    const BinItem* src = items + (size_t)g * bp.cap;
+    for (uint32_t k = threadIdx.x; k < n; k += 256) {
+        const BinItem it = src[k];
+        atomicAdd(&acc[it.e * C], (float)it.v[0]);
+        atomicAdd(&acc[it.e * C + 1], (float)it.v[1]);
+    }
+    __syncthreads();
+    const uint32_t off0 = (uint32_t)offsets[level];
+    const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
+    const uint32_t e0 = lbin * kBinEntries;
+    const uint32_t ne = min(kBinEntries, hs - e0);
+    ngp_half2* tbl = reinterpret_cast<ngp_half2*>(grad_grid + ((size_t)off0 + e0) * C);
+    for (uint32_t e = threadIdx.x; e < ne; e += 256) {
+        const float a0 = acc[e * C], a1 = acc[e * C + 1];
+        if (a0 == 0.0f && a1 == 0.0f) continue;
+        const ngp_half2 old = tbl[e];
+        tbl[e] = ngp_half2{(ngp_half)((float)old[0] + a0), (ngp_half)((float)old[1] + a1)};
+    }
+    if (threadIdx.x == 0) cursor[g] = 0;  // ready for the next step
+}
+
+// Host-side plan from a host copy of the offsets: the binned levels are the
+// hashed suffix whose tables hold at least 8 bins.
+static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D, const GridLevels& lv,
+                             bool align_corners, uint32_t B) {
+    BinPlan bp{};
+    bp.first_level = L;
+    for (int l = (int)L - 1; l >= 0; --l) {
+        const uint32_t hs = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
+        const double side = (double)(align_corners ? lv.res[l] : lv.res[l] + 1);
+        const bool hashed = std::pow(side, (double)D) > (double)hs;
+        const uint32_t nb = (hs + kBinEntries - 1) / kBinEntries;
+        if (!hashed || nb < 8 || nb > kMaxBinsPerLevel) break;
+        bp.first_level = (uint32_t)l;
+    }
+    uint32_t total = 0, maxnb = 1;
+    for (uint32_t l = bp.first_level; l < L; ++l) {
+        const uint32_t hs = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
+        bp.nbins[l] = (hs + kBinEntries - 1) / kBinEntries;
+        bp.bin0[l] = total;
+        total += bp.nbins[l];
+        maxnb = bp.nbins[l] > maxnb ? bp.nbins[l] : maxnb;
+    }
+    for (uint32_t l = L; l < kMaxLevels; ++l) bp.bin0[l] = total;
+    bp.total_bins = total;
+    // twice the mean load of a bin (corners spread uniformly by the hash) + slack
+    bp.cap = (uint32_t)(2ull * ((uint64_t)B * (1u << D) + maxnb - 1) / maxnb + 2048);
+    return bp;
+}
+
+static size_t bin_workspace_bytes(const BinPlan& bp) {
+    const size_t cur = ((size_t)bp.total_bins * 4 + 255) / 256 * 256;
+    return cur + (size_t)bp.total_bins * bp.cap * sizeof(BinItem);
 }
 
 template <typename T, uint32_t D, uint32_t C>
@@ -616,7 +834,7 @@ int bwd_one(const void* grad, const float* inputs, const int32_t* offsets, void*
             const InMap& im) {
     const dim3 grid(ngp_div_up(B, 128), L);  // two lanes per point (corner pairs)
     k_grid_bwd<T, D, C><<<grid, 256, 0, st>>>((const T*)grad, inputs, offsets, (T*)gemb, B, L, lv,
-                                               gridtype, ac, interp, layout, im);
+                                               gridtype, ac, interp, layout, im, 0u);
     if (dy_dx && grad_inputs) {
         k_grid_input_bwd<T, D, C><<<ngp_div_up(B * D, 256), 256, 0, st>>>(
             (const T*)grad, (const T*)dy_dx, (T*)grad_inputs, B, L, layout);
@@ -774,18 +992,69 @@ extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, cons
                                   align_corners != 0, interp, 1, ngp_stream(stream), im);
 }
 
+extern "C" size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, uint32_t C,
+                                                                uint32_t L, float S, uint32_t H,
+                                                                int32_t align_corners,
+                                                                const int32_t* offsets_host) {
+    if (!offsets_host || C != 2 || D < 2 || D > 5 || L == 0 || L > kMaxLevels) return 0;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const BinPlan bp = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B);
+    return bp.total_bins ? bin_workspace_bytes(bp) : 0;
+}
+
 extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
                                               const int32_t* offsets, void* grad_embeddings,
                                               uint32_t B, const int32_t* count, uint32_t D,
                                               uint32_t C, uint32_t L, float S, uint32_t H,
                                               uint32_t gridtype, int32_t align_corners,
-                                              uint32_t interp, void* stream) {
+                                              uint32_t interp, const int32_t* offsets_host,
+                                              void* workspace, size_t workspace_bytes,
+                                              void* stream) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
     NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_backward_fused: null xyz or bound <= 0");
     if (B == 0) return NGP_OK;
     GridLevels lv;
     make_levels(lv, L, S, H);
     const InMap im{bound, 1.0f / (2.0f * bound), count};
-    return bwd_t<ngp_half>(grad, xyz, offsets, grad_embeddings, B, D, C, L, lv, nullptr, nullptr,
-                           gridtype, align_corners != 0, interp, 1, ngp_stream(stream), im);
+    hipStream_t st = ngp_stream(stream);
+    const bool ac = align_corners != 0;
+    BinPlan bp{};
+    bp.first_level = L;
+    if (workspace && offsets_host && C == 2 && D == 3) {
+        bp = make_bin_plan(offsets_host, L, D, lv, ac, B);
+        if (bp.total_bins) {
+            NGP_REQUIRE(workspace_bytes >= bin_workspace_bytes(bp), NGP_ERR_ARG,
+                        "grid_encode_backward_fused: workspace of %zu bytes required, got %zu",
+                        bin_workspace_bytes(bp), workspace_bytes);
+        } else {
+            bp.first_level = L;
+        }
+    }
+    // dense (and any unbinned) levels: merged atomics
+    if (bp.first_level > 0) {
+        const dim3 grid(ngp_div_up(B, 128), bp.first_level);
+        switch (D) {
+            case 3:
+                if (C == 2) {
+                    k_grid_bwd<ngp_half, 3, 2><<<grid, 256, 0, st>>>((const ngp_half*)grad, xyz, offsets,
+                        (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, 1, im, 0u);
+                    break;
+                }
+                [[fallthrough]];
+            default:
+                return bwd_t<ngp_half>(grad, xyz, offsets, grad_embeddings, B, D, C, L, lv, nullptr, nullptr,
+                                       gridtype, ac, interp, 1, st, im);
+        }
+    }
+    if (bp.first_level < L) {
+        uint32_t* cursor = static_cast<uint32_t*>(workspace);
+        BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) +
+                                                    ((size_t)bp.total_bins * 4 + 255) / 256 * 256);
+        const dim3 grid(ngp_div_up(B, 256), L - bp.first_level);
+        k_grid_bwd_bin<3><<<grid, 256, 0, st>>>((const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings,
+                                                B, L, lv, gridtype, ac, interp, im, bp, cursor, items);
+        k_grid_bin_accum<<<bp.total_bins, 256, 0, st>>>(offsets, (ngp_half*)grad_embeddings, L, bp, cursor, items);
+    }
+    return ngp_check_launch("grid_encode_backward_fused");
 }

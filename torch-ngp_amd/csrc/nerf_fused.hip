@@ -11,9 +11,10 @@
 //                     rays (get_rays :52-136), analytic RGBA target, random
 //                     background, march noise, near/far (raymarching.cu:91-145)
 //   k_glue_fwd        sigma = ds * exp(h0); color_in = [half(SH4(d)) | h1..15 | 0]
-//   k_composite_loss  per ray (one wave): composite forward, background blend,
-//                     MSE, d loss / d image (AMP-scaled), composite backward,
-//                     cast/sigmoid/trunc_exp backward -> fp16 MLP-output grads
+//   k_composite_loss  per ray (one wave, shuffle scans): composite forward,
+//                     background blend, MSE, d loss / d image (AMP-scaled),
+//                     composite backward, cast/sigmoid/trunc_exp backward ->
+//                     fp16 MLP-output grads
 //   k_glue_bwd        geo-feature grads (color MLP grad_inputs 16..30) -> h1..15
 //   k_nonfinite       GradScaler's inf/nan check over the fp16 grads
 //   k_adam_multi      Adam over all parameter tensors, unscaled fp16 grads,
@@ -192,18 +193,77 @@ k_glue_bwd(const ngp_half* __restrict__ grad_color_in, ngp_half* __restrict__ gr
 }
 
 // ---- composite + loss + backward (one wave per ray) ---------------------------
+// The transmittance recurrence T_{i+1} = T_i (1 - alpha_i) with
+// 1 - alpha_i = exp(-sigma_i delta_i) is T_i = exp(-sum_{j<i} sigma_j delta_j),
+// a prefix sum: each wave composites its ray 64 samples at a time with
+// shuffle scans instead of a serial loop (whose length, up to several hundred
+// samples on rays crossing the Lego body, set the kernel time). The result
+// equals the sequential composite to float rounding (~1e-6 relative); the
+// early stop is the first sample whose T falls below T_thresh, as in
+// raymarching.cu:551/:665. The reference-API composite_rays_train keeps the
+// bit-exact serial form.
 constexpr uint32_t kLossWaves = 4;
 
-NGP_DEV float lanef(float v, uint32_t j) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)j));
-}
 // torch.sigmoid on a half tensor: fp32 math, half result
 NGP_DEV float sigmoid_h(ngp_half x) { return (float)(ngp_half)(1.0f / (1.0f + expf(-(float)x))); }
+
+NGP_DEV float scan_incl(float v, uint32_t lane) {
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+NGP_DEV float wave_sum(float v) {
+#pragma unroll
+    for (uint32_t o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
 
 struct LossArgs {
     float T_thresh, density_scale, inv_n, inv_c;  // inv_n = 1/N, inv_c = 1/3 (torch mean backward)
     uint32_t gt_channels;                         // 4: RGBA with random background, 3: RGB on white
 };
+
+// One 64-sample chunk of a ray: per-lane sample data and the scanned quantities.
+struct Chunk {
+    bool ok, active;                 // lane holds a sample / sample is before the early stop
+    float d0, c0, c1, c2, w, Tafter, t;
+};
+
+NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __restrict__ color_out,
+                         const float* __restrict__ deltas, uint32_t offset, uint32_t base,
+                         uint32_t num_steps, uint32_t lane, float& S, float& tacc, float T_thresh,
+                         bool& stop) {
+    Chunk c;
+    const uint32_t i = offset + base + lane;
+    c.ok = base + lane < num_steps;
+    const float sg = c.ok ? sigma[i] : 0.0f;
+    c.d0 = c.ok ? deltas[(size_t)i * 2] : 0.0f;
+    const float d1 = c.ok ? deltas[(size_t)i * 2 + 1] : 0.0f;
+    c.c0 = c.c1 = c.c2 = 0.0f;
+    if (c.ok) {
+        c.c0 = sigmoid_h(color_out[(size_t)i * 16 + 0]);
+        c.c1 = sigmoid_h(color_out[(size_t)i * 16 + 1]);
+        c.c2 = sigmoid_h(color_out[(size_t)i * 16 + 2]);
+    }
+    const float sd = sg * c.d0;
+    const float incl = scan_incl(sd, lane);
+    const float alpha = 1.0f - expf(-sd);
+    const float Tbefore = expf(-(S + (incl - sd)));
+    c.Tafter = expf(-(S + incl));
+    c.w = alpha * Tbefore;
+    c.t = tacc + scan_incl(d1, lane);
+    const uint64_t below = __ballot(c.ok && c.Tafter < T_thresh);
+    const uint32_t last = below ? (uint32_t)__ffsll((unsigned long long)below) - 1 : 63u;
+    c.active = c.ok && lane <= last;
+    if (!c.active) c.w = 0.0f;
+    stop = below != 0;
+    S += __shfl(incl, 63, 64);
+    tacc = __shfl(c.t, 63, 64);
+    return c;
+}
 
 __global__ void __launch_bounds__(kLossWaves * 64)
 k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ color_out,
@@ -213,6 +273,7 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
                  StepState* __restrict__ st, ngp_half* __restrict__ grad_color_out,
                  ngp_half* __restrict__ grad_h, float* __restrict__ out_image,
                  float* __restrict__ out_ws, float* __restrict__ loss_ray) {
+    typedef _Float16 half8 __attribute__((ext_vector_type(8)));
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t n = blockIdx.x * kLossWaves + (threadIdx.x >> 6);
     if (n >= N) return;
@@ -221,36 +282,19 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     const uint32_t num_steps = (uint32_t)rays[n * 3 + 2];
     const bool valid = num_steps != 0 && offset + num_steps <= M;
 
-    // ---- forward recurrence (composite_rays_train_forward)
-    float T = 1.0f, r = 0, g = 0, b = 0, ws = 0, t = 0, d = 0;
+    // ---- forward (composite_rays_train_forward)
+    float r = 0, g = 0, b = 0, ws = 0, d = 0;
     if (valid) {
+        float S = 0.0f, tacc = 0.0f;
         for (uint32_t base = 0; base < num_steps; base += 64) {
-            const uint32_t i = offset + base + lane;
-            const bool ok = base + lane < num_steps;
-            const float sg = ok ? sigma[i] : 0.0f;
-            const float d0 = ok ? deltas[(size_t)i * 2] : 0.0f;
-            const float d1 = ok ? deltas[(size_t)i * 2 + 1] : 0.0f;
-            float c0 = 0, c1 = 0, c2 = 0;
-            if (ok) {
-                c0 = sigmoid_h(color_out[(size_t)i * 16 + 0]);
-                c1 = sigmoid_h(color_out[(size_t)i * 16 + 1]);
-                c2 = sigmoid_h(color_out[(size_t)i * 16 + 2]);
-            }
-            const float alpha = 1.0f - expf(-sg * d0);
-            const uint32_t cnt = min(64u, num_steps - base);
-            bool stop = false;
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const float a = lanef(alpha, j);
-                const float weight = a * T;
-                r = fmaf(weight, lanef(c0, j), r);
-                g = fmaf(weight, lanef(c1, j), g);
-                b = fmaf(weight, lanef(c2, j), b);
-                t += lanef(d1, j);
-                d = fmaf(weight, t, d);
-                ws += weight;
-                T *= 1.0f - a;
-                if (T < la.T_thresh) { stop = true; break; }
-            }
+            bool stop;
+            const Chunk c = load_chunk(sigma, color_out, deltas, offset, base, num_steps, lane, S, tacc,
+                                       la.T_thresh, stop);
+            r += wave_sum(c.w * c.c0);
+            g += wave_sum(c.w * c.c1);
+            b += wave_sum(c.w * c.c2);
+            ws += wave_sum(c.w);
+            d += wave_sum(c.w * c.t);
             if (stop) break;
         }
     }
@@ -283,13 +327,11 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     const float gr = G * (2.0f * e0), gg = G * (2.0f * e1), gb = G * (2.0f * e2);
     const float gws = -((gr * bg0 + gg * bg1) + gb * bg2);  // d/dws of image + (1 - ws) * bg
     const float gd = 0.0f;                                  // depth is not in the loss
-    const float r_final = r, g_final = g, b_final = b, ws_final = ws, d_final = d;
 
-    // ---- backward recurrence (composite_rays_train_backward) + activation backward
+    // ---- backward (composite_rays_train_backward) + activation backward
     if (!valid) {
         // a ray dropped for overflowing M still owns rows [offset, M): zero their grads
         for (uint32_t k = offset + lane; k < min(offset + num_steps, M); k += 64) {
-            typedef _Float16 half8 __attribute__((ext_vector_type(8)));
             const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
             reinterpret_cast<half8*>(grad_color_out + (size_t)k * 16)[0] = z;
             reinterpret_cast<half8*>(grad_color_out + (size_t)k * 16)[1] = z;
@@ -297,58 +339,41 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
         }
         return;
     }
-    T = 1.0f; r = 0; g = 0; b = 0; t = 0; d = 0;
+    float S = 0.0f, tacc = 0.0f, rr = 0, rg = 0, rb = 0, rd = 0;
     bool stopped = false;
     for (uint32_t base = 0; base < num_steps; base += 64) {
-        const uint32_t i = offset + base + lane;
-        const bool ok = base + lane < num_steps;
-        const float sg = ok ? sigma[i] : 0.0f;
-        const float d0 = ok ? deltas[(size_t)i * 2] : 0.0f;
-        const float d1 = ok ? deltas[(size_t)i * 2 + 1] : 0.0f;
-        float c0 = 0, c1 = 0, c2 = 0;
-        if (ok) {
-            c0 = sigmoid_h(color_out[(size_t)i * 16 + 0]);
-            c1 = sigmoid_h(color_out[(size_t)i * 16 + 1]);
-            c2 = sigmoid_h(color_out[(size_t)i * 16 + 2]);
-        }
-        const float alpha = 1.0f - expf(-sg * d0);
-        const uint32_t cnt = min(64u, num_steps - base);
-        float mw = 0, mT = 0, mr = 0, mg = 0, mb = 0, mt = 0, md = 0;
-        uint32_t done = stopped ? 0u : cnt;
-        if (!stopped) {
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const float a = lanef(alpha, j);
-                const float weight = a * T;
-                r = fmaf(weight, lanef(c0, j), r);
-                g = fmaf(weight, lanef(c1, j), g);
-                b = fmaf(weight, lanef(c2, j), b);
-                t += lanef(d1, j);
-                d = fmaf(weight, t, d);
-                T *= 1.0f - a;
-                if (lane == j) { mw = weight; mT = T; mr = r; mg = g; mb = b; mt = t; md = d; }
-                if (T < la.T_thresh) { done = j + 1; stopped = true; break; }
+        bool stop = false;
+        Chunk c = load_chunk(sigma, color_out, deltas, offset, base, num_steps, lane, S, tacc,
+                             la.T_thresh, stop);
+        if (stopped) { c.active = false; c.w = 0.0f; }
+        // running sums after this lane's sample (inclusive prefix)
+        const float pr = rr + scan_incl(c.w * c.c0, lane);
+        const float pg = rg + scan_incl(c.w * c.c1, lane);
+        const float pb = rb + scan_incl(c.w * c.c2, lane);
+        const float pd = rd + scan_incl(c.w * c.t, lane);
+        rr = __shfl(pr, 63, 64); rg = __shfl(pg, 63, 64); rb = __shfl(pb, 63, 64); rd = __shfl(pd, 63, 64);
+        if (c.ok) {
+            const uint32_t i = offset + base + lane;
+            float gc0 = 0, gc1 = 0, gc2 = 0, gs = 0;
+            if (c.active) {
+                gc0 = gr * c.w; gc1 = gg * c.w; gc2 = gb * c.w;
+                gs = c.d0 * (gr * (c.Tafter * c.c0 - (r - pr)) + gg * (c.Tafter * c.c1 - (g - pg)) +
+                             gb * (c.Tafter * c.c2 - (b - pb)) + gd * (c.Tafter * c.t - (d - pd)) +
+                             gws * (1 - ws));
             }
+            // rgbs.float() <- half, then sigmoid_backward(grad, y) = grad * (1 - y) * y (fp32 math)
+            half8 o0 = {0, 0, 0, 0, 0, 0, 0, 0}, o1 = {0, 0, 0, 0, 0, 0, 0, 0};
+            o0[0] = (ngp_half)((float)(ngp_half)gc0 * (1.0f - c.c0) * c.c0);
+            o0[1] = (ngp_half)((float)(ngp_half)gc1 * (1.0f - c.c1) * c.c1);
+            o0[2] = (ngp_half)((float)(ngp_half)gc2 * (1.0f - c.c2) * c.c2);
+            half8* go = reinterpret_cast<half8*>(grad_color_out + (size_t)i * 16);
+            go[0] = o0;
+            go[1] = o1;
+            // sigmas = ds * trunc_exp(h0): grad_h0 = (gs * ds) * exp(clamp(h0, -15, 15)), -> half
+            const float h0 = (float)h_sigma[(size_t)i * 16];
+            grad_h[(size_t)i * 16] = (ngp_half)((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
         }
-        if (!ok) continue;
-        float gc0 = 0, gc1 = 0, gc2 = 0, gs = 0;
-        if (lane < done) {
-            gc0 = gr * mw; gc1 = gg * mw; gc2 = gb * mw;
-            gs = d0 * (gr * (mT * c0 - (r_final - mr)) + gg * (mT * c1 - (g_final - mg)) +
-                       gb * (mT * c2 - (b_final - mb)) + gd * (mT * mt - (d_final - md)) +
-                       gws * (1 - ws_final));
-        }
-        // rgbs.float() <- half, then sigmoid_backward(grad, y) = grad * (1 - y) * y (fp32 math)
-        typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-        half8 o0 = {0, 0, 0, 0, 0, 0, 0, 0}, o1 = {0, 0, 0, 0, 0, 0, 0, 0};
-        o0[0] = (ngp_half)((float)(ngp_half)gc0 * (1.0f - c0) * c0);
-        o0[1] = (ngp_half)((float)(ngp_half)gc1 * (1.0f - c1) * c1);
-        o0[2] = (ngp_half)((float)(ngp_half)gc2 * (1.0f - c2) * c2);
-        half8* go = reinterpret_cast<half8*>(grad_color_out + (size_t)i * 16);
-        go[0] = o0;
-        go[1] = o1;
-        // sigmas = ds * trunc_exp(h0): grad_h0 = (gs * ds) * exp(clamp(h0, -15, 15)), -> half
-        const float h0 = (float)h_sigma[(size_t)i * 16];
-        grad_h[(size_t)i * 16] = (ngp_half)((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
+        stopped = stopped || stop;
     }
 }
 

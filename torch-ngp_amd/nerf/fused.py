@@ -91,6 +91,11 @@ class FusedTrainer:
         self.exp_avg = [torch.zeros_like(p) for p in self.params]
         self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
         self.w_half = [None] + [p.detach().half() for p in self.params[1:]]
+        self._offsets_host = (ctypes.c_int32 * enc.offsets.numel())(*enc.offsets.cpu().tolist())
+        gb = nat.lib().ngp_grid_encode_backward_fused_workspace_bytes(
+            M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
+            int(enc.align_corners), self._offsets_host)
+        self.grid_ws = z(max(int(gb), 256), dtype=torch.uint8)  # zero-filled: bin cursors start at 0
         self.mlp_ws = []
         for net in (self.sig_net, self.col_net):
             b = nat.lib().ngp_ffmlp_backward_workspace_bytes(M, net.input_dim, net.padded_output_dim,
@@ -181,7 +186,9 @@ class FusedTrainer:
                                         P(self.grads[1]), _F16, P(self.mlp_ws[0]), self.mlp_ws[0].numel(),
                                         s), "sigma_mlp_backward")
         chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
-                                               P(self.grads[0]), M, cnt, *grid_args), "grid_backward_fused")
+                                               P(self.grads[0]), M, cnt, *grid_args[:-1], self._offsets_host,
+                                               P(self.grid_ws), self.grid_ws.numel(), s),
+            "grid_backward_fused")
 
     def _optimizer(self):
         """GradScaler inf check + Adam (unscaled fp16 grads, LambdaLR) + scaler update."""
