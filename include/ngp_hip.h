@@ -169,8 +169,9 @@ int ngp_sh_encode_backward(const void* grad, const void* inputs, uint32_t B, uin
  * f16 flat (per layer row-major [out, in], nn.Linear layout), outputs f16
  * [B, output_dim]. forward_buffer f16 [num_layers, B, hidden] or NULL (the
  * backward below recomputes activations and never reads it).
- * hidden_dim in {16,32,64,128}, input_dim % 16 == 0, output_dim <= 16 (padded
- * to 16 by the caller, like FFMLP does), B % 16 == 0. */
+ * Supported on this build: hidden_dim in {32, 64}, input_dim % 16 == 0 and
+ * <= 64, output_dim == 16 (FFMLP pads outputs to 16), num_layers 2..4, any B.
+ * Other shapes return NGP_ERR_UNSUPPORTED with the reason in ngp_last_error. */
 int ngp_ffmlp_forward(const void* inputs, const void* weights, uint32_t B, uint32_t input_dim,
                       uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,
                       uint32_t activation, uint32_t output_activation, void* forward_buffer,
