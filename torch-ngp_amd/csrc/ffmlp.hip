@@ -34,7 +34,11 @@ constexpr int kWaves = 4;  // the backward epilogue folds waves pairwise (0+2, 1
 constexpr int kThreads = kWaves * 64;
 constexpr int kNB = 2;          // 16-sample column blocks per wave step (32 samples)
 constexpr int kOut = 16;        // padded output width (FFMLP pads to 16)
-constexpr int kScratchLd = 40;  // halves per row of the per-wave transpose tile (32 + pad)
+// Per-wave staging tiles of the dW products: [32 samples][units], row pitch
+// 80 halves (40 dwords: the 8 rows one 32-lane half of a transposed read
+// touches land on 8 distinct 8-dword bank groups, i.e. conflict-free).
+constexpr int kTileLd = 80;
+constexpr int kTileRows = 32;
 constexpr uint32_t kMaxBwdBlocks = 256;
 
 NGP_DEV f32x4 mfma(half8 a, half8 b, f32x4 c) {
@@ -301,31 +305,64 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
 }
 
 // ---- backward ---------------------------------------------------------------
-// Per-wave transpose tile: rows = units, 32 samples per row (+pad).
+// dW = delta^T . input over a 32-sample chunk is an MFMA whose K is the
+// sample index: both operands need "8 samples of one unit" per lane, while
+// the chunk's activations sit as "4 units of one sample" per lane. The wave
+// stores them sample-major ([sample][unit], 8- or 16-byte row segments) and
+// reads the operands back with ds_read_b64_tr_b16 (gfx950's transposing LDS
+// read: per 16-lane group a 4-row x 16-column block arrives column-major).
+// K slot j of lane group g holds sample perm_unit(g, j) in BOTH operands.
+typedef short short4v __attribute__((ext_vector_type(4)));
+
 template <int KS, bool PERM>
-NGP_DEV void write_transposed(ngp_half* __restrict__ tile, const half8 (&v)[kNB][KS], uint32_t rows) {
+NGP_DEV void write_rows(ngp_half* __restrict__ tile, const half8 (&v)[kNB][KS], uint32_t units) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int nb = 0; nb < kNB; ++nb)
+    for (int nb = 0; nb < kNB; ++nb) {
+        ngp_half* row = tile + (nb * 16 + c) * kTileLd;
 #pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t u = 32 * s + (PERM ? perm_unit(g, j) : 8 * g + j);
-                if (u < rows) tile[u * kScratchLd + nb * 16 + c] = v[nb][s][j];
+        for (int s = 0; s < KS; ++s) {
+            if (PERM) {  // elements 0..3: units 32s+4g.., 4..7: units 32s+16+4g..
+                const half4 lo = {v[nb][s][0], v[nb][s][1], v[nb][s][2], v[nb][s][3]};
+                const half4 hi = {v[nb][s][4], v[nb][s][5], v[nb][s][6], v[nb][s][7]};
+                *reinterpret_cast<half4*>(row + 32 * s + 4 * g) = lo;
+                *reinterpret_cast<half4*>(row + 32 * s + 16 + 4 * g) = hi;
+            } else {     // units 32s+8g .. +7 (zeros past `units`)
+                const uint32_t u0 = 32 * s + 8 * g;
+                const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (u0 < (uint32_t)(32 * KS)) *reinterpret_cast<half8*>(row + u0) = u0 < units ? v[nb][s] : z;
             }
+        }
+    }
 }
 
-// dW[o][i] (MO x MI tiles of 16x16) += dT^T-rows · hT-rows over the 32 samples
+// operand fragment of units 16m..16m+15 over the chunk's 32 samples
+NGP_DEV half8 read_tr(const ngp_half* __restrict__ tile, int m) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const ngp_half* a = tile + (4 * g + q) * kTileLd + 16 * m + 4 * p;
+    const ngp_half* b = a + 16 * kTileLd;
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) short4v*)(a));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) short4v*)(b));
+    return __builtin_shufflevector(__builtin_bit_cast(half4, lo), __builtin_bit_cast(half4, hi),
+                                   0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// dW[o][i] (MO x MI tiles of 16x16) += dT^T . hT over the chunk
 template <int MO, int MI>
 NGP_DEV void dw_accum(const ngp_half* __restrict__ dT, const ngp_half* __restrict__ hT,
                       f32x4 (&acc)[MO][MI]) {
-    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     half8 a[MO], b[MI];
+    // the transposed reads are opaque intrinsics on an LDS address-space cast:
+    // keep the compiler from moving them across the wave's own tile stores
+    // (LDS itself executes one wave's operations in order)
+    asm volatile("" ::: "memory");
 #pragma unroll
-    for (int m = 0; m < MO; ++m) a[m] = *reinterpret_cast<const half8*>(dT + (16 * m + c) * kScratchLd + 8 * g);
+    for (int m = 0; m < MO; ++m) a[m] = read_tr(dT, m);
 #pragma unroll
-    for (int n = 0; n < MI; ++n) b[n] = *reinterpret_cast<const half8*>(hT + (16 * n + c) * kScratchLd + 8 * g);
+    for (int n = 0; n < MI; ++n) b[n] = read_tr(hT, n);
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int m = 0; m < MO; ++m)
 #pragma unroll
@@ -382,9 +419,8 @@ template <int W, int IN_KS, int NH>
 struct BwdLds {
     using N = Net<W, IN_KS, NH>;
     static constexpr int FRAGS = N::FWD_FRAGS + N::BWD_FRAGS;
-    static constexpr int TILE_ROWS = (W > 32 * IN_KS ? W : 32 * IN_KS);
     static constexpr size_t frag_bytes = (size_t)FRAGS * 64 * 16;
-    static constexpr size_t tile_bytes = (size_t)kWaves * 2 * TILE_ROWS * kScratchLd * 2;
+    static constexpr size_t tile_bytes = (size_t)kWaves * 2 * kTileRows * kTileLd * 2;
     static constexpr size_t nparams_max = (size_t)W * (32 * IN_KS) + (size_t)NH * W * W + (size_t)kOut * W;
     static constexpr size_t acc_bytes = nparams_max * 4;
     // the two dW images of the epilogue reuse the fragment + tile space once
@@ -435,8 +471,8 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     __syncthreads();
 
     const uint32_t wave = threadIdx.x >> 6;
-    ngp_half* dT = tiles + (size_t)wave * 2 * L::TILE_ROWS * kScratchLd;
-    ngp_half* hT = dT + (size_t)L::TILE_ROWS * kScratchLd;
+    ngp_half* dT = tiles + (size_t)wave * 2 * kTileRows * kTileLd;
+    ngp_half* hT = dT + (size_t)kTileRows * kTileLd;
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
 
     f32x4 dw_last[1][N::MTW], dw_hid[NH][N::MTW][N::MTW], dw_first[N::MTW][N::IN_MT];
@@ -474,23 +510,23 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
             pack_act<N::MTW, N::KSW>(a, act, h[q]);
         }
         // last matmul: dW += dout^T . h[NH]
-        write_transposed<1, false>(dT, dout, kOut);
-        write_transposed<N::KSW, true>(hT, h[NH], W);
+        write_rows<1, false>(dT, dout, kOut);
+        write_rows<N::KSW, true>(hT, h[NH], W);
         dw_accum<1, N::MTW>(dT, hT, dw_last);
         half8 d[kNB][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
         dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
         pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
 #pragma unroll
         for (int q = NH; q >= 1; --q) {
-            write_transposed<N::KSW, true>(dT, d, W);
-            write_transposed<N::KSW, true>(hT, h[q - 1], W);
+            write_rows<N::KSW, true>(dT, d, W);
+            write_rows<N::KSW, true>(hT, h[q - 1], W);
             dw_accum<N::MTW, N::MTW>(dT, hT, dw_hid[q - 1]);
             dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
             pack_delta<N::MTW, N::KSW>(a, h[q - 1], act, d);
         }
         // first matmul: dW += d^T . x, and grad_inputs = W_0^T d
-        write_transposed<N::KSW, true>(dT, d, W);
-        write_transposed<IN_KS, false>(hT, x, 32 * IN_KS);
+        write_rows<N::KSW, true>(dT, d, W);
+        write_rows<IN_KS, false>(hT, x, in_dim);
         dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
         if (grad_inputs) {
             f32x4 gi[kNB][N::IN_MT];
