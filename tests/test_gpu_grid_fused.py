@@ -1,0 +1,162 @@
+"""GPU: the fused train step's grid-encoder entry points against the oracle.
+
+ngp_grid_encode_forward_fused reads world-space xyz and the fp32 table as half
+(the reference's `(x + bound) / (2 * bound)` and `embeddings.half()` under
+autocast, gridencoder/grid.py + nerf/renderer.py): bit-exact vs the oracle
+forward on the normalised inputs and the half table.
+
+ngp_grid_encode_backward_fused adds into an fp16 grad table through the
+binned path (per-bin LDS accumulation, segmented bins, in-wave merging of
+equal corners) plus atomics for levels with more than 256 bins: compared to
+the oracle's float64 scatter per level, relative norm error <= 2e-3 and
+max abs error <= 4e-3 x max|ref| (fp16 table, one rounding per run / segment).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+LEGO_SCALE = float(np.exp2(np.log2(2048 / 16) / 15))
+
+
+def _lib():
+    import _ngp_native as nat
+    return nat
+
+
+def _world(B, bound, seed, concentrated=0.0, ordered=False):
+    rng = np.random.default_rng(seed)
+    if concentrated:  # everything inside a small cube: a few heavy bins
+        x = (0.3 + concentrated * rng.random((B, 3))).astype(np.float32)
+    else:
+        x = rng.random((B, 3), dtype=np.float32)
+    if ordered:  # rays: runs of samples along a line, as the marcher emits them
+        n = B // 64
+        o = rng.random((n, 1, 3)).astype(np.float32) * 0.6 + 0.2
+        d = rng.standard_normal((n, 1, 3)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=-1, keepdims=True)
+        t = (np.arange(64, dtype=np.float32) * 0.0017)[None, :, None]
+        x = np.clip(o + t * d, 0.0, 1.0).reshape(-1, 3)[:B]
+        if x.shape[0] < B:
+            x = np.concatenate([x, rng.random((B - x.shape[0], 3), dtype=np.float32)])
+    w = (x * np.float32(2 * bound) - np.float32(bound)).astype(np.float32)
+    w[:2] = [[bound * 1.01, 0.0, 0.0], [0.0, -bound * 1.2, 0.0]]  # outside the box: skipped
+    return w
+
+
+def _normalise(w, bound):
+    return ((w + np.float32(bound)) * np.float32(1.0 / (2.0 * bound))).astype(np.float32)
+
+
+def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, reps=1):
+    B = w.shape[0]
+    S = float(np.float32(np.log2(scale)))
+    offs_host = np.ascontiguousarray(offs, dtype=np.int32)
+    hp = offs_host.ctypes.data_as(ctypes.c_void_p)
+    ws_bytes = nat.lib().ngp_grid_encode_backward_fused_workspace_bytes(B, 3, 2, L, S, H, 0, hp)
+    ws = torch.zeros(max(int(ws_bytes), 256), dtype=torch.uint8, device=dev)
+    if table is None:
+        table = torch.zeros(int(offs[-1]), 2, dtype=torch.float16, device=dev)
+    gt, wt, ot = (torch.from_numpy(a).to(dev) for a in (g16, w, offs_host))
+    cnt = torch.tensor([count], dtype=torch.int32, device=dev) if count is not None else None
+    for _ in range(reps):
+        nat.check(nat.lib().ngp_grid_encode_backward_fused(
+            nat.ptr(gt), nat.ptr(wt), float(bound), nat.ptr(ot), nat.ptr(table), B,
+            nat.ptr(cnt) if cnt is not None else None, 3, 2, L, S, H, 0, 0, 0, hp,
+            nat.ptr(ws), ws.numel(), nat.stream_of(table)), "grid_backward_fused")
+    torch.cuda.synchronize()
+    # the workspace's counters are left zeroed for the next call
+    assert int(ws[:256].sum()) == 0
+    return table.float().cpu().numpy()
+
+
+def _check_levels(got, ref, offs, what, rtol=2e-3, mtol=4e-3):
+    for l in range(len(offs) - 1):
+        a, r = got[offs[l]:offs[l + 1]], ref[offs[l]:offs[l + 1]]
+        rn = np.linalg.norm(r)
+        if rn == 0:
+            assert np.abs(a).max() == 0, (what, l)
+            continue
+        rel = np.linalg.norm(a - r) / rn
+        mx = np.abs(a - r).max() / np.abs(r).max()
+        assert rel <= rtol and mx <= mtol, (what, l, rel, mx)
+
+
+CASES = [
+    # B, L, H, scale, log2T, layout
+    (20000, 16, 16, LEGO_SCALE, 19, "uniform"),
+    (60000, 16, 16, LEGO_SCALE, 19, "rays"),
+    (120000, 8, 16, 1.5, 19, "concentrated"),   # heavy bins: several segments per bin
+    (30000, 8, 16, 2.0, 22, "uniform"),          # 512-bin levels: the atomic suffix
+    (513, 4, 8, 2.0, 12, "uniform"),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"B{c[0]}L{c[1]}T{c[4]}{c[5]}")
+def test_grid_backward_fused_vs_oracle(cuda, case):
+    nat = _lib()
+    B, L, H, scale, log2T, layout = case
+    bound = 1.0 if layout != "rays" else 2.0
+    offs = oracle.grid_offsets(3, L, 2, H, scale, log2T)
+    w = _world(B, bound, seed=B + L, concentrated=0.25 * (layout == "concentrated"), ordered=layout == "rays")
+    rng = np.random.default_rng(7)
+    g16 = (rng.standard_normal((B, L * 2)) * 0.5).astype(np.float16)
+    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, bound)
+    x = _normalise(w, bound)
+    ref = oracle.grid_encode_backward(g16, x, offs, 2, scale, H)
+    _check_levels(got, ref, offs, layout)
+
+
+def test_grid_backward_fused_bin_overflow(cuda):
+    """Points in a 0.03-wide cube: on the hashed levels a few entries take all
+    corners, bins overflow their capacity and the excess goes through per-item
+    fp16 atomics (the reference's own accumulation, gridencoder.cu:325), whose
+    rounding grows with the thousands of terms per entry: 2e-2 here."""
+    nat = _lib()
+    B, L, H, scale = 40000, 12, 16, 1.5
+    offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
+    w = _world(B, 1.0, seed=4, concentrated=0.03)
+    g16 = (np.random.default_rng(9).standard_normal((B, L * 2)) * 0.5).astype(np.float16)
+    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, 1.0)
+    ref = oracle.grid_encode_backward(g16, _normalise(w, 1.0), offs, 2, scale, H)
+    _check_levels(got, ref, offs, "overflow", rtol=2e-2, mtol=4e-2)
+
+
+def test_grid_backward_fused_count_clip_and_accumulate(cuda):
+    nat = _lib()
+    B, L, H, scale = 40000, 16, 16, LEGO_SCALE
+    offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
+    w = _world(B, 1.0, seed=11, ordered=True)
+    g16 = (np.random.default_rng(3).standard_normal((B, L * 2)) * 0.5).astype(np.float16)
+    n = 31000
+    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, 1.0, count=n, reps=2)  # two calls add up
+    ref = 2.0 * oracle.grid_encode_backward(g16[:n], _normalise(w[:n], 1.0), offs, 2, scale, H)
+    _check_levels(got, ref, offs, "clip+accumulate")
+
+
+def test_grid_forward_fused_bit_exact(cuda):
+    nat = _lib()
+    B, L, H, scale, bound = 9000, 16, 16, LEGO_SCALE, 2.0
+    offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
+    rng = np.random.default_rng(5)
+    emb = (rng.standard_normal((int(offs[-1]), 2)) * 0.1).astype(np.float32)
+    w = _world(B, bound, seed=5)
+    w[2] = [bound, bound, bound]  # on the far faces: inside
+    n = 8500
+    S = float(np.float32(np.log2(scale)))
+    out = torch.full((B, L * 2), 7.0, dtype=torch.float16, device=cuda)
+    wt, et, ot = (torch.from_numpy(a).to(cuda) for a in (w, emb, offs))
+    cnt = torch.tensor([n], dtype=torch.int32, device=cuda)
+    nat.check(nat.lib().ngp_grid_encode_forward_fused(nat.ptr(wt), bound, nat.ptr(et), nat.ptr(ot), nat.ptr(out),
+                                                      B, nat.ptr(cnt), 3, 2, L, S, H, 0, 0, 0,
+                                                      nat.stream_of(out)), "grid_forward_fused")
+    torch.cuda.synchronize()
+    ref, _ = oracle.grid_encode_forward(_normalise(w[:n], bound), emb.astype(np.float16), offs, scale, H)
+    got = out.cpu().numpy()
+    assert np.array_equal(got[:n].view(np.uint16), ref.view(np.uint16))  # outside rows: zeros in both
+    assert np.all(got[n:] == 7.0)  # rows past the sample count untouched

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Profile the default bench on the GPU box: kernel trace + stats, then two
+# separate PMC passes (FETCH_SIZE, WRITE_SIZE) for the step's big kernels.
+# usage (on the box): bash tools/prof.sh TAG
+set -eo pipefail
+trap 'du -ah "$O" 2>/dev/null | sort -h | tail -20 > "$O/sizes.txt"; find "$O" -type f -size +8M -delete' EXIT
+TAG=${1:-prof}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+export TMPDIR=/tmp
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- \
+    python3 bench.py --no-cpu --steps 30 --warmup 10 > "$O/trace.log" 2>&1
+KRE='k_grid_bwd|k_grid_bin|k_grid_fwd|k_adam|k_mlp|k_march|k_composite|k_glue'
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex "$KRE" -d "$O/fetch" -o run -- \
+    python3 bench.py --no-cpu --steps 5 --warmup 3 --profile-reps 0 > "$O/fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex "$KRE" -d "$O/write" -o run -- \
+    python3 bench.py --no-cpu --steps 5 --warmup 3 --profile-reps 0 > "$O/write.log" 2>&1

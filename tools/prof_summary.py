@@ -1,0 +1,77 @@
+"""Summarise a tools/prof.sh run: per-kernel device time inside the timed
+graph replays of bench.py (steps delimited by k_lego_rays), and per-launch
+FETCH_SIZE / WRITE_SIZE from the two PMC passes.
+
+usage: python tools/prof_summary.py gpurun_out/TAG [profiles/OUT.json]
+FETCH_SIZE / WRITE_SIZE are reported raw (KB x 1024). On gfx950 FETCH_SIZE
+counts half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md,
+HBM section): `fetch_bytes_x2` carries the doubled figure for those kernels.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
+    if n.startswith("_ZN"):  # mangled template instance: keep the kernel identifier
+        import re
+        m = re.search(r"(k_[a-z0-9_]+)", n)
+        n = (m.group(1) if m else n[:40]) + "<" + n[-40:].split("EEv")[0][-12:] + ">"
+    return n
+
+
+def main(tag, out=None):
+    rows = list(csv.DictReader(open(os.path.join(tag, "trace", "run_kernel_trace.csv"))))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "k_lego_rays" in r["Kernel_Name"]]
+    # bench.py: ... timed graph replays (STEPS), then KSTEPS instrumented eager steps
+    steps, ksteps = int(os.environ.get("STEPS", "30")), int(os.environ.get("KSTEPS", "10"))
+    sel = starts[-(steps + ksteps):len(starts) - ksteps]
+    per = collections.defaultdict(list)
+    spans = []
+    for a, i in enumerate(sel):
+        j = sel[a + 1] if a + 1 < len(sel) else None
+        if j is None and starts.index(i) + 1 < len(starts):
+            j = starts[starts.index(i) + 1]
+        seg = rows[i:j] if j else rows[i:]
+        if a + 1 == len(sel):  # last step: up to and including k_step_end
+            k = next(n for n, r in enumerate(seg) if "k_step_end" in r["Kernel_Name"])
+            seg = seg[:k + 1]
+        t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
+        spans.append((t1 - t0) / 1e3)
+        cnt = collections.Counter()
+        for r in seg:
+            key = short(r["Kernel_Name"])
+            cnt[key] += 1
+            per[key + ("" if cnt[key] == 1 else f"#{cnt[key]}")].append(
+                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    kern = {k: round(sum(v) / len(v), 2) for k, v in per.items()}
+    busy = sum(kern.values())
+    pmc = {}
+    for which in ("fetch", "write"):
+        p = os.path.join(tag, which, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        acc = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024)
+        for k, v in acc.items():
+            pmc.setdefault(k, {})[which + "_bytes"] = round(sum(v) / len(v))
+    res = {
+        "steps": len(sel),
+        "step_span_us_mean": round(sum(spans) / len(spans), 1),
+        "kernel_busy_us_per_step": round(busy, 1),
+        "kernels_us_per_step": dict(sorted(kern.items(), key=lambda t: -t[1])),
+        "pmc_per_launch": pmc,
+    }
+    txt = json.dumps(res, indent=1)
+    print(txt)
+    if out:
+        open(out, "w").write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])

@@ -21,6 +21,7 @@
 //     rounded to float) and passed as kernel arguments.
 //   * a hashed level's size is a power of two: the modulo becomes a mask.
 #include "ngp_common.h"
+#include <stdlib.h>
 
 #include <cmath>
 
@@ -476,50 +477,83 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
     }
 }
 
-// ---- binned backward for the hashed levels (fused train step) ----------------
-// Scattered atomics on the hashed levels cost one memory-side request per
-// (point, corner pair) whatever is done (no reuse between points at those
-// resolutions), ~180 us per Lego step. Instead, the corner contributions of a
-// hashed level are sorted into bins of 2^13 table entries: each workgroup
-// (256 points of one level) ranks its 2048 contributions per bin in LDS,
-// reserves space per bin with one atomic, and writes each bin's run
-// contiguously; then one workgroup per bin sums its contributions in an LDS
-// fp32 image of the bin's entries and adds that image to the fp16 table with
-// plain loads/stores (every entry has one owner). Contributions are rounded
-// to half per term, like the reference's Half += float (gridencoder.cu:325),
-// and summed in fp32. Bins that overflow their capacity fall back to atomics.
-constexpr uint32_t kBinShift = 13;
+// ---- binned backward (fused train step) ---------------------------------------
+// Scattered atomics cost one memory-side request per (point, corner pair)
+// whatever is done, and the coarse levels' few entries turn them into hot
+// spots. Instead every level's corner contributions are sorted into bins of
+// 2^13 table entries:
+//   k_grid_bwd_bin   one workgroup = 1024 consecutive samples of one level.
+//                    Consecutive samples walk along a ray, so on coarse
+//                    levels neighbouring lanes hit the same corner: per
+//                    corner, runs of equal keys are summed in-wave (segmented
+//                    shuffle scan) and only the run's last lane keeps an item.
+//                    Items are ranked per bin in LDS (one LDS atomic per wave
+//                    when the whole wave lands in one bin), each bin's run is
+//                    reserved with one global atomic and written contiguously.
+//   k_grid_bin_accum persistent; a work unit = up to kSegItems items of one
+//                    bin, summed in an LDS fp32 image of the bin's entries.
+//                    A bin with one unit is added to the fp16 table with
+//                    plain 16-byte loads and stores (single owner); larger
+//                    bins flush each unit's image with packed fp16 atomics
+//                    (coalesced, one per entry per unit).
+// Contributions are rounded to half once per run (the reference rounds each
+// term, gridencoder.cu:325) and summed in fp32. Items past a bin's capacity
+// fall back to direct atomics. Levels with more than kMaxBinsPerLevel bins
+// use k_grid_bwd.
+constexpr uint32_t kBinShift = 12;
 constexpr uint32_t kBinEntries = 1u << kBinShift;
 constexpr uint32_t kMaxBinsPerLevel = 256;
+constexpr uint32_t kSegItems = 16384;
+// Levels up to this resolution merge runs of equal corners in-wave: on the
+// Lego step the merge cuts their items 3.5-16x (tools/grid_bwd_micro.py);
+// finer levels gain less than the scan costs.
+constexpr uint32_t kMergeMaxRes = 128;
 
 struct BinPlan {
-    uint32_t first_level;            // levels [first_level, L) are binned
+    uint32_t nlev;                   // levels [0, nlev) are binned
     uint32_t total_bins;
-    uint32_t cap;                    // contributions per bin
+    uint32_t merge_mask;             // levels whose equal-corner runs are merged in-wave
     uint32_t nbins[kMaxLevels];
-    uint32_t bin0[kMaxLevels];
+    uint32_t bin0[kMaxLevels];       // first global bin of the level
+    uint32_t cap[kMaxLevels];        // item capacity per bin
+    uint32_t item0[kMaxLevels];      // first item slot of the level; bin b at item0 + b * cap
 };
 
-struct BinItem {
+struct BinItem {  // 8 bytes: the accumulate kernel reads items as one dword pair
     uint32_t e;                      // entry within the bin (| bin << 16 while staged)
     ngp_half2 v;
 };
+static_assert(sizeof(BinItem) == 8, "BinItem layout");
+
+NGP_DEV uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+constexpr uint32_t kBinPts = 512;  // samples (threads) per bin-kernel workgroup
+
+// Workgroup barrier that orders LDS only: unlike __syncthreads() it does not
+// wait for the wave's outstanding global loads, stores and atomics.
+NGP_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <uint32_t D>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kBinPts)
 k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
                const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
                InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items) {
-    constexpr uint32_t C = 2, NC = 1u << D;
-    __shared__ uint32_t cnt[kMaxBinsPerLevel], base[kMaxBinsPerLevel], soff[kMaxBinsPerLevel + 1];
-    __shared__ BinItem stage[256 * NC];
-    const uint32_t level = bp.first_level + blockIdx.y;
+    constexpr uint32_t C = 2, NC = 1u << D, NW = kBinPts / 64;
+    static_assert(kMaxBinsPerLevel <= kBinPts, "one bin per thread in the reservation step");
+    __shared__ uint32_t cnt[kMaxBinsPerLevel], soff[kMaxBinsPerLevel + 1], wsum[NW];
+    __shared__ uint2 binfo[kMaxBinsPerLevel];  // (slot - stage index, end of the bin's in-capacity stage run)
+    extern __shared__ BinItem stage[];  // kBinPts * NC
+    const uint32_t level = blockIdx.y;
     const uint32_t nb = bp.nbins[level];
-    for (uint32_t t = threadIdx.x; t < nb; t += 256) cnt[t] = 0;
-    __syncthreads();
+    const bool merge = (bp.merge_mask >> level) & 1u;
+    const int lane = (int)(threadIdx.x & 63);
+    if (threadIdx.x < nb) cnt[threadIdx.x] = 0;
+    lds_barrier();
 
-    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t b = blockIdx.x * kBinPts + threadIdx.x;
     bool valid = b < rows_of(B, im);
     float x[D];
 #pragma unroll
@@ -552,6 +586,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
 
     uint32_t key[NC], rank[NC];
     ngp_half2 val[NC];
+    bool live[NC];
 #pragma unroll
     for (uint32_t idx = 0; idx < NC; idx++) {
         float w = 1;
@@ -566,132 +601,372 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
                 pl[d] = pg[d] + 1;
             }
         }
-        key[idx] = valid ? grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl) : 0u;
-        val[idx] = ngp_half2{(ngp_half)(w * g0), (ngp_half)(w * g1)};
-        rank[idx] = valid ? atomicAdd(&cnt[key[idx] >> kBinShift], 1u) : 0u;
-    }
-    __syncthreads();
-    // reserve each bin's run; exclusive scan of the counts for the staging layout
-    for (uint32_t t = threadIdx.x; t < nb; t += 256) {
-        const uint32_t c = cnt[t];
-        uint32_t bs = 0;
-        if (c) {
-            bs = atomicAdd(&cursor[bp.bin0[level] + t], c);
-            if (bs + c > bp.cap) bs = 0xffffffffu;  // overflow: this block's items of bin t go atomic
-        }
-        base[t] = bs;
-    }
-    {   // block-wide exclusive scan of cnt[0..nb) (nb <= 256 = blockDim)
-        __shared__ uint32_t wsum[4];
-        const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-        const uint32_t v = t < nb ? cnt[t] : 0u;
-        uint32_t incl = v;
+        const uint32_t k = valid ? grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl)
+                                 : 0xffffffffu;
+        float v0 = w * g0, v1 = w * g1;
+        bool lv_ = valid;
+        if (merge) {
+            const uint32_t kprev = __shfl_up(k, 1, 64);
+            const bool same = valid && lane > 0 && kprev == k;
+            if (__ballot(same)) {
+                int start = same ? 0 : lane;
 #pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += u;
-        }
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        uint32_t before = 0, all = 0;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(start, o, 64);
+                    if (lane >= o) start = max(start, t);
+                }
 #pragma unroll
-        for (uint32_t w = 0; w < 4; ++w) {
-            before += w < wv ? wsum[w] : 0u;
-            all += wsum[w];
+                for (int o = 1; o < 64; o <<= 1) {
+                    const float t0 = __shfl_up(v0, o, 64), t1 = __shfl_up(v1, o, 64);
+                    if (lane - o >= start) {
+                        v0 += t0;
+                        v1 += t1;
+                    }
+                }
+                const uint32_t knext = __shfl_down(k, 1, 64);
+                lv_ = valid && (lane == 63 || knext != k);
+            }
         }
-        if (t < nb) soff[t] = before + incl - v;
-        if (t == 0) soff[nb] = all;
-    }
-    __syncthreads();
-    if (valid) {
-        ngp_half* gg = grad_grid + (size_t)off0 * C;
-#pragma unroll
-        for (uint32_t idx = 0; idx < NC; idx++) {
-            const uint32_t bin = key[idx] >> kBinShift;
-            if (base[bin] == 0xffffffffu) {
-                __builtin_amdgcn_global_atomic_fadd_v2f16(reinterpret_cast<ngp_half2*>(gg + (size_t)key[idx] * C),
-                                                          val[idx]);
-            } else {
-                stage[soff[bin] + rank[idx]] = BinItem{(key[idx] & (kBinEntries - 1)) | (bin << 16), val[idx]};
+        key[idx] = k;
+        live[idx] = lv_;
+        val[idx] = ngp_half2{(ngp_half)v0, (ngp_half)v1};
+        // rank within the bin: one LDS atomic per wave when the wave shares a bin
+        const uint32_t bin = k >> kBinShift;
+        const uint64_t lm = __ballot(lv_);
+        rank[idx] = 0;
+        if (lm) {
+            const int first = __ffsll((unsigned long long)lm) - 1;
+            const uint32_t b0 = __shfl(bin, first, 64);
+            if (__ballot(lv_ && bin != b0) == 0) {
+                uint32_t r0 = 0;
+                if (lane == first) r0 = atomicAdd(&cnt[b0], (uint32_t)__popcll(lm));
+                rank[idx] = __shfl(r0, first, 64) + lanes_below(lm);
+            } else if (lv_) {
+                rank[idx] = atomicAdd(&cnt[bin], 1u);
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
+    // reserve each bin's run now (one global atomic per bin); the results are
+    // needed only by the write-out, so the scan and the staging overlap them.
+    // The part of a run past the bin's capacity goes atomic, so slots
+    // [0, min(cursor, cap)) are always all written.
+    const uint32_t cap = bp.cap[level];
+    uint32_t c_mine = 0, bs_mine = 0;
+    if (threadIdx.x < nb) {
+        c_mine = cnt[threadIdx.x];
+        if (c_mine) bs_mine = atomicAdd(&cursor[bp.bin0[level] + threadIdx.x], c_mine);
+    }
+    {   // block-wide exclusive scan of cnt[0..nb)
+        const uint32_t t = threadIdx.x, wv = t >> 6;
+        uint32_t incl = c_mine;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if ((uint32_t)lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        lds_barrier();
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) {
+            before += w < wv ? wsum[w] : 0u;
+            all += wsum[w];
+        }
+        if (t < nb) soff[t] = before + incl - c_mine;
+        if (t == 0) soff[nb] = all;
+    }
+    lds_barrier();
+#pragma unroll
+    for (uint32_t idx = 0; idx < NC; idx++) {
+        if (!live[idx]) continue;
+        const uint32_t bin = key[idx] >> kBinShift;
+        stage[soff[bin] + rank[idx]] = BinItem{(key[idx] & (kBinEntries - 1)) | (bin << 16), val[idx]};
+    }
+    if (threadIdx.x < nb) {
+        const uint32_t t = threadIdx.x, lim = bs_mine >= cap ? 0u : min(c_mine, cap - bs_mine);
+        binfo[t] = uint2{t * cap + bs_mine - soff[t], soff[t] + lim};
+    }
+    lds_barrier();
     const uint32_t total = soff[nb];
-    for (uint32_t k = threadIdx.x; k < total; k += 256) {
+    BinItem* lvl_items = items + bp.item0[level];
+    ngp_half* gg = grad_grid + (size_t)off0 * C;
+    for (uint32_t k = threadIdx.x; k < total; k += kBinPts) {
         const BinItem it = stage[k];
         const uint32_t bin = it.e >> 16;
-        if (base[bin] == 0xffffffffu) continue;
-        BinItem* dst = items + (size_t)(bp.bin0[level] + bin) * bp.cap + base[bin] + (k - soff[bin]);
-        *dst = BinItem{it.e & 0xffffu, it.v};
+        const uint2 bi = binfo[bin];
+        if (k < bi.y) {
+            lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
+        } else {  // past the bin's capacity
+            const size_t e = (size_t)bin * kBinEntries + (it.e & 0xffffu);
+            __builtin_amdgcn_global_atomic_fadd_v2f16(reinterpret_cast<ngp_half2*>(gg + e * C), it.v);
+        }
     }
 }
 
-__global__ void __launch_bounds__(256)
-k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t L,
-                 BinPlan bp, uint32_t* __restrict__ cursor, const BinItem* __restrict__ items) {
-    constexpr uint32_t C = 2;
-    __shared__ float acc[kBinEntries * C];
-    const uint32_t g = blockIdx.x;
-    uint32_t level = bp.first_level;
-    while (level + 1 < L && g >= bp.bin0[level + 1]) ++level;
-    const uint32_t lbin = g - bp.bin0[level];
-    for (uint32_t t = threadIdx.x; t < kBinEntries * C; t += 256) acc[t] = 0.0f;
-    __syncthreads();
-    const uint32_t n = min(cursor[g], bp.cap);
-    const BinItem* src = items + (size_t)g * bp.cap;
-    for (uint32_t k = threadIdx.x; k < n; k += 256) {
-        const BinItem it = src[k];
-        atomicAdd(&acc[it.e * C], (float)it.v[0]);
-        atomicAdd(&acc[it.e * C + 1], (float)it.v[1]);
-    }
-    __syncthreads();
-    const uint32_t off0 = (uint32_t)offsets[level];
-    const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
-    const uint32_t e0 = lbin * kBinEntries;
-    const uint32_t ne = min(kBinEntries, hs - e0);
-    ngp_half2* tbl = reinterpret_cast<ngp_half2*>(grad_grid + ((size_t)off0 + e0) * C);
-    for (uint32_t e = threadIdx.x; e < ne; e += 256) {
-        const float a0 = acc[e * C], a1 = acc[e * C + 1];
-        if (a0 == 0.0f && a1 == 0.0f) continue;
-        const ngp_half2 old = tbl[e];
-        tbl[e] = ngp_half2{(ngp_half)((float)old[0] + a0), (ngp_half)((float)old[1] + a1)};
-    }
-    if (threadIdx.x == 0) cursor[g] = 0;  // ready for the next step
+// An fp16 value as a signed count of 2^-24 (every finite fp16 is one:
+// (1024 + m) << (e - 1) for normals, m for subnormals); |x| < 2^41.
+NGP_DEV int64_t half_fixed24(uint32_t bits) {
+    const uint32_t e = (bits >> 10) & 31u, m = bits & 1023u;
+    const int64_t mag = e ? (int64_t)(1024u | m) << (e - 1) : (int64_t)m;
+    return (bits & 0x8000u) ? -mag : mag;
 }
 
-// Host-side plan from a host copy of the offsets: the binned levels are the
-// hashed suffix whose tables hold at least 8 bins.
+// Persistent accumulation: every workgroup reads all bins' counts, forms the
+// work units (bin, segment of kSegItems items) and takes units blockIdx.x,
+// blockIdx.x + gridDim.x, ... The last workgroup to have read the counts
+// zeroes them for the next step. Per unit the items are summed EXACTLY in an
+// LDS image of 64-bit fixed-point counts of 2^-24 (the fp16 quantum) with
+// integer LDS atomics: ds_add_u64 costs ~15 cycles per wave-instruction on
+// gfx950 against ~195 for ds_add_f32 / ds_pk_add_f16 (tools/lds_atomic_probe).
+// All item loads of a batch are issued before its adds. The image is then
+// written to the fp16 table: a plain 16-byte read-modify-write when the unit
+// is its bin's only one, packed fp16 atomics otherwise. A non-finite item
+// (inf / NaN: fp16 overflow under the loss scale) cannot be carried by the
+// integers, so it marks the unit and the unit stores a NaN into its bin's
+// first entry, which is what GradScaler's inf check looks for.
+constexpr uint32_t kAccThreads = 512, kAccBatch = 16;
+__global__ void __launch_bounds__(kAccThreads)
+k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
+                 uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
+                 const BinItem* __restrict__ items) {
+    constexpr uint32_t C = 2, NW = kAccThreads / 64;
+    __shared__ unsigned long long acc[kBinEntries * C];
+    __shared__ uint32_t wsum[NW];
+    __shared__ uint32_t s_last, s_bad;
+    extern __shared__ uint32_t dyn[];
+    const uint32_t nbins = bp.total_bins;
+    uint32_t* upre = dyn;              // [nbins + 1] first unit of each bin
+    uint32_t* bn = dyn + nbins + 1;    // [nbins] items of each bin (clipped at its capacity)
+    // the plan's per-level arrays, indexed per lane below: kernel arguments
+    // indexed by a varying value are memory loads, so keep a copy in LDS
+    __shared__ uint32_t s_bin0[kMaxLevels + 1], s_cap[kMaxLevels], s_item0[kMaxLevels], s_off[kMaxLevels + 1];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t nlev = bp.nlev;
+    if (t <= nlev) {
+        s_bin0[t] = t < nlev ? bp.bin0[t] : nbins;
+        s_off[t] = (uint32_t)offsets[t];
+        if (t < nlev) {
+            s_cap[t] = bp.cap[t];
+            s_item0[t] = bp.item0[t];
+        }
+    }
+    lds_barrier();
+    auto level_of = [&](uint32_t b) {
+        uint32_t l = 0;
+        while (l + 1 < nlev && b >= s_bin0[l + 1]) ++l;
+        return l;
+    };
+
+    // 1. units per bin, exclusive prefix (thread t owns bins [t*per, t*per + per))
+    const uint32_t per = (nbins + kAccThreads - 1) / kAccThreads;
+    uint32_t mine = 0;
+    uint32_t level = t * per < nbins ? level_of(t * per) : 0;
+    for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t b = t * per + j;
+        if (b >= nbins) break;
+        while (level + 1 < nlev && b >= s_bin0[level + 1]) ++level;
+        const uint32_t n = min(cursor[b], s_cap[level]);
+        bn[b] = n;
+        upre[b] = (n + kSegItems - 1) / kSegItems;
+        mine += upre[b];
+    }
+    uint32_t incl = mine;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - mine, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+        run += w < wv ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t b = t * per + j;
+        if (b >= nbins) break;
+        const uint32_t u = upre[b];
+        upre[b] = run;
+        run += u;
+    }
+    if (t == 0) upre[nbins] = total;
+    // 2. retire: once every workgroup holds the counts, the last one zeroes them
+    if (t == 0) {
+        __threadfence();
+        s_last = atomicAdd(retire, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last) {
+        for (uint32_t b = t; b < nbins; b += kAccThreads) cursor[b] = 0;
+        if (t == 0) *retire = 0;
+    }
+
+    // 3. units. The first item batch of a unit and, for a single-owner unit,
+    // its slice of the table are loaded one unit ahead (while the previous
+    // unit does its LDS adds and writes), hiding the memory latency.
+    struct Unit {
+        uint32_t level, lbin, s0, s1;
+        bool owner;
+        const uint64_t* src;
+        ngp_half2* tbl;
+        uint32_t ne;
+    };
+    auto locate = [&](uint32_t u) {
+        uint32_t lo = 0, hi = nbins - 1;  // last bin whose first unit <= u
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (upre[mid] <= u) lo = mid; else hi = mid - 1;
+        }
+        Unit r;
+        const uint32_t gb = lo, seg = u - upre[gb];
+        r.owner = upre[gb + 1] - upre[gb] == 1;
+        r.level = level_of(gb);
+        r.lbin = gb - s_bin0[r.level];
+        r.s0 = seg * kSegItems;
+        r.s1 = min(bn[gb], r.s0 + kSegItems);
+        r.src = reinterpret_cast<const uint64_t*>(items + s_item0[r.level] + (size_t)r.lbin * s_cap[r.level]);
+        const uint32_t off0 = s_off[r.level];
+        const uint32_t hs = s_off[r.level + 1] - off0;
+        const uint32_t e0 = r.lbin * kBinEntries;
+        r.ne = min(kBinEntries, hs - e0);  // a multiple of 8 (offsets are)
+        r.tbl = reinterpret_cast<ngp_half2*>(grad_grid + ((size_t)off0 + e0) * C);
+        return r;
+    };
+    constexpr uint32_t G = kBinEntries / 4 / kAccThreads;  // 16-byte table groups per thread
+    auto load_batch = [&](const Unit& w, uint32_t k0, uint64_t (&it)[kAccBatch]) {
+#pragma unroll
+        for (uint32_t q = 0; q < kAccBatch; ++q) {
+            const uint32_t k = k0 + q * kAccThreads + t;
+            it[q] = k < w.s1 ? __builtin_nontemporal_load(w.src + k) : ~0ull;
+        }
+    };
+    auto load_old = [&](const Unit& w, uint4 (&old)[G]) {
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) {
+            const uint32_t g = j * kAccThreads + t;
+            if (w.owner && 4 * g < w.ne) old[j] = reinterpret_cast<const uint4*>(w.tbl)[g];
+        }
+    };
+    uint64_t it[kAccBatch];
+    uint4 old[G];
+    Unit cur{};
+    if (blockIdx.x < total) {
+        cur = locate(blockIdx.x);
+        load_batch(cur, cur.s0, it);
+        load_old(cur, old);
+    }
+    for (uint32_t u = blockIdx.x; u < total; u += gridDim.x) {
+        for (uint32_t i = t; i < kBinEntries * C / 2; i += kAccThreads)
+            reinterpret_cast<uint4*>(acc)[i] = uint4{0u, 0u, 0u, 0u};
+        if (t == 0) s_bad = 0;
+        lds_barrier();
+        bool bad = false;
+        for (uint32_t k0 = cur.s0;;) {
+#pragma unroll
+            for (uint32_t q = 0; q < kAccBatch; ++q) {
+                if (it[q] == ~0ull) continue;
+                const uint32_t e = (uint32_t)it[q], v = (uint32_t)(it[q] >> 32);
+                bad |= ((v >> 10) & 31u) == 31u || ((v >> 26) & 31u) == 31u;
+                atomicAdd(&acc[e * C], (unsigned long long)half_fixed24(v & 0xffffu));
+                atomicAdd(&acc[e * C + 1], (unsigned long long)half_fixed24(v >> 16));
+            }
+            k0 += kAccThreads * kAccBatch;
+            if (k0 >= cur.s1) break;
+            load_batch(cur, k0, it);
+        }
+        uint4 old_cur[G];
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) old_cur[j] = old[j];
+        // prefetch the next unit
+        const uint32_t un = u + gridDim.x;
+        Unit nxt = cur;
+        if (un < total) {
+            nxt = locate(un);
+            load_batch(nxt, nxt.s0, it);
+            load_old(nxt, old);
+        }
+        if (__ballot(bad)) s_bad = 1;  // benign race: every writer stores 1
+        lds_barrier();
+        const float q24 = 1.0f / 16777216.0f;
+        if (cur.owner) {  // groups of 4 entries = 16 bytes of the table
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j) {
+                const uint32_t g = j * kAccThreads + t;
+                if (4 * g >= cur.ne) continue;
+                float a[8];
+                bool any = false;
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) {
+                    const int64_t x = (int64_t)acc[8 * g + q];
+                    a[q] = (float)x * q24;
+                    any |= x != 0;
+                }
+                if (!any) continue;
+                uint32_t w4[4] = {old_cur[j].x, old_cur[j].y, old_cur[j].z, old_cur[j].w};
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const ngp_half2 o = __builtin_bit_cast(ngp_half2, w4[q]);
+                    w4[q] = __builtin_bit_cast(uint32_t, ngp_half2{(ngp_half)((float)o[0] + a[2 * q]),
+                                                                   (ngp_half)((float)o[1] + a[2 * q + 1])});
+                }
+                reinterpret_cast<uint4*>(cur.tbl)[g] = uint4{w4[0], w4[1], w4[2], w4[3]};
+            }
+        } else {
+            for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
+                const int64_t x0 = (int64_t)acc[e * C], x1 = (int64_t)acc[e * C + 1];
+                if (x0 != 0 || x1 != 0)
+                    __builtin_amdgcn_global_atomic_fadd_v2f16(
+                        cur.tbl + e, ngp_half2{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)});
+            }
+        }
+        if (s_bad && t == 0) cur.tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
+        lds_barrier();  // the image is rezeroed by the next unit
+        cur = nxt;
+    }
+}
+
+// Host-side plan from a host copy of the offsets. Bins of hashed levels get
+// twice their mean load (the hash spreads corners uniformly) + slack; bins of
+// dense levels are z-slabs whose load follows the scene, so they get the
+// worst case (every corner of every sample).
 static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D, const GridLevels& lv,
                              bool align_corners, uint32_t B) {
     BinPlan bp{};
-    bp.first_level = L;
-    for (int l = (int)L - 1; l >= 0; --l) {
+    const uint64_t items_all = (uint64_t)B << D;
+    uint32_t bins = 0;
+    uint64_t slots = 0;
+    for (uint32_t l = 0; l < L; ++l) {
         const uint32_t hs = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
+        const uint32_t nb = (hs + kBinEntries - 1) / kBinEntries;
+        if (nb > kMaxBinsPerLevel) break;
         const double side = (double)(align_corners ? lv.res[l] : lv.res[l] + 1);
         const bool hashed = std::pow(side, (double)D) > (double)hs;
-        const uint32_t nb = (hs + kBinEntries - 1) / kBinEntries;
-        if (!hashed || nb < 8 || nb > kMaxBinsPerLevel) break;
-        bp.first_level = (uint32_t)l;
+        const uint64_t cap = hashed ? std::min<uint64_t>(items_all, 2 * ((items_all + nb - 1) / nb) + 2048)
+                                    : items_all;
+        bp.nbins[l] = nb;
+        bp.bin0[l] = bins;
+        bp.cap[l] = (uint32_t)std::max<uint64_t>(cap, 1);
+        bp.item0[l] = (uint32_t)slots;
+        if (lv.res[l] <= kMergeMaxRes) bp.merge_mask |= 1u << l;  // cells span several ray steps
+        bins += nb;
+        slots += (uint64_t)nb * bp.cap[l];
+        bp.nlev = l + 1;
     }
-    uint32_t total = 0, maxnb = 1;
-    for (uint32_t l = bp.first_level; l < L; ++l) {
-        const uint32_t hs = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
-        bp.nbins[l] = (hs + kBinEntries - 1) / kBinEntries;
-        bp.bin0[l] = total;
-        total += bp.nbins[l];
-        maxnb = bp.nbins[l] > maxnb ? bp.nbins[l] : maxnb;
-    }
-    for (uint32_t l = L; l < kMaxLevels; ++l) bp.bin0[l] = total;
-    bp.total_bins = total;
-    // twice the mean load of a bin (corners spread uniformly by the hash) + slack
-    bp.cap = (uint32_t)(2ull * ((uint64_t)B * (1u << D) + maxnb - 1) / maxnb + 2048);
+    if (slots >= 0xffffffffull) bp.nlev = 0;  // item offsets are 32-bit: fall back to atomics
+    bp.total_bins = bins;
     return bp;
 }
 
+static size_t bin_counters_bytes(const BinPlan& bp) { return ((size_t)bp.total_bins * 4 + 255) / 256 * 256; }
+
+// workspace: [bin cursors][retire counter][items]
 static size_t bin_workspace_bytes(const BinPlan& bp) {
-    const size_t cur = ((size_t)bp.total_bins * 4 + 255) / 256 * 256;
-    return cur + (size_t)bp.total_bins * bp.cap * sizeof(BinItem);
+    size_t slots = 0;
+    for (uint32_t l = 0; l < bp.nlev; ++l) slots += (size_t)bp.nbins[l] * bp.cap[l];
+    return bin_counters_bytes(bp) + 256 + slots * sizeof(BinItem);
 }
 
 template <typename T, uint32_t D, uint32_t C>
@@ -1000,7 +1275,7 @@ extern "C" size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uin
     GridLevels lv;
     make_levels(lv, L, S, H);
     const BinPlan bp = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B);
-    return bp.total_bins ? bin_workspace_bytes(bp) : 0;
+    return bp.nlev ? bin_workspace_bytes(bp) : 0;
 }
 
 extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
@@ -1020,41 +1295,33 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
     hipStream_t st = ngp_stream(stream);
     const bool ac = align_corners != 0;
     BinPlan bp{};
-    bp.first_level = L;
     if (workspace && offsets_host && C == 2 && D == 3) {
         bp = make_bin_plan(offsets_host, L, D, lv, ac, B);
-        if (bp.total_bins) {
+        if (bp.nlev)
             NGP_REQUIRE(workspace_bytes >= bin_workspace_bytes(bp), NGP_ERR_ARG,
                         "grid_encode_backward_fused: workspace of %zu bytes required, got %zu",
                         bin_workspace_bytes(bp), workspace_bytes);
-        } else {
-            bp.first_level = L;
-        }
     }
-    // dense (and any unbinned) levels: merged atomics
-    if (bp.first_level > 0) {
-        const dim3 grid(ngp_div_up(B, 128), bp.first_level);
-        switch (D) {
-            case 3:
-                if (C == 2) {
-                    k_grid_bwd<ngp_half, 3, 2><<<grid, 256, 0, st>>>((const ngp_half*)grad, xyz, offsets,
-                        (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, 1, im, 0u);
-                    break;
-                }
-                [[fallthrough]];
-            default:
-                return bwd_t<ngp_half>(grad, xyz, offsets, grad_embeddings, B, D, C, L, lv, nullptr, nullptr,
-                                       gridtype, ac, interp, 1, st, im);
-        }
-    }
-    if (bp.first_level < L) {
+    if (bp.nlev) {  // the workspace's counters start zeroed and are left zeroed
         uint32_t* cursor = static_cast<uint32_t*>(workspace);
-        BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) +
-                                                    ((size_t)bp.total_bins * 4 + 255) / 256 * 256);
-        const dim3 grid(ngp_div_up(B, 256), L - bp.first_level);
-        k_grid_bwd_bin<3><<<grid, 256, 0, st>>>((const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings,
-                                                B, L, lv, gridtype, ac, interp, im, bp, cursor, items);
-        k_grid_bin_accum<<<bp.total_bins, 256, 0, st>>>(offsets, (ngp_half*)grad_embeddings, L, bp, cursor, items);
+        uint32_t* retire = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_counters_bytes(bp));
+        BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) + bin_counters_bytes(bp) + 256);
+        const dim3 grid(ngp_div_up(B, kBinPts), bp.nlev);
+        k_grid_bwd_bin<3><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
+            (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, im,
+            bp, cursor, items);
+        k_grid_bin_accum<<<2 * ngp_num_cus(), kAccThreads, (2 * bp.total_bins + 1) * sizeof(uint32_t), st>>>(
+            offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items);
+    }
+    if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
+        if (D == 3 && C == 2) {
+            const dim3 grid(ngp_div_up(B, 128), L - bp.nlev);
+            k_grid_bwd<ngp_half, 3, 2><<<grid, 256, 0, st>>>((const ngp_half*)grad, xyz, offsets,
+                (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, 1, im, bp.nlev);
+        } else {
+            return bwd_t<ngp_half>(grad, xyz, offsets, grad_embeddings, B, D, C, L, lv, nullptr, nullptr,
+                                   gridtype, ac, interp, 1, st, im);
+        }
     }
     return ngp_check_launch("grid_encode_backward_fused");
 }

@@ -24,6 +24,15 @@ typedef _Float16 ngp_half2 __attribute__((ext_vector_type(2)));
 __host__ __device__ static inline uint32_t ngp_div_up(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 static inline hipStream_t ngp_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Compute units of the current device (persistent-grid sizing).
+static inline uint32_t ngp_num_cus() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        return 256;
+    return (uint32_t)n;
+}
+
 // scalar_t-generic arithmetic used by the templated encoder kernels.
 //   S = storage type, F = compute type of one product.
 // For half storage these reproduce c10::Half semantics of `Half += float`:

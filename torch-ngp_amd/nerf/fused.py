@@ -119,6 +119,7 @@ class FusedTrainer:
             sizes=(ctypes.c_uint64 * 3)(*[p.numel() for p in self.params]))
         self.graph = None
         self.graph_opt = None
+        self._events = None
 
     def refresh_occupancy(self):
         """Rebuild the marcher's occupancy image after density_bitfield changed
@@ -130,6 +131,34 @@ class FusedTrainer:
             "march_occupancy_build")
 
     # ------------------------------------------------------------------ step
+    def _tick(self, name):
+        """Event after each launch while `timed_steps` instruments eager steps."""
+        if self._events is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._events.append((name, ev))
+
+    def timed_steps(self, k):
+        """Device time per phase (ms, mean over k eager steps), measured with
+        events on the launch stream between consecutive launches: each phase's
+        kernels run in the cache state of a real step (the previous step's
+        optimizer has streamed the parameters through), unlike back-to-back
+        repeats of one kernel. A spin kernel ahead of each step lets the host
+        queue every launch first, so no phase includes host launch gaps."""
+        acc = {}
+        for _ in range(k):
+            torch.cuda.synchronize()
+            torch.cuda._sleep(4_000_000)  # keep the GPU busy while the host queues the step
+            self._events = []
+            self._tick("start")
+            self._launch()
+            self.model.local_step += 1
+            torch.cuda.synchronize()
+            ev, self._events = self._events, None
+            for (_, a), (name, b) in zip(ev[:-1], ev[1:]):
+                acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
+        return {n: v / k for n, v in acc.items()}
+
     def _launch(self):
         self._sample()
         self._forward_backward()
@@ -139,6 +168,7 @@ class FusedTrainer:
     def _allreduce(self):
         if self.world > 1:
             dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+            self._tick("allreduce")
 
     def _sample(self):
         """Batch of N rays: rays, RGBA target, background, march noise, near/far."""
@@ -149,6 +179,7 @@ class FusedTrainer:
                                     P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
                                     P(self.nears), P(self.fars), P(self.noises), P(self.counter), s),
                   "lego_rays")
+        self._tick("lego_rays")
 
     def _forward_backward(self):
         """march -> network -> composite + MSE -> full backward into the fp16 grads."""
@@ -161,34 +192,44 @@ class FusedTrainer:
                                      m.grid_size, M, P(self.nears), P(self.fars), P(self.xyzs),
                                      P(self.dirs), P(self.deltas), P(self.rays), cnt, P(self.noises),
                                      P(self.march_ws), self.march_ws.numel(), s), "march_rays_train")
+        self._tick("march_rays_train")
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
         chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(e.embeddings), P(e.offsets),
                                               P(self.enc_out), M, cnt, *grid_args), "grid_encode_fused")
+        self._tick("grid_encode_forward")
         sn, cn = self.sig_net, self.col_net
         chk(lib.ngp_ffmlp_forward_rows(P(self.enc_out), P(self.w_half[1]), M, cnt, 32, 16, sn.hidden_dim,
                                        sn.num_layers, _RELU, _NONE, P(self.h_sigma), s), "sigma_mlp")
+        self._tick("ffmlp_forward_sigma")
         chk(lib.ngp_nerf_glue_forward(P(self.h_sigma), P(self.dirs), float(m.density_scale), P(self.sigma),
                                       P(self.color_in), M, cnt, s), "glue_forward")
+        self._tick("glue_forward")
         chk(lib.ngp_ffmlp_forward_rows(P(self.color_in), P(self.w_half[2]), M, cnt, 32, 16, cn.hidden_dim,
                                        cn.num_layers, _RELU, _NONE, P(self.color_out), s), "color_mlp")
+        self._tick("ffmlp_forward_color")
         chk(lib.ngp_nerf_composite_loss(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
                                         P(self.rays), M, N, self.T_thresh, float(m.density_scale),
                                         P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
                                         P(self.g_h), None, None, P(self.loss_ray), s), "composite_loss")
+        self._tick("composite_loss")
         chk(lib.ngp_ffmlp_backward_rows(P(self.g_color_out), P(self.color_in), P(self.w_half[2]), M, cnt,
                                         32, 16, cn.hidden_dim, cn.num_layers, _RELU, P(self.g_color_in),
                                         P(self.grads[2]), _F16, P(self.mlp_ws[1]), self.mlp_ws[1].numel(),
                                         s), "color_mlp_backward")
+        self._tick("ffmlp_backward_color")
         chk(lib.ngp_nerf_glue_backward(P(self.g_color_in), P(self.g_h), M, cnt, s), "glue_backward")
+        self._tick("glue_backward")
         chk(lib.ngp_ffmlp_backward_rows(P(self.g_h), P(self.enc_out), P(self.w_half[1]), M, cnt, 32, 16,
                                         sn.hidden_dim, sn.num_layers, _RELU, P(self.g_enc),
                                         P(self.grads[1]), _F16, P(self.mlp_ws[0]), self.mlp_ws[0].numel(),
                                         s), "sigma_mlp_backward")
+        self._tick("ffmlp_backward_sigma")
         chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
                                                P(self.grads[0]), M, cnt, *grid_args[:-1], self._offsets_host,
                                                P(self.grid_ws), self.grid_ws.numel(), s),
             "grid_backward_fused")
+        self._tick("grid_encode_backward")
 
     def _optimizer(self):
         """GradScaler inf check + Adam (unscaled fp16 grads, LambdaLR) + scaler update."""
@@ -199,6 +240,7 @@ class FusedTrainer:
                                          1.0 / self.world, 2.0, 0.5, self.growth_interval, 1, N, cnt,
                                          P(m.step_counter), P(self.loss_ray),
                                          P(self.state), s), "fused_optimizer_step")
+        self._tick("optimizer")
 
     def step(self):
         if self.graph is None:
