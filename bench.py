@@ -291,7 +291,7 @@ def kernel_profile(ft, reps):
             P(ft.g_enc), P(ft.xyzs), float(m.bound), P(e.offsets), P(ft.grads[0]), M, cnt, *ga[:-1],
             ft._offsets_host, P(ft.grid_ws), ft.grid_ws.numel(), s),
         "grid_encode_forward": lambda: lib.ngp_grid_encode_forward_fused(
-            P(ft.xyzs), float(m.bound), P(e.embeddings), P(e.offsets), P(ft.enc_out), M, cnt, *ga),
+            P(ft.xyzs), float(m.bound), P(ft.w_half[0]), 1, P(e.offsets), P(ft.enc_out), M, cnt, *ga),
         "march_rays_train": lambda: lib.ngp_march_rays_train_prebuilt(
             P(ft.rays_o), P(ft.rays_d), P(m.density_bitfield), float(m.bound), ft.dt_gamma, ft.max_steps, N,
             m.cascade, m.grid_size, M, P(ft.nears), P(ft.fars), P(ft.xyzs), P(ft.dirs), P(ft.deltas),
@@ -354,7 +354,7 @@ def run_fused(args, model, data, bits, world, dev):
             used_graph = True
         except Exception as e:  # eager launches are the same kernels; record why
             print(f"[bench] graph capture failed, running eager: {e!r}", file=sys.stderr)
-            ft.graph = ft.graph_opt = None
+            ft.graph = None
     torch.cuda.synchronize()
 
     # ---------------- timed region ----------------

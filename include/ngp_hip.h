@@ -221,8 +221,11 @@ int ngp_adam_step(float* params, const void* grads, int32_t grad_dtype, float* e
  * arguments are device pointers to the marcher's sample count: rows at or
  * past it are not computed. `state` is a device StepState
  * (ngp_fused_state_bytes). */
-int ngp_grid_encode_forward_fused(const float* xyz, float bound, const float* embeddings,
-                                  const int32_t* offsets, void* outputs, uint32_t B,
+/* embeddings: the fp32 table (emb_dtype NGP_DTYPE_F32, rounded to half on
+ * load) or its fp16 copy (NGP_DTYPE_F16, e.g. the one the fused optimizer
+ * refreshes after every update): identical results, half the gather bytes. */
+int ngp_grid_encode_forward_fused(const float* xyz, float bound, const void* embeddings,
+                                  int32_t emb_dtype, const int32_t* offsets, void* outputs, uint32_t B,
                                   const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
                                   uint32_t H, uint32_t gridtype, int32_t align_corners,
                                   uint32_t interp, void* stream);
@@ -252,12 +255,16 @@ size_t ngp_fused_state_bytes(void);
 int ngp_fused_state_init(void* state, float init_scale, void* stream);
 /* Synthetic Lego batch (nerf/provider.py SyntheticLego): boxes = nboxes x
  * (lo[3], hi[3], rgb[3]); poses [n_poses, 4, 4]; intrinsics (fx, fy, cx, cy).
- * Also zeroes counter[0..1] for the marcher. */
+ * The batch index is the state's own draw counter. Also records the previous
+ * batch's counter[0..1] into step_counter[(draw - 1) % 16] (nullable; the
+ * reference's per-step record for update_extra_state) and zeroes counter for
+ * the marcher. Touches no state the optimizer uses, so it may run beside
+ * ngp_fused_optimizer_step of the previous step. */
 int ngp_lego_rays(const float* poses, uint32_t n_poses, const float* intrinsics4, uint32_t H,
                   uint32_t W, uint32_t N, const float* boxes, int32_t nboxes, const float* aabb6,
                   float min_near, uint32_t seed, void* state, float* rays_o, float* rays_d,
                   float* rgba, float* bg, float* nears, float* fars, float* noises,
-                  int32_t* counter, void* stream);
+                  int32_t* counter, int32_t* step_counter, void* stream);
 int ngp_nerf_glue_forward(const void* h_sigma, const float* dirs, float density_scale, float* sigma,
                           void* color_in, uint32_t B, const int32_t* count, void* stream);
 int ngp_nerf_glue_backward(const void* grad_color_in, void* grad_h_sigma, uint32_t B,
@@ -271,7 +278,9 @@ int ngp_nerf_composite_loss(const float* sigma, const void* color_out, const voi
 /* Adam (+ GradScaler inf check/unscale/update, LambdaLR 0.1^(epoch/iters))
  * over n_tensors fp32 params with fp16 grads; half_params[k] (nullable) is
  * refreshed with half(p) after the update; grads are zeroed when zero_grads;
- * grads are multiplied by grad_mult as well as unscaled (data-parallel mean). */
+ * grads are multiplied by grad_mult as well as unscaled (data-parallel mean).
+ * step_counter (nullable; pass null when ngp_lego_rays records it) gets
+ * counter[0..1] at slot iter % 16. */
 int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* const* grads,
                              float* const* exp_avg, float* const* exp_avg_sq,
                              void* const* half_params, const uint64_t* sizes, float lr, float beta1,

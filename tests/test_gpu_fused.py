@@ -67,10 +67,11 @@ def test_lego_sampler(cuda):
     assert torch.equal(nears, ft.nears) and torch.equal(fars, ft.fars)
     assert 0.0 <= float(ft.bg.min()) and float(ft.bg.max()) < 1.0
     assert int(ft.counter.abs().sum()) == 0
-    # a new step draws a new batch
+    # a new step draws a new batch (the sampler bumps its own draw counter)
     r0 = ft.rays_d.clone()
-    ft._state_i()[8] += 1
+    d0 = int(ft._state_i()[9])
     ft._sample()
+    assert int(ft._state_i()[9]) == d0 + 1
     assert not torch.equal(r0, ft.rays_d)
 
 
@@ -120,7 +121,8 @@ def test_fused_optimizer_matches_torch_adam_and_scaler(cuda):
         assert not torch.equal(a.detach(), p0), name  # the step moved the parameter
     assert all(int(g.abs().sum()) == 0 for g in ft.grads)   # grads zeroed for the next step
     assert ft.optimizer_steps == 1
-    # MLP fp16 forward copies refreshed from the fp32 masters
+    # fp16 forward copies (grid table, MLPs) refreshed from the fp32 masters
+    assert torch.equal(ft.w_half[0], ft.params[0].detach().half())
     assert torch.equal(ft.w_half[1], ft.params[1].detach().half())
     assert torch.equal(ft.w_half[2], ft.params[2].detach().half())
 
@@ -136,6 +138,30 @@ def test_fused_optimizer_skips_on_inf(cuda):
         assert torch.equal(a.detach(), b)
     assert ft.scale == s0 * 0.5 and ft.optimizer_steps == 0
     assert all(int(torch.isinf(g.float()).sum()) == 0 for g in ft.grads)
+
+
+def test_pipelined_steps_match_serial_steps(cuda):
+    """step() overlaps the previous step's optimizer with sampling + marching
+    (and replays a captured graph of that): after flush() the parameters must
+    be bit-identical to running sample -> forward/backward -> optimizer
+    serially the same number of times."""
+    _, _, _, a = _setup(cuda)
+    _, _, _, b = _setup(cuda)
+    for _ in range(3):
+        a.step()
+    a.capture(warmup=2)
+    for _ in range(4):
+        a.step()
+    a.flush()
+    for _ in range(3 + 2 + 4):
+        b._sample()
+        b._forward_backward()
+        b._optimizer()
+    torch.cuda.synchronize()
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+    assert a.optimizer_steps == b.optimizer_steps
+    assert torch.equal(a.model.step_counter, b.model.step_counter)
 
 
 def test_fused_training_reduces_loss_and_captures(cuda):

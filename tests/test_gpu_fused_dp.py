@@ -49,6 +49,7 @@ def _worker(rank, world, port, q):
     ft.capture(warmup=1)
     for _ in range(3):
         ft.step()
+    ft.flush()
     torch.cuda.synchronize()
     q.put((rank, [p.detach().cpu().numpy() for p in ft.params], ft.optimizer_steps))
     if world > 1:

@@ -2,8 +2,8 @@
 
 ngp_grid_encode_forward_fused reads world-space xyz and the fp32 table as half
 (the reference's `(x + bound) / (2 * bound)` and `embeddings.half()` under
-autocast, gridencoder/grid.py + nerf/renderer.py): bit-exact vs the oracle
-forward on the normalised inputs and the half table.
+autocast, gridencoder/grid.py + nerf/renderer.py), or directly an fp16 copy:
+bit-exact vs the oracle forward on the normalised inputs and the half table.
 
 ngp_grid_encode_backward_fused adds into an fp16 grad table through the
 binned path (per-bin LDS accumulation, segmented bins, in-wave merging of
@@ -139,7 +139,8 @@ def test_grid_backward_fused_count_clip_and_accumulate(cuda):
     _check_levels(got, ref, offs, "clip+accumulate")
 
 
-def test_grid_forward_fused_bit_exact(cuda):
+@pytest.mark.parametrize("table", ["f32", "f16"])
+def test_grid_forward_fused_bit_exact(cuda, table):
     nat = _lib()
     B, L, H, scale, bound = 9000, 16, 16, LEGO_SCALE, 2.0
     offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
@@ -151,10 +152,12 @@ def test_grid_forward_fused_bit_exact(cuda):
     S = float(np.float32(np.log2(scale)))
     out = torch.full((B, L * 2), 7.0, dtype=torch.float16, device=cuda)
     wt, et, ot = (torch.from_numpy(a).to(cuda) for a in (w, emb, offs))
+    if table == "f16":
+        et = et.half()  # the fp16 copy the fused optimizer keeps
     cnt = torch.tensor([n], dtype=torch.int32, device=cuda)
-    nat.check(nat.lib().ngp_grid_encode_forward_fused(nat.ptr(wt), bound, nat.ptr(et), nat.ptr(ot), nat.ptr(out),
-                                                      B, nat.ptr(cnt), 3, 2, L, S, H, 0, 0, 0,
-                                                      nat.stream_of(out)), "grid_forward_fused")
+    nat.check(nat.lib().ngp_grid_encode_forward_fused(nat.ptr(wt), bound, nat.ptr(et), nat.DTYPE_CODE[et.dtype],
+                                                      nat.ptr(ot), nat.ptr(out), B, nat.ptr(cnt), 3, 2, L, S, H,
+                                                      0, 0, 0, nat.stream_of(out)), "grid_forward_fused")
     torch.cuda.synchronize()
     ref, _ = oracle.grid_encode_forward(_normalise(w[:n], bound), emb.astype(np.float16), offs, scale, H)
     got = out.cpu().numpy()

@@ -63,7 +63,7 @@ SIGNATURES = {
     "ngp_ffmlp_free_splitk": [],
     "ngp_adam_step": [c_vp, c_vp, c_i32, c_vp, c_vp, c_sz, c_f32, c_f32, c_f32, c_f32, c_f32,
                       c_i32, c_f32, c_vp],
-    "ngp_grid_encode_forward_fused": [c_vp, c_f32, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
+    "ngp_grid_encode_forward_fused": [c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
                                       c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp],
     "ngp_grid_encode_backward_fused_workspace_bytes": [c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32,
                                                        c_vp],
@@ -76,7 +76,7 @@ SIGNATURES = {
     "ngp_fused_state_bytes": [],
     "ngp_fused_state_init": [c_vp, c_f32, c_vp],
     "ngp_lego_rays": [c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32,
-                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_nerf_glue_forward": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_vp],
     "ngp_nerf_glue_backward": [c_vp, c_vp, c_u32, c_vp, c_vp],
     "ngp_nerf_composite_loss": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,

@@ -1252,8 +1252,9 @@ extern "C" int ngp_grad_total_variation(const void* inputs, const void* embeddin
  * normalised in-kernel exactly as GridEncoder.forward does, an fp32 table
  * read as half (the reference's embeddings.half()), fp16 [B, L*C] outputs /
  * output grads, fp16 grad table, rows clipped at *count. */
-extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, const float* embeddings,
-                                             const int32_t* offsets, void* outputs, uint32_t B,
+extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, const void* embeddings,
+                                             int32_t emb_dtype, const int32_t* offsets, void* outputs,
+                                             uint32_t B,
                                              const int32_t* count, uint32_t D, uint32_t C, uint32_t L,
                                              float S, uint32_t H, uint32_t gridtype,
                                              int32_t align_corners, uint32_t interp, void* stream) {
@@ -1263,6 +1264,11 @@ extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, cons
     GridLevels lv;
     make_levels(lv, L, S, H);
     const InMap im{bound, 1.0f / (2.0f * bound), count};
+    NGP_REQUIRE(emb_dtype == NGP_DTYPE_F32 || emb_dtype == NGP_DTYPE_F16, NGP_ERR_ARG,
+                "grid_encode_forward_fused: emb_dtype %d (F32 or F16)", emb_dtype);
+    if (emb_dtype == NGP_DTYPE_F16)
+        return fwd_t<ngp_half, ngp_half>(xyz, embeddings, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
+                                         align_corners != 0, interp, 1, ngp_stream(stream), im);
     return fwd_t<ngp_half, float>(xyz, embeddings, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
                                   align_corners != 0, interp, 1, ngp_stream(stream), im);
 }

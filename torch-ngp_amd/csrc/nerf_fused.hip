@@ -23,6 +23,7 @@
 #include "ngp_common.h"
 #include "sh_basis.h"
 
+#include <algorithm>
 #include <cfloat>
 
 namespace {
@@ -46,8 +47,10 @@ struct StepState {
     int32_t found_inf;
     int32_t adam_step;     // optimizer steps taken (skipped steps excluded)
     int32_t epoch;         // LambdaLR epoch (every step)
-    int32_t iter;          // sampler counter
-    int32_t pad2[3];
+    int32_t iter;          // finished steps (k_step_end)
+    int32_t draw;          // batches drawn by the sampler (k_lego_rays)
+    int32_t lego_done;     // k_lego_rays' finished-block count (last block bumps draw)
+    int32_t pad2;
 };
 
 // counter-based RNG (no state, graph-safe): 32-bit mix of (seed, a, b, c)
@@ -99,10 +102,28 @@ __global__ void __launch_bounds__(256)
 k_lego_rays(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState* __restrict__ st,
             float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ rgba,
             float* __restrict__ bg, float* __restrict__ nears, float* __restrict__ fars,
-            float* __restrict__ noises, int32_t* __restrict__ counter) {
+            float* __restrict__ noises, int32_t* __restrict__ counter, int32_t* __restrict__ step_counter) {
     const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t it = (uint32_t)st->iter;
-    if (n == 0) { counter[0] = 0; counter[1] = 0; }
+    const uint32_t it = (uint32_t)st->draw;
+    // Only this kernel touches draw / lego_done / counter / step_counter, so it
+    // can run beside the previous step's optimizer (nerf/fused.py pipelining).
+    if (n == 0) {
+        if (step_counter && it > 0) {  // the previous batch's counts (mean_count, update_extra_state)
+            const uint32_t slot = (it - 1) & 15u;
+            step_counter[slot * 2] = counter[0];
+            step_counter[slot * 2 + 1] = counter[1];
+        }
+        counter[0] = 0;
+        counter[1] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // every block has read draw before the last one bumps it
+        __threadfence();
+        if (atomicAdd(&st->lego_done, 1) == (int32_t)gridDim.x - 1) {
+            st->draw = (int32_t)it + 1;
+            st->lego_done = 0;
+        }
+    }
     if (n >= N) return;
     const uint32_t pose = rng_u32(sc.seed, it, 0xffffffffu, 0) % sc.n_poses;
     const float* P = poses + (size_t)pose * 16;
@@ -427,7 +448,13 @@ struct AdamArgs {
 // torch.optim.Adam (weight_decay 0) on p, with g = half_grad * (1 / scale);
 // skipped (state untouched) when the check found an inf/nan, like
 // GradScaler.step. Grads are zeroed afterwards either way.
-__global__ void __launch_bounds__(256)
+//
+// Layout: chunks of kAdamChunk elements of the flat (8-aligned per tensor)
+// index space, chunk c to block c mod gridDim; every thread keeps two 16-byte
+// groups of each stream in flight. A chunk inside one tensor (all but the few
+// at the seams) takes its pointers from scalar loads.
+constexpr uint32_t kAdamThreads = 256, kAdamChunk = kAdamThreads * 8;
+__global__ void __launch_bounds__(kAdamThreads)
 k_adam_multi(TensorList tl, const StepState* __restrict__ st, AdamArgs aa) {
     const bool skip = st->found_inf != 0;
     const int32_t step = st->adam_step + 1;
@@ -437,52 +464,69 @@ k_adam_multi(TensorList tl, const StepState* __restrict__ st, AdamArgs aa) {
     const float step_size = (float)(lr / bc1);
     const float inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
     const float inv_scale = (float)(1.0 / (double)st->scale) * aa.grad_mult;
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    auto adam1 = [&](float& p, float& m, float& v, float gh) {
+        const float gk = gh * inv_scale;
+        m = m + (1.0f - aa.beta1) * (gk - m);
+        v = v * aa.beta2 + (1.0f - aa.beta2) * gk * gk;
+        const float denom = sqrtf(v) * inv_bc2_sqrt + aa.eps;
+        p = p - step_size * (m / denom);
+    };
     const uint64_t total = tl.start[tl.n];
-    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < total;
-         i0 += (uint64_t)gridDim.x * blockDim.x * 4) {
-        const int k = find_tensor(tl, i0);
-        const uint64_t off = i0 - tl.start[k];
-        if (off >= tl.size[k]) continue;  // alignment padding between tensors
-        float* p = tl.p[k] + off;
-        float* m = tl.m[k] + off;
-        float* v = tl.v[k] + off;
-        ngp_half* g = tl.g[k] + off;
-        ngp_half* ph = tl.ph[k] ? tl.ph[k] + off : nullptr;
-        const uint64_t n4 = min((uint64_t)4, tl.size[k] - off);
-        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-        if (n4 == 4) {
-            float4 pv = *reinterpret_cast<float4*>(p);
-            float4 mv = *reinterpret_cast<float4*>(m);
-            float4 vv = *reinterpret_cast<float4*>(v);
-            const half4 gh = *reinterpret_cast<const half4*>(g);
-            if (!skip) {
-                float* pp = &pv.x; float* mm = &mv.x; float* vq = &vv.x;
+    const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
+    for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint64_t c0 = c * kAdamChunk, c1 = min(c0 + kAdamChunk, total);
+        const int k = find_tensor(tl, c0);
+        if (find_tensor(tl, c1 - 1) == k && c1 - tl.start[k] <= tl.size[k]) {
+            // whole chunk inside tensor k: two float4 groups per thread, loads first
+            const uint64_t base = c0 - tl.start[k] + threadIdx.x * 4;
+            float4 pv[2], mv[2], vv[2];
+            half4 gh[2];
+            bool in[2];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float gk = (float)gh[j] * inv_scale;
-                    mm[j] = mm[j] + (1.0f - aa.beta1) * (gk - mm[j]);
-                    vq[j] = vq[j] * aa.beta2 + (1.0f - aa.beta2) * gk * gk;
-                    const float denom = sqrtf(vq[j]) * inv_bc2_sqrt + aa.eps;
-                    pp[j] = pp[j] - step_size * (mm[j] / denom);
-                }
-                *reinterpret_cast<float4*>(p) = pv;
-                *reinterpret_cast<float4*>(m) = mv;
-                *reinterpret_cast<float4*>(v) = vv;
-                if (ph) *reinterpret_cast<half4*>(ph) = half4{(ngp_half)pv.x, (ngp_half)pv.y, (ngp_half)pv.z, (ngp_half)pv.w};
+            for (int u = 0; u < 2; ++u) {
+                const uint64_t off = base + u * (kAdamChunk / 2);
+                in[u] = c0 + (off - (c0 - tl.start[k])) < c1;
+                if (!in[u]) continue;
+                pv[u] = *reinterpret_cast<const float4*>(tl.p[k] + off);
+                mv[u] = *reinterpret_cast<const float4*>(tl.m[k] + off);
+                vv[u] = *reinterpret_cast<const float4*>(tl.v[k] + off);
+                gh[u] = *reinterpret_cast<const half4*>(tl.g[k] + off);
             }
-            if (aa.zero_grads) *reinterpret_cast<half4*>(g) = half4{0, 0, 0, 0};
-        } else {
-            for (uint64_t j = 0; j < n4; ++j) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (!in[u]) continue;
+                const uint64_t off = base + u * (kAdamChunk / 2);
                 if (!skip) {
-                    const float gk = (float)g[j] * inv_scale;
-                    m[j] = m[j] + (1.0f - aa.beta1) * (gk - m[j]);
-                    v[j] = v[j] * aa.beta2 + (1.0f - aa.beta2) * gk * gk;
-                    const float denom = sqrtf(v[j]) * inv_bc2_sqrt + aa.eps;
-                    p[j] = p[j] - step_size * (m[j] / denom);
-                    if (ph) ph[j] = (ngp_half)p[j];
+                    adam1(pv[u].x, mv[u].x, vv[u].x, (float)gh[u][0]);
+                    adam1(pv[u].y, mv[u].y, vv[u].y, (float)gh[u][1]);
+                    adam1(pv[u].z, mv[u].z, vv[u].z, (float)gh[u][2]);
+                    adam1(pv[u].w, mv[u].w, vv[u].w, (float)gh[u][3]);
+                    *reinterpret_cast<float4*>(tl.p[k] + off) = pv[u];
+                    *reinterpret_cast<float4*>(tl.m[k] + off) = mv[u];
+                    *reinterpret_cast<float4*>(tl.v[k] + off) = vv[u];
+                    if (tl.ph[k])
+                        *reinterpret_cast<half4*>(tl.ph[k] + off) =
+                            half4{(ngp_half)pv[u].x, (ngp_half)pv[u].y, (ngp_half)pv[u].z, (ngp_half)pv[u].w};
                 }
-                if (aa.zero_grads) g[j] = (ngp_half)0.0f;
+                if (aa.zero_grads) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
             }
+            continue;
+        }
+        // a seam chunk: per element
+        for (uint64_t i = c0 + threadIdx.x; i < c1; i += kAdamThreads) {
+            const int kk = find_tensor(tl, i);
+            const uint64_t off = i - tl.start[kk];
+            if (off >= tl.size[kk]) continue;  // alignment padding between tensors
+            if (!skip) {
+                float p = tl.p[kk][off], m = tl.m[kk][off], v = tl.v[kk][off];
+                adam1(p, m, v, (float)tl.g[kk][off]);
+                tl.p[kk][off] = p;
+                tl.m[kk][off] = m;
+                tl.v[kk][off] = v;
+                if (tl.ph[kk]) tl.ph[kk][off] = (ngp_half)p;
+            }
+            if (aa.zero_grads) tl.g[kk][off] = (ngp_half)0.0f;
         }
     }
 }
@@ -574,7 +618,8 @@ extern "C" int ngp_lego_rays(const float* poses, uint32_t n_poses, const float* 
                              uint32_t H, uint32_t W, uint32_t N, const float* boxes, int32_t nboxes,
                              const float* aabb6, float min_near, uint32_t seed, void* state,
                              float* rays_o, float* rays_d, float* rgba, float* bg, float* nears,
-                             float* fars, float* noises, int32_t* counter, void* stream) {
+                             float* fars, float* noises, int32_t* counter, int32_t* step_counter,
+                             void* stream) {
     NGP_REQUIRE(nboxes >= 0 && nboxes <= kMaxBoxes, NGP_ERR_ARG, "lego_rays: at most %d boxes", kMaxBoxes);
     NGP_REQUIRE(n_poses > 0 && H > 0 && W > 0, NGP_ERR_ARG, "lego_rays: empty pose set or image");
     if (N == 0) return NGP_OK;
@@ -592,7 +637,8 @@ extern "C" int ngp_lego_rays(const float* poses, uint32_t n_poses, const float* 
     sc.min_near = min_near;
     sc.seed = seed;
     k_lego_rays<<<ngp_div_up(N, 256), 256, 0, ngp_stream(stream)>>>(
-        poses, sc, N, static_cast<StepState*>(state), rays_o, rays_d, rgba, bg, nears, fars, noises, counter);
+        poses, sc, N, static_cast<StepState*>(state), rays_o, rays_d, rgba, bg, nears, fars, noises, counter,
+        step_counter);
     return ngp_check_launch("lego_rays");
 }
 
@@ -660,9 +706,12 @@ extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params,
                     NGP_ERR_ARG, "fused_optimizer_step: half shadow %d misaligned", k);
     const TensorList tl = make_list(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes);
     const uint64_t total = tl.start[n_tensors];
-    if (scaler_enabled) k_nonfinite<<<sweep_blocks(total, 8), 256, 0, s>>>(tl, st);
+    if (scaler_enabled)
+        k_nonfinite<<<sweep_blocks(total, 8), 256, 0, s>>>(tl, st);
     AdamArgs aa{lr, beta1, beta2, eps, iters, zero_grads, grad_mult};
-    k_adam_multi<<<sweep_blocks(total, 4), 256, 0, s>>>(tl, st, aa);
+    const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
+    const uint64_t adam_blocks = std::min<uint64_t>(nchunks, 16ull * ngp_num_cus());
+    k_adam_multi<<<(uint32_t)(adam_blocks ? adam_blocks : 1), kAdamThreads, 0, s>>>(tl, st, aa);
     ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled,
                   num_rays ? 1.0f / (float)num_rays : 0.0f};
     k_step_end<<<1, 256, 0, s>>>(st, sa, counter, step_counter, loss_ray, num_rays);

@@ -16,6 +16,16 @@ Static shapes: N rays per step, M = the sample buffer (mean_count); rows past
 the marcher's sample count are skipped on the device, so a fixed M costs
 nothing beyond its memory. Every launch goes to the current stream, so the
 whole step captures into one hipGraph (`capture`).
+
+Step order: `step()` runs [optimizer of the PREVIOUS step's gradients ->
+sample -> march -> network], so one graph holds a whole step even when a
+data-parallel all-reduce has to sit between the backward and the optimizer
+(it runs after the graph). The arithmetic is the reference's, in the
+reference's order; only the last step's update stays pending until
+`flush()` (the read-outs below flush first). Running that optimizer on a side
+stream beside sample + march was measured and lost: Adam and the marcher's
+scan/emit are both memory-bound and slowed each other more than they
+overlapped (profiles/r01u_overlap_trace.txt).
 """
 import ctypes
 
@@ -90,7 +100,9 @@ class FusedTrainer:
                       for a, n, p in zip(starts[:-1], sizes, self.params)]
         self.exp_avg = [torch.zeros_like(p) for p in self.params]
         self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
-        self.w_half = [None] + [p.detach().half() for p in self.params[1:]]
+        # fp16 copies the forward kernels read (the reference's autocast casts), refreshed by the
+        # optimizer after every update; the grid's copy also halves the forward gather bytes
+        self.w_half = [p.detach().half() for p in self.params]
         self._offsets_host = (ctypes.c_int32 * enc.offsets.numel())(*enc.offsets.cpu().tolist())
         gb = nat.lib().ngp_grid_encode_backward_fused_workspace_bytes(
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
@@ -115,11 +127,18 @@ class FusedTrainer:
             grads=_vp_array([nat.ptr(g) for g in self.grads]),
             m=_vp_array([nat.ptr(t) for t in self.exp_avg]),
             v=_vp_array([nat.ptr(t) for t in self.exp_avg_sq]),
-            half=_vp_array([None] + [nat.ptr(t) for t in self.w_half[1:]]),
+            half=_vp_array([nat.ptr(t) for t in self.w_half]),
             sizes=(ctypes.c_uint64 * 3)(*[p.numel() for p in self.params]))
         self.graph = None
-        self.graph_opt = None
         self._events = None
+        self._pending = False  # gradients of the last forward/backward not yet applied
+
+    def sync_half(self):
+        """Refresh the fp16 forward copies after the fp32 parameters were
+        changed outside the fused optimizer (loading, manual edits)."""
+        with torch.no_grad():
+            for h, p in zip(self.w_half, self.params):
+                h.copy_(p)
 
     def refresh_occupancy(self):
         """Rebuild the marcher's occupancy image after density_bitfield changed
@@ -144,14 +163,20 @@ class FusedTrainer:
         kernels run in the cache state of a real step (the previous step's
         optimizer has streamed the parameters through), unlike back-to-back
         repeats of one kernel. A spin kernel ahead of each step lets the host
-        queue every launch first, so no phase includes host launch gaps."""
+        queue every launch first, so no phase includes host launch gaps. The
+        phases run serially here (no optimizer / march overlap)."""
+        self.flush()
         acc = {}
         for _ in range(k):
             torch.cuda.synchronize()
             torch.cuda._sleep(4_000_000)  # keep the GPU busy while the host queues the step
             self._events = []
             self._tick("start")
-            self._launch()
+            self._sample()
+            self._march()
+            self._network()
+            self._allreduce()
+            self._optimizer()
             self.model.local_step += 1
             torch.cuda.synchronize()
             ev, self._events = self._events, None
@@ -159,11 +184,14 @@ class FusedTrainer:
                 acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
         return {n: v / k for n, v in acc.items()}
 
-    def _launch(self):
+    def _body(self, pending):
+        """One step's launches: [optimizer(previous grads)] -> sample -> march
+        -> network forward/backward."""
+        if pending:
+            self._optimizer()
         self._sample()
-        self._forward_backward()
-        self._allreduce()
-        self._optimizer()
+        self._march()
+        self._network()
 
     def _allreduce(self):
         if self.world > 1:
@@ -177,25 +205,34 @@ class FusedTrainer:
         nat.check(lib.ngp_lego_rays(P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N,
                                     self._boxes, self._nboxes, self._aabb, float(m.min_near), self.seed,
                                     P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
-                                    P(self.nears), P(self.fars), P(self.noises), P(self.counter), s),
+                                    P(self.nears), P(self.fars), P(self.noises), P(self.counter),
+                                    P(m.step_counter), s),
                   "lego_rays")
         self._tick("lego_rays")
 
     def _forward_backward(self):
         """march -> network -> composite + MSE -> full backward into the fp16 grads."""
+        self._march()
+        self._network()
+
+    def _march(self):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
-        m, e = self.model, self.enc
-        M, N, cnt = self.M, self.N, P(self.counter)
-        chk = nat.check
-        chk(lib.ngp_march_rays_train_prebuilt(P(self.rays_o), P(self.rays_d), P(m.density_bitfield),
+        m, M, N, cnt = self.model, self.M, self.N, P(self.counter)
+        nat.check(lib.ngp_march_rays_train_prebuilt(P(self.rays_o), P(self.rays_d), P(m.density_bitfield),
                                      float(m.bound), self.dt_gamma, self.max_steps, N, m.cascade,
                                      m.grid_size, M, P(self.nears), P(self.fars), P(self.xyzs),
                                      P(self.dirs), P(self.deltas), P(self.rays), cnt, P(self.noises),
                                      P(self.march_ws), self.march_ws.numel(), s), "march_rays_train")
         self._tick("march_rays_train")
+
+    def _network(self):
+        lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
+        m, e = self.model, self.enc
+        M, N, cnt = self.M, self.N, P(self.counter)
+        chk = nat.check
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
-        chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(e.embeddings), P(e.offsets),
+        chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(self.w_half[0]), _F16, P(e.offsets),
                                               P(self.enc_out), M, cnt, *grid_args), "grid_encode_fused")
         self._tick("grid_encode_forward")
         sn, cn = self.sig_net, self.col_net
@@ -238,41 +275,40 @@ class FusedTrainer:
         chk(lib.ngp_fused_optimizer_step(3, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"],
                                          self.lr, self.betas[0], self.betas[1], self.eps, self.iters, 1,
                                          1.0 / self.world, 2.0, 0.5, self.growth_interval, 1, N, cnt,
-                                         P(m.step_counter), P(self.loss_ray),
+                                         None, P(self.loss_ray),
                                          P(self.state), s), "fused_optimizer_step")
         self._tick("optimizer")
 
     def step(self):
-        if self.graph is None:
-            self._launch()
-        elif self.graph_opt is None:
+        """One training iteration (the optimizer half lags by one step, see
+        the module docstring)."""
+        if self.graph is not None and self._pending:
             self.graph.replay()
-        else:  # data parallel: graph, RCCL all-reduce (eager), optimizer graph
-            self.graph.replay()
-            self._allreduce()
-            self.graph_opt.replay()
+        else:
+            self._body(self._pending)
+        self._allreduce()
+        self._pending = True
         self.model.local_step += 1
 
-    def capture(self, warmup=2):
-        """One hipGraph for the whole step (two around the all-reduce when
-        data parallel)."""
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
-                self._launch()
-        torch.cuda.current_stream().wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        if self.world == 1:
-            with torch.cuda.graph(self.graph):
-                self._launch()
-            return
-        with torch.cuda.graph(self.graph):
-            self._sample()
-            self._forward_backward()
-        self.graph_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_opt):
+    def flush(self):
+        """Apply the pending optimizer step (before reading or saving the
+        parameters, or evaluating)."""
+        if self._pending:
             self._optimizer()
+            self._pending = False
+
+    def capture(self, warmup=2):
+        """One hipGraph of the step body (optimizer of the previous gradients,
+        sample, march, network). The RCCL all-reduce of a data-parallel run
+        stays outside, between replays."""
+        for _ in range(max(1, warmup)):
+            self.step()
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._body(True)
+        # capture recorded the launches without running them: the pending
+        # update is still pending and the next step() replays it first
 
     # ----------------------------------------------------------- read-outs
     def _state_f(self):
@@ -283,14 +319,17 @@ class FusedTrainer:
 
     @property
     def last_loss(self):
+        self.flush()
         return float(self._state_f()[2].item())
 
     @property
     def scale(self):
+        self.flush()
         return float(self._state_f()[0].item())
 
     @property
     def optimizer_steps(self):
+        self.flush()
         return int(self._state_i()[6].item())
 
     def sample_count(self):
