@@ -46,8 +46,6 @@ def parse():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
     ap.add_argument("--engine", choices=["fused", "autograd"], default="fused")
-    ap.add_argument("--profile-reps", type=int, default=0,
-                    help="also time each kernel alone, this many back-to-back launches (hot caches)")
     return ap.parse_args()
 
 
@@ -261,7 +259,6 @@ def run_autograd(args, model, data, bits, world, dev):
             "avg_launch_ms": round(kernel_ms[dominant], 5),
         },
         "kernels_ms": {k: round(v, 5) for k, v in kernel_ms.items()},
-        "isolated_ms": {k: round(v, 5) for k, v in isolated_ms.items()},
         "ffmlp_mfma": {"flops_per_step": ffmlp_flops, "ms": round(mlp_ms, 5),
                         "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
                         "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
@@ -271,59 +268,6 @@ def run_autograd(args, model, data, bits, world, dev):
 
     result["config"]["engine"] = "autograd"
     return result
-
-
-def kernel_profile(ft, reps):
-    """Average device time per launch of the fused step's main kernels: each
-    is launched `reps` times back to back between two HIP events on the
-    stream it runs on, with the buffers of the last step (the launch queue
-    stays ahead of the GPU, so host gaps do not count)."""
-    import _ngp_native as nat
-    lib, P = nat.lib(), nat.ptr
-    m, e = ft.model, ft.enc
-    s = nat.stream_of(ft.rays_o)
-    M, N, cnt = ft.M, ft.N, P(ft.counter)
-    ga = (e.input_dim, e.level_dim, e.num_levels, ft.S, e.base_resolution, e.gridtype_id,
-          int(e.align_corners), e.interp_id, s)
-    sn, cn = ft.sig_net, ft.col_net
-    calls = {
-        "grid_encode_backward": lambda: lib.ngp_grid_encode_backward_fused(
-            P(ft.g_enc), P(ft.xyzs), float(m.bound), P(e.offsets), P(ft.grads[0]), M, cnt, *ga[:-1],
-            ft._offsets_host, P(ft.grid_ws), ft.grid_ws.numel(), s),
-        "grid_encode_forward": lambda: lib.ngp_grid_encode_forward_fused(
-            P(ft.xyzs), float(m.bound), P(ft.w_half[0]), 1, P(e.offsets), P(ft.enc_out), M, cnt, *ga),
-        "march_rays_train": lambda: lib.ngp_march_rays_train_prebuilt(
-            P(ft.rays_o), P(ft.rays_d), P(m.density_bitfield), float(m.bound), ft.dt_gamma, ft.max_steps, N,
-            m.cascade, m.grid_size, M, P(ft.nears), P(ft.fars), P(ft.xyzs), P(ft.dirs), P(ft.deltas),
-            P(ft.rays), P(ft.march_cnt_scratch), P(ft.noises), P(ft.march_ws), ft.march_ws.numel(), s),
-        "ffmlp_forward_sigma": lambda: lib.ngp_ffmlp_forward_rows(
-            P(ft.enc_out), P(ft.w_half[1]), M, cnt, 32, 16, sn.hidden_dim, sn.num_layers, 0, 6, P(ft.h_sigma), s),
-        "ffmlp_forward_color": lambda: lib.ngp_ffmlp_forward_rows(
-            P(ft.color_in), P(ft.w_half[2]), M, cnt, 32, 16, cn.hidden_dim, cn.num_layers, 0, 6, P(ft.color_out), s),
-        "ffmlp_backward_sigma": lambda: lib.ngp_ffmlp_backward_rows(
-            P(ft.g_h), P(ft.enc_out), P(ft.w_half[1]), M, cnt, 32, 16, sn.hidden_dim, sn.num_layers, 0,
-            P(ft.g_enc), P(ft.grads[1]), 1, P(ft.mlp_ws[0]), ft.mlp_ws[0].numel(), s),
-        "ffmlp_backward_color": lambda: lib.ngp_ffmlp_backward_rows(
-            P(ft.g_color_out), P(ft.color_in), P(ft.w_half[2]), M, cnt, 32, 16, cn.hidden_dim, cn.num_layers,
-            0, P(ft.g_color_in), P(ft.grads[2]), 1, P(ft.mlp_ws[1]), ft.mlp_ws[1].numel(), s),
-        "composite_loss": lambda: lib.ngp_nerf_composite_loss(
-            P(ft.sigma), P(ft.color_out), P(ft.h_sigma), P(ft.deltas), P(ft.rays), M, N, ft.T_thresh,
-            float(m.density_scale), P(ft.rgba), 4, P(ft.bg), P(ft.scratch_state), P(ft.g_color_out),
-            P(ft.g_h), None, None, P(ft.loss_ray), s),
-    }
-    out = {}
-    if reps <= 0:
-        return {name: float("nan") for name in calls}
-    for name, fn in calls.items():
-        nat.check(fn(), name)
-        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        start.record()
-        for _ in range(reps):
-            fn()
-        end.record()
-        end.synchronize()
-        out[name] = start.elapsed_time(end) / reps
-    return out
 
 
 def run_fused(args, model, data, bits, world, dev):
@@ -379,12 +323,8 @@ def run_fused(args, model, data, bits, world, dev):
     loss = ft.last_loss
 
     # ---------------- per-kernel device time (roofline) ----------------
-    # in-step device time of each launch (eager steps with events between
-    # launches); `isolated_ms`: the same kernels repeated back to back (hot caches)
+    # in-step device time of each launch (eager steps with events between launches)
     kernel_ms = ft.timed_steps(args.kernel_steps)
-    ft.march_cnt_scratch = torch.zeros(2, dtype=torch.int32, device=dev)
-    ft.scratch_state = ft.state.clone()
-    isolated_ms = kernel_profile(ft, args.profile_reps) if args.profile_reps > 0 else {}
     rows = min(ft.sample_count(), ft.M)
     grid_fwd_bytes, grid_bwd_bytes = 588 * rows, 1100 * rows  # SURVEY §8(d), per sample
     dominant = max(("grid_encode_backward", "grid_encode_forward"), key=lambda k: kernel_ms[k])
@@ -440,7 +380,6 @@ def run_fused(args, model, data, bits, world, dev):
             "avg_launch_ms": round(kernel_ms[dominant], 5),
         },
         "kernels_ms": {k: round(v, 5) for k, v in kernel_ms.items()},
-        "isolated_ms": {k: round(v, 5) for k, v in isolated_ms.items()},
         "ffmlp_mfma": {"flops_per_step": ffmlp_flops, "ms": round(mlp_ms, 5),
                         "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
                         "peak_tflops": FP16_MFMA_PEAK_TFLOPS},

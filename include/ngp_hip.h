@@ -242,15 +242,38 @@ int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bou
                                    uint32_t H, uint32_t gridtype, int32_t align_corners,
                                    uint32_t interp, const int32_t* offsets_host, void* workspace,
                                    size_t workspace_bytes, void* stream);
-int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, uint32_t B, const int32_t* count,
-                           uint32_t in_dim, uint32_t output_dim, uint32_t hidden_dim,
-                           uint32_t num_layers, uint32_t activation, uint32_t output_activation,
-                           void* outputs, void* stream);
-int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* weights, uint32_t B,
-                            const int32_t* count, uint32_t in_dim, uint32_t output_dim,
-                            uint32_t hidden_dim, uint32_t num_layers, uint32_t activation,
-                            void* grad_inputs, void* grad_weights, int32_t gw_dtype,
-                            void* workspace, size_t workspace_bytes, void* stream);
+/* Weight-fragment images (forward + transposed, per matmul) of n networks in
+ * one launch; image k needs ngp_ffmlp_image_bytes of its network. The
+ * forward/backward *_rows calls below take the image (nullable: the weights
+ * are packed per call). */
+size_t ngp_ffmlp_image_bytes(uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers);
+int ngp_ffmlp_pack(int32_t n, const void* const* weights, const uint32_t* in_dims,
+                   const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* images,
+                   void* stream);
+int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, const void* image, uint32_t B,
+                           const int32_t* count, uint32_t in_dim, uint32_t output_dim,
+                           uint32_t hidden_dim, uint32_t num_layers, uint32_t activation,
+                           uint32_t output_activation, void* outputs, void* stream);
+/* The NeRF sigma network with its glue as the epilogue (network_ff.py:61-68):
+ * h_out [B,16] half, sigma [B] = density_scale * exp(h[:,0]) fp32, color_in
+ * [B,32] half = [SH4(dirs) | h[:,1:16] | 0]. */
+int ngp_nerf_sigma_forward(const void* inputs, const void* weights, const void* image, uint32_t B,
+                           const int32_t* count, uint32_t in_dim, uint32_t hidden_dim,
+                           uint32_t num_layers, void* h_out, float* sigma, void* color_in,
+                           const float* dirs, float density_scale, void* stream);
+#define NGP_FFMLP_DEFER_REDUCE 1u /* leave dW partials for ngp_ffmlp_reduce */
+#define NGP_FFMLP_NERF_GEO 2u     /* grad_inputs [B,16]: input-grad cols 16..30 -> cols 1..15 */
+int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* weights,
+                            const void* image, uint32_t B, const int32_t* count, uint32_t in_dim,
+                            uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,
+                            uint32_t activation, void* grad_inputs, void* grad_weights,
+                            int32_t gw_dtype, uint32_t flags, void* workspace,
+                            size_t workspace_bytes, void* stream);
+/* Sums the deferred dW partials of n backward calls (same B and shapes as
+ * those calls) into grad_weights[k], in one launch (n <= 4). */
+int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32_t* Bs, const uint32_t* in_dims,
+                     const uint32_t* hidden_dims, const uint32_t* num_layers,
+                     void* const* grad_weights, int32_t gw_dtype, void* stream);
 size_t ngp_fused_state_bytes(void);
 int ngp_fused_state_init(void* state, float init_scale, void* stream);
 /* Synthetic Lego batch (nerf/provider.py SyntheticLego): boxes = nboxes x

@@ -177,3 +177,81 @@ def test_fused_training_reduces_loss_and_captures(cuda):
     late = ft.last_loss
     assert np.isfinite(late) and late < losses[0], (losses, late)
     assert ft.optimizer_steps >= 60
+
+
+def test_mlp_fused_epilogues_match_unfused(cuda):
+    """The fused step's MLP calls against the unfused ones, bit for bit: the
+    prepacked-image path vs per-call packing, the sigma network with its glue
+    epilogue vs ffmlp forward + ngp_nerf_glue_forward, the color backward that
+    writes its geo-feature gradient into g_h[:, 1:16] vs plain backward +
+    ngp_nerf_glue_backward, and the deferred two-network dW reduce."""
+    import ctypes
+
+    import _ngp_native as nat
+    lib, P, s = nat.lib(), nat.ptr, None
+    g = torch.Generator(device="cpu").manual_seed(4)
+    B, n = 5000, 4700
+    cnt = torch.tensor([n, 0], dtype=torch.int32, device=cuda)
+    nets = [(32, 64, 2), (32, 64, 3)]
+    ws = []
+    for i, h, nl in nets:
+        npar = h * (i + h * (nl - 1) + 16)
+        ws.append(((torch.rand(npar, generator=g) - 0.5) * 0.3).half().to(cuda))
+    x = torch.randn(B, 32, generator=g).half().to(cuda)
+    d = torch.randn(B, 3, generator=g)
+    dirs = (d / d.norm(dim=-1, keepdim=True)).to(cuda)
+    imgs = [torch.zeros(int(lib.ngp_ffmlp_image_bytes(i, h, nl)), dtype=torch.uint8, device=cuda)
+            for i, h, nl in nets]
+    arr = lambda ts: (ctypes.c_void_p * len(ts))(*[P(t) if t is not None else None for t in ts])  # noqa: E731
+    u32 = lambda v: (ctypes.c_uint32 * len(v))(*v)  # noqa: E731
+    nat.check(lib.ngp_ffmlp_pack(2, arr(ws), u32([a for a, _, _ in nets]), u32([b for _, b, _ in nets]),
+                                 u32([c for _, _, c in nets]), arr(imgs), s), "pack")
+    # sigma network + glue
+    h_ref = torch.zeros(B, 16, dtype=torch.half, device=cuda)
+    sig_ref, ci_ref = torch.zeros(B, device=cuda), torch.zeros(B, 32, dtype=torch.half, device=cuda)
+    nat.check(lib.ngp_ffmlp_forward_rows(P(x), P(ws[0]), None, B, P(cnt), 32, 16, 64, 2, 0, 6, P(h_ref), s), "f")
+    nat.check(lib.ngp_nerf_glue_forward(P(h_ref), P(dirs), 1.0, P(sig_ref), P(ci_ref), B, P(cnt), s), "glue")
+    h, sig = torch.zeros_like(h_ref), torch.zeros_like(sig_ref)
+    ci = torch.zeros_like(ci_ref)
+    nat.check(lib.ngp_nerf_sigma_forward(P(x), P(ws[0]), P(imgs[0]), B, P(cnt), 32, 64, 2, P(h), P(sig), P(ci),
+                                         P(dirs), 1.0, s), "sigma_fwd")
+    torch.cuda.synchronize()
+    assert torch.equal(h[:n].view(torch.int16), h_ref[:n].view(torch.int16))
+    assert torch.equal(sig[:n], sig_ref[:n]), int((sig[:n] != sig_ref[:n]).sum())
+    bad = (ci[:n].view(torch.int16) != ci_ref[:n].view(torch.int16))
+    assert not bad.any(), (int(bad.sum()), bad.nonzero()[:8].tolist(), ci[:n][bad][:8].tolist(), ci_ref[:n][bad][:8].tolist())
+    assert int(h[n:].view(torch.int16).abs().sum()) == 0  # rows past the count untouched
+    # color network forward: image vs per-call packing
+    o_ref, o = (torch.zeros(B, 16, dtype=torch.half, device=cuda) for _ in range(2))
+    nat.check(lib.ngp_ffmlp_forward_rows(P(ci), P(ws[1]), None, B, P(cnt), 32, 16, 64, 3, 0, 6, P(o_ref), s), "f")
+    nat.check(lib.ngp_ffmlp_forward_rows(P(ci), P(ws[1]), P(imgs[1]), B, P(cnt), 32, 16, 64, 3, 0, 6, P(o), s), "f")
+    # backward: color with geo output + sigma, deferred reduce of both
+    go = torch.randn(B, 16, generator=g).half().to(cuda)
+    gh0 = torch.randn(B, 16, generator=g).half().to(cuda)  # column 0: the density gradient
+    wsb = [torch.zeros(int(lib.ngp_ffmlp_backward_workspace_bytes(B, i, 16, h, nl)), dtype=torch.uint8,
+                       device=cuda) for i, h, nl in nets]
+    gi_c = torch.zeros(B, 32, dtype=torch.half, device=cuda)
+    gw_ref = [torch.zeros(t.numel(), dtype=torch.half, device=cuda) for t in ws]
+    gh_ref = gh0.clone()
+    nat.check(lib.ngp_ffmlp_backward_rows(P(go), P(ci), P(ws[1]), None, B, P(cnt), 32, 16, 64, 3, 0, P(gi_c),
+                                          P(gw_ref[1]), 1, 0, P(wsb[1]), wsb[1].numel(), s), "b")
+    nat.check(lib.ngp_nerf_glue_backward(P(gi_c), P(gh_ref), B, P(cnt), s), "glue_b")
+    gx_ref = torch.zeros(B, 32, dtype=torch.half, device=cuda)
+    nat.check(lib.ngp_ffmlp_backward_rows(P(gh_ref), P(x), P(ws[0]), None, B, P(cnt), 32, 16, 64, 2, 0, P(gx_ref),
+                                          P(gw_ref[0]), 1, 0, P(wsb[0]), wsb[0].numel(), s), "b")
+    torch.cuda.synchronize()
+    gh = gh0.clone()
+    gw = [torch.zeros_like(t) for t in gw_ref]
+    gx = torch.zeros_like(gx_ref)
+    nat.check(lib.ngp_ffmlp_backward_rows(P(go), P(ci), P(ws[1]), P(imgs[1]), B, P(cnt), 32, 16, 64, 3, 0, P(gh),
+                                          None, 1, 3, P(wsb[1]), wsb[1].numel(), s), "b_geo")
+    nat.check(lib.ngp_ffmlp_backward_rows(P(gh), P(x), P(ws[0]), P(imgs[0]), B, P(cnt), 32, 16, 64, 2, 0, P(gx),
+                                          None, 1, 1, P(wsb[0]), wsb[0].numel(), s), "b_defer")
+    nat.check(lib.ngp_ffmlp_reduce(2, arr([wsb[1], wsb[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
+                                   u32([3, 2]), arr([gw[1], gw[0]]), 1, s), "reduce")
+    torch.cuda.synchronize()
+    assert torch.equal(o[:n].view(torch.int16), o_ref[:n].view(torch.int16))
+    assert torch.equal(gh[:n].view(torch.int16), gh_ref[:n].view(torch.int16))
+    assert torch.equal(gx[:n].view(torch.int16), gx_ref[:n].view(torch.int16))
+    for a, b in zip(gw, gw_ref):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))

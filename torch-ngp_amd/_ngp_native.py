@@ -69,10 +69,15 @@ SIGNATURES = {
                                                        c_vp],
     "ngp_grid_encode_backward_fused": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
                                        c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_vp],
-    "ngp_ffmlp_forward_rows": [c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
+    "ngp_ffmlp_image_bytes": [c_u32, c_u32, c_u32],
+    "ngp_ffmlp_pack": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_ffmlp_forward_rows": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
                                c_vp, c_vp],
-    "ngp_ffmlp_backward_rows": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32,
-                                c_vp, c_vp, c_i32, c_vp, c_sz, c_vp],
+    "ngp_nerf_sigma_forward": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp,
+                               c_f32, c_vp],
+    "ngp_ffmlp_backward_rows": [c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32,
+                                c_vp, c_vp, c_i32, c_u32, c_vp, c_sz, c_vp],
+    "ngp_ffmlp_reduce": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],
     "ngp_fused_state_bytes": [],
     "ngp_fused_state_init": [c_vp, c_f32, c_vp],
     "ngp_lego_rays": [c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32,
@@ -91,6 +96,7 @@ _RESTYPES = {
     "ngp_march_rays_train_workspace_bytes": c_sz,
     "ngp_fused_state_bytes": c_sz,
     "ngp_grid_encode_backward_fused_workspace_bytes": c_sz,
+    "ngp_ffmlp_image_bytes": c_sz,
 }
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}

@@ -23,6 +23,7 @@
 //     partial dW land in a slab and one reduce kernel sums them in fixed
 //     order: no atomics, bit-reproducible weight gradients.
 #include "ngp_common.h"
+#include "sh_basis.h"
 
 namespace {
 
@@ -161,7 +162,7 @@ struct Net {
 };
 
 template <int W, int IN_KS, int NH>
-NGP_DEV MatDesc fwd_desc(int q, uint32_t in_dim) {
+__host__ __device__ inline MatDesc fwd_desc(int q, uint32_t in_dim) {
     using N = Net<W, IN_KS, NH>;
     MatDesc m;
     if (q == 0) {
@@ -177,7 +178,7 @@ NGP_DEV MatDesc fwd_desc(int q, uint32_t in_dim) {
 }
 
 template <int W, int IN_KS, int NH>
-NGP_DEV MatDesc bwd_desc(int q, uint32_t in_dim) {
+__host__ __device__ inline MatDesc bwd_desc(int q, uint32_t in_dim) {
     using N = Net<W, IN_KS, NH>;
     MatDesc m;
     if (q == 0) {  // W_0^T: M over input features, K over hidden units (permuted deltas)
@@ -269,15 +270,65 @@ NGP_DEV void store_tiles(ngp_half* __restrict__ dst, uint32_t width, uint32_t ro
 }
 
 // ---- forward ----------------------------------------------------------------
-template <int W, int IN_KS, int NH, typename FA, typename FO>
+// Output epilogues: the plain [B, 16] store, or the NeRF sigma network's
+// glue (nerf/network_ff.py:61-68): h [B,16] half, sigma = density_scale *
+// trunc_exp(h[:,0]) (activation.py, fp32 exp of the half value) and
+// color_in [B,32] = [half(SH4(dir)) | h[:,1:16] | 0] for the color network.
+struct EpiStore {
+    ngp_half* out;
+    template <typename FO>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act) const {
+        if (out) store_tiles<1>(out, kOut, row0, B, o, out_act);
+    }
+};
+
+struct EpiNerfSigma {
+    ngp_half* h;
+    float* sigma;
+    ngp_half* color_in;
+    const float* dirs;
+    float density_scale;
+    template <typename FO>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act) const {
+        const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+            const uint32_t row = row0 + nb * 16 + c;
+            half4 v;  // h[row][4g .. 4g+3]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (ngp_half)out_act.fwd(o[nb][0][r]);
+            // h[row][4g+4] from the next lane group (color_in shifts h by one column)
+            const uint32_t nx = __shfl((uint32_t)__builtin_bit_cast(uint16_t, v[0]), lane + 16, 64);
+            const ngp_half next = g < 3 ? __builtin_bit_cast(ngp_half, (uint16_t)nx) : (ngp_half)0.0f;
+            if (row >= B) continue;
+            *reinterpret_cast<half4*>(h + (size_t)row * kOut + 4 * g) = v;
+            if (g == 0) sigma[row] = density_scale * expf((float)v[0]);
+            ngp_half* ci = color_in + (size_t)row * 32;
+            *reinterpret_cast<half4*>(ci + 16 + 4 * g) = half4{v[1], v[2], v[3], next};
+            float sh[16];
+            ngp_sh::sh_basis<float>(dirs[(size_t)row * 3], dirs[(size_t)row * 3 + 1], dirs[(size_t)row * 3 + 2],
+                                    4u, [&](uint32_t k, float x) { sh[k] = x; });
+            half4 s4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s4[k] = ngp_f2h(sh[4 * g + k]);
+            *reinterpret_cast<half4*>(ci + 4 * g) = s4;
+        }
+    }
+};
+
+template <int W, int IN_KS, int NH, typename FA, typename FO, typename EPI>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weights,
-          ngp_half* __restrict__ outputs, ngp_half* __restrict__ fwd_buf, uint32_t B,
-          uint32_t in_dim, FA act, FO out_act, const int32_t* __restrict__ count) {
+          const half8* __restrict__ image, ngp_half* __restrict__ fwd_buf, uint32_t B,
+          uint32_t in_dim, FA act, FO out_act, const int32_t* __restrict__ count, EPI epi) {
     using N = Net<W, IN_KS, NH>;
     if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);  // rows past the sample count
     extern __shared__ half8 lds[];
-    for (int q = 0; q < N::NMAT; ++q) build_frags(lds, weights, fwd_desc<W, IN_KS, NH>(q, in_dim), false);
+    if (image) {  // prepacked (ngp_ffmlp_pack): straight 16-byte copies
+        for (uint32_t t = threadIdx.x; t < (uint32_t)N::FWD_FRAGS * 64; t += blockDim.x) lds[t] = image[t];
+    } else {
+        for (int q = 0; q < N::NMAT; ++q) build_frags(lds, weights, fwd_desc<W, IN_KS, NH>(q, in_dim), false);
+    }
     __syncthreads();
 
     const uint32_t wave = threadIdx.x >> 6;
@@ -300,7 +351,7 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
         }
         f32x4 o[kNB][1];
         dense<1, N::KSW>(lds, fwd_desc<W, IN_KS, NH>(NH + 1, in_dim).frag0, h, o);
-        if (outputs) store_tiles<1>(outputs, kOut, row0, B, o, out_act);
+        epi(row0, B, o, out_act);
     }
 }
 
@@ -429,23 +480,6 @@ struct BwdLds {
         frag_bytes + tile_bytes > 2 * acc_bytes ? frag_bytes + tile_bytes : 2 * acc_bytes;
 };
 
-// Writes the permuted forward and transposed-backward fragment images of
-// every matmul once per call (workspace), so each backward workgroup fills
-// its LDS with straight 16-byte copies. One block per (matmul, direction).
-template <int W, int IN_KS, int NH>
-__global__ void __launch_bounds__(256)
-k_mlp_pack(const ngp_half* __restrict__ weights, uint32_t in_dim, half8* __restrict__ image) {
-    using N = Net<W, IN_KS, NH>;
-    const int q = blockIdx.x >> 1;
-    if (blockIdx.x & 1) {
-        MatDesc mb = bwd_desc<W, IN_KS, NH>(q, in_dim);
-        mb.frag0 += N::FWD_FRAGS;
-        build_frags(image, weights, mb, true);
-    } else {
-        build_frags(image, weights, fwd_desc<W, IN_KS, NH>(q, in_dim), false);
-    }
-}
-
 // Single-pass fused backward: per 32-sample chunk a wave recomputes the
 // forward (activations stay in registers), walks the deltas down through
 // W^T fragments, and for every matmul forms dW += delta^T . input over the
@@ -453,10 +487,49 @@ k_mlp_pack(const ngp_half* __restrict__ weights, uint32_t in_dim, half8* __restr
 // wave's registers (accumulation VGPRs) for the whole chunk loop; only at the
 // end do the waves fold them, in fixed order, into an LDS image of dW that
 // the workgroup publishes as its slab row.
-template <int W, int IN_KS, int NH, typename FA>
+// grad_inputs epilogues: the plain [B, in_dim] store, or the NeRF color
+// network's (nerf/network_ff.py:67-68, the cat's backward): only the geo
+// columns 16..30 of the input gradient are kept, written to columns 1..15 of
+// the sigma network's output gradient [B, 16] (column 0 holds the density
+// gradient, written by the composite kernel).
+struct GiStore {
+    ngp_half* gi;
+    template <int IN_MT>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[kNB][IN_MT]) const {
+        store_tiles<IN_MT>(gi, in_dim, row0, B, t, ActNone{});
+    }
+};
+
+struct GiNerfGeo {
+    ngp_half* gh;
+    template <int IN_MT>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t, const f32x4 (&t)[kNB][IN_MT]) const {
+        static_assert(IN_MT == 2, "the color network input is 32 wide");  // see launch_bwd
+        const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+            // lane group g holds input columns 16 + 4g .. +3 (tile 1); output
+            // columns 4g .. 4g+3 take input columns 15 + 4g .. 18 + 4g
+            const ngp_half r0 = (ngp_half)t[nb][1][0], r1 = (ngp_half)t[nb][1][1], r2 = (ngp_half)t[nb][1][2];
+            const uint32_t pv = __shfl((uint32_t)__builtin_bit_cast(uint16_t, (ngp_half)t[nb][1][3]), lane - 16, 64);
+            const uint32_t row = row0 + nb * 16 + c;
+            if (row >= B) continue;
+            ngp_half* d = gh + (size_t)row * kOut + 4 * g;
+            if (g == 0) {
+                d[1] = r0;
+                d[2] = r1;
+                d[3] = r2;
+            } else {
+                *reinterpret_cast<half4*>(d) = half4{__builtin_bit_cast(ngp_half, (uint16_t)pv), r0, r1, r2};
+            }
+        }
+    }
+};
+
+template <int W, int IN_KS, int NH, typename FA, typename GI>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
-          const half8* __restrict__ image, ngp_half* __restrict__ grad_inputs,
+          const half8* __restrict__ image, GI gi_out, bool want_gi,
           float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, FA act,
           const int32_t* __restrict__ count) {
     using N = Net<W, IN_KS, NH>;
@@ -528,10 +601,10 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
         write_rows<N::KSW, true>(dT, d, W);
         write_rows<IN_KS, false>(hT, x, in_dim);
         dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
-        if (grad_inputs) {
+        if (want_gi) {
             f32x4 gi[kNB][N::IN_MT];
             dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
-            store_tiles<N::IN_MT>(grad_inputs, in_dim, row0, B, gi, ActNone{});
+            gi_out(row0, B, in_dim, gi);
         }
     }
 
@@ -562,14 +635,27 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
 // grad_weights[p] = sum over workgroup rows of the slab, in a fixed order
 // (deterministic). Block = 64 parameters (one 256 B row segment per wave) x
 // kReducePhases row phases; each thread keeps 4 independent partial sums so
-// its loads stay in flight.
+// its loads stay in flight. Several networks' slabs in one launch (jobs).
 constexpr int kReducePhases = 16;
+constexpr int kMaxReduceJobs = 4;
+struct ReduceJobs {
+    int n;
+    const float* slab[kMaxReduceJobs];
+    void* out[kMaxReduceJobs];
+    uint32_t rows[kMaxReduceJobs], np[kMaxReduceJobs];
+    uint32_t block0[kMaxReduceJobs + 1];
+};
+
 template <typename OUT>
 __global__ void __launch_bounds__(64 * kReducePhases)
-k_slab_reduce(const float* __restrict__ slab, uint32_t rows, uint32_t n, OUT* __restrict__ out) {
+k_slab_reduce(ReduceJobs jobs) {
     __shared__ float part[kReducePhases][64];
+    int j = 0;
+    while (j + 1 < jobs.n && blockIdx.x >= jobs.block0[j + 1]) ++j;
+    const float* __restrict__ slab = jobs.slab[j];
+    const uint32_t rows = jobs.rows[j], n = jobs.np[j];
     const uint32_t lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
-    const uint32_t p = blockIdx.x * 64 + lane;
+    const uint32_t p = (blockIdx.x - jobs.block0[j]) * 64 + lane;
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
     if (p < n) {
         uint32_t r = ph;
@@ -587,8 +673,28 @@ k_slab_reduce(const float* __restrict__ slab, uint32_t rows, uint32_t n, OUT* __
         float t = 0.0f;
 #pragma unroll
         for (int k = 0; k < kReducePhases; ++k) t += part[k][lane];
-        out[p] = (OUT)t;
+        static_cast<OUT*>(jobs.out[j])[p] = (OUT)t;
     }
+}
+
+// Fragment images of several networks in one launch: one block per (network,
+// matmul, direction) job, descriptors computed on the host.
+constexpr int kMaxPackJobs = 32;
+struct PackJob {
+    const ngp_half* w;
+    half8* image;
+    MatDesc m;
+    uint32_t transposed;
+};
+struct PackJobs {
+    int n;
+    PackJob job[kMaxPackJobs];
+};
+
+__global__ void __launch_bounds__(256)
+k_mlp_pack_jobs(PackJobs jobs) {
+    const PackJob& j = jobs.job[blockIdx.x];
+    build_frags(j.image, j.w, j.m, j.transposed != 0);
 }
 
 // ---- host dispatch ----------------------------------------------------------
@@ -614,75 +720,116 @@ int check_shape(uint32_t B, uint32_t in_dim, uint32_t out_dim, uint32_t hidden, 
     return NGP_OK;
 }
 
-template <int W, int IN_KS, int NH, typename FA, typename FO>
-int launch_fwd_t(const void* in, const void* w, uint32_t B, uint32_t in_dim, FA act, FO out_act,
-                 void* fwd_buf, void* out, const int32_t* count, hipStream_t st);
-
-template <int W, int IN_KS, int NH>
-int launch_fwd(const void* in, const void* w, uint32_t B, uint32_t in_dim, uint32_t act,
-               uint32_t out_act, void* fwd_buf, void* out, const int32_t* count, hipStream_t st) {
-    if (act == kReLU && out_act == kNone)
-        return launch_fwd_t<W, IN_KS, NH>(in, w, B, in_dim, ActReLU{}, ActNone{}, fwd_buf, out, count, st);
-    return launch_fwd_t<W, IN_KS, NH>(in, w, B, in_dim, ActAny{act}, ActAny{out_act}, fwd_buf, out, count, st);
-}
-
-template <int W, int IN_KS, int NH, typename FA, typename FO>
-int launch_fwd_t(const void* in, const void* w, uint32_t B, uint32_t in_dim, FA act, FO out_act,
-                 void* fwd_buf, void* out, const int32_t* count, hipStream_t st) {
+// Forward launch: w (built per workgroup) or a prepacked image; epilogue EPI.
+template <int W, int IN_KS, int NH, typename FA, typename FO, typename EPI>
+int launch_fwd_t(const void* in, const void* w, const void* image, uint32_t B, uint32_t in_dim, FA act,
+                 FO out_act, void* fwd_buf, const int32_t* count, EPI epi, hipStream_t st) {
     using N = Net<W, IN_KS, NH>;
     const size_t lds = (size_t)N::FWD_FRAGS * 64 * 16;
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
     uint32_t blocks = ngp_div_up(nchunks, kWaves);
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) return NGP_OK;
-    hipLaunchKernelGGL((k_mlp_fwd<W, IN_KS, NH, FA, FO>), dim3(blocks), dim3(kThreads), lds, st,
-                       (const ngp_half*)in, (const ngp_half*)w, (ngp_half*)out, (ngp_half*)fwd_buf,
-                       B, in_dim, act, out_act, count);
+    hipLaunchKernelGGL((k_mlp_fwd<W, IN_KS, NH, FA, FO, EPI>), dim3(blocks), dim3(kThreads), lds, st,
+                       (const ngp_half*)in, (const ngp_half*)w, (const half8*)image, (ngp_half*)fwd_buf,
+                       B, in_dim, act, out_act, count, epi);
     return ngp_check_launch("ffmlp_forward");
+}
+
+template <int W, int IN_KS, int NH>
+int launch_fwd(const void* in, const void* w, const void* image, uint32_t B, uint32_t in_dim, uint32_t act,
+               uint32_t out_act, void* fwd_buf, void* out, const int32_t* count, hipStream_t st) {
+    const EpiStore epi{static_cast<ngp_half*>(out)};
+    if (act == kReLU && out_act == kNone)
+        return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActReLU{}, ActNone{}, fwd_buf, count, epi, st);
+    return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActAny{act}, ActAny{out_act}, fwd_buf, count,
+                                      epi, st);
+}
+
+template <int W, int IN_KS, int NH>
+int launch_fwd_nerf(const void* in, const void* w, const void* image, uint32_t B, uint32_t in_dim,
+                    const int32_t* count, const EpiNerfSigma& epi, hipStream_t st) {
+    return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActReLU{}, ActNone{}, nullptr, count, epi, st);
 }
 
 constexpr size_t kImageBytes = 128 * 1024;  // fragment image slot at the head of the workspace
 
-template <int W, int IN_KS, int NH, typename FA>
-int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
-                 FA act, void* grad_in, void* gw, int32_t gw_dtype, void* ws, const int32_t* count,
-                 hipStream_t st);
-
 template <int W, int IN_KS, int NH>
-int launch_bwd(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
-               uint32_t act, void* grad_in, void* gw, int32_t gw_dtype, void* ws,
-               const int32_t* count, hipStream_t st) {
-    if (act == kReLU)
-        return launch_bwd_t<W, IN_KS, NH>(grad, in, w, B, in_dim, ActReLU{}, grad_in, gw, gw_dtype, ws, count, st);
-    return launch_bwd_t<W, IN_KS, NH>(grad, in, w, B, in_dim, ActAny{act}, grad_in, gw, gw_dtype, ws, count, st);
+size_t image_bytes_t() {
+    using N = Net<W, IN_KS, NH>;
+    return (size_t)(N::FWD_FRAGS + N::BWD_FRAGS) * 64 * sizeof(half8);
 }
 
-template <int W, int IN_KS, int NH, typename FA>
-int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, uint32_t in_dim,
-                 FA act, void* grad_in, void* gw, int32_t gw_dtype, void* ws, const int32_t* count,
-                 hipStream_t st) {
+// Pack jobs of one network: forward fragments of every matmul, then the
+// transposed (backward) ones, into one image.
+template <int W, int IN_KS, int NH>
+int add_pack_jobs(PackJobs& jobs, const void* w, uint32_t in_dim, void* image) {
     using N = Net<W, IN_KS, NH>;
+    NGP_REQUIRE(jobs.n + 2 * N::NMAT <= kMaxPackJobs, NGP_ERR_ARG, "ffmlp_pack: too many networks");
+    for (int q = 0; q < N::NMAT; ++q) {
+        jobs.job[jobs.n++] = PackJob{(const ngp_half*)w, (half8*)image, fwd_desc<W, IN_KS, NH>(q, in_dim), 0u};
+        MatDesc mb = bwd_desc<W, IN_KS, NH>(q, in_dim);
+        mb.frag0 += N::FWD_FRAGS;
+        jobs.job[jobs.n++] = PackJob{(const ngp_half*)w, (half8*)image, mb, 1u};
+    }
+    return NGP_OK;
+}
+
+template <int W, int IN_KS, int NH, typename FA, typename GI>
+int launch_bwd_t(const void* grad, const void* in, const void* w, const void* image, uint32_t B,
+                 uint32_t in_dim, FA act, GI gi, bool want_gi, void* gw, int32_t gw_dtype, bool defer,
+                 void* ws, const int32_t* count, hipStream_t st) {
     using L = BwdLds<W, IN_KS, NH>;
     static_assert(L::frag_bytes <= kImageBytes, "fragment image exceeds its workspace slot");
     static_assert(L::total <= 160 * 1024, "backward LDS budget exceeded");
     const uint32_t blocks = bwd_blocks(B);
     const uint32_t np = num_params(in_dim, W, NH + 1);
     if (blocks == 0) return NGP_OK;
-    half8* image = reinterpret_cast<half8*>(ws);
     float* slab = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kImageBytes);
-    hipLaunchKernelGGL((k_mlp_pack<W, IN_KS, NH>), dim3(2 * N::NMAT), dim3(256), 0, st,
-                       (const ngp_half*)w, in_dim, image);
-    hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH, FA>), dim3(blocks), dim3(kThreads), L::total, st,
-                       (const ngp_half*)grad, (const ngp_half*)in, (const half8*)image,
-                       (ngp_half*)grad_in, slab, np, B, in_dim, act, count);
-    if (gw_dtype == NGP_DTYPE_F16) {
-        hipLaunchKernelGGL((k_slab_reduce<ngp_half>), dim3(ngp_div_up(np, 64)), dim3(64 * kReducePhases), 0, st,
-                           (const float*)slab, blocks, np, (ngp_half*)gw);
-    } else {
-        hipLaunchKernelGGL((k_slab_reduce<float>), dim3(ngp_div_up(np, 64)), dim3(64 * kReducePhases), 0, st,
-                           (const float*)slab, blocks, np, (float*)gw);
+    if (!image) {
+        PackJobs jobs{};
+        add_pack_jobs<W, IN_KS, NH>(jobs, w, in_dim, ws);
+        hipLaunchKernelGGL(k_mlp_pack_jobs, dim3(jobs.n), dim3(256), 0, st, jobs);
+        image = ws;
+    }
+    hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH, FA, GI>), dim3(blocks), dim3(kThreads), L::total, st,
+                       (const ngp_half*)grad, (const ngp_half*)in, (const half8*)image, gi, want_gi, slab, np,
+                       B, in_dim, act, count);
+    if (!defer) {
+        ReduceJobs rj{};
+        rj.n = 1;
+        rj.slab[0] = slab;
+        rj.out[0] = gw;
+        rj.rows[0] = blocks;
+        rj.np[0] = np;
+        rj.block0[0] = 0;
+        rj.block0[1] = ngp_div_up(np, 64);
+        if (gw_dtype == NGP_DTYPE_F16)
+            hipLaunchKernelGGL(k_slab_reduce<ngp_half>, dim3(rj.block0[1]), dim3(64 * kReducePhases), 0, st, rj);
+        else
+            hipLaunchKernelGGL(k_slab_reduce<float>, dim3(rj.block0[1]), dim3(64 * kReducePhases), 0, st, rj);
     }
     return ngp_check_launch("ffmlp_backward");
+}
+
+template <int W, int IN_KS, int NH>
+int launch_bwd(const void* grad, const void* in, const void* w, const void* image, uint32_t B,
+               uint32_t in_dim, uint32_t act, void* grad_in, bool nerf_geo, void* gw, int32_t gw_dtype,
+               bool defer, void* ws, const int32_t* count, hipStream_t st) {
+    const bool want = grad_in != nullptr;
+    ngp_half* gi = static_cast<ngp_half*>(grad_in);
+    if (nerf_geo) {
+        NGP_REQUIRE(act == kReLU && IN_KS == 1 && in_dim == 32, NGP_ERR_UNSUPPORTED,
+                    "ffmlp_backward: NeRF geo-feature gradients need ReLU and a 32-wide input");
+        if constexpr (IN_KS == 1)
+            return launch_bwd_t<W, IN_KS, NH>(grad, in, w, image, B, in_dim, ActReLU{}, GiNerfGeo{gi}, want, gw,
+                                              gw_dtype, defer, ws, count, st);
+    }
+    if (act == kReLU)
+        return launch_bwd_t<W, IN_KS, NH>(grad, in, w, image, B, in_dim, ActReLU{}, GiStore{gi}, want, gw,
+                                          gw_dtype, defer, ws, count, st);
+    return launch_bwd_t<W, IN_KS, NH>(grad, in, w, image, B, in_dim, ActAny{act}, GiStore{gi}, want, gw,
+                                      gw_dtype, defer, ws, count, st);
 }
 
 #define NGP_MLP_DISPATCH(FN, ...)                                                              \
@@ -700,6 +847,15 @@ int launch_bwd_t(const void* grad, const void* in, const void* w, uint32_t B, ui
         }                                                                                       \
     } while (0)
 
+size_t image_bytes(uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers) {
+    NGP_MLP_DISPATCH(image_bytes_t);
+}
+
+int pack_one(PackJobs& jobs, const void* w, uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers,
+             void* image) {
+    NGP_MLP_DISPATCH(add_pack_jobs, jobs, w, in_dim, image);
+}
+
 }  // namespace
 
 extern "C" int ngp_ffmlp_forward(const void* inputs, const void* weights, uint32_t B,
@@ -710,21 +866,35 @@ extern "C" int ngp_ffmlp_forward(const void* inputs, const void* weights, uint32
     if (int e = check_shape(B, in_dim, output_dim, hidden_dim, num_layers)) return e;
     if (B == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
-    NGP_MLP_DISPATCH(launch_fwd, inputs, weights, B, in_dim, activation, output_activation,
+    NGP_MLP_DISPATCH(launch_fwd, inputs, weights, nullptr, B, in_dim, activation, output_activation,
                      forward_buffer, outputs, nullptr, st);
 }
 
 /* Fused-step variant: rows at or past *count are not computed (count may be
- * null). */
-extern "C" int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, uint32_t B,
-                                      const int32_t* count, uint32_t in_dim, uint32_t output_dim,
-                                      uint32_t hidden_dim, uint32_t num_layers, uint32_t activation,
-                                      uint32_t output_activation, void* outputs, void* stream) {
+ * null); image (nullable) is the network's ngp_ffmlp_pack image. */
+extern "C" int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, const void* image,
+                                      uint32_t B, const int32_t* count, uint32_t in_dim,
+                                      uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,
+                                      uint32_t activation, uint32_t output_activation, void* outputs,
+                                      void* stream) {
     if (int e = check_shape(B, in_dim, output_dim, hidden_dim, num_layers)) return e;
     if (B == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
-    NGP_MLP_DISPATCH(launch_fwd, inputs, weights, B, in_dim, activation, output_activation,
+    NGP_MLP_DISPATCH(launch_fwd, inputs, weights, image, B, in_dim, activation, output_activation,
                      nullptr, outputs, count, st);
+}
+
+extern "C" int ngp_nerf_sigma_forward(const void* inputs, const void* weights, const void* image, uint32_t B,
+                                      const int32_t* count, uint32_t in_dim, uint32_t hidden_dim,
+                                      uint32_t num_layers, void* h_out, float* sigma, void* color_in,
+                                      const float* dirs, float density_scale, void* stream) {
+    if (int e = check_shape(B, in_dim, kOut, hidden_dim, num_layers)) return e;
+    NGP_REQUIRE(h_out && sigma && color_in && dirs, NGP_ERR_ARG, "nerf_sigma_forward: null output");
+    if (B == 0) return NGP_OK;
+    hipStream_t st = ngp_stream(stream);
+    const EpiNerfSigma epi{static_cast<ngp_half*>(h_out), sigma, static_cast<ngp_half*>(color_in), dirs,
+                           density_scale};
+    NGP_MLP_DISPATCH(launch_fwd_nerf, inputs, weights, image, B, in_dim, count, epi, st);
 }
 
 extern "C" int ngp_ffmlp_inference(const void* inputs, const void* weights, uint32_t B,
@@ -742,6 +912,26 @@ extern "C" size_t ngp_ffmlp_backward_workspace_bytes(uint32_t B, uint32_t input_
                                                      uint32_t num_layers) {
     (void)output_dim;
     return kImageBytes + (size_t)bwd_blocks(B) * num_params(input_dim, hidden_dim, num_layers) * sizeof(float);
+}
+
+extern "C" size_t ngp_ffmlp_image_bytes(uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers) {
+    if (check_shape(0, in_dim, kOut, hidden_dim, num_layers)) return 0;
+    return image_bytes(in_dim, hidden_dim, num_layers);
+}
+
+extern "C" int ngp_ffmlp_pack(int32_t n, const void* const* weights, const uint32_t* in_dims,
+                              const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* images,
+                              void* stream) {
+    NGP_REQUIRE(n >= 1 && weights && in_dims && hidden_dims && num_layers && images, NGP_ERR_ARG,
+                "ffmlp_pack: bad arguments");
+    PackJobs jobs{};
+    for (int k = 0; k < n; ++k) {
+        if (int e = check_shape(0, in_dims[k], kOut, hidden_dims[k], num_layers[k])) return e;
+        NGP_REQUIRE(weights[k] && images[k], NGP_ERR_ARG, "ffmlp_pack: null weights or image %d", k);
+        if (int e = pack_one(jobs, weights[k], in_dims[k], hidden_dims[k], num_layers[k], images[k])) return e;
+    }
+    hipLaunchKernelGGL(k_mlp_pack_jobs, dim3(jobs.n), dim3(256), 0, ngp_stream(stream), jobs);
+    return ngp_check_launch("ffmlp_pack");
 }
 
 extern "C" int ngp_ffmlp_backward(const void* grad, const void* inputs, const void* weights,
@@ -763,18 +953,22 @@ extern "C" int ngp_ffmlp_backward(const void* grad, const void* inputs, const vo
                 "ffmlp_backward: workspace of %zu bytes required, got %zu", need, workspace_bytes);
     hipStream_t st = ngp_stream(stream);
     void* gi = calc_grad_inputs ? grad_inputs : nullptr;
-    NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, B, in_dim, activation, gi, grad_weights,
-                     gw_dtype, workspace, nullptr, st);
+    NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, nullptr, B, in_dim, activation, gi, false, grad_weights,
+                     gw_dtype, false, workspace, nullptr, st);
 }
 
 /* Fused-step variant: rows at or past *count contribute nothing (their
- * grad_inputs are not written). */
+ * grad_inputs are not written). image: the ngp_ffmlp_pack image (nullable:
+ * packed into the workspace). flags: NGP_FFMLP_DEFER_REDUCE leaves the
+ * per-workgroup dW partial sums in the workspace for ngp_ffmlp_reduce;
+ * NGP_FFMLP_NERF_GEO writes the input gradient's columns 16..30 into columns
+ * 1..15 of grad_inputs [B, 16] (the NeRF color network's geo features). */
 extern "C" int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* weights,
-                                       uint32_t B, const int32_t* count, uint32_t in_dim,
+                                       const void* image, uint32_t B, const int32_t* count, uint32_t in_dim,
                                        uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,
                                        uint32_t activation, void* grad_inputs, void* grad_weights,
-                                       int32_t gw_dtype, void* workspace, size_t workspace_bytes,
-                                       void* stream) {
+                                       int32_t gw_dtype, uint32_t flags, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
     if (int e = check_shape(B, in_dim, output_dim, hidden_dim, num_layers)) return e;
     NGP_REQUIRE(gw_dtype == NGP_DTYPE_F16 || gw_dtype == NGP_DTYPE_F32, NGP_ERR_ARG,
                 "grad_weights must be float16 or float32");
@@ -783,8 +977,40 @@ extern "C" int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, con
     NGP_REQUIRE(workspace && workspace_bytes >= need, NGP_ERR_ARG,
                 "ffmlp_backward: workspace of %zu bytes required, got %zu", need, workspace_bytes);
     hipStream_t st = ngp_stream(stream);
-    NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, B, in_dim, activation, grad_inputs, grad_weights,
-                     gw_dtype, workspace, count, st);
+    const bool geo = (flags & NGP_FFMLP_NERF_GEO) != 0, defer = (flags & NGP_FFMLP_DEFER_REDUCE) != 0;
+    NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, image, B, in_dim, activation, grad_inputs, geo,
+                     grad_weights, gw_dtype, defer, workspace, count, st);
+}
+
+/* Sums the deferred dW partials of n backward calls (same B / shapes as
+ * those calls) into grad_weights[k], one launch. */
+extern "C" int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32_t* Bs, const uint32_t* in_dims,
+                                const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* grad_weights,
+                                int32_t gw_dtype, void* stream) {
+    NGP_REQUIRE(n >= 1 && n <= kMaxReduceJobs, NGP_ERR_ARG, "ffmlp_reduce: 1..%d networks", kMaxReduceJobs);
+    NGP_REQUIRE(gw_dtype == NGP_DTYPE_F16 || gw_dtype == NGP_DTYPE_F32, NGP_ERR_ARG,
+                "grad_weights must be float16 or float32");
+    ReduceJobs rj{};
+    rj.n = 0;
+    uint32_t blocks = 0;
+    for (int k = 0; k < n; ++k) {
+        const uint32_t rows = bwd_blocks(Bs[k]);
+        if (rows == 0) continue;
+        const int j = rj.n++;
+        rj.slab[j] = reinterpret_cast<const float*>(static_cast<const char*>(workspaces[k]) + kImageBytes);
+        rj.out[j] = grad_weights[k];
+        rj.rows[j] = rows;
+        rj.np[j] = num_params(in_dims[k], hidden_dims[k], num_layers[k]);
+        rj.block0[j] = blocks;
+        blocks += ngp_div_up(rj.np[j], 64);
+    }
+    rj.block0[rj.n] = blocks;
+    if (blocks == 0) return NGP_OK;
+    if (gw_dtype == NGP_DTYPE_F16)
+        hipLaunchKernelGGL(k_slab_reduce<ngp_half>, dim3(blocks), dim3(64 * kReducePhases), 0, ngp_stream(stream), rj);
+    else
+        hipLaunchKernelGGL(k_slab_reduce<float>, dim3(blocks), dim3(64 * kReducePhases), 0, ngp_stream(stream), rj);
+    return ngp_check_launch("ffmlp_reduce");
 }
 
 extern "C" int ngp_ffmlp_allocate_splitk(size_t size) { (void)size; return NGP_OK; }

@@ -188,7 +188,7 @@ k_glue_fwd(const ngp_half* __restrict__ h, const float* __restrict__ dirs, float
                             [&](uint32_t k, float v) { sh[k] = v; });
     half8 o0, o1, o2, o3;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { o0[k] = (ngp_half)sh[k]; o1[k] = (ngp_half)sh[8 + k]; }
+    for (int k = 0; k < 8; ++k) { o0[k] = ngp_f2h(sh[k]); o1[k] = ngp_f2h(sh[8 + k]); }
     // geo features h[1..15], then the zero pad column
 #pragma unroll
     for (int k = 0; k < 7; ++k) o2[k] = h0[k + 1];

@@ -18,6 +18,15 @@
 
 #define NGP_DEV __device__ __forceinline__
 
+// float -> half of an already rounded float. The backend folds
+// fptrunc(fmul(a, b)) into v_fma_mix*_f16 (one rounding of the exact product
+// instead of the float product's two), which torch's `.half()` of a float
+// tensor does not do; the empty asm pins the float first.
+NGP_DEV _Float16 ngp_f2h(float x) {
+    asm volatile("" : "+v"(x));
+    return (_Float16)x;
+}
+
 typedef _Float16 ngp_half;
 typedef _Float16 ngp_half2 __attribute__((ext_vector_type(2)));
 

@@ -39,6 +39,7 @@ from .provider import LEGO_BOXES, LEGO_COLORS
 
 _F16 = nat.DTYPE_CODE[torch.float16]
 _RELU, _NONE = 0, 6
+_DEFER, _GEO = 1, 2  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO
 
 
 def _vp_array(ptrs):
@@ -89,7 +90,7 @@ class FusedTrainer:
         self.enc_out, self.h_sigma = z(M, 32, dtype=h), z(M, 16, dtype=h)
         self.sigma, self.color_in, self.color_out = z(M), z(M, 32, dtype=h), z(M, 16, dtype=h)
         self.g_color_out, self.g_h = z(M, 16, dtype=h), z(M, 16, dtype=h)
-        self.g_color_in, self.g_enc = z(M, 32, dtype=h), z(M, 32, dtype=h)
+        self.g_enc = z(M, 32, dtype=h)
         # parameters: fp32 masters, fp16 grads, fp16 forward copies of the MLPs
         self.params = [enc.embeddings, self.sig_net.weights, self.col_net.weights]
         # one flat fp16 gradient (one all-reduce in data-parallel mode), 8-aligned views
@@ -113,6 +114,19 @@ class FusedTrainer:
             b = nat.lib().ngp_ffmlp_backward_workspace_bytes(M, net.input_dim, net.padded_output_dim,
                                                              net.hidden_dim, net.num_layers)
             self.mlp_ws.append(z(b, dtype=torch.uint8))
+        # weight-fragment images of both networks, packed once per step
+        nets = (self.sig_net, self.col_net)
+        self.mlp_img = [z(int(nat.lib().ngp_ffmlp_image_bytes(n.input_dim, n.hidden_dim, n.num_layers)),
+                          dtype=torch.uint8) for n in nets]
+        self._pk = dict(
+            w=_vp_array([nat.ptr(t) for t in self.w_half[1:]]),
+            ins=(ctypes.c_uint32 * 2)(*[n.input_dim for n in nets]),
+            hid=(ctypes.c_uint32 * 2)(*[n.hidden_dim for n in nets]),
+            nl=(ctypes.c_uint32 * 2)(*[n.num_layers for n in nets]),
+            img=_vp_array([nat.ptr(t) for t in self.mlp_img]),
+            ws=_vp_array([nat.ptr(t) for t in self.mlp_ws]),
+            B=(ctypes.c_uint32 * 2)(M, M),
+            gw=_vp_array([nat.ptr(g) for g in self.grads[1:]]))
         self.state = z(nat.lib().ngp_fused_state_bytes(), dtype=torch.uint8)
         nat.check(nat.lib().ngp_fused_state_init(nat.ptr(self.state), float(init_scale),
                                                  nat.stream_of(self.state)), "fused_state_init")
@@ -230,38 +244,42 @@ class FusedTrainer:
         m, e = self.model, self.enc
         M, N, cnt = self.M, self.N, P(self.counter)
         chk = nat.check
+        pk = self._pk
+        chk(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
+        self._tick("ffmlp_pack")
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
         chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(self.w_half[0]), _F16, P(e.offsets),
                                               P(self.enc_out), M, cnt, *grid_args), "grid_encode_fused")
         self._tick("grid_encode_forward")
-        sn, cn = self.sig_net, self.col_net
-        chk(lib.ngp_ffmlp_forward_rows(P(self.enc_out), P(self.w_half[1]), M, cnt, 32, 16, sn.hidden_dim,
-                                       sn.num_layers, _RELU, _NONE, P(self.h_sigma), s), "sigma_mlp")
+        sn, cn, img, pk = self.sig_net, self.col_net, self.mlp_img, self._pk
+        chk(lib.ngp_nerf_sigma_forward(P(self.enc_out), P(self.w_half[1]), P(img[0]), M, cnt, 32, sn.hidden_dim,
+                                       sn.num_layers, P(self.h_sigma), P(self.sigma), P(self.color_in),
+                                       P(self.dirs), float(m.density_scale), s), "sigma_mlp")
         self._tick("ffmlp_forward_sigma")
-        chk(lib.ngp_nerf_glue_forward(P(self.h_sigma), P(self.dirs), float(m.density_scale), P(self.sigma),
-                                      P(self.color_in), M, cnt, s), "glue_forward")
-        self._tick("glue_forward")
-        chk(lib.ngp_ffmlp_forward_rows(P(self.color_in), P(self.w_half[2]), M, cnt, 32, 16, cn.hidden_dim,
-                                       cn.num_layers, _RELU, _NONE, P(self.color_out), s), "color_mlp")
+        chk(lib.ngp_ffmlp_forward_rows(P(self.color_in), P(self.w_half[2]), P(img[1]), M, cnt, 32, 16,
+                                       cn.hidden_dim, cn.num_layers, _RELU, _NONE, P(self.color_out), s),
+            "color_mlp")
         self._tick("ffmlp_forward_color")
         chk(lib.ngp_nerf_composite_loss(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
                                         P(self.rays), M, N, self.T_thresh, float(m.density_scale),
                                         P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
                                         P(self.g_h), None, None, P(self.loss_ray), s), "composite_loss")
         self._tick("composite_loss")
-        chk(lib.ngp_ffmlp_backward_rows(P(self.g_color_out), P(self.color_in), P(self.w_half[2]), M, cnt,
-                                        32, 16, cn.hidden_dim, cn.num_layers, _RELU, P(self.g_color_in),
-                                        P(self.grads[2]), _F16, P(self.mlp_ws[1]), self.mlp_ws[1].numel(),
-                                        s), "color_mlp_backward")
+        # color backward: its input gradient's geo columns land in g_h[:, 1:16]
+        chk(lib.ngp_ffmlp_backward_rows(P(self.g_color_out), P(self.color_in), P(self.w_half[2]), P(img[1]), M,
+                                        cnt, 32, 16, cn.hidden_dim, cn.num_layers, _RELU, P(self.g_h),
+                                        None, _F16, _DEFER | _GEO, P(self.mlp_ws[1]), self.mlp_ws[1].numel(), s),
+            "color_mlp_backward")
         self._tick("ffmlp_backward_color")
-        chk(lib.ngp_nerf_glue_backward(P(self.g_color_in), P(self.g_h), M, cnt, s), "glue_backward")
-        self._tick("glue_backward")
-        chk(lib.ngp_ffmlp_backward_rows(P(self.g_h), P(self.enc_out), P(self.w_half[1]), M, cnt, 32, 16,
-                                        sn.hidden_dim, sn.num_layers, _RELU, P(self.g_enc),
-                                        P(self.grads[1]), _F16, P(self.mlp_ws[0]), self.mlp_ws[0].numel(),
-                                        s), "sigma_mlp_backward")
+        chk(lib.ngp_ffmlp_backward_rows(P(self.g_h), P(self.enc_out), P(self.w_half[1]), P(img[0]), M, cnt, 32,
+                                        16, sn.hidden_dim, sn.num_layers, _RELU, P(self.g_enc), None, _F16,
+                                        _DEFER, P(self.mlp_ws[0]), self.mlp_ws[0].numel(), s),
+            "sigma_mlp_backward")
         self._tick("ffmlp_backward_sigma")
+        chk(lib.ngp_ffmlp_reduce(2, pk["ws"], pk["B"], pk["ins"], pk["hid"], pk["nl"], pk["gw"], _F16, s),
+            "ffmlp_reduce")
+        self._tick("ffmlp_reduce")
         chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
                                                P(self.grads[0]), M, cnt, *grid_args[:-1], self._offsets_host,
                                                P(self.grid_ws), self.grid_ws.numel(), s),
