@@ -725,7 +725,7 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // (inf / NaN: fp16 overflow under the loss scale) cannot be carried by the
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
-constexpr uint32_t kAccThreads = 512, kAccBatch = 16;
+constexpr uint32_t kAccThreads = 512, kAccBatch = 16, kRetireGroups = 16;
 __global__ void __launch_bounds__(kAccThreads)
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
@@ -793,15 +793,25 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         run += u;
     }
     if (t == 0) upre[nbins] = total;
-    // 2. retire: once every workgroup holds the counts, the last one zeroes them
+    // 2. retire: once every workgroup holds the counts, the last one zeroes
+    // them for the next step. Two-level counter (kRetireGroups group counters,
+    // then one), so no address takes more than ~gridDim / kRetireGroups
+    // atomics: 512 workgroups through one counter cost ~10 us.
     if (t == 0) {
         __threadfence();
-        s_last = atomicAdd(retire, 1u) == gridDim.x - 1;
+        const uint32_t grp = blockIdx.x % kRetireGroups;
+        const uint32_t members = gridDim.x / kRetireGroups + (grp < gridDim.x % kRetireGroups ? 1u : 0u);
+        s_last = 0;
+        if (atomicAdd(&retire[1 + grp], 1u) == members - 1) {
+            retire[1 + grp] = 0;
+            const uint32_t groups = min(gridDim.x, kRetireGroups);
+            s_last = atomicAdd(&retire[0], 1u) == groups - 1;
+        }
     }
     __syncthreads();
     if (s_last) {
         for (uint32_t b = t; b < nbins; b += kAccThreads) cursor[b] = 0;
-        if (t == 0) *retire = 0;
+        if (t == 0) retire[0] = 0;
     }
 
     // 3. units. The first item batch of a unit and, for a single-owner unit,

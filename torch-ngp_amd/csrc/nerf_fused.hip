@@ -447,7 +447,9 @@ struct AdamArgs {
 
 // torch.optim.Adam (weight_decay 0) on p, with g = half_grad * (1 / scale);
 // skipped (state untouched) when the check found an inf/nan, like
-// GradScaler.step. Grads are zeroed afterwards either way.
+// GradScaler.step. Grads are zeroed afterwards either way. (Ending the step
+// in Adam's last block instead of k_step_end was measured: 4096 blocks
+// retiring through one counter cost ~180 us of contended atomics.)
 //
 // Layout: chunks of kAdamChunk elements of the flat (8-aligned per tensor)
 // index space, chunk c to block c mod gridDim; every thread keeps two 16-byte
