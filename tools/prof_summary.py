@@ -26,20 +26,20 @@ def short(name):
 def main(tag, out=None):
     rows = list(csv.DictReader(open(os.path.join(tag, "trace", "run_kernel_trace.csv"))))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "k_lego_rays" in r["Kernel_Name"]]
-    # bench.py: ... timed graph replays (STEPS), then KSTEPS instrumented eager steps
-    steps, ksteps = int(os.environ.get("STEPS", "30")), int(os.environ.get("KSTEPS", "10"))
-    sel = starts[-(steps + ksteps):len(starts) - ksteps]
+    # bench.py order: ... timed graph replays (STEPS), each one step body
+    # [k_nonfinite, k_adam_multi, k_step_end (previous grads), k_lego_rays, ...,
+    # grid backward]; then FusedTrainer.timed_steps: flush() (3 optimizer
+    # kernels) and eager steps behind torch's spin kernel.
+    steps = int(os.environ.get("STEPS", "30"))
+    spin = next((i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]), len(rows))
+    name = lambda i: rows[i]["Kernel_Name"] if i < len(rows) else ""  # noqa: E731
+    starts = [i for i in range(spin) if "k_nonfinite" in name(i) and "k_lego_rays" in name(i + 3)]
+    sel = starts[-steps:]
     per = collections.defaultdict(list)
     spans = []
-    for a, i in enumerate(sel):
-        j = sel[a + 1] if a + 1 < len(sel) else None
-        if j is None and starts.index(i) + 1 < len(starts):
-            j = starts[starts.index(i) + 1]
-        seg = rows[i:j] if j else rows[i:]
-        if a + 1 == len(sel):  # last step: up to and including k_step_end
-            k = next(n for n, r in enumerate(seg) if "k_step_end" in r["Kernel_Name"])
-            seg = seg[:k + 1]
+    for i in sel:
+        j = next(k for k in range(i, len(rows)) if "k_grid_bin_accum" in name(k)) + 1
+        seg = rows[i:j]
         t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
         spans.append((t1 - t0) / 1e3)
         cnt = collections.Counter()

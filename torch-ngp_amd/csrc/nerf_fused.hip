@@ -265,9 +265,11 @@ NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __rest
     const float d1 = c.ok ? deltas[(size_t)i * 2 + 1] : 0.0f;
     c.c0 = c.c1 = c.c2 = 0.0f;
     if (c.ok) {
-        c.c0 = sigmoid_h(color_out[(size_t)i * 16 + 0]);
-        c.c1 = sigmoid_h(color_out[(size_t)i * 16 + 1]);
-        c.c2 = sigmoid_h(color_out[(size_t)i * 16 + 2]);
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+        const half4 co = *reinterpret_cast<const half4*>(color_out + (size_t)i * 16);
+        c.c0 = sigmoid_h(co[0]);
+        c.c1 = sigmoid_h(co[1]);
+        c.c2 = sigmoid_h(co[2]);
     }
     const float sd = sg * c.d0;
     const float incl = scan_incl(sd, lane);
@@ -304,13 +306,24 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     const bool valid = num_steps != 0 && offset + num_steps <= M;
 
     // ---- forward (composite_rays_train_forward)
+    // The first 64-sample chunk (all of most rays) is kept for the backward
+    // pass instead of being loaded and scanned again.
     float r = 0, g = 0, b = 0, ws = 0, d = 0;
+    Chunk first{};
+    float S1 = 0.0f, tacc1 = 0.0f;
+    bool stop1 = false;
     if (valid) {
         float S = 0.0f, tacc = 0.0f;
         for (uint32_t base = 0; base < num_steps; base += 64) {
             bool stop;
             const Chunk c = load_chunk(sigma, color_out, deltas, offset, base, num_steps, lane, S, tacc,
                                        la.T_thresh, stop);
+            if (base == 0) {
+                first = c;
+                S1 = S;
+                tacc1 = tacc;
+                stop1 = stop;
+            }
             r += wave_sum(c.w * c.c0);
             g += wave_sum(c.w * c.c1);
             b += wave_sum(c.w * c.c2);
@@ -364,8 +377,15 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     bool stopped = false;
     for (uint32_t base = 0; base < num_steps; base += 64) {
         bool stop = false;
-        Chunk c = load_chunk(sigma, color_out, deltas, offset, base, num_steps, lane, S, tacc,
-                             la.T_thresh, stop);
+        Chunk c;
+        if (base == 0) {
+            c = first;
+            S = S1;
+            tacc = tacc1;
+            stop = stop1;
+        } else {
+            c = load_chunk(sigma, color_out, deltas, offset, base, num_steps, lane, S, tacc, la.T_thresh, stop);
+        }
         if (stopped) { c.active = false; c.w = 0.0f; }
         // running sums after this lane's sample (inclusive prefix)
         const float pr = rr + scan_incl(c.w * c.c0, lane);
@@ -384,15 +404,15 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
             }
             // rgbs.float() <- half, then sigmoid_backward(grad, y) = grad * (1 - y) * y (fp32 math)
             half8 o0 = {0, 0, 0, 0, 0, 0, 0, 0}, o1 = {0, 0, 0, 0, 0, 0, 0, 0};
-            o0[0] = (ngp_half)((float)(ngp_half)gc0 * (1.0f - c.c0) * c.c0);
-            o0[1] = (ngp_half)((float)(ngp_half)gc1 * (1.0f - c.c1) * c.c1);
-            o0[2] = (ngp_half)((float)(ngp_half)gc2 * (1.0f - c.c2) * c.c2);
+            o0[0] = ngp_f2h((float)ngp_f2h(gc0) * (1.0f - c.c0) * c.c0);
+            o0[1] = ngp_f2h((float)ngp_f2h(gc1) * (1.0f - c.c1) * c.c1);
+            o0[2] = ngp_f2h((float)ngp_f2h(gc2) * (1.0f - c.c2) * c.c2);
             half8* go = reinterpret_cast<half8*>(grad_color_out + (size_t)i * 16);
             go[0] = o0;
             go[1] = o1;
             // sigmas = ds * trunc_exp(h0): grad_h0 = (gs * ds) * exp(clamp(h0, -15, 15)), -> half
             const float h0 = (float)h_sigma[(size_t)i * 16];
-            grad_h[(size_t)i * 16] = (ngp_half)((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
+            grad_h[(size_t)i * 16] = ngp_f2h((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
         }
         stopped = stopped || stop;
     }
