@@ -245,6 +245,15 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
 // cache line per lane PAIR. The partner's values arrive by one shuffle and
 // both lanes accumulate all 2^D corners in the reference's order, so the
 // result is bit-identical to k_grid_fwd; the even lane stores it.
+//
+// XCD-aware block -> work mapping: blocks are dealt round-robin over the 8
+// XCDs (MI355X_MICROARCH.md, workgroup dispatch), so block id % 8 picks the
+// XCD. XCD j gets only levels j, j + 8, j + 16, ... (each XCD's 4 MiB L2 then
+// holds at most ceil(L / 8) level tables), and one block does KL of them for
+// its 128 points: the point is loaded once and the KL levels' gathers are all
+// in flight together.
+constexpr uint32_t kFwdLevelsPerBlock = 2;
+
 template <typename T, typename E, uint32_t D, uint32_t C>
 __global__ void __launch_bounds__(256)
 k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
@@ -253,9 +262,15 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
                 int32_t out_layout, InMap im) {
     using A = Acc<T>;
     using F = typename A::F;
-    const uint32_t b = blockIdx.x * (blockDim.x / 2) + (threadIdx.x >> 1);
+    constexpr uint32_t KL = kFwdLevelsPerBlock, NR = 1u << (D - 1);
+    const uint32_t lpx = (L + 7) / 8;                       // levels per XCD
+    const uint32_t gpx = (lpx + KL - 1) / KL;               // level groups per XCD
+    const uint32_t k = blockIdx.x >> 3;
+    const uint32_t grp = k % gpx, chunk = k / gpx;
+    const uint32_t level0 = (blockIdx.x & 7) + 8 * KL * grp;  // this block: level0, level0 + 8, ...
+    if (level0 >= L) return;
+    const uint32_t b = chunk * (blockDim.x / 2) + (threadIdx.x >> 1);
     const uint32_t xbit = threadIdx.x & 1;
-    const uint32_t level = blockIdx.y;
     const bool live = b < rows_of(B, im);
     if (__ballot(live) == 0) return;  // wave-uniform exit; pairs stay together below
 
@@ -267,63 +282,73 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
         if (im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
         if (x[d] < 0 || x[d] > 1) oob = true;
     }
-    T* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C
-                             : outputs + ((size_t)b * L + level) * C;
 
-    const uint32_t off0 = (uint32_t)offsets[level];
-    const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
-    const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
-    const E* __restrict__ g = grid + (size_t)off0 * C;
-    const float scale = lv.scale[level];
-    const uint32_t resolution = lv.res[level];
-
-    float pos[D];
-    uint32_t pg[D];
+    // gathers of every level first
+    float pos[KL][D];
+    F mine[KL][NR][C];
 #pragma unroll
-    for (uint32_t d = 0; d < D; d++) {
-        pos[d] = fmaf(x[d], scale, align_corners ? 0.0f : 0.5f);
-        pg[d] = (uint32_t)floorf(pos[d]);
-        pos[d] -= (float)pg[d];
-        if (interp == 1) pos[d] = smoothstep(pos[d]);
-    }
-    // this lane's corners: idx = (rest << 1) | xbit
-    F mine[1u << (D - 1)][C];
+    for (uint32_t q = 0; q < KL; ++q) {
+        const uint32_t level = level0 + 8 * q;
+        if (level >= L) break;
+        const uint32_t off0 = (uint32_t)offsets[level];
+        const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
+        const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
+        const E* __restrict__ g = grid + (size_t)off0 * C;
+        const float scale = lv.scale[level];
+        const uint32_t resolution = lv.res[level];
+        uint32_t pg[D];
 #pragma unroll
-    for (uint32_t rest = 0; rest < (1u << (D - 1)); rest++) {
-        const uint32_t idx = (rest << 1) | xbit;
-        uint32_t pl[D];
+        for (uint32_t d = 0; d < D; d++) {
+            pos[q][d] = fmaf(x[d], scale, align_corners ? 0.0f : 0.5f);
+            pg[d] = (uint32_t)floorf(pos[q][d]);
+            pos[q][d] -= (float)pg[d];
+            if (interp == 1) pos[q][d] = smoothstep(pos[q][d]);
+        }
+        // this lane's corners: idx = (rest << 1) | xbit
 #pragma unroll
-        for (uint32_t d = 0; d < D; d++) pl[d] = (idx & (1u << d)) ? pg[d] + 1 : pg[d];
-        if (!oob) {
-            const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
-            load_entry_as<T, E, C>(g + (size_t)e * C, mine[rest]);
-        } else {
+        for (uint32_t rest = 0; rest < NR; rest++) {
+            const uint32_t idx = (rest << 1) | xbit;
+            uint32_t pl[D];
 #pragma unroll
-            for (uint32_t c = 0; c < C; ++c) mine[rest][c] = 0;
+            for (uint32_t d = 0; d < D; d++) pl[d] = (idx & (1u << d)) ? pg[d] + 1 : pg[d];
+            if (!oob) {
+                const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
+                load_entry_as<T, E, C>(g + (size_t)e * C, mine[q][rest]);
+            } else {
+#pragma unroll
+                for (uint32_t c = 0; c < C; ++c) mine[q][rest][c] = 0;
+            }
         }
     }
-    typename A::S res[C];
 #pragma unroll
-    for (uint32_t c = 0; c < C; ++c) res[c] = A::zero();
+    for (uint32_t q = 0; q < KL; ++q) {
+        const uint32_t level = level0 + 8 * q;
+        if (level >= L) break;
+        typename A::S res[C];
 #pragma unroll
-    for (uint32_t idx = 0; idx < (1u << D); idx++) {
-        float w = 1;
+        for (uint32_t c = 0; c < C; ++c) res[c] = A::zero();
 #pragma unroll
-        for (uint32_t d = 0; d < D; d++) w *= (idx & (1u << d)) ? pos[d] : 1 - pos[d];
-        const uint32_t rest = idx >> 1;
+        for (uint32_t idx = 0; idx < (1u << D); idx++) {
+            float w = 1;
 #pragma unroll
-        for (uint32_t c = 0; c < C; ++c) {
-            const F other = (F)__shfl_xor((float)mine[rest][c], 1, 64);
-            const F v = ((idx & 1u) == xbit) ? mine[rest][c] : other;
-            res[c] = A::mac(res[c], (F)w, v);
+            for (uint32_t d = 0; d < D; d++) w *= (idx & (1u << d)) ? pos[q][d] : 1 - pos[q][d];
+            const uint32_t rest = idx >> 1;
+#pragma unroll
+            for (uint32_t c = 0; c < C; ++c) {
+                const F other = (F)__shfl_xor((float)mine[q][rest][c], 1, 64);
+                const F v = ((idx & 1u) == xbit) ? mine[q][rest][c] : other;
+                res[c] = A::mac(res[c], (F)w, v);
+            }
         }
-    }
-    if (live && xbit == 0) {
-        if (oob) {
+        if (live && xbit == 0) {
+            if (oob) {
 #pragma unroll
-            for (uint32_t c = 0; c < C; ++c) res[c] = A::zero();
+                for (uint32_t c = 0; c < C; ++c) res[c] = A::zero();
+            }
+            T* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C
+                                     : outputs + ((size_t)b * L + level) * C;
+            store_entry<T, C>(out, res);
         }
-        store_entry<T, C>(out, res);
     }
 }
 
@@ -1078,7 +1103,9 @@ int fwd_c(const float* inputs, const void* emb, const int32_t* offsets, void* ou
     T* o = (T*)out;
     T* dd = (T*)dy_dx;
     if (!dd && (sizeof(T) <= 4)) {
-        const dim3 gp(ngp_div_up(B, 128), L);
+        // XCD-aware 1-D grid (see the kernel): 8 XCDs x level groups x point chunks
+        const uint32_t gpx = ((L + 7) / 8 + kFwdLevelsPerBlock - 1) / kFwdLevelsPerBlock;
+        const dim3 gp(8 * gpx * ngp_div_up(B, 128));
         switch (C) {
             case 1: k_grid_fwd_pair<T, E, D, 1><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
             case 2: k_grid_fwd_pair<T, E, D, 2><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
