@@ -228,7 +228,7 @@ int ngp_grid_encode_forward_fused(const float* xyz, float bound, const void* emb
                                   int32_t emb_dtype, const int32_t* offsets, void* outputs, uint32_t B,
                                   const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
                                   uint32_t H, uint32_t gridtype, int32_t align_corners,
-                                  uint32_t interp, void* stream);
+                                  uint32_t interp, int32_t out_layout, void* stream);
 /* Binned backward (hashed levels without scattered atomics) when workspace is
  * given: offsets_host is a host copy of offsets; the workspace (size from
  * ngp_grid_encode_backward_fused_workspace_bytes, 0 if nothing is binned) must
@@ -241,7 +241,7 @@ int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bou
                                    const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
                                    uint32_t H, uint32_t gridtype, int32_t align_corners,
                                    uint32_t interp, const int32_t* offsets_host, void* workspace,
-                                   size_t workspace_bytes, void* stream);
+                                   size_t workspace_bytes, int32_t grad_layout, void* stream);
 /* Weight-fragment images (forward + transposed, per matmul) of n networks in
  * one launch; image k needs ngp_ffmlp_image_bytes of its network. The
  * forward/backward *_rows calls below take the image (nullable: the weights
@@ -260,9 +260,10 @@ int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, const void* 
 int ngp_nerf_sigma_forward(const void* inputs, const void* weights, const void* image, uint32_t B,
                            const int32_t* count, uint32_t in_dim, uint32_t hidden_dim,
                            uint32_t num_layers, void* h_out, float* sigma, void* color_in,
-                           const float* dirs, float density_scale, void* stream);
+                           const float* dirs, float density_scale, uint32_t flags, void* stream);
 #define NGP_FFMLP_DEFER_REDUCE 1u /* leave dW partials for ngp_ffmlp_reduce */
 #define NGP_FFMLP_NERF_GEO 2u     /* grad_inputs [B,16]: input-grad cols 16..30 -> cols 1..15 */
+#define NGP_FFMLP_PAIR_MAJOR 4u   /* inputs and grad_inputs as [in_dim/2][B][2] (the grid's [L,B,2]) */
 int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* weights,
                             const void* image, uint32_t B, const int32_t* count, uint32_t in_dim,
                             uint32_t output_dim, uint32_t hidden_dim, uint32_t num_layers,

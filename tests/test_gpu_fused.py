@@ -214,7 +214,7 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
     h, sig = torch.zeros_like(h_ref), torch.zeros_like(sig_ref)
     ci = torch.zeros_like(ci_ref)
     nat.check(lib.ngp_nerf_sigma_forward(P(x), P(ws[0]), P(imgs[0]), B, P(cnt), 32, 64, 2, P(h), P(sig), P(ci),
-                                         P(dirs), 1.0, s), "sigma_fwd")
+                                         P(dirs), 1.0, 0, s), "sigma_fwd")
     torch.cuda.synchronize()
     assert torch.equal(h[:n].view(torch.int16), h_ref[:n].view(torch.int16))
     assert torch.equal(sig[:n], sig_ref[:n]), int((sig[:n] != sig_ref[:n]).sum())
@@ -255,3 +255,18 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
     assert torch.equal(gx[:n].view(torch.int16), gx_ref[:n].view(torch.int16))
     for a, b in zip(gw, gw_ref):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    # pair-major ([16][B][2], the grid's level-major layout) input and input gradient
+    xp = x.view(B, 16, 2).permute(1, 0, 2).contiguous()
+    h2, sig2, ci2 = torch.zeros_like(h_ref), torch.zeros_like(sig_ref), torch.zeros_like(ci_ref)
+    nat.check(lib.ngp_nerf_sigma_forward(P(xp), P(ws[0]), P(imgs[0]), B, P(cnt), 32, 64, 2, P(h2), P(sig2),
+                                         P(ci2), P(dirs), 1.0, 4, s), "sigma_fwd_pair")
+    gxp = torch.zeros_like(gx_ref)
+    gw2 = torch.zeros_like(gw_ref[0])
+    nat.check(lib.ngp_ffmlp_backward_rows(P(gh), P(xp), P(ws[0]), P(imgs[0]), B, P(cnt), 32, 16, 64, 2, 0, P(gxp),
+                                          P(gw2), 1, 4, P(wsb[0]), wsb[0].numel(), s), "b_pair")
+    torch.cuda.synchronize()
+    assert torch.equal(h2[:n].view(torch.int16), h_ref[:n].view(torch.int16))
+    assert torch.equal(sig2[:n], sig_ref[:n])
+    gx_rows = gxp.view(16, B, 2).permute(1, 0, 2).reshape(B, 32)
+    assert torch.equal(gx_rows[:n].view(torch.int16), gx_ref[:n].view(torch.int16))
+    assert torch.equal(gw2.view(torch.int16), gw_ref[0].view(torch.int16))

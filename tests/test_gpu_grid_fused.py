@@ -53,7 +53,7 @@ def _normalise(w, bound):
     return ((w + np.float32(bound)) * np.float32(1.0 / (2.0 * bound))).astype(np.float32)
 
 
-def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, reps=1):
+def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, reps=1, layout=1):
     B = w.shape[0]
     S = float(np.float32(np.log2(scale)))
     offs_host = np.ascontiguousarray(offs, dtype=np.int32)
@@ -63,12 +63,14 @@ def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, rep
     if table is None:
         table = torch.zeros(int(offs[-1]), 2, dtype=torch.float16, device=dev)
     gt, wt, ot = (torch.from_numpy(a).to(dev) for a in (g16, w, offs_host))
+    if layout == 0:  # [L, B, C]
+        gt = gt.view(B, L, 2).permute(1, 0, 2).contiguous()
     cnt = torch.tensor([count], dtype=torch.int32, device=dev) if count is not None else None
     for _ in range(reps):
         nat.check(nat.lib().ngp_grid_encode_backward_fused(
             nat.ptr(gt), nat.ptr(wt), float(bound), nat.ptr(ot), nat.ptr(table), B,
             nat.ptr(cnt) if cnt is not None else None, 3, 2, L, S, H, 0, 0, 0, hp,
-            nat.ptr(ws), ws.numel(), nat.stream_of(table)), "grid_backward_fused")
+            nat.ptr(ws), ws.numel(), layout, nat.stream_of(table)), "grid_backward_fused")
     torch.cuda.synchronize()
     # the workspace's counters are left zeroed for the next call
     assert int(ws[:256].sum()) == 0
@@ -127,20 +129,21 @@ def test_grid_backward_fused_bin_overflow(cuda):
     _check_levels(got, ref, offs, "overflow", rtol=2e-2, mtol=4e-2)
 
 
-def test_grid_backward_fused_count_clip_and_accumulate(cuda):
+@pytest.mark.parametrize("layout", [1, 0])
+def test_grid_backward_fused_count_clip_and_accumulate(cuda, layout):
     nat = _lib()
     B, L, H, scale = 40000, 16, 16, LEGO_SCALE
     offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
     w = _world(B, 1.0, seed=11, ordered=True)
     g16 = (np.random.default_rng(3).standard_normal((B, L * 2)) * 0.5).astype(np.float16)
     n = 31000
-    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, 1.0, count=n, reps=2)  # two calls add up
+    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, 1.0, count=n, reps=2, layout=layout)  # two calls add up
     ref = 2.0 * oracle.grid_encode_backward(g16[:n], _normalise(w[:n], 1.0), offs, 2, scale, H)
     _check_levels(got, ref, offs, "clip+accumulate")
 
 
-@pytest.mark.parametrize("table", ["f32", "f16"])
-def test_grid_forward_fused_bit_exact(cuda, table):
+@pytest.mark.parametrize("table,layout", [("f32", 1), ("f16", 1), ("f16", 0)])
+def test_grid_forward_fused_bit_exact(cuda, table, layout):
     nat = _lib()
     B, L, H, scale, bound = 9000, 16, 16, LEGO_SCALE, 2.0
     offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
@@ -157,9 +160,11 @@ def test_grid_forward_fused_bit_exact(cuda, table):
     cnt = torch.tensor([n], dtype=torch.int32, device=cuda)
     nat.check(nat.lib().ngp_grid_encode_forward_fused(nat.ptr(wt), bound, nat.ptr(et), nat.DTYPE_CODE[et.dtype],
                                                       nat.ptr(ot), nat.ptr(out), B, nat.ptr(cnt), 3, 2, L, S, H,
-                                                      0, 0, 0, nat.stream_of(out)), "grid_forward_fused")
+                                                      0, 0, 0, layout, nat.stream_of(out)), "grid_forward_fused")
     torch.cuda.synchronize()
     ref, _ = oracle.grid_encode_forward(_normalise(w[:n], bound), emb.astype(np.float16), offs, scale, H)
     got = out.cpu().numpy()
+    if layout == 0:  # [L, B, 2] in the same buffer
+        got = out.view(-1).view(L, B, 2).permute(1, 0, 2).reshape(B, L * 2).cpu().numpy()
     assert np.array_equal(got[:n].view(np.uint16), ref.view(np.uint16))  # outside rows: zeros in both
     assert np.all(got[n:] == 7.0)  # rows past the sample count untouched

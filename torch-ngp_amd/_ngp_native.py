@@ -64,17 +64,18 @@ SIGNATURES = {
     "ngp_adam_step": [c_vp, c_vp, c_i32, c_vp, c_vp, c_sz, c_f32, c_f32, c_f32, c_f32, c_f32,
                       c_i32, c_f32, c_vp],
     "ngp_grid_encode_forward_fused": [c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
-                                      c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp],
+                                      c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_i32, c_vp],
     "ngp_grid_encode_backward_fused_workspace_bytes": [c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32,
                                                        c_vp],
     "ngp_grid_encode_backward_fused": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
-                                       c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_vp],
+                                       c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_i32,
+                                       c_vp],
     "ngp_ffmlp_image_bytes": [c_u32, c_u32, c_u32],
     "ngp_ffmlp_pack": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_ffmlp_forward_rows": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
                                c_vp, c_vp],
     "ngp_nerf_sigma_forward": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp,
-                               c_f32, c_vp],
+                               c_f32, c_u32, c_vp],
     "ngp_ffmlp_backward_rows": [c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32,
                                 c_vp, c_vp, c_i32, c_u32, c_vp, c_sz, c_vp],
     "ngp_ffmlp_reduce": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],

@@ -248,6 +248,45 @@ NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_
     }
 }
 
+// First-layer input loaders (natural-K B operands).
+struct InRowMajor {  // [B, width] row-major
+    template <int KS>
+    NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
+                            half8 (&out)[kNB][KS]) const {
+        load_rows<KS>(src, width, row0, B, out);
+    }
+};
+// [width / 2][ld][2]: column pairs stored pair-major, the hash grid's
+// [L, B, C = 2] layout, so the grid kernels read and write whole lines per
+// level. Lane (g, c) gathers its 8 columns as 4 pairs; the 16 lanes of a
+// group read 64 contiguous bytes per pair.
+struct InPairMajor {
+    uint32_t ld;  // allocated rows
+    template <int KS>
+    NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
+                            half8 (&out)[kNB][KS]) const {
+        const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+            const uint32_t row = row0 + nb * 16 + c;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const uint32_t col = 32 * s + 8 * g;
+                half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (row < B && col < width) {
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        const ngp_half2 h = *reinterpret_cast<const ngp_half2*>(src + ((size_t)(col / 2 + p) * ld + row) * 2);
+                        v[2 * p] = h[0];
+                        v[2 * p + 1] = h[1];
+                    }
+                }
+                out[nb][s] = v;
+            }
+        }
+    }
+};
+
 // store accumulator tiles (optionally activated) as fp16 rows [row][16 mt + 4g .. +3]
 template <int MT, typename ACT>
 NGP_DEV void store_tiles(ngp_half* __restrict__ dst, uint32_t width, uint32_t row0, uint32_t B,
@@ -316,11 +355,11 @@ struct EpiNerfSigma {
     }
 };
 
-template <int W, int IN_KS, int NH, typename FA, typename FO, typename EPI>
+template <int W, int IN_KS, int NH, typename FA, typename FO, typename XL, typename EPI>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weights,
           const half8* __restrict__ image, ngp_half* __restrict__ fwd_buf, uint32_t B,
-          uint32_t in_dim, FA act, FO out_act, const int32_t* __restrict__ count, EPI epi) {
+          uint32_t in_dim, FA act, FO out_act, const int32_t* __restrict__ count, XL xl, EPI epi) {
     using N = Net<W, IN_KS, NH>;
     if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);  // rows past the sample count
     extern __shared__ half8 lds[];
@@ -336,7 +375,7 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
     for (uint32_t chunk = blockIdx.x * kWaves + wave; chunk < nchunks; chunk += gridDim.x * kWaves) {
         const uint32_t row0 = chunk * 16 * kNB;
         half8 x[kNB][IN_KS];
-        load_rows<IN_KS>(inputs, in_dim, row0, B, x);
+        xl.template operator()<IN_KS>(inputs, in_dim, row0, B, x);
 
         f32x4 acc[kNB][N::MTW];
         half8 h[kNB][N::KSW];
@@ -526,10 +565,35 @@ struct GiNerfGeo {
     }
 };
 
-template <int W, int IN_KS, int NH, typename FA, typename GI>
+// [in_dim / 2][ld][2] pair-major input gradient (see InPairMajor)
+struct GiPairMajor {
+    ngp_half* gi;
+    uint32_t ld;
+    template <int IN_MT>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[kNB][IN_MT]) const {
+        const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+            const uint32_t row = row0 + nb * 16 + c;
+            if (row >= B) continue;
+#pragma unroll
+            for (int mt = 0; mt < IN_MT; ++mt) {
+                const uint32_t col = 16 * mt + 4 * g;
+                if (col >= in_dim) continue;
+                const uint32_t p = col / 2;
+                *reinterpret_cast<ngp_half2*>(gi + ((size_t)p * ld + row) * 2) =
+                    ngp_half2{(ngp_half)t[nb][mt][0], (ngp_half)t[nb][mt][1]};
+                *reinterpret_cast<ngp_half2*>(gi + ((size_t)(p + 1) * ld + row) * 2) =
+                    ngp_half2{(ngp_half)t[nb][mt][2], (ngp_half)t[nb][mt][3]};
+            }
+        }
+    }
+};
+
+template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
-          const half8* __restrict__ image, GI gi_out, bool want_gi,
+          const half8* __restrict__ image, XL xl, GI gi_out, bool want_gi,
           float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, FA act,
           const int32_t* __restrict__ count) {
     using N = Net<W, IN_KS, NH>;
@@ -559,7 +623,7 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     const uint32_t stride = gridDim.x * kWaves;
     uint32_t chunk = blockIdx.x * kWaves + wave;
     half8 xn[kNB][IN_KS], dn[kNB][1];
-    load_rows<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
+    xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
     load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn);  // output activation ignored (ffmlp.cu:783)
     for (; chunk < nchunks; chunk += stride) {
         const uint32_t row0 = chunk * 16 * kNB;
@@ -570,7 +634,7 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
             for (int s = 0; s < IN_KS; ++s) x[nb][s] = xn[nb][s];
             dout[nb][0] = dn[nb][0];
         }
-        load_rows<IN_KS>(inputs, in_dim, row0 + stride * 16 * kNB, B, xn);
+        xl.template operator()<IN_KS>(inputs, in_dim, row0 + stride * 16 * kNB, B, xn);
         load_rows<1>(grad, kOut, row0 + stride * 16 * kNB, B, dn);
         // recompute the post-activations of every hidden layer
         half8 h[NH + 1][kNB][N::KSW];
@@ -721,18 +785,18 @@ int check_shape(uint32_t B, uint32_t in_dim, uint32_t out_dim, uint32_t hidden, 
 }
 
 // Forward launch: w (built per workgroup) or a prepacked image; epilogue EPI.
-template <int W, int IN_KS, int NH, typename FA, typename FO, typename EPI>
+template <int W, int IN_KS, int NH, typename FA, typename FO, typename EPI, typename XL = InRowMajor>
 int launch_fwd_t(const void* in, const void* w, const void* image, uint32_t B, uint32_t in_dim, FA act,
-                 FO out_act, void* fwd_buf, const int32_t* count, EPI epi, hipStream_t st) {
+                 FO out_act, void* fwd_buf, const int32_t* count, EPI epi, hipStream_t st, XL xl = XL{}) {
     using N = Net<W, IN_KS, NH>;
     const size_t lds = (size_t)N::FWD_FRAGS * 64 * 16;
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
     uint32_t blocks = ngp_div_up(nchunks, kWaves);
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) return NGP_OK;
-    hipLaunchKernelGGL((k_mlp_fwd<W, IN_KS, NH, FA, FO, EPI>), dim3(blocks), dim3(kThreads), lds, st,
+    hipLaunchKernelGGL((k_mlp_fwd<W, IN_KS, NH, FA, FO, XL, EPI>), dim3(blocks), dim3(kThreads), lds, st,
                        (const ngp_half*)in, (const ngp_half*)w, (const half8*)image, (ngp_half*)fwd_buf,
-                       B, in_dim, act, out_act, count, epi);
+                       B, in_dim, act, out_act, count, xl, epi);
     return ngp_check_launch("ffmlp_forward");
 }
 
@@ -748,7 +812,10 @@ int launch_fwd(const void* in, const void* w, const void* image, uint32_t B, uin
 
 template <int W, int IN_KS, int NH>
 int launch_fwd_nerf(const void* in, const void* w, const void* image, uint32_t B, uint32_t in_dim,
-                    const int32_t* count, const EpiNerfSigma& epi, hipStream_t st) {
+                    const int32_t* count, const EpiNerfSigma& epi, bool pair_major, hipStream_t st) {
+    if (pair_major)
+        return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActReLU{}, ActNone{}, nullptr, count, epi, st,
+                                          InPairMajor{B});
     return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActReLU{}, ActNone{}, nullptr, count, epi, st);
 }
 
@@ -775,10 +842,10 @@ int add_pack_jobs(PackJobs& jobs, const void* w, uint32_t in_dim, void* image) {
     return NGP_OK;
 }
 
-template <int W, int IN_KS, int NH, typename FA, typename GI>
+template <int W, int IN_KS, int NH, typename FA, typename GI, typename XL = InRowMajor>
 int launch_bwd_t(const void* grad, const void* in, const void* w, const void* image, uint32_t B,
                  uint32_t in_dim, FA act, GI gi, bool want_gi, void* gw, int32_t gw_dtype, bool defer,
-                 void* ws, const int32_t* count, hipStream_t st) {
+                 void* ws, const int32_t* count, hipStream_t st, XL xl = XL{}) {
     using L = BwdLds<W, IN_KS, NH>;
     static_assert(L::frag_bytes <= kImageBytes, "fragment image exceeds its workspace slot");
     static_assert(L::total <= 160 * 1024, "backward LDS budget exceeded");
@@ -792,9 +859,9 @@ int launch_bwd_t(const void* grad, const void* in, const void* w, const void* im
         hipLaunchKernelGGL(k_mlp_pack_jobs, dim3(jobs.n), dim3(256), 0, st, jobs);
         image = ws;
     }
-    hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH, FA, GI>), dim3(blocks), dim3(kThreads), L::total, st,
-                       (const ngp_half*)grad, (const ngp_half*)in, (const half8*)image, gi, want_gi, slab, np,
-                       B, in_dim, act, count);
+    hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH, FA, XL, GI>), dim3(blocks), dim3(kThreads), L::total, st,
+                       (const ngp_half*)grad, (const ngp_half*)in, (const half8*)image, xl, gi, want_gi, slab,
+                       np, B, in_dim, act, count);
     if (!defer) {
         ReduceJobs rj{};
         rj.n = 1;
@@ -815,9 +882,15 @@ int launch_bwd_t(const void* grad, const void* in, const void* w, const void* im
 template <int W, int IN_KS, int NH>
 int launch_bwd(const void* grad, const void* in, const void* w, const void* image, uint32_t B,
                uint32_t in_dim, uint32_t act, void* grad_in, bool nerf_geo, void* gw, int32_t gw_dtype,
-               bool defer, void* ws, const int32_t* count, hipStream_t st) {
+               bool defer, void* ws, const int32_t* count, hipStream_t st, bool pair_major = false) {
     const bool want = grad_in != nullptr;
     ngp_half* gi = static_cast<ngp_half*>(grad_in);
+    if (pair_major) {
+        NGP_REQUIRE(!nerf_geo && act == kReLU, NGP_ERR_UNSUPPORTED,
+                    "ffmlp_backward: pair-major inputs need ReLU and a plain grad_inputs store");
+        return launch_bwd_t<W, IN_KS, NH>(grad, in, w, image, B, in_dim, ActReLU{}, GiPairMajor{gi, B}, want, gw,
+                                          gw_dtype, defer, ws, count, st, InPairMajor{B});
+    }
     if (nerf_geo) {
         NGP_REQUIRE(act == kReLU && IN_KS == 1 && in_dim == 32, NGP_ERR_UNSUPPORTED,
                     "ffmlp_backward: NeRF geo-feature gradients need ReLU and a 32-wide input");
@@ -887,14 +960,15 @@ extern "C" int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, c
 extern "C" int ngp_nerf_sigma_forward(const void* inputs, const void* weights, const void* image, uint32_t B,
                                       const int32_t* count, uint32_t in_dim, uint32_t hidden_dim,
                                       uint32_t num_layers, void* h_out, float* sigma, void* color_in,
-                                      const float* dirs, float density_scale, void* stream) {
+                                      const float* dirs, float density_scale, uint32_t flags, void* stream) {
     if (int e = check_shape(B, in_dim, kOut, hidden_dim, num_layers)) return e;
     NGP_REQUIRE(h_out && sigma && color_in && dirs, NGP_ERR_ARG, "nerf_sigma_forward: null output");
     if (B == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
     const EpiNerfSigma epi{static_cast<ngp_half*>(h_out), sigma, static_cast<ngp_half*>(color_in), dirs,
                            density_scale};
-    NGP_MLP_DISPATCH(launch_fwd_nerf, inputs, weights, image, B, in_dim, count, epi, st);
+    NGP_MLP_DISPATCH(launch_fwd_nerf, inputs, weights, image, B, in_dim, count, epi,
+                     (flags & NGP_FFMLP_PAIR_MAJOR) != 0, st);
 }
 
 extern "C" int ngp_ffmlp_inference(const void* inputs, const void* weights, uint32_t B,
@@ -978,8 +1052,9 @@ extern "C" int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, con
                 "ffmlp_backward: workspace of %zu bytes required, got %zu", need, workspace_bytes);
     hipStream_t st = ngp_stream(stream);
     const bool geo = (flags & NGP_FFMLP_NERF_GEO) != 0, defer = (flags & NGP_FFMLP_DEFER_REDUCE) != 0;
+    const bool pm = (flags & NGP_FFMLP_PAIR_MAJOR) != 0;
     NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, image, B, in_dim, activation, grad_inputs, geo,
-                     grad_weights, gw_dtype, defer, workspace, count, st);
+                     grad_weights, gw_dtype, defer, workspace, count, st, pm);
 }
 
 /* Sums the deferred dW partials of n backward calls (same B / shapes as

@@ -565,7 +565,8 @@ __global__ void __launch_bounds__(kBinPts)
 k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
                const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
-               InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items) {
+               InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
+               int32_t grad_layout) {
     constexpr uint32_t C = 2, NC = 1u << D, NW = kBinPts / 64;
     static_assert(kMaxBinsPerLevel <= kBinPts, "one bin per thread in the reservation step");
     __shared__ uint32_t cnt[kMaxBinsPerLevel], soff[kMaxBinsPerLevel + 1], wsum[NW];
@@ -603,7 +604,8 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     }
     float g0 = 0.0f, g1 = 0.0f;
     if (valid) {
-        const ngp_half2 gv = *reinterpret_cast<const ngp_half2*>(grad + ((size_t)b * L + level) * C);
+        const size_t gi = grad_layout == 0 ? (size_t)level * B + b : (size_t)b * L + level;
+        const ngp_half2 gv = *reinterpret_cast<const ngp_half2*>(grad + gi * C);
         g0 = (float)gv[0];
         g1 = (float)gv[1];
     }
@@ -1294,7 +1296,8 @@ extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, cons
                                              uint32_t B,
                                              const int32_t* count, uint32_t D, uint32_t C, uint32_t L,
                                              float S, uint32_t H, uint32_t gridtype,
-                                             int32_t align_corners, uint32_t interp, void* stream) {
+                                             int32_t align_corners, uint32_t interp, int32_t out_layout,
+                                             void* stream) {
     if (int e = check_common(L, embeddings, offsets, outputs)) return e;
     NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_forward_fused: null xyz or bound <= 0");
     if (B == 0) return NGP_OK;
@@ -1305,9 +1308,9 @@ extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, cons
                 "grid_encode_forward_fused: emb_dtype %d (F32 or F16)", emb_dtype);
     if (emb_dtype == NGP_DTYPE_F16)
         return fwd_t<ngp_half, ngp_half>(xyz, embeddings, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
-                                         align_corners != 0, interp, 1, ngp_stream(stream), im);
+                                         align_corners != 0, interp, out_layout, ngp_stream(stream), im);
     return fwd_t<ngp_half, float>(xyz, embeddings, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
-                                  align_corners != 0, interp, 1, ngp_stream(stream), im);
+                                  align_corners != 0, interp, out_layout, ngp_stream(stream), im);
 }
 
 extern "C" size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, uint32_t C,
@@ -1327,9 +1330,11 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
                                               uint32_t C, uint32_t L, float S, uint32_t H,
                                               uint32_t gridtype, int32_t align_corners,
                                               uint32_t interp, const int32_t* offsets_host,
-                                              void* workspace, size_t workspace_bytes,
+                                              void* workspace, size_t workspace_bytes, int32_t grad_layout,
                                               void* stream) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
+    NGP_REQUIRE(grad_layout == 0 || grad_layout == 1, NGP_ERR_ARG,
+                "grid_encode_backward_fused: grad_layout 0 ([L,B,C]) or 1 ([B,L*C])");
     NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_backward_fused: null xyz or bound <= 0");
     if (B == 0) return NGP_OK;
     GridLevels lv;
@@ -1352,7 +1357,7 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
         const dim3 grid(ngp_div_up(B, kBinPts), bp.nlev);
         k_grid_bwd_bin<3><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
             (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, im,
-            bp, cursor, items);
+            bp, cursor, items, grad_layout);
         k_grid_bin_accum<<<2 * ngp_num_cus(), kAccThreads, (2 * bp.total_bins + 1) * sizeof(uint32_t), st>>>(
             offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items);
     }
@@ -1360,10 +1365,10 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
         if (D == 3 && C == 2) {
             const dim3 grid(ngp_div_up(B, 128), L - bp.nlev);
             k_grid_bwd<ngp_half, 3, 2><<<grid, 256, 0, st>>>((const ngp_half*)grad, xyz, offsets,
-                (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, 1, im, bp.nlev);
+                (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, grad_layout, im, bp.nlev);
         } else {
             return bwd_t<ngp_half>(grad, xyz, offsets, grad_embeddings, B, D, C, L, lv, nullptr, nullptr,
-                                   gridtype, ac, interp, 1, st, im);
+                                   gridtype, ac, interp, grad_layout, st, im);
         }
     }
     return ngp_check_launch("grid_encode_backward_fused");

@@ -39,7 +39,7 @@ from .provider import LEGO_BOXES, LEGO_COLORS
 
 _F16 = nat.DTYPE_CODE[torch.float16]
 _RELU, _NONE = 0, 6
-_DEFER, _GEO = 1, 2  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO
+_DEFER, _GEO, _PAIR = 1, 2, 4  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO, NGP_FFMLP_PAIR_MAJOR
 
 
 def _vp_array(ptrs):
@@ -87,6 +87,9 @@ class FusedTrainer:
         self.march_ws = z(ws, dtype=torch.uint8)
         self.refresh_occupancy()
         h = torch.float16
+        # enc_out / g_enc are [L=16][M][2] (the grid's level-major layout; the
+        # sigma network reads / writes them pair-major): every grid kernel then
+        # moves whole lines per level
         self.enc_out, self.h_sigma = z(M, 32, dtype=h), z(M, 16, dtype=h)
         self.sigma, self.color_in, self.color_out = z(M), z(M, 32, dtype=h), z(M, 16, dtype=h)
         self.g_color_out, self.g_h = z(M, 16, dtype=h), z(M, 16, dtype=h)
@@ -250,12 +253,12 @@ class FusedTrainer:
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
         chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(self.w_half[0]), _F16, P(e.offsets),
-                                              P(self.enc_out), M, cnt, *grid_args), "grid_encode_fused")
+                                              P(self.enc_out), M, cnt, *grid_args[:-1], 0, s), "grid_encode_fused")
         self._tick("grid_encode_forward")
         sn, cn, img, pk = self.sig_net, self.col_net, self.mlp_img, self._pk
         chk(lib.ngp_nerf_sigma_forward(P(self.enc_out), P(self.w_half[1]), P(img[0]), M, cnt, 32, sn.hidden_dim,
                                        sn.num_layers, P(self.h_sigma), P(self.sigma), P(self.color_in),
-                                       P(self.dirs), float(m.density_scale), s), "sigma_mlp")
+                                       P(self.dirs), float(m.density_scale), _PAIR, s), "sigma_mlp")
         self._tick("ffmlp_forward_sigma")
         chk(lib.ngp_ffmlp_forward_rows(P(self.color_in), P(self.w_half[2]), P(img[1]), M, cnt, 32, 16,
                                        cn.hidden_dim, cn.num_layers, _RELU, _NONE, P(self.color_out), s),
@@ -274,7 +277,7 @@ class FusedTrainer:
         self._tick("ffmlp_backward_color")
         chk(lib.ngp_ffmlp_backward_rows(P(self.g_h), P(self.enc_out), P(self.w_half[1]), P(img[0]), M, cnt, 32,
                                         16, sn.hidden_dim, sn.num_layers, _RELU, P(self.g_enc), None, _F16,
-                                        _DEFER, P(self.mlp_ws[0]), self.mlp_ws[0].numel(), s),
+                                        _DEFER | _PAIR, P(self.mlp_ws[0]), self.mlp_ws[0].numel(), s),
             "sigma_mlp_backward")
         self._tick("ffmlp_backward_sigma")
         chk(lib.ngp_ffmlp_reduce(2, pk["ws"], pk["B"], pk["ins"], pk["hid"], pk["nl"], pk["gw"], _F16, s),
@@ -282,7 +285,7 @@ class FusedTrainer:
         self._tick("ffmlp_reduce")
         chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
                                                P(self.grads[0]), M, cnt, *grid_args[:-1], self._offsets_host,
-                                               P(self.grid_ws), self.grid_ws.numel(), s),
+                                               P(self.grid_ws), self.grid_ws.numel(), 0, s),
             "grid_backward_fused")
         self._tick("grid_encode_backward")
 
