@@ -59,7 +59,10 @@ def main(tag, out=None):
         for r in csv.DictReader(open(p)):
             acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024)
         for k, v in acc.items():
-            pmc.setdefault(k, {})[which + "_bytes"] = round(sum(v) / len(v))
+            # median: the bench's density-grid update also launches the grid
+            # forward (2M points), a few outliers among the step's launches
+            v = sorted(v)
+            pmc.setdefault(k, {})[which + "_bytes"] = round(v[len(v) // 2])
     res = {
         "steps": len(sel),
         "step_span_us_mean": round(sum(spans) / len(spans), 1),
