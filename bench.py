@@ -285,6 +285,7 @@ def run_fused(args, model, data, bits, world, dev):
         t = torch.tensor([mean_count], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         mean_count = int(t.item())
+    probe.flush()  # data parallel: every rank's shard of the masters gathered back
     del probe
     torch.cuda.empty_cache()
     ft = FusedTrainer(model, data, M=mean_count, distributed=world > 1)

@@ -314,6 +314,16 @@ int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* cons
                              int32_t scaler_enabled, uint32_t num_rays, const int32_t* counter,
                              int32_t* step_counter, const float* loss_ray, void* state,
                              void* stream);
+/* Data-parallel GradScaler guard for the sharded optimizer (nerf/fused.py,
+ * world > 1), run on each rank's own fp16 gradient before the averaging
+ * reduce-scatter: if any of its n elements is inf/nan, a NaN is written to
+ * grad[r * chunk] for r in [0, world), so every rank's shard of the reduced
+ * gradient carries it and every rank's ngp_fused_optimizer_step skips.
+ * n % 8 == 0, grad 16-byte aligned, world * chunk <= n. No reference
+ * counterpart (the reference trains on one GPU; GradScaler.unscale_ checks
+ * the whole gradient, torch/amp/grad_scaler.py). */
+int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, void* state,
+                   void* stream);
 
 #ifdef __cplusplus
 }

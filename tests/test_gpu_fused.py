@@ -270,3 +270,28 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
     gx_rows = gxp.view(16, B, 2).permute(1, 0, 2).reshape(B, 32)
     assert torch.equal(gx_rows[:n].view(torch.int16), gx_ref[:n].view(torch.int16))
     assert torch.equal(gw2.view(torch.int16), gw_ref[0].view(torch.int16))
+
+
+def test_grad_guard_poisons_every_shard(cuda):
+    """ngp_grad_guard (data-parallel GradScaler guard): an inf/nan anywhere in
+    the rank's gradient puts a NaN at the head of every rank's chunk; a finite
+    gradient is left untouched and the flag is cleared either way."""
+    import _ngp_native as nat
+    _, _, _, ft = _setup(cuda)
+    world, chunk = 4, 1024
+    g = torch.randn(world * chunk + 64, device=cuda).half()
+    ref = g.clone()
+    nat.check(nat.lib().ngp_grad_guard(nat.ptr(g), g.numel(), chunk, world, nat.ptr(ft.state),
+                                       nat.stream_of(g)), "grad_guard")
+    torch.cuda.synchronize()
+    assert torch.equal(g, ref)
+    g[3000] = float("inf")
+    nat.check(nat.lib().ngp_grad_guard(nat.ptr(g), g.numel(), chunk, world, nat.ptr(ft.state),
+                                       nat.stream_of(g)), "grad_guard")
+    torch.cuda.synchronize()
+    heads = g[torch.arange(world, device=cuda) * chunk].float()
+    assert torch.isnan(heads).all()
+    g[torch.arange(world, device=cuda) * chunk] = ref[torch.arange(world, device=cuda) * chunk]
+    g[3000] = ref[3000]
+    assert torch.equal(g, ref)
+    assert int(ft.state.view(torch.int32)[11].item()) == 0  # local_inf cleared

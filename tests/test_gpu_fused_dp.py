@@ -2,8 +2,9 @@
 
 Both ranks run on the one visible GPU (gloo backend, which stages device
 tensors through the host; RCCL needs one GPU per rank). Each rank draws its
-own rays, the flat fp16 gradient is all-reduced, and the optimizer averages
-(grad_mult = 1/world): after a few steps, captured included, both ranks must
+own rays; the flat fp16 gradient is averaged by a reduce-scatter, each rank's
+optimizer updates its shard and the fp16 forward copy is all-gathered
+(ZeRO-1): after a few steps, captured included, and flush(), both ranks must
 hold bit-identical parameters, and they must differ from a single-rank run.
 """
 import os
@@ -51,7 +52,23 @@ def _worker(rank, world, port, q):
         ft.step()
     ft.flush()
     torch.cuda.synchronize()
-    q.put((rank, [p.detach().cpu().numpy() for p in ft.params], ft.optimizer_steps))
+    params = [p.detach().cpu().numpy() for p in ft.params]
+    steps = ft.optimizer_steps
+    # GradScaler under the sharded optimizer: an inf on ONE rank must make
+    # every rank skip the step and back the scale off (ngp_grad_guard)
+    scale0 = ft.scale
+    ft._sample()
+    ft._march()
+    ft._network()
+    if rank == 0:
+        ft.grads[1][3] = float("inf")
+    ft._reduce()
+    ft._optimizer()
+    ft._gather_half(wait=True)
+    torch.cuda.synchronize()
+    skipped = (ft.optimizer_steps == steps, ft.scale == scale0 * 0.5,
+               all(np.array_equal(a, p.detach().cpu().numpy()) for a, p in zip(params, ft.params)))
+    q.put((rank, params, steps, skipped))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -73,9 +90,10 @@ def _run(world):
 
 def test_fused_data_parallel_two_ranks_stay_in_sync():
     two = _run(2)
-    (_, p0, s0), (_, p1, s1) = two
+    (_, p0, s0, k0), (_, p1, s1, k1) = two
     assert s0 == s1 >= 6
     for a, b in zip(p0, p1):
         assert np.array_equal(a, b)
-    (_, ps, _), = _run(1)
+    assert all(k0) and all(k1), (k0, k1)  # both ranks skipped the step with rank 0's inf
+    (_, ps, _, _), = _run(1)
     assert any(not np.array_equal(a, b) for a, b in zip(p0, ps))  # the other rank's rays mattered

@@ -50,7 +50,7 @@ struct StepState {
     int32_t iter;          // finished steps (k_step_end)
     int32_t draw;          // batches drawn by the sampler (k_lego_rays)
     int32_t lego_done;     // k_lego_rays' finished-block count (last block bumps draw)
-    int32_t pad2;
+    int32_t local_inf;     // data parallel: this rank's own grads held an inf/nan (k_guard_*)
 };
 
 // counter-based RNG (no state, graph-safe): 32-bit mix of (seed, a, b, c)
@@ -553,6 +553,36 @@ k_adam_multi(TensorList tl, const StepState* __restrict__ st, AdamArgs aa) {
     }
 }
 
+// ---- data-parallel GradScaler guard ----------------------------------------------
+// With the sharded optimizer (nerf/fused.py, world > 1) each rank sees only
+// its shard of the reduced gradient, but GradScaler must skip (and back off)
+// on every rank together. Each rank checks its own pre-reduction fp16
+// gradient; a rank that found an inf/nan writes a NaN into the first element
+// of every rank's chunk. The reduction is an average (each input pre-scaled by
+// 1/world), so finite inputs cannot overflow into an inf, and after the
+// reduce-scatter every owner finds a non-finite value in its shard exactly
+// when some rank had one: all ranks skip together.
+__global__ void __launch_bounds__(256)
+k_guard_scan(const ngp_half* __restrict__ g, uint64_t n8, StepState* __restrict__ st) {
+    typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * blockDim.x) {
+        const half8 v = reinterpret_cast<const half8*>(g)[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bad |= !__builtin_isfinite((float)v[j]);
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&st->local_inf, 1);
+}
+
+__global__ void __launch_bounds__(64)
+k_guard_poison(ngp_half* __restrict__ g, uint64_t chunk, int32_t world, StepState* __restrict__ st) {
+    const bool bad = st->local_inf != 0;
+    __syncthreads();
+    if (bad)
+        for (int r = threadIdx.x; r < world; r += 64) g[(uint64_t)r * chunk] = (ngp_half)__builtin_nanf("");
+    if (threadIdx.x == 0) st->local_inf = 0;
+}
+
 struct ScalerArgs {
     float growth_factor, backoff_factor;
     int32_t growth_interval, enabled;
@@ -738,4 +768,18 @@ extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params,
                   num_rays ? 1.0f / (float)num_rays : 0.0f};
     k_step_end<<<1, 256, 0, s>>>(st, sa, counter, step_counter, loss_ray, num_rays);
     return ngp_check_launch("fused_optimizer_step");
+}
+
+extern "C" int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, void* state,
+                              void* stream) {
+    NGP_REQUIRE(grad_half && state, NGP_ERR_ARG, "grad_guard: null buffer");
+    NGP_REQUIRE(n % 8 == 0 && (reinterpret_cast<uintptr_t>(grad_half) & 15) == 0, NGP_ERR_ARG,
+                "grad_guard: gradient must be 16-byte aligned with a multiple of 8 elements");
+    NGP_REQUIRE(world >= 1 && (uint64_t)world * chunk <= n, NGP_ERR_ARG,
+                "grad_guard: world * chunk exceeds the gradient");
+    hipStream_t s = ngp_stream(stream);
+    StepState* st = static_cast<StepState*>(state);
+    if (n) k_guard_scan<<<sweep_blocks(n, 8), 256, 0, s>>>(static_cast<const ngp_half*>(grad_half), n / 8, st);
+    k_guard_poison<<<1, 64, 0, s>>>(static_cast<ngp_half*>(grad_half), chunk, world, st);
+    return ngp_check_launch("grad_guard");
 }

@@ -18,9 +18,11 @@ nothing beyond its memory. Every launch goes to the current stream, so the
 whole step captures into one hipGraph (`capture`).
 
 Step order: `step()` runs [optimizer of the PREVIOUS step's gradients ->
-sample -> march -> network], so one graph holds a whole step even when a
-data-parallel all-reduce has to sit between the backward and the optimizer
-(it runs after the graph). The arithmetic is the reference's, in the
+sample -> march -> network], so one graph holds a whole step. Data parallel
+(world > 1, ZeRO-1): [optimizer of this rank's shard] -> all-gather of the
+fp16 forward copy, overlapped with [sample -> march] -> [network] -> guard +
+averaging reduce-scatter of the gradient; the collectives sit between three
+graphs. The arithmetic is the reference's, in the
 reference's order; only the last step's update stays pending until
 `flush()` (the read-outs below flush first). Running that optimizer on a side
 stream beside sample + march was measured and lost: Adam and the marcher's
@@ -51,8 +53,10 @@ class FusedTrainer:
                  dt_gamma=0.0, seed=0, betas=(0.9, 0.99), eps=1e-15, init_scale=65536.0,
                  growth_interval=2000, distributed=False):
         """distributed: ray-sharded data parallelism over the initialised
-        torch.distributed group (each rank draws its own rays; the flat fp16
-        gradient is summed with one RCCL all-reduce, the optimizer averages)."""
+        torch.distributed group: each rank draws its own rays; the flat fp16
+        gradient is averaged with one RCCL reduce-scatter, each rank's Adam
+        updates its 1/world shard and the fp16 forward copy is all-gathered
+        (ZeRO-1; see `_reduce`)."""
         assert model.cuda_ray, "the fused step marches the density bitfield (cuda_ray=True)"
         enc = model.encoder
         assert enc.level_dim == 2 and enc.num_levels * enc.level_dim == 32 and enc.input_dim == 3
@@ -94,19 +98,37 @@ class FusedTrainer:
         self.sigma, self.color_in, self.color_out = z(M), z(M, 32, dtype=h), z(M, 16, dtype=h)
         self.g_color_out, self.g_h = z(M, 16, dtype=h), z(M, 16, dtype=h)
         self.g_enc = z(M, 32, dtype=h)
-        # parameters: fp32 masters, fp16 grads, fp16 forward copies of the MLPs
+        # parameters: fp32 masters, fp16 grads and fp16 forward copies, each one
+        # flat buffer with the same 8-aligned layout (tensor k at starts[k]):
+        # the optimizer is one elementwise sweep over [lo, hi) of it, and a
+        # data-parallel step moves the gradient and the forward copy with one
+        # collective each
         self.params = [enc.embeddings, self.sig_net.weights, self.col_net.weights]
-        # one flat fp16 gradient (one all-reduce in data-parallel mode), 8-aligned views
         sizes = [p.numel() for p in self.params]
         starts = np.cumsum([0] + [(n + 7) // 8 * 8 for n in sizes])
-        self.flat_grad = z(int(starts[-1]), dtype=h)
+        W = self.world
+        # shard: 64-element aligned chunk per rank (world * chunk >= the layout)
+        self.chunk = chunk = int(-(-int(starts[-1]) // (64 * W)) * 64)
+        self.total = total = chunk * W
+        self.rank = dist.get_rank() if W > 1 else 0
+        self.lo, self.hi = self.rank * chunk, (self.rank + 1) * chunk
+        self.flat_param = z(total)
+        self.flat_grad = z(total, dtype=h)
+        self.flat_half = z(total, dtype=h)
+        with torch.no_grad():
+            for a, p in zip(starts[:-1], self.params):  # re-home the model's parameters
+                view = self.flat_param[int(a):int(a) + p.numel()].view(p.shape)
+                view.copy_(p.detach())
+                p.data = view
+                self.flat_half[int(a):int(a) + p.numel()].copy_(view.reshape(-1))
         self.grads = [self.flat_grad[int(a):int(a) + n].view(p.shape)
                       for a, n, p in zip(starts[:-1], sizes, self.params)]
-        self.exp_avg = [torch.zeros_like(p) for p in self.params]
-        self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
-        # fp16 copies the forward kernels read (the reference's autocast casts), refreshed by the
-        # optimizer after every update; the grid's copy also halves the forward gather bytes
-        self.w_half = [p.detach().half() for p in self.params]
+        self.w_half = [self.flat_half[int(a):int(a) + n].view(p.shape)
+                       for a, n, p in zip(starts[:-1], sizes, self.params)]
+        # Adam moments of this rank's shard only (ZeRO-1); world 1: everything
+        self.exp_avg, self.exp_avg_sq = z(chunk), z(chunk)
+        # the averaged gradient shard (reduce-scatter output); world 1: the flat grad itself
+        self.grad_shard = self.flat_grad if W == 1 else z(chunk, dtype=h)
         self._offsets_host = (ctypes.c_int32 * enc.offsets.numel())(*enc.offsets.cpu().tolist())
         gb = nat.lib().ngp_grid_encode_backward_fused_workspace_bytes(
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
@@ -140,12 +162,13 @@ class FusedTrainer:
         self._intr = (ctypes.c_float * 4)(*[float(v) for v in dataset.intrinsics])
         self._aabb = (ctypes.c_float * 6)(*model.aabb_train.detach().cpu().tolist())
         self._opt = dict(
-            params=_vp_array([nat.ptr(p) for p in self.params]),
-            grads=_vp_array([nat.ptr(g) for g in self.grads]),
-            m=_vp_array([nat.ptr(t) for t in self.exp_avg]),
-            v=_vp_array([nat.ptr(t) for t in self.exp_avg_sq]),
-            half=_vp_array([nat.ptr(t) for t in self.w_half]),
-            sizes=(ctypes.c_uint64 * 3)(*[p.numel() for p in self.params]))
+            params=_vp_array([nat.ptr(self.flat_param) + 4 * self.lo]),
+            grads=_vp_array([nat.ptr(self.grad_shard)]),
+            m=_vp_array([nat.ptr(self.exp_avg)]),
+            v=_vp_array([nat.ptr(self.exp_avg_sq)]),
+            half=_vp_array([nat.ptr(self.flat_half) + 2 * self.lo]),
+            sizes=(ctypes.c_uint64 * 1)(chunk))
+        self._nccl = W > 1 and dist.get_backend() == "nccl"
         self.graph = None
         self._events = None
         self._pending = False  # gradients of the last forward/backward not yet applied
@@ -181,7 +204,7 @@ class FusedTrainer:
         optimizer has streamed the parameters through), unlike back-to-back
         repeats of one kernel. A spin kernel ahead of each step lets the host
         queue every launch first, so no phase includes host launch gaps. The
-        phases run serially here (no optimizer / march overlap)."""
+        phases run serially here (the all-gather is waited for right away)."""
         self.flush()
         acc = {}
         for _ in range(k):
@@ -192,8 +215,9 @@ class FusedTrainer:
             self._sample()
             self._march()
             self._network()
-            self._allreduce()
+            self._reduce()
             self._optimizer()
+            self._gather_half(wait=True)
             self.model.local_step += 1
             torch.cuda.synchronize()
             ev, self._events = self._events, None
@@ -202,18 +226,64 @@ class FusedTrainer:
         return {n: v / k for n, v in acc.items()}
 
     def _body(self, pending):
-        """One step's launches: [optimizer(previous grads)] -> sample -> march
-        -> network forward/backward."""
+        """One step's launches (world 1): [optimizer(previous grads)] ->
+        sample -> march -> network forward/backward."""
         if pending:
             self._optimizer()
         self._sample()
         self._march()
         self._network()
 
-    def _allreduce(self):
-        if self.world > 1:
-            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
-            self._tick("allreduce")
+    # ---- data parallel (world > 1): ZeRO-1 --------------------------------
+    # The flat fp16 gradient is guarded (ngp_grad_guard) and averaged with one
+    # reduce-scatter; each rank's optimizer updates its shard of the fp32
+    # masters, the moments and the fp16 forward copy; the forward copy is
+    # all-gathered on the collective stream while the next batch is sampled
+    # and marched (neither reads a parameter). Per step each rank moves the
+    # gradient once and the forward copy once (what one all-reduce moves) and
+    # sweeps 1/world of the Adam state.
+    def _reduce(self):
+        if self.world == 1:
+            return
+        nat.check(nat.lib().ngp_grad_guard(nat.ptr(self.flat_grad), self.total, self.chunk, self.world,
+                                           nat.ptr(self.state), nat.stream_of(self.flat_grad)), "grad_guard")
+        if self._nccl:
+            dist.reduce_scatter_tensor(self.grad_shard, self.flat_grad, op=dist.ReduceOp.AVG)
+        else:  # gloo (tests): host-staged
+            out = torch.empty(self.chunk, dtype=self.flat_grad.dtype)
+            dist.reduce_scatter_tensor(out, self.flat_grad.cpu(), op=dist.ReduceOp.AVG)
+            self.grad_shard.copy_(out)
+        self.flat_grad.zero_()  # the next backward accumulates into it
+        self._tick("reduce_scatter")
+
+    def _gather_half(self, wait):
+        """All-gather of the fp16 forward copy; returns the pending work."""
+        if self.world == 1:
+            return None
+        shard = self.flat_half[self.lo:self.hi]
+        work = None
+        if self._nccl:
+            work = dist.all_gather_into_tensor(self.flat_half, shard, async_op=True)
+        else:
+            full = torch.empty(self.total, dtype=self.flat_half.dtype)
+            dist.all_gather_into_tensor(full, shard.cpu())
+            self.flat_half.copy_(full)
+        if wait and work is not None:
+            work.wait()
+            work = None
+        self._tick("all_gather")
+        return work
+
+    def _gather_masters(self):
+        if self.world == 1:
+            return
+        shard = self.flat_param[self.lo:self.hi]
+        if self._nccl:
+            dist.all_gather_into_tensor(self.flat_param, shard)
+        else:
+            full = torch.empty(self.total, dtype=self.flat_param.dtype)
+            dist.all_gather_into_tensor(full, shard.cpu())
+            self.flat_param.copy_(full)
 
     def _sample(self):
         """Batch of N rays: rays, RGBA target, background, march noise, near/far."""
@@ -293,9 +363,11 @@ class FusedTrainer:
         """GradScaler inf check + Adam (unscaled fp16 grads, LambdaLR) + scaler update."""
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         o, chk, N, cnt, m = self._opt, nat.check, self.N, P(self.counter), self.model
-        chk(lib.ngp_fused_optimizer_step(3, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"],
-                                         self.lr, self.betas[0], self.betas[1], self.eps, self.iters, 1,
-                                         1.0 / self.world, 2.0, 0.5, self.growth_interval, 1, N, cnt,
+        # world 1 zeroes the grads here; data parallel: the shard is the reduce-scatter's
+        # output and the flat gradient is cleared after the collective read it
+        chk(lib.ngp_fused_optimizer_step(1, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"],
+                                         self.lr, self.betas[0], self.betas[1], self.eps, self.iters,
+                                         int(self.world == 1), 1.0, 2.0, 0.5, self.growth_interval, 1, N, cnt,
                                          None, P(self.loss_ray),
                                          P(self.state), s), "fused_optimizer_step")
         self._tick("optimizer")
@@ -303,31 +375,67 @@ class FusedTrainer:
     def step(self):
         """One training iteration (the optimizer half lags by one step, see
         the module docstring)."""
-        if self.graph is not None and self._pending:
-            self.graph.replay()
+        if self.world == 1:
+            if self.graph is not None and self._pending:
+                self.graph.replay()
+            else:
+                self._body(self._pending)
         else:
-            self._body(self._pending)
-        self._allreduce()
+            g = self.graph if self._pending else None
+            work = None
+            if self._pending:
+                if g:
+                    g["opt"].replay()
+                else:
+                    self._optimizer()
+                work = self._gather_half(wait=False)
+            if g:
+                g["pre"].replay()
+            else:
+                self._sample()
+                self._march()
+            if work is not None:
+                work.wait()
+            if g:
+                g["net"].replay()
+            else:
+                self._network()
+            self._reduce()
         self._pending = True
         self.model.local_step += 1
 
     def flush(self):
         """Apply the pending optimizer step (before reading or saving the
-        parameters, or evaluating)."""
+        parameters, or evaluating); data parallel: every rank then holds the
+        full fp32 masters and fp16 forward copies."""
         if self._pending:
             self._optimizer()
+            self._gather_half(wait=True)
+            self._gather_masters()
             self._pending = False
 
     def capture(self, warmup=2):
-        """One hipGraph of the step body (optimizer of the previous gradients,
-        sample, march, network). The RCCL all-reduce of a data-parallel run
-        stays outside, between replays."""
+        """hipGraph(s) of the step body. World 1: one graph (optimizer of the
+        previous gradients, sample, march, network). Data parallel: three
+        (optimizer | sample + march | network); the collectives between them
+        stay outside."""
         for _ in range(max(1, warmup)):
             self.step()
         torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self._body(True)
+        if self.world == 1:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._body(True)
+        else:
+            graphs = {k: torch.cuda.CUDAGraph() for k in ("opt", "pre", "net")}
+            with torch.cuda.graph(graphs["opt"]):
+                self._optimizer()
+            with torch.cuda.graph(graphs["pre"]):
+                self._sample()
+                self._march()
+            with torch.cuda.graph(graphs["net"]):
+                self._network()
+            self.graph = graphs
         # capture recorded the launches without running them: the pending
         # update is still pending and the next step() replays it first
 
