@@ -314,6 +314,30 @@ int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* cons
                              int32_t scaler_enabled, uint32_t num_rays, const int32_t* counter,
                              int32_t* step_counter, const float* loss_ray, void* state,
                              void* stream);
+/* ngp_fused_optimizer_step without its bookkeeping launch: the GradScaler
+ * update, LR epoch, step counts and loss of this update are marked pending in
+ * `state` and done by the next ngp_fused_step_head (the fused step's first
+ * launch), saving one latency-bound single-block launch per step. */
+int ngp_fused_optimizer_update(int32_t n_tensors, float* const* params, void* const* grads,
+                               float* const* exp_avg, float* const* exp_avg_sq, void* const* half_params,
+                               const uint64_t* sizes, float lr, float beta1, float beta2, float eps,
+                               int32_t iters, int32_t zero_grads, float grad_mult, int32_t scaler_enabled,
+                               void* state, void* stream);
+/* The fused step's first launch: ngp_lego_rays's batch (same arguments), the
+ * pending bookkeeping of the last ngp_fused_optimizer_update if any (scaler
+ * arguments as ngp_fused_optimizer_step; loss_ray holds the previous batch's
+ * per-ray losses, N rays), and ngp_ffmlp_pack of n_nets networks (n_nets may
+ * be 0), as disjoint block ranges of one kernel. */
+int ngp_fused_step_head(const float* poses, uint32_t n_poses, const float* intrinsics4, uint32_t H,
+                        uint32_t W, uint32_t N, const float* boxes, int32_t nboxes, const float* aabb6,
+                        float min_near, uint32_t seed, void* state, float* rays_o, float* rays_d,
+                        float* rgba, float* bg, float* nears, float* fars, float* noises, int32_t* counter,
+                        int32_t* step_counter, float growth_factor, float backoff_factor,
+                        int32_t growth_interval, int32_t scaler_enabled, const float* loss_ray,
+                        int32_t n_nets, const void* const* mlp_weights, const uint32_t* in_dims,
+                        const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* images,
+                        void* stream);
+
 /* Data-parallel GradScaler guard for the sharded optimizer (nerf/fused.py,
  * world > 1), run on each rank's own fp16 gradient before the averaging
  * reduce-scatter: if any of its n elements is inf/nan, a NaN is written to

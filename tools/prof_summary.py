@@ -27,13 +27,13 @@ def main(tag, out=None):
     rows = list(csv.DictReader(open(os.path.join(tag, "trace", "run_kernel_trace.csv"))))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # bench.py order: ... timed graph replays (STEPS), each one step body
-    # [k_nonfinite, k_adam_multi, k_step_end (previous grads), k_lego_rays, ...,
+    # [k_nonfinite, k_adam_multi (previous grads), k_step_head, ...,
     # grid backward]; then FusedTrainer.timed_steps: flush() (3 optimizer
     # kernels) and eager steps behind torch's spin kernel.
     steps = int(os.environ.get("STEPS", "30"))
     spin = next((i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]), len(rows))
     name = lambda i: rows[i]["Kernel_Name"] if i < len(rows) else ""  # noqa: E731
-    starts = [i for i in range(spin) if "k_nonfinite" in name(i) and "k_lego_rays" in name(i + 3)]
+    starts = [i for i in range(spin) if "k_nonfinite" in name(i) and "k_step_head" in name(i + 2)]
     sel = starts[-steps:]
     per = collections.defaultdict(list)
     spans = []

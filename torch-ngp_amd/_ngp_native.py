@@ -72,6 +72,11 @@ SIGNATURES = {
                                        c_vp],
     "ngp_ffmlp_image_bytes": [c_u32, c_u32, c_u32],
     "ngp_grad_guard": [c_vp, ctypes.c_uint64, ctypes.c_uint64, c_i32, c_vp, c_vp],
+    "ngp_fused_optimizer_update": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
+                                   c_i32, c_i32, c_f32, c_i32, c_vp, c_vp],
+    "ngp_fused_step_head": [c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32, c_vp,
+                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_i32, c_i32,
+                            c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_ffmlp_pack": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_ffmlp_forward_rows": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
                                c_vp, c_vp],

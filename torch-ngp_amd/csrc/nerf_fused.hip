@@ -20,6 +20,7 @@
 //   k_adam_multi      Adam over all parameter tensors, unscaled fp16 grads,
 //                     skip on inf, device-side lr schedule; zeroes the grads
 //   k_step_end        GradScaler.update, counters, loss
+#include "ffmlp_pack.h"
 #include "ngp_common.h"
 #include "sh_basis.h"
 
@@ -51,6 +52,8 @@ struct StepState {
     int32_t draw;          // batches drawn by the sampler (k_lego_rays)
     int32_t lego_done;     // k_lego_rays' finished-block count (last block bumps draw)
     int32_t local_inf;     // data parallel: this rank's own grads held an inf/nan (k_guard_*)
+    int32_t end_pending;   // an optimizer update whose GradScaler/LR bookkeeping is deferred to k_step_head
+    int32_t pad3[3];
 };
 
 // counter-based RNG (no state, graph-safe): 32-bit mix of (seed, a, b, c)
@@ -98,12 +101,24 @@ NGP_DEV void near_far(const float o[3], const float d[3], const float aabb[6], f
     if (near < min_near) near = min_near;
 }
 
-__global__ void __launch_bounds__(256)
-k_lego_rays(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState* __restrict__ st,
-            float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ rgba,
-            float* __restrict__ bg, float* __restrict__ nears, float* __restrict__ fars,
-            float* __restrict__ noises, int32_t* __restrict__ counter, int32_t* __restrict__ step_counter) {
-    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+struct LegoOut {
+    float *rays_o, *rays_d, *rgba, *bg, *nears, *fars, *noises;
+    int32_t *counter, *step_counter;
+};
+
+// Block `blk` of the `nblk` blocks (256 threads) drawing one batch.
+NGP_DEV void lego_rays_block(uint32_t blk, uint32_t nblk, const float* __restrict__ poses, const LegoScene& sc,
+                             uint32_t N, StepState* __restrict__ st, const LegoOut& out) {
+    float* __restrict__ rays_o = out.rays_o;
+    float* __restrict__ rays_d = out.rays_d;
+    float* __restrict__ rgba = out.rgba;
+    float* __restrict__ bg = out.bg;
+    float* __restrict__ nears = out.nears;
+    float* __restrict__ fars = out.fars;
+    float* __restrict__ noises = out.noises;
+    int32_t* __restrict__ counter = out.counter;
+    int32_t* __restrict__ step_counter = out.step_counter;
+    const uint32_t n = blk * blockDim.x + threadIdx.x;
     const uint32_t it = (uint32_t)st->draw;
     // Only this kernel touches draw / lego_done / counter / step_counter, so it
     // can run beside the previous step's optimizer (nerf/fused.py pipelining).
@@ -119,7 +134,7 @@ k_lego_rays(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState
     __syncthreads();
     if (threadIdx.x == 0) {  // every block has read draw before the last one bumps it
         __threadfence();
-        if (atomicAdd(&st->lego_done, 1) == (int32_t)gridDim.x - 1) {
+        if (atomicAdd(&st->lego_done, 1) == (int32_t)nblk - 1) {
             st->draw = (int32_t)it + 1;
             st->lego_done = 0;
         }
@@ -167,6 +182,11 @@ k_lego_rays(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState
     near_far(o, d, sc.aabb, sc.min_near, nr, fr);
     nears[n] = nr;
     fars[n] = fr;
+}
+
+__global__ void __launch_bounds__(256)
+k_lego_rays(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState* __restrict__ st, LegoOut out) {
+    lego_rays_block(blockIdx.x, gridDim.x, poses, sc, N, st, out);
 }
 
 // ---- network glue -------------------------------------------------------------
@@ -463,6 +483,7 @@ struct AdamArgs {
     int32_t iters;   // LambdaLR: lr = base_lr * 0.1 ** min(epoch / iters, 1)
     int32_t zero_grads;
     float grad_mult; // e.g. 1 / world_size after a data-parallel all-reduce (sum)
+    int32_t defer_end;  // the step's bookkeeping runs in the next k_step_head
 };
 
 // torch.optim.Adam (weight_decay 0) on p, with g = half_grad * (1 / scale);
@@ -477,8 +498,9 @@ struct AdamArgs {
 // at the seams) takes its pointers from scalar loads.
 constexpr uint32_t kAdamThreads = 256, kAdamChunk = kAdamThreads * 8;
 __global__ void __launch_bounds__(kAdamThreads)
-k_adam_multi(TensorList tl, const StepState* __restrict__ st, AdamArgs aa) {
+k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa) {
     const bool skip = st->found_inf != 0;
+    if (aa.defer_end && blockIdx.x == 0 && threadIdx.x == 0) st->end_pending = 1;  // read by k_step_head only
     const int32_t step = st->adam_step + 1;
     const double lr = (double)aa.base_lr * pow(0.1, fmin((double)st->epoch / (double)aa.iters, 1.0));
     const double bc1 = 1.0 - pow((double)aa.beta1, step);
@@ -592,9 +614,8 @@ struct ScalerArgs {
 // GradScaler.update, LambdaLR epoch, Adam step count, loss bookkeeping (mean
 // of the per-ray losses, fixed-order tree sum); also records this step's
 // sample count into step_counter[iter % 16]
-__global__ void __launch_bounds__(256)
-k_step_end(StepState* __restrict__ st, ScalerArgs sa, const int32_t* __restrict__ counter,
-           int32_t* __restrict__ step_counter, const float* __restrict__ loss_ray, uint32_t n_rays) {
+NGP_DEV void step_end_block(StepState* __restrict__ st, const ScalerArgs& sa, const int32_t* __restrict__ counter,
+                            int32_t* __restrict__ step_counter, const float* __restrict__ loss_ray, uint32_t n_rays) {
     __shared__ float part[256];
     float acc = 0.0f;
     if (loss_ray)
@@ -628,6 +649,34 @@ k_step_end(StepState* __restrict__ st, ScalerArgs sa, const int32_t* __restrict_
     st->last_loss = st->loss_sum * sa.inv_n;
     st->loss_sum = 0.0f;
     st->found_inf = 0;
+    st->end_pending = 0;
+}
+
+__global__ void __launch_bounds__(256)
+k_step_end(StepState* __restrict__ st, ScalerArgs sa, const int32_t* __restrict__ counter,
+           int32_t* __restrict__ step_counter, const float* __restrict__ loss_ray, uint32_t n_rays) {
+    step_end_block(st, sa, counter, step_counter, loss_ray, n_rays);
+}
+
+// The head of a fused step, one launch of three independent parts:
+//   blocks [0, nlego)      the batch (k_lego_rays)
+//   block nlego            the deferred end of the previous optimizer update
+//                          (k_step_end: GradScaler.update, LR epoch, loss), if one is pending
+//   blocks nlego + 1 ...   the MLP fragment images from the fp16 weights it wrote (ngp_ffmlp_pack)
+// The parts touch disjoint state: the sampler only draw / lego_done /
+// counter, the end only the scaler / optimizer fields; both read nothing the
+// other writes. Each on its own was a latency-bound launch of ~5 us.
+__global__ void __launch_bounds__(256)
+k_step_head(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState* __restrict__ st, LegoOut out,
+            uint32_t nlego, ScalerArgs sa, const float* __restrict__ loss_ray, ngp_pack::PackJobs jobs) {
+    if (blockIdx.x < nlego) {
+        lego_rays_block(blockIdx.x, nlego, poses, sc, N, st, out);
+    } else if (blockIdx.x == nlego) {
+        if (st->end_pending) step_end_block(st, sa, nullptr, nullptr, loss_ray, N);
+    } else {
+        const ngp_pack::PackJob& j = jobs.job[blockIdx.x - nlego - 1];
+        ngp_pack::build_frags(j.image, j.w, j.m, j.transposed != 0);
+    }
 }
 
 TensorList make_list(int n, float* const* p, void* const* g, float* const* m, float* const* v,
@@ -653,6 +702,58 @@ uint32_t sweep_blocks(uint64_t total, uint32_t per_thread) {
     return b ? (uint32_t)b : 1u;
 }
 
+LegoScene make_scene(uint32_t n_poses, const float* intrinsics4, uint32_t H, uint32_t W, const float* boxes,
+                     int32_t nboxes, const float* aabb6, float min_near, uint32_t seed) {
+    LegoScene sc{};
+    for (int b = 0; b < nboxes; ++b)
+        for (int k = 0; k < 3; ++k) {
+            sc.lo[b][k] = boxes[b * 9 + k];
+            sc.hi[b][k] = boxes[b * 9 + 3 + k];
+            sc.rgb[b][k] = boxes[b * 9 + 6 + k];
+        }
+    sc.nboxes = nboxes;
+    sc.fx = intrinsics4[0]; sc.fy = intrinsics4[1]; sc.cx = intrinsics4[2]; sc.cy = intrinsics4[3];
+    sc.H = H; sc.W = W; sc.n_poses = n_poses;
+    for (int k = 0; k < 6; ++k) sc.aabb[k] = aabb6[k];
+    sc.min_near = min_near;
+    sc.seed = seed;
+    return sc;
+}
+
+int optimizer_launch(int32_t n_tensors, float* const* params, void* const* grads, float* const* exp_avg,
+                     float* const* exp_avg_sq, void* const* half_params, const uint64_t* sizes, float lr,
+                     float beta1, float beta2, float eps, int32_t iters, int32_t zero_grads, float grad_mult,
+                     float growth_factor, float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
+                     uint32_t num_rays, const int32_t* counter, int32_t* step_counter, const float* loss_ray,
+                     void* state, void* stream, bool defer_end) {
+    NGP_REQUIRE(n_tensors >= 1 && n_tensors <= kMaxTensors, NGP_ERR_ARG,
+                "fused_optimizer_step: 1..%d tensors", kMaxTensors);
+    for (int k = 0; k < n_tensors; ++k)
+        NGP_REQUIRE(((reinterpret_cast<uintptr_t>(params[k]) | reinterpret_cast<uintptr_t>(exp_avg[k]) |
+                      reinterpret_cast<uintptr_t>(exp_avg_sq[k])) & 15) == 0 &&
+                        (reinterpret_cast<uintptr_t>(grads[k]) & 7) == 0,
+                    NGP_ERR_ARG, "fused_optimizer_step: tensor %d misaligned", k);
+    hipStream_t s = ngp_stream(stream);
+    StepState* st = static_cast<StepState*>(state);
+    for (int k = 0; k < n_tensors; ++k)
+        NGP_REQUIRE(!half_params || !half_params[k] || (reinterpret_cast<uintptr_t>(half_params[k]) & 7) == 0,
+                    NGP_ERR_ARG, "fused_optimizer_step: half shadow %d misaligned", k);
+    const TensorList tl = make_list(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes);
+    const uint64_t total = tl.start[n_tensors];
+    if (scaler_enabled)
+        k_nonfinite<<<sweep_blocks(total, 8), 256, 0, s>>>(tl, st);
+    AdamArgs aa{lr, beta1, beta2, eps, iters, zero_grads, grad_mult, defer_end ? 1 : 0};
+    const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
+    const uint64_t adam_blocks = std::min<uint64_t>(nchunks, 16ull * ngp_num_cus());
+    k_adam_multi<<<(uint32_t)(adam_blocks ? adam_blocks : 1), kAdamThreads, 0, s>>>(tl, st, aa);
+    if (!defer_end) {
+        ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled,
+                      num_rays ? 1.0f / (float)num_rays : 0.0f};
+        k_step_end<<<1, 256, 0, s>>>(st, sa, counter, step_counter, loss_ray, num_rays);
+    }
+    return ngp_check_launch("fused_optimizer_step");
+}
+
 }  // namespace
 
 extern "C" size_t ngp_fused_state_bytes(void) { return sizeof(StepState); }
@@ -675,22 +776,10 @@ extern "C" int ngp_lego_rays(const float* poses, uint32_t n_poses, const float* 
     NGP_REQUIRE(nboxes >= 0 && nboxes <= kMaxBoxes, NGP_ERR_ARG, "lego_rays: at most %d boxes", kMaxBoxes);
     NGP_REQUIRE(n_poses > 0 && H > 0 && W > 0, NGP_ERR_ARG, "lego_rays: empty pose set or image");
     if (N == 0) return NGP_OK;
-    LegoScene sc{};
-    for (int b = 0; b < nboxes; ++b)
-        for (int k = 0; k < 3; ++k) {
-            sc.lo[b][k] = boxes[b * 9 + k];
-            sc.hi[b][k] = boxes[b * 9 + 3 + k];
-            sc.rgb[b][k] = boxes[b * 9 + 6 + k];
-        }
-    sc.nboxes = nboxes;
-    sc.fx = intrinsics4[0]; sc.fy = intrinsics4[1]; sc.cx = intrinsics4[2]; sc.cy = intrinsics4[3];
-    sc.H = H; sc.W = W; sc.n_poses = n_poses;
-    for (int k = 0; k < 6; ++k) sc.aabb[k] = aabb6[k];
-    sc.min_near = min_near;
-    sc.seed = seed;
-    k_lego_rays<<<ngp_div_up(N, 256), 256, 0, ngp_stream(stream)>>>(
-        poses, sc, N, static_cast<StepState*>(state), rays_o, rays_d, rgba, bg, nears, fars, noises, counter,
-        step_counter);
+    const LegoScene sc = make_scene(n_poses, intrinsics4, H, W, boxes, nboxes, aabb6, min_near, seed);
+    const LegoOut out{rays_o, rays_d, rgba, bg, nears, fars, noises, counter, step_counter};
+    k_lego_rays<<<ngp_div_up(N, 256), 256, 0, ngp_stream(stream)>>>(poses, sc, N, static_cast<StepState*>(state),
+                                                                     out);
     return ngp_check_launch("lego_rays");
 }
 
@@ -744,30 +833,45 @@ extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params,
                                         uint32_t num_rays, const int32_t* counter,
                                         int32_t* step_counter, const float* loss_ray, void* state,
                                         void* stream) {
-    NGP_REQUIRE(n_tensors >= 1 && n_tensors <= kMaxTensors, NGP_ERR_ARG,
-                "fused_optimizer_step: 1..%d tensors", kMaxTensors);
-    for (int k = 0; k < n_tensors; ++k)
-        NGP_REQUIRE(((reinterpret_cast<uintptr_t>(params[k]) | reinterpret_cast<uintptr_t>(exp_avg[k]) |
-                      reinterpret_cast<uintptr_t>(exp_avg_sq[k])) & 15) == 0 &&
-                        (reinterpret_cast<uintptr_t>(grads[k]) & 7) == 0,
-                    NGP_ERR_ARG, "fused_optimizer_step: tensor %d misaligned", k);
-    hipStream_t s = ngp_stream(stream);
-    StepState* st = static_cast<StepState*>(state);
-    for (int k = 0; k < n_tensors; ++k)
-        NGP_REQUIRE(!half_params || !half_params[k] || (reinterpret_cast<uintptr_t>(half_params[k]) & 7) == 0,
-                    NGP_ERR_ARG, "fused_optimizer_step: half shadow %d misaligned", k);
-    const TensorList tl = make_list(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes);
-    const uint64_t total = tl.start[n_tensors];
-    if (scaler_enabled)
-        k_nonfinite<<<sweep_blocks(total, 8), 256, 0, s>>>(tl, st);
-    AdamArgs aa{lr, beta1, beta2, eps, iters, zero_grads, grad_mult};
-    const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
-    const uint64_t adam_blocks = std::min<uint64_t>(nchunks, 16ull * ngp_num_cus());
-    k_adam_multi<<<(uint32_t)(adam_blocks ? adam_blocks : 1), kAdamThreads, 0, s>>>(tl, st, aa);
-    ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled,
-                  num_rays ? 1.0f / (float)num_rays : 0.0f};
-    k_step_end<<<1, 256, 0, s>>>(st, sa, counter, step_counter, loss_ray, num_rays);
-    return ngp_check_launch("fused_optimizer_step");
+    return optimizer_launch(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes, lr, beta1, beta2,
+                            eps, iters, zero_grads, grad_mult, growth_factor, backoff_factor, growth_interval,
+                            scaler_enabled, num_rays, counter, step_counter, loss_ray, state, stream, false);
+}
+
+extern "C" int ngp_fused_optimizer_update(int32_t n_tensors, float* const* params, void* const* grads,
+                                          float* const* exp_avg, float* const* exp_avg_sq,
+                                          void* const* half_params, const uint64_t* sizes, float lr,
+                                          float beta1, float beta2, float eps, int32_t iters,
+                                          int32_t zero_grads, float grad_mult, int32_t scaler_enabled,
+                                          void* state, void* stream) {
+    return optimizer_launch(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes, lr, beta1, beta2,
+                            eps, iters, zero_grads, grad_mult, 0.0f, 0.0f, 0, scaler_enabled, 0, nullptr, nullptr,
+                            nullptr, state, stream, true);
+}
+
+extern "C" int ngp_fused_step_head(const float* poses, uint32_t n_poses, const float* intrinsics4, uint32_t H,
+                                   uint32_t W, uint32_t N, const float* boxes, int32_t nboxes, const float* aabb6,
+                                   float min_near, uint32_t seed, void* state, float* rays_o, float* rays_d,
+                                   float* rgba, float* bg, float* nears, float* fars, float* noises,
+                                   int32_t* counter, int32_t* step_counter, float growth_factor,
+                                   float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
+                                   const float* loss_ray, int32_t n_nets, const void* const* mlp_weights,
+                                   const uint32_t* in_dims, const uint32_t* hidden_dims,
+                                   const uint32_t* num_layers, void* const* images, void* stream) {
+    NGP_REQUIRE(nboxes >= 0 && nboxes <= kMaxBoxes, NGP_ERR_ARG, "step_head: at most %d boxes", kMaxBoxes);
+    NGP_REQUIRE(n_poses > 0 && H > 0 && W > 0 && N > 0, NGP_ERR_ARG, "step_head: empty pose set, image or batch");
+    NGP_REQUIRE(state && loss_ray, NGP_ERR_ARG, "step_head: null state or loss_ray");
+    ngp_pack::PackJobs jobs{};
+    if (n_nets > 0)
+        if (int e = ngp_pack::build_jobs(n_nets, mlp_weights, in_dims, hidden_dims, num_layers, images, jobs))
+            return e;
+    const LegoScene sc = make_scene(n_poses, intrinsics4, H, W, boxes, nboxes, aabb6, min_near, seed);
+    const LegoOut out{rays_o, rays_d, rgba, bg, nears, fars, noises, counter, step_counter};
+    const ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled, 1.0f / (float)N};
+    const uint32_t nlego = ngp_div_up(N, 256);
+    k_step_head<<<nlego + 1 + (uint32_t)jobs.n, 256, 0, ngp_stream(stream)>>>(
+        poses, sc, N, static_cast<StepState*>(state), out, nlego, sa, loss_ray, jobs);
+    return ngp_check_launch("fused_step_head");
 }
 
 extern "C" int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, void* state,

@@ -207,7 +207,7 @@ class FusedTrainer:
         phases run serially here (the all-gather is waited for right away)."""
         self.flush()
         acc = {}
-        for _ in range(k):
+        for i in range(k):
             torch.cuda.synchronize()
             torch.cuda._sleep(4_000_000)  # keep the GPU busy while the host queues the step
             self._events = []
@@ -216,7 +216,7 @@ class FusedTrainer:
             self._march()
             self._network()
             self._reduce()
-            self._optimizer()
+            self._optimizer(defer=i < k - 1)
             self._gather_half(wait=True)
             self.model.local_step += 1
             torch.cuda.synchronize()
@@ -229,7 +229,7 @@ class FusedTrainer:
         """One step's launches (world 1): [optimizer(previous grads)] ->
         sample -> march -> network forward/backward."""
         if pending:
-            self._optimizer()
+            self._optimizer(defer=True)
         self._sample()
         self._march()
         self._network()
@@ -286,16 +286,19 @@ class FusedTrainer:
             self.flat_param.copy_(full)
 
     def _sample(self):
-        """Batch of N rays: rays, RGBA target, background, march noise, near/far."""
+        """The step head: batch of N rays (rays, RGBA target, background, march
+        noise, near/far), the pending bookkeeping of a deferred optimizer
+        update, and both networks' MLP fragment images, in one launch."""
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
-        m, d = self.model, self.data
-        nat.check(lib.ngp_lego_rays(P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N,
-                                    self._boxes, self._nboxes, self._aabb, float(m.min_near), self.seed,
-                                    P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
-                                    P(self.nears), P(self.fars), P(self.noises), P(self.counter),
-                                    P(m.step_counter), s),
-                  "lego_rays")
-        self._tick("lego_rays")
+        m, d, pk = self.model, self.data, self._pk
+        nat.check(lib.ngp_fused_step_head(P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N,
+                                          self._boxes, self._nboxes, self._aabb, float(m.min_near), self.seed,
+                                          P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
+                                          P(self.nears), P(self.fars), P(self.noises), P(self.counter),
+                                          P(m.step_counter), 2.0, 0.5, self.growth_interval, 1, P(self.loss_ray),
+                                          2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s),
+                  "fused_step_head")
+        self._tick("step_head")
 
     def _forward_backward(self):
         """march -> network -> composite + MSE -> full backward into the fp16 grads."""
@@ -318,8 +321,6 @@ class FusedTrainer:
         M, N, cnt = self.M, self.N, P(self.counter)
         chk = nat.check
         pk = self._pk
-        chk(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
-        self._tick("ffmlp_pack")
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
         chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(self.w_half[0]), _F16, P(e.offsets),
@@ -359,17 +360,21 @@ class FusedTrainer:
             "grid_backward_fused")
         self._tick("grid_encode_backward")
 
-    def _optimizer(self):
-        """GradScaler inf check + Adam (unscaled fp16 grads, LambdaLR) + scaler update."""
+    def _optimizer(self, defer=False):
+        """GradScaler inf check + Adam (unscaled fp16 grads, LambdaLR) + scaler
+        update. defer: the scaler / LR / loss bookkeeping is left to the next
+        step head (_sample), which runs right after it in a step."""
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
-        o, chk, N, cnt, m = self._opt, nat.check, self.N, P(self.counter), self.model
+        o, chk, N, cnt = self._opt, nat.check, self.N, P(self.counter)
         # world 1 zeroes the grads here; data parallel: the shard is the reduce-scatter's
         # output and the flat gradient is cleared after the collective read it
-        chk(lib.ngp_fused_optimizer_step(1, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"],
-                                         self.lr, self.betas[0], self.betas[1], self.eps, self.iters,
-                                         int(self.world == 1), 1.0, 2.0, 0.5, self.growth_interval, 1, N, cnt,
-                                         None, P(self.loss_ray),
-                                         P(self.state), s), "fused_optimizer_step")
+        args = (1, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
+                self.betas[1], self.eps, self.iters, int(self.world == 1), 1.0)
+        if defer:
+            chk(lib.ngp_fused_optimizer_update(*args, 1, P(self.state), s), "fused_optimizer_update")
+        else:
+            chk(lib.ngp_fused_optimizer_step(*args, 2.0, 0.5, self.growth_interval, 1, N, cnt, None,
+                                             P(self.loss_ray), P(self.state), s), "fused_optimizer_step")
         self._tick("optimizer")
 
     def step(self):
@@ -387,7 +392,7 @@ class FusedTrainer:
                 if g:
                     g["opt"].replay()
                 else:
-                    self._optimizer()
+                    self._optimizer(defer=True)
                 work = self._gather_half(wait=False)
             if g:
                 g["pre"].replay()
@@ -429,7 +434,7 @@ class FusedTrainer:
         else:
             graphs = {k: torch.cuda.CUDAGraph() for k in ("opt", "pre", "net")}
             with torch.cuda.graph(graphs["opt"]):
-                self._optimizer()
+                self._optimizer(defer=True)
             with torch.cuda.graph(graphs["pre"]):
                 self._sample()
                 self._march()
