@@ -232,7 +232,11 @@ int ngp_grid_encode_forward_fused(const float* xyz, float bound, const void* emb
 /* Binned backward (hashed levels without scattered atomics) when workspace is
  * given: offsets_host is a host copy of offsets; the workspace (size from
  * ngp_grid_encode_backward_fused_workspace_bytes, 0 if nothing is binned) must
- * be zero-filled before its first use and is left ready for the next call. */
+ * be zero-filled before its first use and is left ready for the next call.
+ * nonfinite (nullable; needs offsets_host): set to 1 when a grad entry this
+ * call leaves in grad_embeddings is inf/nan: GradScaler's check (torch
+ * amp _amp_foreach_non_finite_check_and_unscale_) made by the kernels that
+ * write the values (binned levels) or a scan of the other levels. */
 size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
                                                       float S, uint32_t H, int32_t align_corners,
                                                       const int32_t* offsets_host);
@@ -241,7 +245,8 @@ int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bou
                                    const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
                                    uint32_t H, uint32_t gridtype, int32_t align_corners,
                                    uint32_t interp, const int32_t* offsets_host, void* workspace,
-                                   size_t workspace_bytes, int32_t grad_layout, void* stream);
+                                   size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
+                                   void* stream);
 /* Weight-fragment images (forward + transposed, per matmul) of n networks in
  * one launch; image k needs ngp_ffmlp_image_bytes of its network. The
  * forward/backward *_rows calls below take the image (nullable: the weights
@@ -271,10 +276,11 @@ int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* we
                             int32_t gw_dtype, uint32_t flags, void* workspace,
                             size_t workspace_bytes, void* stream);
 /* Sums the deferred dW partials of n backward calls (same B and shapes as
- * those calls) into grad_weights[k], in one launch (n <= 4). */
+ * those calls) into grad_weights[k], in one launch (n <= 4). nonfinite
+ * (nullable): set to 1 when a written grad is inf/nan (GradScaler's check). */
 int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32_t* Bs, const uint32_t* in_dims,
                      const uint32_t* hidden_dims, const uint32_t* num_layers,
-                     void* const* grad_weights, int32_t gw_dtype, void* stream);
+                     void* const* grad_weights, int32_t gw_dtype, int32_t* nonfinite, void* stream);
 size_t ngp_fused_state_bytes(void);
 int ngp_fused_state_init(void* state, float init_scale, void* stream);
 /* Synthetic Lego batch (nerf/provider.py SyntheticLego): boxes = nboxes x
@@ -299,6 +305,16 @@ int ngp_nerf_composite_loss(const float* sigma, const void* color_out, const voi
                             uint32_t gt_channels, const float* bg, void* state,
                             void* grad_color_out, void* grad_h_sigma, float* out_image,
                             float* out_ws, float* loss_ray, void* stream);
+/* scaler_enabled of the optimizer entries: GradScaler off; on, with its inf
+ * check as a sweep over the grads; on, with the check already made by the
+ * kernels that wrote the grads into the state's flag (ngp_fused_inf_flag). */
+#define NGP_SCALER_OFF 0
+#define NGP_SCALER_SCAN 1
+#define NGP_SCALER_PRECHECKED 2
+/* The state's GradScaler flag (local == 0: the found-inf flag the optimizer
+ * reads; local != 0: the data-parallel guard's per-rank flag), for the
+ * nonfinite arguments of the grid backward and the MLP reduce. */
+int32_t* ngp_fused_inf_flag(void* state, int32_t local);
 /* Adam (+ GradScaler inf check/unscale/update, LambdaLR 0.1^(epoch/iters))
  * over n_tensors fp32 params with fp16 grads; half_params[k] (nullable) is
  * refreshed with half(p) after the update; grads are zeroed when zero_grads;
@@ -348,6 +364,8 @@ int ngp_fused_step_head(const float* poses, uint32_t n_poses, const float* intri
  * the whole gradient, torch/amp/grad_scaler.py). */
 int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, void* state,
                    void* stream);
+/* (n == 0: no scan; the per-rank flag ngp_fused_inf_flag(state, 1) was set by
+ * the kernels that wrote the gradient.) */
 
 #ifdef __cplusplus
 }

@@ -248,7 +248,7 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
     nat.check(lib.ngp_ffmlp_backward_rows(P(gh), P(x), P(ws[0]), P(imgs[0]), B, P(cnt), 32, 16, 64, 2, 0, P(gx),
                                           None, 1, 1, P(wsb[0]), wsb[0].numel(), s), "b_defer")
     nat.check(lib.ngp_ffmlp_reduce(2, arr([wsb[1], wsb[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
-                                   u32([3, 2]), arr([gw[1], gw[0]]), 1, s), "reduce")
+                                   u32([3, 2]), arr([gw[1], gw[0]]), 1, None, s), "reduce")
     torch.cuda.synchronize()
     assert torch.equal(o[:n].view(torch.int16), o_ref[:n].view(torch.int16))
     assert torch.equal(gh[:n].view(torch.int16), gh_ref[:n].view(torch.int16))
@@ -295,3 +295,20 @@ def test_grad_guard_poisons_every_shard(cuda):
     g[3000] = ref[3000]
     assert torch.equal(g, ref)
     assert int(ft.state.view(torch.int32)[11].item()) == 0  # local_inf cleared
+
+
+def test_step_overflow_skips_via_kernel_flags(cuda):
+    """Inside a step the optimizer trusts the found-inf flag the grid backward
+    and the MLP reduce set (no sweep over the grads): a loss scale that makes
+    the fp16 grads overflow must skip the update and back the scale off."""
+    _, _, _, ft = _setup(cuda)
+    ft.state.view(torch.float32)[0] = 2.0 ** 40  # GradScaler scale
+    before = [p.detach().clone() for p in ft.params]
+    ft.step()   # grads overflow
+    ft.step()   # applies the pending update (kernel-flag mode): skipped
+    ft.flush()  # the second step's update (sweep mode): skipped as well
+    torch.cuda.synchronize()
+    assert ft.optimizer_steps == 0
+    assert ft.scale == 2.0 ** 38
+    for a, b in zip(ft.params, before):
+        assert torch.equal(a.detach(), b)

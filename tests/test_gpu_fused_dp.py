@@ -54,14 +54,15 @@ def _worker(rank, world, port, q):
     torch.cuda.synchronize()
     params = [p.detach().cpu().numpy() for p in ft.params]
     steps = ft.optimizer_steps
-    # GradScaler under the sharded optimizer: an inf on ONE rank must make
-    # every rank skip the step and back the scale off (ngp_grad_guard)
+    # GradScaler under the sharded optimizer: an overflow on ONE rank must make
+    # every rank skip the step and back the scale off (its backward's kernels
+    # raise the rank's flag, ngp_grad_guard spreads it to every shard)
+    if rank == 0:
+        ft.state.view(torch.float32)[0] = 2.0 ** 40  # this rank's fp16 grads overflow
     scale0 = ft.scale
     ft._sample()
     ft._march()
     ft._network()
-    if rank == 0:
-        ft.grads[1][3] = float("inf")
     ft._reduce()
     ft._optimizer()
     ft._gather_half(wait=True)

@@ -53,7 +53,7 @@ def _normalise(w, bound):
     return ((w + np.float32(bound)) * np.float32(1.0 / (2.0 * bound))).astype(np.float32)
 
 
-def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, reps=1, layout=1):
+def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, reps=1, layout=1, flag=None):
     B = w.shape[0]
     S = float(np.float32(np.log2(scale)))
     offs_host = np.ascontiguousarray(offs, dtype=np.int32)
@@ -70,7 +70,8 @@ def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, rep
         nat.check(nat.lib().ngp_grid_encode_backward_fused(
             nat.ptr(gt), nat.ptr(wt), float(bound), nat.ptr(ot), nat.ptr(table), B,
             nat.ptr(cnt) if cnt is not None else None, 3, 2, L, S, H, 0, 0, 0, hp,
-            nat.ptr(ws), ws.numel(), layout, nat.stream_of(table)), "grid_backward_fused")
+            nat.ptr(ws), ws.numel(), layout, nat.ptr(flag) if flag is not None else None,
+            nat.stream_of(table)), "grid_backward_fused")
     torch.cuda.synchronize()
     # the workspace's counters are left zeroed for the next call
     assert int(ws[:256].sum()) == 0
@@ -108,7 +109,9 @@ def test_grid_backward_fused_vs_oracle(cuda, case):
     w = _world(B, bound, seed=B + L, concentrated=0.25 * (layout == "concentrated"), ordered=layout == "rays")
     rng = np.random.default_rng(7)
     g16 = (rng.standard_normal((B, L * 2)) * 0.5).astype(np.float16)
-    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, bound)
+    flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, bound, flag=flag)
+    assert int(flag.item()) == 0  # finite grads: GradScaler's check stays clear
     x = _normalise(w, bound)
     ref = oracle.grid_encode_backward(g16, x, offs, 2, scale, H)
     _check_levels(got, ref, offs, layout)
@@ -168,3 +171,26 @@ def test_grid_forward_fused_bit_exact(cuda, table, layout):
         got = out.view(-1).view(L, B, 2).permute(1, 0, 2).reshape(B, L * 2).cpu().numpy()
     assert np.array_equal(got[:n].view(np.uint16), ref.view(np.uint16))  # outside rows: zeros in both
     assert np.all(got[n:] == 7.0)  # rows past the sample count untouched
+
+
+@pytest.mark.parametrize("log2T", [19, 22])
+def test_grid_backward_fused_flags_nonfinite(cuda, log2T):
+    """The nonfinite flag is GradScaler's inf check made by the kernels that
+    write the grads: an inf output grad, or finite terms whose fp16 sum
+    overflows, must set it, on the binned levels and (T = 2^22: levels past
+    the binned prefix) the scanned ones."""
+    nat = _lib()
+    B, L, H, scale = 20000, 16, 16, LEGO_SCALE
+    offs = oracle.grid_offsets(3, L, 2, H, scale, log2T)
+    w = _world(B, 1.0, seed=5)
+    g16 = (np.random.default_rng(2).standard_normal((B, L * 2)) * 0.5).astype(np.float16)
+    for lvl in (0, L - 1):
+        g = g16.copy()
+        g[B // 2, 2 * lvl] = np.float16(np.inf)
+        flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+        _bwd(nat, cuda, g, w, offs, L, H, scale, 1.0, flag=flag)
+        assert int(flag.item()) == 1, ("inf grad", lvl)
+    big = np.full((B, L * 2), 60000.0, np.float16)  # finite terms, their fp16 sums overflow
+    flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+    _bwd(nat, cuda, big, w, offs, L, H, scale, 1.0, flag=flag)
+    assert int(flag.item()) == 1, "sum overflow"

@@ -36,7 +36,7 @@ def call():
     nat.check(lib.ngp_grid_encode_backward_fused(
         P(ft.g_enc), P(ft.xyzs), float(m.bound), P(e.offsets), P(ft.grads[0]), ft.M, P(ft.counter),
         e.input_dim, e.level_dim, e.num_levels, ft.S, e.base_resolution, e.gridtype_id, int(e.align_corners),
-        e.interp_id, ft._offsets_host, P(ft.grid_ws), ft.grid_ws.numel(), 0, s), "grid_bwd")
+        e.interp_id, ft._offsets_host, P(ft.grid_ws), ft.grid_ws.numel(), 0, None, s), "grid_bwd")
 
 
 os.environ.update(KNOBS)  # debug knobs only for the timed calls (training above runs the product path)

@@ -27,13 +27,14 @@ def main(tag, out=None):
     rows = list(csv.DictReader(open(os.path.join(tag, "trace", "run_kernel_trace.csv"))))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # bench.py order: ... timed graph replays (STEPS), each one step body
-    # [k_nonfinite, k_adam_multi (previous grads), k_step_head, ...,
+    # [k_adam_multi (previous grads; the inf check comes from the backward's
+    # kernels), k_step_head, ...,
     # grid backward]; then FusedTrainer.timed_steps: flush() (3 optimizer
     # kernels) and eager steps behind torch's spin kernel.
     steps = int(os.environ.get("STEPS", "30"))
     spin = next((i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]), len(rows))
     name = lambda i: rows[i]["Kernel_Name"] if i < len(rows) else ""  # noqa: E731
-    starts = [i for i in range(spin) if "k_nonfinite" in name(i) and "k_step_head" in name(i + 2)]
+    starts = [i for i in range(spin) if "k_adam_multi" in name(i) and "k_step_head" in name(i + 1)]
     sel = starts[-steps:]
     per = collections.defaultdict(list)
     spans = []

@@ -69,9 +69,10 @@ SIGNATURES = {
                                                        c_vp],
     "ngp_grid_encode_backward_fused": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
                                        c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_i32,
-                                       c_vp],
+                                       c_vp, c_vp],
     "ngp_ffmlp_image_bytes": [c_u32, c_u32, c_u32],
     "ngp_grad_guard": [c_vp, ctypes.c_uint64, ctypes.c_uint64, c_i32, c_vp, c_vp],
+    "ngp_fused_inf_flag": [c_vp, c_i32],
     "ngp_fused_optimizer_update": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
                                    c_i32, c_i32, c_f32, c_i32, c_vp, c_vp],
     "ngp_fused_step_head": [c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32, c_vp,
@@ -84,7 +85,7 @@ SIGNATURES = {
                                c_f32, c_u32, c_vp],
     "ngp_ffmlp_backward_rows": [c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32,
                                 c_vp, c_vp, c_i32, c_u32, c_vp, c_sz, c_vp],
-    "ngp_ffmlp_reduce": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],
+    "ngp_ffmlp_reduce": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
     "ngp_fused_state_bytes": [],
     "ngp_fused_state_init": [c_vp, c_f32, c_vp],
     "ngp_lego_rays": [c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32,
@@ -99,6 +100,7 @@ SIGNATURES = {
 }
 _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,
+    "ngp_fused_inf_flag": c_vp,
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
     "ngp_march_rays_train_workspace_bytes": c_sz,
     "ngp_fused_state_bytes": c_sz,

@@ -660,6 +660,7 @@ struct ReduceJobs {
     void* out[kMaxReduceJobs];
     uint32_t rows[kMaxReduceJobs], np[kMaxReduceJobs];
     uint32_t block0[kMaxReduceJobs + 1];
+    int32_t* nonfinite;  // nullable: set when a written grad is inf/nan (GradScaler's check)
 };
 
 template <typename OUT>
@@ -689,7 +690,9 @@ k_slab_reduce(ReduceJobs jobs) {
         float t = 0.0f;
 #pragma unroll
         for (int k = 0; k < kReducePhases; ++k) t += part[k][lane];
-        static_cast<OUT*>(jobs.out[j])[p] = (OUT)t;
+        const OUT o = (OUT)t;
+        static_cast<OUT*>(jobs.out[j])[p] = o;
+        if (jobs.nonfinite && !__builtin_isfinite((float)o)) atomicOr(jobs.nonfinite, 1);
     }
 }
 
@@ -1006,12 +1009,13 @@ extern "C" int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, con
  * those calls) into grad_weights[k], one launch. */
 extern "C" int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32_t* Bs, const uint32_t* in_dims,
                                 const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* grad_weights,
-                                int32_t gw_dtype, void* stream) {
+                                int32_t gw_dtype, int32_t* nonfinite, void* stream) {
     NGP_REQUIRE(n >= 1 && n <= kMaxReduceJobs, NGP_ERR_ARG, "ffmlp_reduce: 1..%d networks", kMaxReduceJobs);
     NGP_REQUIRE(gw_dtype == NGP_DTYPE_F16 || gw_dtype == NGP_DTYPE_F32, NGP_ERR_ARG,
                 "grad_weights must be float16 or float32");
     ReduceJobs rj{};
     rj.n = 0;
+    rj.nonfinite = nonfinite;
     uint32_t blocks = 0;
     for (int k = 0; k < n; ++k) {
         const uint32_t rows = bwd_blocks(Bs[k]);

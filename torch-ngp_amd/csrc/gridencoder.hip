@@ -550,6 +550,14 @@ struct BinItem {  // 8 bytes: the accumulate kernel reads items as one dword pai
 };
 static_assert(sizeof(BinItem) == 8, "BinItem layout");
 
+// Is the fp16 sum old + v (what a packed fp16 atomic stores) finite in both
+// channels? The float sum of two halves rounds to the same half as the
+// half-precision add.
+NGP_DEV bool half2_sum_finite(ngp_half2 old, ngp_half2 v) {
+    const ngp_half a = (ngp_half)((float)old[0] + (float)v[0]), b = (ngp_half)((float)old[1] + (float)v[1]);
+    return __builtin_isfinite((float)a) && __builtin_isfinite((float)b);
+}
+
 NGP_DEV uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -566,7 +574,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
                const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
                InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
-               int32_t grad_layout) {
+               int32_t grad_layout, int32_t* __restrict__ nonfinite) {
     constexpr uint32_t C = 2, NC = 1u << D, NW = kBinPts / 64;
     static_assert(kMaxBinsPerLevel <= kBinPts, "one bin per thread in the reservation step");
     __shared__ uint32_t cnt[kMaxBinsPerLevel], soff[kMaxBinsPerLevel + 1], wsum[NW];
@@ -726,7 +734,13 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
             lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
         } else {  // past the bin's capacity
             const size_t e = (size_t)bin * kBinEntries + (it.e & 0xffffu);
-            __builtin_amdgcn_global_atomic_fadd_v2f16(reinterpret_cast<ngp_half2*>(gg + e * C), it.v);
+            ngp_half2* p = reinterpret_cast<ngp_half2*>(gg + e * C);
+            if (nonfinite) {  // the returning atomic: the entry's new value is checked
+                const ngp_half2 o = __builtin_amdgcn_global_atomic_fadd_v2f16(p, it.v);
+                if (!half2_sum_finite(o, it.v)) atomicOr(nonfinite, 1);
+            } else {
+                __builtin_amdgcn_global_atomic_fadd_v2f16(p, it.v);
+            }
         }
     }
 }
@@ -756,7 +770,7 @@ constexpr uint32_t kAccThreads = 512, kAccBatch = 16, kRetireGroups = 16;
 __global__ void __launch_bounds__(kAccThreads)
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
-                 const BinItem* __restrict__ items) {
+                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     __shared__ unsigned long long acc[kBinEntries * C];
     __shared__ uint32_t wsum[NW];
@@ -928,6 +942,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         if (__ballot(bad)) s_bad = 1;  // benign race: every writer stores 1
         lds_barrier();
         const float q24 = 1.0f / 16777216.0f;
+        bool inf_out = false;  // a stored grad is inf/nan (GradScaler's check, when `nonfinite` is given)
         if (cur.owner) {  // groups of 4 entries = 16 bytes of the table
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j) {
@@ -946,23 +961,40 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
                     const ngp_half2 o = __builtin_bit_cast(ngp_half2, w4[q]);
-                    w4[q] = __builtin_bit_cast(uint32_t, ngp_half2{(ngp_half)((float)o[0] + a[2 * q]),
-                                                                   (ngp_half)((float)o[1] + a[2 * q + 1])});
+                    const ngp_half2 n{(ngp_half)((float)o[0] + a[2 * q]), (ngp_half)((float)o[1] + a[2 * q + 1])};
+                    inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
+                    w4[q] = __builtin_bit_cast(uint32_t, n);
                 }
                 reinterpret_cast<uint4*>(cur.tbl)[g] = uint4{w4[0], w4[1], w4[2], w4[3]};
             }
         } else {
             for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
                 const int64_t x0 = (int64_t)acc[e * C], x1 = (int64_t)acc[e * C + 1];
-                if (x0 != 0 || x1 != 0)
-                    __builtin_amdgcn_global_atomic_fadd_v2f16(
-                        cur.tbl + e, ngp_half2{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)});
+                if (x0 == 0 && x1 == 0) continue;
+                const ngp_half2 v{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
+                if (nonfinite) {  // the returning atomic: the entry's new value is checked
+                    const ngp_half2 o = __builtin_amdgcn_global_atomic_fadd_v2f16(cur.tbl + e, v);
+                    inf_out |= !half2_sum_finite(o, v);
+                } else {
+                    __builtin_amdgcn_global_atomic_fadd_v2f16(cur.tbl + e, v);
+                }
             }
         }
         if (s_bad && t == 0) cur.tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
+        if (nonfinite && (__ballot(inf_out) != 0 || s_bad) && (t & 63) == 0) atomicOr(nonfinite, 1);
         lds_barrier();  // the image is rezeroed by the next unit
         cur = nxt;
     }
+}
+
+// GradScaler's inf/nan check over a grad range (levels the binned path does
+// not cover): sets *flag.
+__global__ void __launch_bounds__(256)
+k_flag_nonfinite(const ngp_half* __restrict__ g, size_t n, int32_t* __restrict__ flag) {
+    bool bad = false;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        bad |= !__builtin_isfinite((float)g[i]);
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
 // Host-side plan from a host copy of the offsets. Bins of hashed levels get
@@ -1331,11 +1363,13 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
                                               uint32_t gridtype, int32_t align_corners,
                                               uint32_t interp, const int32_t* offsets_host,
                                               void* workspace, size_t workspace_bytes, int32_t grad_layout,
-                                              void* stream) {
+                                              int32_t* nonfinite, void* stream) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
     NGP_REQUIRE(grad_layout == 0 || grad_layout == 1, NGP_ERR_ARG,
                 "grid_encode_backward_fused: grad_layout 0 ([L,B,C]) or 1 ([B,L*C])");
     NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_backward_fused: null xyz or bound <= 0");
+    NGP_REQUIRE(!nonfinite || offsets_host, NGP_ERR_ARG,
+                "grid_encode_backward_fused: the nonfinite check needs offsets_host");
     if (B == 0) return NGP_OK;
     GridLevels lv;
     make_levels(lv, L, S, H);
@@ -1357,9 +1391,9 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
         const dim3 grid(ngp_div_up(B, kBinPts), bp.nlev);
         k_grid_bwd_bin<3><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
             (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, im,
-            bp, cursor, items, grad_layout);
+            bp, cursor, items, grad_layout, nonfinite);
         k_grid_bin_accum<<<2 * ngp_num_cus(), kAccThreads, (2 * bp.total_bins + 1) * sizeof(uint32_t), st>>>(
-            offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items);
+            offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
@@ -1367,8 +1401,14 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
             k_grid_bwd<ngp_half, 3, 2><<<grid, 256, 0, st>>>((const ngp_half*)grad, xyz, offsets,
                 (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, grad_layout, im, bp.nlev);
         } else {
-            return bwd_t<ngp_half>(grad, xyz, offsets, grad_embeddings, B, D, C, L, lv, nullptr, nullptr,
-                                   gridtype, ac, interp, grad_layout, st, im);
+            if (int e = bwd_t<ngp_half>(grad, xyz, offsets, grad_embeddings, B, D, C, L, lv, nullptr, nullptr,
+                                        gridtype, ac, interp, grad_layout, st, im))
+                return e;
+        }
+        if (nonfinite) {  // those levels' atomics are not checked: scan their grads
+            const size_t e0 = (size_t)offsets_host[bp.nlev] * C, e1 = (size_t)offsets_host[L] * C;
+            const uint32_t blocks = (uint32_t)std::min<size_t>(ngp_div_up(e1 - e0, 256), 4096);
+            k_flag_nonfinite<<<blocks, 256, 0, st>>>((const ngp_half*)grad_embeddings + e0, e1 - e0, nonfinite);
         }
     }
     return ngp_check_launch("grid_encode_backward_fused");

@@ -740,7 +740,7 @@ int optimizer_launch(int32_t n_tensors, float* const* params, void* const* grads
                     NGP_ERR_ARG, "fused_optimizer_step: half shadow %d misaligned", k);
     const TensorList tl = make_list(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes);
     const uint64_t total = tl.start[n_tensors];
-    if (scaler_enabled)
+    if (scaler_enabled == NGP_SCALER_SCAN)
         k_nonfinite<<<sweep_blocks(total, 8), 256, 0, s>>>(tl, st);
     AdamArgs aa{lr, beta1, beta2, eps, iters, zero_grads, grad_mult, defer_end ? 1 : 0};
     const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
@@ -879,11 +879,16 @@ extern "C" int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32
     NGP_REQUIRE(grad_half && state, NGP_ERR_ARG, "grad_guard: null buffer");
     NGP_REQUIRE(n % 8 == 0 && (reinterpret_cast<uintptr_t>(grad_half) & 15) == 0, NGP_ERR_ARG,
                 "grad_guard: gradient must be 16-byte aligned with a multiple of 8 elements");
-    NGP_REQUIRE(world >= 1 && (uint64_t)world * chunk <= n, NGP_ERR_ARG,
+    NGP_REQUIRE(world >= 1 && (n == 0 || (uint64_t)world * chunk <= n), NGP_ERR_ARG,
                 "grad_guard: world * chunk exceeds the gradient");
     hipStream_t s = ngp_stream(stream);
     StepState* st = static_cast<StepState*>(state);
     if (n) k_guard_scan<<<sweep_blocks(n, 8), 256, 0, s>>>(static_cast<const ngp_half*>(grad_half), n / 8, st);
     k_guard_poison<<<1, 64, 0, s>>>(static_cast<ngp_half*>(grad_half), chunk, world, st);
     return ngp_check_launch("grad_guard");
+}
+
+extern "C" int32_t* ngp_fused_inf_flag(void* state, int32_t local) {
+    StepState* st = static_cast<StepState*>(state);
+    return st ? (local ? &st->local_inf : &st->found_inf) : nullptr;
 }

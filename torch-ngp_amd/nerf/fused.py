@@ -42,6 +42,7 @@ from .provider import LEGO_BOXES, LEGO_COLORS
 _F16 = nat.DTYPE_CODE[torch.float16]
 _RELU, _NONE = 0, 6
 _DEFER, _GEO, _PAIR = 1, 2, 4  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO, NGP_FFMLP_PAIR_MAJOR
+_SCAN, _PRECHECKED = 1, 2  # NGP_SCALER_SCAN, NGP_SCALER_PRECHECKED
 
 
 def _vp_array(ptrs):
@@ -169,6 +170,10 @@ class FusedTrainer:
             half=_vp_array([nat.ptr(self.flat_half) + 2 * self.lo]),
             sizes=(ctypes.c_uint64 * 1)(chunk))
         self._nccl = W > 1 and dist.get_backend() == "nccl"
+        # GradScaler's inf check is made by the kernels that write the grads
+        # (grid backward, MLP dW reduce) into this flag: the optimizer's found-inf
+        # flag (world 1) or the data-parallel guard's per-rank flag
+        self._inf_flag = nat.lib().ngp_fused_inf_flag(nat.ptr(self.state), int(W > 1))
         self.graph = None
         self._events = None
         self._pending = False  # gradients of the last forward/backward not yet applied
@@ -245,7 +250,8 @@ class FusedTrainer:
     def _reduce(self):
         if self.world == 1:
             return
-        nat.check(nat.lib().ngp_grad_guard(nat.ptr(self.flat_grad), self.total, self.chunk, self.world,
+        # the backward's kernels set the per-rank flag: no scan (n = 0)
+        nat.check(nat.lib().ngp_grad_guard(nat.ptr(self.flat_grad), 0, self.chunk, self.world,
                                            nat.ptr(self.state), nat.stream_of(self.flat_grad)), "grad_guard")
         if self._nccl:
             dist.reduce_scatter_tensor(self.grad_shard, self.flat_grad, op=dist.ReduceOp.AVG)
@@ -351,12 +357,13 @@ class FusedTrainer:
                                         _DEFER | _PAIR, P(self.mlp_ws[0]), self.mlp_ws[0].numel(), s),
             "sigma_mlp_backward")
         self._tick("ffmlp_backward_sigma")
-        chk(lib.ngp_ffmlp_reduce(2, pk["ws"], pk["B"], pk["ins"], pk["hid"], pk["nl"], pk["gw"], _F16, s),
+        chk(lib.ngp_ffmlp_reduce(2, pk["ws"], pk["B"], pk["ins"], pk["hid"], pk["nl"], pk["gw"], _F16,
+                                 self._inf_flag, s),
             "ffmlp_reduce")
         self._tick("ffmlp_reduce")
         chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
                                                P(self.grads[0]), M, cnt, *grid_args[:-1], self._offsets_host,
-                                               P(self.grid_ws), self.grid_ws.numel(), 0, s),
+                                               P(self.grid_ws), self.grid_ws.numel(), 0, self._inf_flag, s),
             "grid_backward_fused")
         self._tick("grid_encode_backward")
 
@@ -370,10 +377,13 @@ class FusedTrainer:
         # output and the flat gradient is cleared after the collective read it
         args = (1, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
                 self.betas[1], self.eps, self.iters, int(self.world == 1), 1.0)
+        # inside a step (world 1) the found-inf flag was set by the backward's kernels;
+        # otherwise (flush, direct calls, the averaged shard) the grads are swept
+        mode = _PRECHECKED if defer and self.world == 1 else _SCAN
         if defer:
-            chk(lib.ngp_fused_optimizer_update(*args, 1, P(self.state), s), "fused_optimizer_update")
+            chk(lib.ngp_fused_optimizer_update(*args, mode, P(self.state), s), "fused_optimizer_update")
         else:
-            chk(lib.ngp_fused_optimizer_step(*args, 2.0, 0.5, self.growth_interval, 1, N, cnt, None,
+            chk(lib.ngp_fused_optimizer_step(*args, 2.0, 0.5, self.growth_interval, mode, N, cnt, None,
                                              P(self.loss_ray), P(self.state), s), "fused_optimizer_step")
         self._tick("optimizer")
 
