@@ -292,10 +292,12 @@ NGP_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds_waves, uint32_t&
 // Three kernels, all deterministic:
 //   k_march_train  one WAVE per ray (below): the t of every occupied sample goes
 //                  to the workspace row ts[n][0..count), rays[n] = (n, -, count)
-//   k_march_scan   one workgroup: exclusive scan of the counts in ray order ->
-//                  rays[n].offset, counter
-//   k_march_emit   per SAMPLE (flat, balanced): xyzs/dirs/deltas recomputed
-//                  from the recorded t with the reference's exact float ops
+//   k_march_emit   per SAMPLE (flat, balanced): each workgroup forms its ray
+//                  group's offsets itself (counts of all earlier rays + an
+//                  in-group scan: an exclusive scan in ray order, no separate
+//                  scan launch), writes rays[n].offset and counter, then
+//                  xyzs/dirs/deltas recomputed from the recorded t with the
+//                  reference's exact float ops
 //
 // Why one wave per ray. Marching is a serial recurrence on t: ~150-500 probes
 // per Lego ray, ~130 dependent VALU each. One lane per ray gives 64 waves for
@@ -577,8 +579,12 @@ __global__ void __launch_bounds__(kSegThreads)
 k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
               const uint8_t* __restrict__ grid, const uint8_t* __restrict__ img, OccLayout L,
               MarchConst k, uint32_t N, const float* __restrict__ nears, const float* __restrict__ fars,
-              const float* __restrict__ noises, int32_t* __restrict__ rays, float* __restrict__ ts) {
+              const float* __restrict__ noises, int32_t* __restrict__ rays, float* __restrict__ ts,
+              const int32_t* __restrict__ counter, uint32_t* __restrict__ scan) {
     extern __shared__ uint4 dyn[];
+    // scan[0] = the offset of the first sample (the reference's counter[0] on entry,
+    // raymarching.cu:405); scan[4 + n] = ray n's count (read by k_march_emit)
+    if (blockIdx.x == 0 && threadIdx.x == 0) scan[0] = (uint32_t)counter[0];
     uint32_t* sum = reinterpret_cast<uint32_t*>(dyn);
     uint32_t* pre = sum + 4 * L.ngroups;
     const bool lds = L.ngroups > 0 && load_occ_index(img, L, dyn);
@@ -601,58 +607,48 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
         if ((threadIdx.x & 63) == 0) {
             rays[n * 3 + 0] = (int32_t)n;
             rays[n * 3 + 2] = (int32_t)cnt;
+            scan[4 + n] = cnt;
         }
     }
 }
 
-// One workgroup: exclusive scan of the per-ray counts in ray order (4 rays per
-// thread per round), then counter[0] += total, counter[1] += N.
-__global__ void __launch_bounds__(1024)
-k_march_scan(int32_t* __restrict__ rays, uint32_t N, int32_t* counter) {
-    __shared__ uint32_t lds_waves[1024 / 64];
-    uint32_t carry = (uint32_t)counter[0];
-    for (uint32_t base = 0; base < N; base += 4096) {
-        const uint32_t i0 = base + 4 * threadIdx.x;
-        uint32_t v[4], local = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            v[j] = i0 + j < N ? (uint32_t)rays[(size_t)(i0 + j) * 3 + 2] : 0u;
-            local += v[j];
-        }
-        uint32_t total;
-        uint32_t run = carry + block_exclusive_scan<1024>(local, lds_waves, total);
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            if (i0 + j < N) rays[(size_t)(i0 + j) * 3 + 1] = (int32_t)run;
-            run += v[j];
-        }
-        carry += total;
-    }
-    if (threadIdx.x == 0) {
-        counter[0] = (int32_t)carry;
-        counter[1] += (int32_t)N;
-    }
-}
-
-// Grid (ray groups of 256, kEmitSplit): each workgroup loads its group's
-// offsets and writes its 1/kEmitSplit slice of the group's samples. Outputs
-// of rays with offset + count > M are skipped (reference :416).
+// Grid (ray groups of 256, kEmitSplit): each workgroup sums the counts of all
+// rays before its group (a few thousand coalesced L2 reads), scans the
+// group's counts, and writes its 1/kEmitSplit slice of the group's samples;
+// the y == 0 workgroup of each group also writes the group's offsets, and the
+// last group's the counter (counter[0] = end, counter[1] += N, the
+// reference's two atomics :405-406). Outputs of rays with offset + count > M
+// are skipped (reference :416).
 __global__ void __launch_bounds__(kMarchThreads)
 k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d, MarchConst k,
              uint32_t N, uint32_t M, const float* __restrict__ nears, const float* __restrict__ noises,
              const float* __restrict__ ts, float* __restrict__ xyzs, float* __restrict__ dirs,
-             float* __restrict__ deltas, const int32_t* __restrict__ rays) {
+             float* __restrict__ deltas, int32_t* __restrict__ rays, const uint32_t* __restrict__ scan,
+             int32_t* __restrict__ counter) {
     __shared__ uint32_t off[kMarchThreads + 1];
+    __shared__ uint32_t lds_waves[kMarchThreads / 64];
+    const uint32_t* __restrict__ counts = scan + 4;
     const uint32_t n0 = blockIdx.x * kMarchThreads;
-    const uint32_t nlast = min(N, n0 + kMarchThreads) - 1;
-    const uint32_t base = (uint32_t)rays[(size_t)n0 * 3 + 1];
-    const uint32_t end = (uint32_t)rays[(size_t)nlast * 3 + 1] + (uint32_t)rays[(size_t)nlast * 3 + 2];
+    uint32_t part = 0;
+    for (uint32_t i = threadIdx.x; i < n0; i += kMarchThreads) part += counts[i];
+    uint32_t before;
+    block_exclusive_scan<kMarchThreads>(part, lds_waves, before);
+    const uint32_t base = scan[0] + before;
     const uint32_t n = n0 + threadIdx.x;
-    off[threadIdx.x] = n < N ? (uint32_t)rays[(size_t)n * 3 + 1] - base : end - base;
-    if (threadIdx.x == 0) off[kMarchThreads] = end - base;
+    const uint32_t c = n < N ? counts[n] : 0u;
+    uint32_t total;
+    const uint32_t excl = block_exclusive_scan<kMarchThreads>(c, lds_waves, total);
+    off[threadIdx.x] = excl;
+    if (threadIdx.x == 0) off[kMarchThreads] = total;
+    if (blockIdx.y == 0) {
+        if (n < N) rays[(size_t)n * 3 + 1] = (int32_t)(base + excl);
+        if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+            counter[0] = (int32_t)(base + total);
+            counter[1] += (int32_t)N;
+        }
+    }
     __syncthreads();
 
-    const uint32_t total = end - base;
     const uint32_t chunk = ngp_div_up(total, kEmitSplit);
     const uint32_t j0 = blockIdx.y * chunk, j1 = min(total, j0 + chunk);
     for (uint32_t j = j0 + threadIdx.x; j < j1; j += kMarchThreads) {
@@ -963,16 +959,17 @@ extern "C" int ngp_packbits(const float* grid, uint32_t N, float density_thresh,
     return ngp_check_launch("packbits");
 }
 
-// workspace = [t scratch: N * max_steps floats][occupancy image]
+// workspace = [t scratch: N * max_steps floats][scan: base + N counts][occupancy image][its build scratch]
 static size_t march_ts_bytes(uint32_t N, uint32_t max_steps) {
     return ((size_t)N * max_steps * sizeof(float) + 255) / 256 * 256;
 }
+static size_t march_scan_bytes(uint32_t N) { return ((size_t)(N + 4) * sizeof(uint32_t) + 255) / 256 * 256; }
 
 extern "C" size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_steps, uint32_t C,
                                                         uint32_t H) {
     // the image size does not depend on the grid pointer's alignment
     OccLayout L = occ_layout(nullptr, C, H);
-    return march_ts_bytes(N, max_steps) + occ_image_bytes(L) + occ_scratch_bytes(L);
+    return march_ts_bytes(N, max_steps) + march_scan_bytes(N) + occ_image_bytes(L) + occ_scratch_bytes(L);
 }
 
 static int march_train_impl(const float* rays_o, const float* rays_d, const uint8_t* grid,
@@ -996,7 +993,8 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
     const uint32_t wgs = ngp_div_up(N, kSegWaves);
     const uint32_t blocks = wgs < kMaxMarchBlocks ? wgs : kMaxMarchBlocks;
     float* ts = static_cast<float*>(workspace);
-    uint8_t* img = static_cast<uint8_t*>(workspace) + march_ts_bytes(N, max_steps);
+    uint32_t* scan = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + march_ts_bytes(N, max_steps));
+    uint8_t* img = reinterpret_cast<uint8_t*>(scan) + march_scan_bytes(N);
     if (L.ngroups && build_image) {
         uint32_t* cnt = reinterpret_cast<uint32_t*>(img + occ_image_bytes(L));
         const uint32_t wg = ngp_div_up(L.ngroups, kBuildThreads);
@@ -1004,10 +1002,9 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
         k_occ_compact<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
     }
     k_march_train<<<blocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
-        rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts);
-    k_march_scan<<<1, 1024, 0, st>>>(rays, N, counter);
+        rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan);
     k_march_emit<<<dim3(groups, kEmitSplit), kMarchThreads, 0, st>>>(rays_o, rays_d, k, N, M, nears, noises,
-                                                                    ts, xyzs, dirs, deltas, rays);
+                                                                    ts, xyzs, dirs, deltas, rays, scan, counter);
     return ngp_check_launch("march_rays_train");
 }
 
@@ -1032,7 +1029,7 @@ extern "C" int ngp_march_occupancy_build(const uint8_t* grid, uint32_t C, uint32
     const OccLayout L = occ_layout(grid, C, H);
     if (!L.ngroups) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
-    uint8_t* img = static_cast<uint8_t*>(workspace) + march_ts_bytes(N, max_steps);
+    uint8_t* img = static_cast<uint8_t*>(workspace) + march_ts_bytes(N, max_steps) + march_scan_bytes(N);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(img + occ_image_bytes(L));
     const uint32_t wg = ngp_div_up(L.ngroups, kBuildThreads);
     k_occ_count<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
