@@ -240,6 +240,10 @@ int ngp_grid_encode_forward_fused(const float* xyz, float bound, const void* emb
 size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
                                                       float S, uint32_t H, int32_t align_corners,
                                                       const int32_t* offsets_host);
+/* grad_layout | NGP_GRID_GRAD_ZEROED: grad_embeddings is all zeros on entry
+ * (the fused optimizer clears it), so bins that own their table slice store
+ * their sums instead of reading the slice back first. */
+#define NGP_GRID_GRAD_ZEROED 0x10
 int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
                                    const int32_t* offsets, void* grad_embeddings, uint32_t B,
                                    const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,

@@ -53,7 +53,8 @@ def _normalise(w, bound):
     return ((w + np.float32(bound)) * np.float32(1.0 / (2.0 * bound))).astype(np.float32)
 
 
-def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, reps=1, layout=1, flag=None):
+def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, reps=1, layout=1, flag=None,
+         zeroed=False):
     B = w.shape[0]
     S = float(np.float32(np.log2(scale)))
     offs_host = np.ascontiguousarray(offs, dtype=np.int32)
@@ -70,7 +71,7 @@ def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, rep
         nat.check(nat.lib().ngp_grid_encode_backward_fused(
             nat.ptr(gt), nat.ptr(wt), float(bound), nat.ptr(ot), nat.ptr(table), B,
             nat.ptr(cnt) if cnt is not None else None, 3, 2, L, S, H, 0, 0, 0, hp,
-            nat.ptr(ws), ws.numel(), layout, nat.ptr(flag) if flag is not None else None,
+            nat.ptr(ws), ws.numel(), layout | (0x10 if zeroed else 0), nat.ptr(flag) if flag is not None else None,
             nat.stream_of(table)), "grid_backward_fused")
     torch.cuda.synchronize()
     # the workspace's counters are left zeroed for the next call
@@ -110,7 +111,7 @@ def test_grid_backward_fused_vs_oracle(cuda, case):
     rng = np.random.default_rng(7)
     g16 = (rng.standard_normal((B, L * 2)) * 0.5).astype(np.float16)
     flag = torch.zeros(1, dtype=torch.int32, device=cuda)
-    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, bound, flag=flag)
+    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, bound, flag=flag, zeroed=True)  # fresh table
     assert int(flag.item()) == 0  # finite grads: GradScaler's check stays clear
     x = _normalise(w, bound)
     ref = oracle.grid_encode_backward(g16, x, offs, 2, scale, H)
@@ -127,7 +128,7 @@ def test_grid_backward_fused_bin_overflow(cuda):
     offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
     w = _world(B, 1.0, seed=4, concentrated=0.03)
     g16 = (np.random.default_rng(9).standard_normal((B, L * 2)) * 0.5).astype(np.float16)
-    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, 1.0)
+    got = _bwd(nat, cuda, g16, w, offs, L, H, scale, 1.0, zeroed=True)  # overflowed bins still read back
     ref = oracle.grid_encode_backward(g16, _normalise(w, 1.0), offs, 2, scale, H)
     _check_levels(got, ref, offs, "overflow", rtol=2e-2, mtol=4e-2)
 

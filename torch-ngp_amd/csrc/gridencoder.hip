@@ -770,7 +770,7 @@ constexpr uint32_t kAccThreads = 512, kAccBatch = 16, kRetireGroups = 16;
 __global__ void __launch_bounds__(kAccThreads)
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
-                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite) {
+                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite, bool zeroed) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     __shared__ unsigned long long acc[kBinEntries * C];
     __shared__ uint32_t wsum[NW];
@@ -808,8 +808,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         if (b >= nbins) break;
         while (level + 1 < nlev && b >= s_bin0[level + 1]) ++level;
         const uint32_t n = min(cursor[b], s_cap[level]);
-        bn[b] = n;
-        upre[b] = (n + kSegItems - 1) / kSegItems;
+        bn[b] = n | (cursor[b] > s_cap[level] ? 0x80000000u : 0u);  // top bit: items went atomic
+        upre[b] = (n + kSegItems - 1) / kSegItems;  // n: the clipped count
         mine += upre[b];
     }
     uint32_t incl = mine;
@@ -860,7 +860,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // unit does its LDS adds and writes), hiding the memory latency.
     struct Unit {
         uint32_t level, lbin, s0, s1;
-        bool owner;
+        bool owner, fresh;  // fresh: the table slice is known to be zero (no read-modify-write)
         const uint64_t* src;
         ngp_half2* tbl;
         uint32_t ne;
@@ -874,10 +874,11 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         Unit r;
         const uint32_t gb = lo, seg = u - upre[gb];
         r.owner = upre[gb + 1] - upre[gb] == 1;
+        r.fresh = r.owner && zeroed && (bn[gb] >> 31) == 0;
         r.level = level_of(gb);
         r.lbin = gb - s_bin0[r.level];
         r.s0 = seg * kSegItems;
-        r.s1 = min(bn[gb], r.s0 + kSegItems);
+        r.s1 = min(bn[gb] & 0x7fffffffu, r.s0 + kSegItems);
         r.src = reinterpret_cast<const uint64_t*>(items + s_item0[r.level] + (size_t)r.lbin * s_cap[r.level]);
         const uint32_t off0 = s_off[r.level];
         const uint32_t hs = s_off[r.level + 1] - off0;
@@ -898,7 +899,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
             const uint32_t g = j * kAccThreads + t;
-            if (w.owner && 4 * g < w.ne) old[j] = reinterpret_cast<const uint4*>(w.tbl)[g];
+            if (w.owner && 4 * g < w.ne)
+                old[j] = w.fresh ? uint4{0u, 0u, 0u, 0u} : reinterpret_cast<const uint4*>(w.tbl)[g];
         }
     };
     uint64_t it[kAccBatch];
@@ -1365,6 +1367,8 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
                                               void* workspace, size_t workspace_bytes, int32_t grad_layout,
                                               int32_t* nonfinite, void* stream) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
+    const bool zeroed = (grad_layout & NGP_GRID_GRAD_ZEROED) != 0;
+    grad_layout &= ~NGP_GRID_GRAD_ZEROED;
     NGP_REQUIRE(grad_layout == 0 || grad_layout == 1, NGP_ERR_ARG,
                 "grid_encode_backward_fused: grad_layout 0 ([L,B,C]) or 1 ([B,L*C])");
     NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_backward_fused: null xyz or bound <= 0");
@@ -1393,7 +1397,7 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
             (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, im,
             bp, cursor, items, grad_layout, nonfinite);
         k_grid_bin_accum<<<2 * ngp_num_cus(), kAccThreads, (2 * bp.total_bins + 1) * sizeof(uint32_t), st>>>(
-            offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite);
+            offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, zeroed);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {

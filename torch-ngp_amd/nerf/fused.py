@@ -43,6 +43,7 @@ _F16 = nat.DTYPE_CODE[torch.float16]
 _RELU, _NONE = 0, 6
 _DEFER, _GEO, _PAIR = 1, 2, 4  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO, NGP_FFMLP_PAIR_MAJOR
 _SCAN, _PRECHECKED = 1, 2  # NGP_SCALER_SCAN, NGP_SCALER_PRECHECKED
+_ZEROED = 0x10  # NGP_GRID_GRAD_ZEROED: grad layout 0 ([L,M,2]) on a table grad the optimizer cleared
 
 
 def _vp_array(ptrs):
@@ -363,7 +364,7 @@ class FusedTrainer:
         self._tick("ffmlp_reduce")
         chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
                                                P(self.grads[0]), M, cnt, *grid_args[:-1], self._offsets_host,
-                                               P(self.grid_ws), self.grid_ws.numel(), 0, self._inf_flag, s),
+                                               P(self.grid_ws), self.grid_ws.numel(), _ZEROED, self._inf_flag, s),
             "grid_backward_fused")
         self._tick("grid_encode_backward")
 
