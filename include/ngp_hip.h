@@ -244,6 +244,14 @@ size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, ui
  * (the fused optimizer clears it), so bins that own their table slice store
  * their sums instead of reading the slice back first. */
 #define NGP_GRID_GRAD_ZEROED 0x10
+/* grad_layout | NGP_GRID_CURSORS_EXTERNAL: the caller zeroes the workspace's
+ * first ngp_grid_encode_backward_fused_counter_bytes bytes (the bin cursors)
+ * between calls (the fused step's head kernel does), so the call does not
+ * leave them zeroed itself. */
+#define NGP_GRID_CURSORS_EXTERNAL 0x20
+size_t ngp_grid_encode_backward_fused_counter_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S,
+                                                    uint32_t H, int32_t align_corners,
+                                                    const int32_t* offsets_host);
 int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
                                    const int32_t* offsets, void* grad_embeddings, uint32_t B,
                                    const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
@@ -347,7 +355,8 @@ int ngp_fused_optimizer_update(int32_t n_tensors, float* const* params, void* co
  * pending bookkeeping of the last ngp_fused_optimizer_update if any (scaler
  * arguments as ngp_fused_optimizer_step; loss_ray holds the previous batch's
  * per-ray losses, N rays), and ngp_ffmlp_pack of n_nets networks (n_nets may
- * be 0), as disjoint block ranges of one kernel. */
+ * be 0), as disjoint block ranges of one kernel; it also zeroes clear_bytes
+ * (a multiple of 16) at clear (nullable: the grid backward's bin cursors). */
 int ngp_fused_step_head(const float* poses, uint32_t n_poses, const float* intrinsics4, uint32_t H,
                         uint32_t W, uint32_t N, const float* boxes, int32_t nboxes, const float* aabb6,
                         float min_near, uint32_t seed, void* state, float* rays_o, float* rays_d,
@@ -356,7 +365,7 @@ int ngp_fused_step_head(const float* poses, uint32_t n_poses, const float* intri
                         int32_t growth_interval, int32_t scaler_enabled, const float* loss_ray,
                         int32_t n_nets, const void* const* mlp_weights, const uint32_t* in_dims,
                         const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* images,
-                        void* stream);
+                        void* clear, uint32_t clear_bytes, void* stream);
 
 /* Data-parallel GradScaler guard for the sharded optimizer (nerf/fused.py,
  * world > 1), run on each rank's own fp16 gradient before the averaging

@@ -1,0 +1,64 @@
+"""Phase clocks of the grid accumulate kernel (diagnostic build with
+-DNGP_STAMPS, built by this script's caller into torch-ngp_amd/dbg/):
+runs fused steps, then one grid backward, and summarises the per-workgroup
+s_memtime stamps (step 1 / retire / per unit: zero, adds, flush).
+    NGP_HIP_LIB=torch-ngp_amd/dbg/libngp_hip_stamps.so python tools/accum_stamps.py"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "torch-ngp_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import _ngp_native as nat  # noqa: E402
+from nerf.fused import FusedTrainer  # noqa: E402
+from nerf.network_ff import NeRFNetwork  # noqa: E402
+from nerf.provider import SyntheticLego, lego_bitfield  # noqa: E402
+
+dev = torch.device("cuda:0")
+torch.manual_seed(0)
+model = NeRFNetwork(bound=1, cuda_ray=True).to(dev)
+model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
+ft = FusedTrainer(model, SyntheticLego(dev, num_rays=4096), M=101762)
+stamps = torch.zeros(4096 * 64, dtype=torch.int64, device=dev)
+lib = nat.lib()
+assert lib.ngp_debug_stamps(ctypes.c_void_p(nat.ptr(stamps))) == 0
+for _ in range(12):
+    ft.step()
+torch.cuda.synchronize()
+st = stamps.view(-1, 64).cpu().numpy().astype(np.int64)
+nwg = int((st[:, 0] > 0).sum())
+st = st[:nwg]
+t0 = st[:, 0].min()
+res = {"workgroups": nwg, "kernel_cycles": int(max(st[i, 4 + 5 * (int(st[i, 3]) - 1) + 2] if st[i, 3] else st[i, 2]
+                                                    for i in range(nwg)) - t0)}
+res["entry_spread"] = int(st[:, 0].max() - t0)
+res["step1_med"] = int(np.median(st[:, 1] - st[:, 0]))
+res["retire_med"] = int(np.median(st[:, 2] - st[:, 1]))
+res["retire_max"] = int(np.max(st[:, 2] - st[:, 1]))
+units = []
+for i in range(nwg):
+    prev = st[i, 2]
+    for u in range(int(min(st[i, 3], 11))):
+        a, b, c, info = st[i, 4 + 5 * u: 8 + 5 * u]
+        units.append((a - prev, b - a, c - b, info & 0xffffffff, (info >> 32) & 0xff, (info >> 40) & 0xff))
+        prev = c
+u = np.array(units, dtype=np.int64)
+res["units"] = len(u)
+res["units_per_wg_max"] = int(st[:, 3].max())
+for k, name in enumerate(["gap_to_start", "adds", "flush"]):
+    res[name + "_med"] = int(np.median(u[:, k]))
+    res[name + "_p90"] = int(np.percentile(u[:, k], 90))
+    res[name + "_sum_per_wg"] = int(u[:, k].sum() / nwg)
+res["items_med"] = int(np.median(u[:, 3]))
+res["owner_frac"] = float(u[:, 4].mean())
+by_level = {}
+for lv in np.unique(u[:, 5]):
+    m = u[:, 5] == lv
+    by_level[int(lv)] = {"units": int(m.sum()), "items_med": int(np.median(u[m, 3])),
+                         "adds_med": int(np.median(u[m, 1])), "flush_med": int(np.median(u[m, 2]))}
+res["by_level"] = by_level
+print(json.dumps(res, indent=1))

@@ -73,11 +73,12 @@ SIGNATURES = {
     "ngp_ffmlp_image_bytes": [c_u32, c_u32, c_u32],
     "ngp_grad_guard": [c_vp, ctypes.c_uint64, ctypes.c_uint64, c_i32, c_vp, c_vp],
     "ngp_fused_inf_flag": [c_vp, c_i32],
+    "ngp_grid_encode_backward_fused_counter_bytes": [c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32, c_vp],
     "ngp_fused_optimizer_update": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
                                    c_i32, c_i32, c_f32, c_i32, c_vp, c_vp],
     "ngp_fused_step_head": [c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32, c_vp,
                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_i32, c_i32,
-                            c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+                            c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp],
     "ngp_ffmlp_pack": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_ffmlp_forward_rows": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
                                c_vp, c_vp],
@@ -101,6 +102,7 @@ SIGNATURES = {
 _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,
     "ngp_fused_inf_flag": c_vp,
+    "ngp_grid_encode_backward_fused_counter_bytes": c_sz,
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
     "ngp_march_rays_train_workspace_bytes": c_sz,
     "ngp_fused_state_bytes": c_sz,

@@ -766,17 +766,25 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // (inf / NaN: fp16 overflow under the loss scale) cannot be carried by the
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
+#ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-workgroup phase clocks
+__device__ unsigned long long* g_stamps;
+#define STAMP(slot, v) do { if (threadIdx.x == 0) g_stamps[blockIdx.x * 64 + (slot)] = (v); } while (0)
+#else
+#define STAMP(slot, v) do { } while (0)
+#endif
 constexpr uint32_t kAccThreads = 512, kAccBatch = 16, kRetireGroups = 16;
 __global__ void __launch_bounds__(kAccThreads)
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
-                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite, bool zeroed) {
+                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite, bool zeroed,
+                 bool external) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
-    __shared__ unsigned long long acc[kBinEntries * C];
+    __shared__ __attribute__((aligned(16))) unsigned long long acc[kBinEntries * C];
     __shared__ uint32_t wsum[NW];
     __shared__ uint32_t s_last, s_bad;
     extern __shared__ uint32_t dyn[];
     const uint32_t nbins = bp.total_bins;
+    STAMP(0, __builtin_amdgcn_s_memtime());
     uint32_t* upre = dyn;              // [nbins + 1] first unit of each bin
     uint32_t* bn = dyn + nbins + 1;    // [nbins] items of each bin (clipped at its capacity)
     // the plan's per-level arrays, indexed per lane below: kernel arguments
@@ -834,11 +842,15 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         run += u;
     }
     if (t == 0) upre[nbins] = total;
+    STAMP(1, __builtin_amdgcn_s_memtime());
     // 2. retire: once every workgroup holds the counts, the last one zeroes
     // them for the next step. Two-level counter (kRetireGroups group counters,
     // then one), so no address takes more than ~gridDim / kRetireGroups
-    // atomics: 512 workgroups through one counter cost ~10 us.
-    if (t == 0) {
+    // atomics: 512 workgroups through one counter cost ~10 us; this one still
+    // ~7 us (phase clocks, tools/accum_stamps.py), so a caller that clears the
+    // counters itself (NGP_GRID_CURSORS_EXTERNAL: the fused step's head
+    // kernel) skips it.
+    if (!external && t == 0) {
         __threadfence();
         const uint32_t grp = blockIdx.x % kRetireGroups;
         const uint32_t members = gridDim.x / kRetireGroups + (grp < gridDim.x % kRetireGroups ? 1u : 0u);
@@ -850,10 +862,12 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         }
     }
     __syncthreads();
-    if (s_last) {
+    if (!external && s_last) {
         for (uint32_t b = t; b < nbins; b += kAccThreads) cursor[b] = 0;
         if (t == 0) retire[0] = 0;
     }
+    STAMP(2, __builtin_amdgcn_s_memtime());
+    uint32_t nstamp = 0;
 
     // 3. units. The first item batch of a unit and, for a single-owner unit,
     // its slice of the table are loaded one unit ahead (while the previous
@@ -887,7 +901,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         r.tbl = reinterpret_cast<ngp_half2*>(grad_grid + ((size_t)off0 + e0) * C);
         return r;
     };
-    constexpr uint32_t G = kBinEntries / 4 / kAccThreads;  // 16-byte table groups per thread
+    constexpr uint32_t G = kBinEntries / kAccThreads;  // table entries per thread (flush)
     auto load_batch = [&](const Unit& w, uint32_t k0, uint64_t (&it)[kAccBatch]) {
 #pragma unroll
         for (uint32_t q = 0; q < kAccBatch; ++q) {
@@ -895,16 +909,15 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             it[q] = k < w.s1 ? __builtin_nontemporal_load(w.src + k) : ~0ull;
         }
     };
-    auto load_old = [&](const Unit& w, uint4 (&old)[G]) {
+    auto load_old = [&](const Unit& w, uint32_t (&old)[G]) {
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
-            const uint32_t g = j * kAccThreads + t;
-            if (w.owner && 4 * g < w.ne)
-                old[j] = w.fresh ? uint4{0u, 0u, 0u, 0u} : reinterpret_cast<const uint4*>(w.tbl)[g];
+            const uint32_t e = j * kAccThreads + t;
+            if (w.owner && e < w.ne) old[j] = w.fresh ? 0u : reinterpret_cast<const uint32_t*>(w.tbl)[e];
         }
     };
     uint64_t it[kAccBatch];
-    uint4 old[G];
+    uint32_t old[G];
     Unit cur{};
     if (blockIdx.x < total) {
         cur = locate(blockIdx.x);
@@ -916,6 +929,9 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             reinterpret_cast<uint4*>(acc)[i] = uint4{0u, 0u, 0u, 0u};
         if (t == 0) s_bad = 0;
         lds_barrier();
+        const uint32_t sb = 4 + 5 * min(nstamp, 11u);
+        STAMP(sb, __builtin_amdgcn_s_memtime());
+        STAMP(sb + 3, (cur.s1 - cur.s0) | ((uint64_t)cur.owner << 32) | ((uint64_t)cur.level << 40));
         bool bad = false;
         for (uint32_t k0 = cur.s0;;) {
 #pragma unroll
@@ -930,7 +946,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             if (k0 >= cur.s1) break;
             load_batch(cur, k0, it);
         }
-        uint4 old_cur[G];
+        STAMP(sb + 1, __builtin_amdgcn_s_memtime());
+        uint32_t old_cur[G];
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) old_cur[j] = old[j];
         // prefetch the next unit
@@ -945,33 +962,28 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         lds_barrier();
         const float q24 = 1.0f / 16777216.0f;
         bool inf_out = false;  // a stored grad is inf/nan (GradScaler's check, when `nonfinite` is given)
-        if (cur.owner) {  // groups of 4 entries = 16 bytes of the table
+        if (cur.owner) {
+            // one entry per lane per step: a lane reads its entry's two 8-byte
+            // sums as one 16-byte LDS read (consecutive lanes, consecutive 16 B:
+            // conflict-free; the former 4-entry groups per lane read at a 64-B
+            // lane stride, 4-16-way conflicted) and stores the entry's half2
+            // (256 B per wave)
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j) {
-                const uint32_t g = j * kAccThreads + t;
-                if (4 * g >= cur.ne) continue;
-                float a[8];
-                bool any = false;
-#pragma unroll
-                for (uint32_t q = 0; q < 8; ++q) {
-                    const int64_t x = (int64_t)acc[8 * g + q];
-                    a[q] = (float)x * q24;
-                    any |= x != 0;
-                }
-                if (!any) continue;
-                uint32_t w4[4] = {old_cur[j].x, old_cur[j].y, old_cur[j].z, old_cur[j].w};
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) {
-                    const ngp_half2 o = __builtin_bit_cast(ngp_half2, w4[q]);
-                    const ngp_half2 n{(ngp_half)((float)o[0] + a[2 * q]), (ngp_half)((float)o[1] + a[2 * q + 1])};
-                    inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
-                    w4[q] = __builtin_bit_cast(uint32_t, n);
-                }
-                reinterpret_cast<uint4*>(cur.tbl)[g] = uint4{w4[0], w4[1], w4[2], w4[3]};
+                const uint32_t e = j * kAccThreads + t;
+                if (e >= cur.ne) continue;
+                const ulonglong2 xx = reinterpret_cast<const ulonglong2*>(acc)[e];
+                const int64_t x0 = (int64_t)xx.x, x1 = (int64_t)xx.y;
+                if (x0 == 0 && x1 == 0) continue;
+                const ngp_half2 o = __builtin_bit_cast(ngp_half2, old_cur[j]);
+                const ngp_half2 n{(ngp_half)((float)o[0] + (float)x0 * q24), (ngp_half)((float)o[1] + (float)x1 * q24)};
+                inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
+                cur.tbl[e] = n;
             }
         } else {
             for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
-                const int64_t x0 = (int64_t)acc[e * C], x1 = (int64_t)acc[e * C + 1];
+                const ulonglong2 xx = reinterpret_cast<const ulonglong2*>(acc)[e];
+                const int64_t x0 = (int64_t)xx.x, x1 = (int64_t)xx.y;
                 if (x0 == 0 && x1 == 0) continue;
                 const ngp_half2 v{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
                 if (nonfinite) {  // the returning atomic: the entry's new value is checked
@@ -985,6 +997,9 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         if (s_bad && t == 0) cur.tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
         if (nonfinite && (__ballot(inf_out) != 0 || s_bad) && (t & 63) == 0) atomicOr(nonfinite, 1);
         lds_barrier();  // the image is rezeroed by the next unit
+        STAMP(sb + 2, __builtin_amdgcn_s_memtime());
+        ++nstamp;
+        STAMP(3, nstamp);
         cur = nxt;
     }
 }
@@ -1358,6 +1373,16 @@ extern "C" size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uin
     return bp.nlev ? bin_workspace_bytes(bp) : 0;
 }
 
+extern "C" size_t ngp_grid_encode_backward_fused_counter_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                                               float S, uint32_t H, int32_t align_corners,
+                                                               const int32_t* offsets_host) {
+    if (!offsets_host || C != 2 || D < 2 || D > 5 || L == 0 || L > kMaxLevels) return 0;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const BinPlan bp = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B);
+    return bp.nlev ? bin_counters_bytes(bp) : 0;
+}
+
 extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
                                               const int32_t* offsets, void* grad_embeddings,
                                               uint32_t B, const int32_t* count, uint32_t D,
@@ -1368,7 +1393,8 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
                                               int32_t* nonfinite, void* stream) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
     const bool zeroed = (grad_layout & NGP_GRID_GRAD_ZEROED) != 0;
-    grad_layout &= ~NGP_GRID_GRAD_ZEROED;
+    const bool external = (grad_layout & NGP_GRID_CURSORS_EXTERNAL) != 0;
+    grad_layout &= ~(NGP_GRID_GRAD_ZEROED | NGP_GRID_CURSORS_EXTERNAL);
     NGP_REQUIRE(grad_layout == 0 || grad_layout == 1, NGP_ERR_ARG,
                 "grid_encode_backward_fused: grad_layout 0 ([L,B,C]) or 1 ([B,L*C])");
     NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_backward_fused: null xyz or bound <= 0");
@@ -1397,7 +1423,7 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
             (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, im,
             bp, cursor, items, grad_layout, nonfinite);
         k_grid_bin_accum<<<2 * ngp_num_cus(), kAccThreads, (2 * bp.total_bins + 1) * sizeof(uint32_t), st>>>(
-            offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, zeroed);
+            offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, zeroed, external);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
@@ -1417,3 +1443,9 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
     }
     return ngp_check_launch("grid_encode_backward_fused");
 }
+
+#ifdef NGP_STAMPS
+extern "C" int ngp_debug_stamps(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) == hipSuccess ? NGP_OK : NGP_ERR_HIP;
+}
+#endif

@@ -668,10 +668,12 @@ k_step_end(StepState* __restrict__ st, ScalerArgs sa, const int32_t* __restrict_
 // other writes. Each on its own was a latency-bound launch of ~5 us.
 __global__ void __launch_bounds__(256)
 k_step_head(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState* __restrict__ st, LegoOut out,
-            uint32_t nlego, ScalerArgs sa, const float* __restrict__ loss_ray, ngp_pack::PackJobs jobs) {
+            uint32_t nlego, ScalerArgs sa, const float* __restrict__ loss_ray, ngp_pack::PackJobs jobs,
+            uint4* __restrict__ clear, uint32_t clear16) {
     if (blockIdx.x < nlego) {
         lego_rays_block(blockIdx.x, nlego, poses, sc, N, st, out);
     } else if (blockIdx.x == nlego) {
+        for (uint32_t i = threadIdx.x; i < clear16; i += blockDim.x) clear[i] = uint4{0u, 0u, 0u, 0u};
         if (st->end_pending) step_end_block(st, sa, nullptr, nullptr, loss_ray, N);
     } else {
         const ngp_pack::PackJob& j = jobs.job[blockIdx.x - nlego - 1];
@@ -857,10 +859,13 @@ extern "C" int ngp_fused_step_head(const float* poses, uint32_t n_poses, const f
                                    float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
                                    const float* loss_ray, int32_t n_nets, const void* const* mlp_weights,
                                    const uint32_t* in_dims, const uint32_t* hidden_dims,
-                                   const uint32_t* num_layers, void* const* images, void* stream) {
+                                   const uint32_t* num_layers, void* const* images, void* clear,
+                                   uint32_t clear_bytes, void* stream) {
     NGP_REQUIRE(nboxes >= 0 && nboxes <= kMaxBoxes, NGP_ERR_ARG, "step_head: at most %d boxes", kMaxBoxes);
     NGP_REQUIRE(n_poses > 0 && H > 0 && W > 0 && N > 0, NGP_ERR_ARG, "step_head: empty pose set, image or batch");
     NGP_REQUIRE(state && loss_ray, NGP_ERR_ARG, "step_head: null state or loss_ray");
+    NGP_REQUIRE(clear_bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(clear) & 15) == 0, NGP_ERR_ARG,
+                "step_head: clear must be 16-byte aligned, a multiple of 16 bytes");
     ngp_pack::PackJobs jobs{};
     if (n_nets > 0)
         if (int e = ngp_pack::build_jobs(n_nets, mlp_weights, in_dims, hidden_dims, num_layers, images, jobs))
@@ -870,7 +875,8 @@ extern "C" int ngp_fused_step_head(const float* poses, uint32_t n_poses, const f
     const ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled, 1.0f / (float)N};
     const uint32_t nlego = ngp_div_up(N, 256);
     k_step_head<<<nlego + 1 + (uint32_t)jobs.n, 256, 0, ngp_stream(stream)>>>(
-        poses, sc, N, static_cast<StepState*>(state), out, nlego, sa, loss_ray, jobs);
+        poses, sc, N, static_cast<StepState*>(state), out, nlego, sa, loss_ray, jobs, static_cast<uint4*>(clear),
+        clear ? clear_bytes / 16 : 0u);
     return ngp_check_launch("fused_step_head");
 }
 

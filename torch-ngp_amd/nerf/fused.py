@@ -43,7 +43,7 @@ _F16 = nat.DTYPE_CODE[torch.float16]
 _RELU, _NONE = 0, 6
 _DEFER, _GEO, _PAIR = 1, 2, 4  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO, NGP_FFMLP_PAIR_MAJOR
 _SCAN, _PRECHECKED = 1, 2  # NGP_SCALER_SCAN, NGP_SCALER_PRECHECKED
-_ZEROED = 0x10  # NGP_GRID_GRAD_ZEROED: grad layout 0 ([L,M,2]) on a table grad the optimizer cleared
+_ZEROED, _EXTERNAL = 0x10, 0x20  # NGP_GRID_GRAD_ZEROED, NGP_GRID_CURSORS_EXTERNAL (grad layout 0: [L,M,2])
 
 
 def _vp_array(ptrs):
@@ -136,6 +136,11 @@ class FusedTrainer:
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
             int(enc.align_corners), self._offsets_host)
         self.grid_ws = z(max(int(gb), 256), dtype=torch.uint8)  # zero-filled: bin cursors start at 0
+        # the step head clears the bin cursors for the grid backward (NGP_GRID_CURSORS_EXTERNAL)
+        self._grid_counter_bytes = int(nat.lib().ngp_grid_encode_backward_fused_counter_bytes(
+            M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
+            int(enc.align_corners), self._offsets_host))
+        self._grid_flags = _ZEROED | (_EXTERNAL if self._grid_counter_bytes else 0)
         self.mlp_ws = []
         for net in (self.sig_net, self.col_net):
             b = nat.lib().ngp_ffmlp_backward_workspace_bytes(M, net.input_dim, net.padded_output_dim,
@@ -303,7 +308,9 @@ class FusedTrainer:
                                           P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
                                           P(self.nears), P(self.fars), P(self.noises), P(self.counter),
                                           P(m.step_counter), 2.0, 0.5, self.growth_interval, 1, P(self.loss_ray),
-                                          2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s),
+                                          2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"],
+                                          P(self.grid_ws) if self._grid_counter_bytes else None,
+                                          self._grid_counter_bytes, s),
                   "fused_step_head")
         self._tick("step_head")
 
@@ -364,7 +371,8 @@ class FusedTrainer:
         self._tick("ffmlp_reduce")
         chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
                                                P(self.grads[0]), M, cnt, *grid_args[:-1], self._offsets_host,
-                                               P(self.grid_ws), self.grid_ws.numel(), _ZEROED, self._inf_flag, s),
+                                               P(self.grid_ws), self.grid_ws.numel(), self._grid_flags,
+                                               self._inf_flag, s),
             "grid_backward_fused")
         self._tick("grid_encode_backward")
 
