@@ -29,7 +29,7 @@ assert lib.ngp_debug_stamps(ctypes.c_void_p(nat.ptr(stamps))) == 0
 for _ in range(12):
     ft.step()
 torch.cuda.synchronize()
-st = stamps.view(-1, 64).cpu().numpy().astype(np.int64)
+st = stamps[:32768].view(-1, 64).cpu().numpy().astype(np.int64)  # accumulate: 2 workgroups per CU
 nwg = int((st[:, 0] > 0).sum())
 st = st[:nwg]
 t0 = st[:, 0].min()
@@ -62,3 +62,21 @@ for lv in np.unique(u[:, 5]):
                          "adds_med": int(np.median(u[m, 1])), "flush_med": int(np.median(u[m, 2]))}
 res["by_level"] = by_level
 print(json.dumps(res, indent=1))
+
+# k_grid_bwd_bin: per (point block, level) workgroup, 5 stamps: after the
+# counter init, after corners + ranks, after reservation + scan, after
+# staging, end
+b = stamps[32768:32768 + 8 * 4096].view(-1, 8).cpu().numpy().astype(np.int64)
+b = b[b[:, 0] > 0]
+d = np.diff(b[:, :5], axis=1)
+print(json.dumps({"bin_workgroups": int(len(b)),
+                  "bin_phase_med": [int(x) for x in np.median(d, axis=0)],
+                  "bin_phase_p90": [int(x) for x in np.percentile(d, 90, axis=0)],
+                  "bin_phases": ["corners+rank", "reserve+scan", "stage", "write-out"]}))
+nx = len(b) // 16 if len(b) % 16 == 0 else None
+if nx:
+    per = {}
+    for lv in range(16):
+        dd = d[lv * nx:(lv + 1) * nx]
+        per[lv] = [int(x) for x in np.median(dd, axis=0)]
+    print(json.dumps({"bin_phase_med_by_level": per}))

@@ -21,6 +21,7 @@
 //     rounded to float) and passed as kernel arguments.
 //   * a hashed level's size is a power of two: the modulo becomes a mask.
 #include "ngp_common.h"
+#include "ngp_dpp.h"
 #include <stdlib.h>
 
 #include <cmath>
@@ -568,6 +569,15 @@ constexpr uint32_t kBinPts = 512;  // samples (threads) per bin-kernel workgroup
 // wait for the wave's outstanding global loads, stores and atomics.
 NGP_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+#ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-workgroup phase clocks
+__device__ unsigned long long* g_stamps;
+#define STAMP(slot, v) do { if (threadIdx.x == 0) g_stamps[blockIdx.x * 64 + (slot)] = (v); } while (0)
+#define BSTAMP(slot) do { if (threadIdx.x == 0) g_stamps[32768 + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(slot, v) do { } while (0)
+#define BSTAMP(slot) do { } while (0)
+#endif
+
 template <uint32_t D>
 __global__ void __launch_bounds__(kBinPts)
 k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
@@ -586,6 +596,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     const int lane = (int)(threadIdx.x & 63);
     if (threadIdx.x < nb) cnt[threadIdx.x] = 0;
     lds_barrier();
+    BSTAMP(0);
 
     const uint32_t b = blockIdx.x * kBinPts + threadIdx.x;
     bool valid = b < rows_of(B, im);
@@ -643,23 +654,12 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         if (merge) {
             const uint32_t kprev = __shfl_up(k, 1, 64);
             const bool same = valid && lane > 0 && kprev == k;
-            if (__ballot(same)) {
-                int start = same ? 0 : lane;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int t = __shfl_up(start, o, 64);
-                    if (lane >= o) start = max(start, t);
-                }
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const float t0 = __shfl_up(v0, o, 64), t1 = __shfl_up(v1, o, 64);
-                    if (lane - o >= start) {
-                        v0 += t0;
-                        v1 += t1;
-                    }
-                }
-                const uint32_t knext = __shfl_down(k, 1, 64);
-                lv_ = valid && (lane == 63 || knext != k);
+            const uint64_t sm = __ballot(same);
+            if (sm) {
+                // runs of equal keys: segmented DPP scan, the run's last lane keeps the sum
+                ngp_dpp::seg_scan2(v0, v1, !same);
+                const bool next_same = lane < 63 && ((sm >> (lane + 1)) & 1ull);
+                lv_ = valid && !next_same;
             }
         }
         key[idx] = k;
@@ -682,6 +682,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         }
     }
     lds_barrier();
+    BSTAMP(1);
     // reserve each bin's run now (one global atomic per bin); the results are
     // needed only by the write-out, so the scan and the staging overlap them.
     // The part of a run past the bin's capacity goes atomic, so slots
@@ -712,6 +713,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         if (t == 0) soff[nb] = all;
     }
     lds_barrier();
+    BSTAMP(2);
 #pragma unroll
     for (uint32_t idx = 0; idx < NC; idx++) {
         if (!live[idx]) continue;
@@ -723,6 +725,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         binfo[t] = uint2{t * cap + bs_mine - soff[t], soff[t] + lim};
     }
     lds_barrier();
+    BSTAMP(3);
     const uint32_t total = soff[nb];
     BinItem* lvl_items = items + bp.item0[level];
     ngp_half* gg = grad_grid + (size_t)off0 * C;
@@ -743,6 +746,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
             }
         }
     }
+    BSTAMP(4);
 }
 
 // An fp16 value as a signed count of 2^-24 (every finite fp16 is one:
@@ -766,12 +770,6 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // (inf / NaN: fp16 overflow under the loss scale) cannot be carried by the
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
-#ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-workgroup phase clocks
-__device__ unsigned long long* g_stamps;
-#define STAMP(slot, v) do { if (threadIdx.x == 0) g_stamps[blockIdx.x * 64 + (slot)] = (v); } while (0)
-#else
-#define STAMP(slot, v) do { } while (0)
-#endif
 constexpr uint32_t kAccThreads = 512, kAccBatch = 16, kRetireGroups = 16;
 __global__ void __launch_bounds__(kAccThreads)
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,

@@ -22,6 +22,7 @@
 //   k_step_end        GradScaler.update, counters, loss
 #include "ffmlp_pack.h"
 #include "ngp_common.h"
+#include "ngp_dpp.h"
 #include "sh_basis.h"
 
 #include <algorithm>
@@ -248,18 +249,11 @@ constexpr uint32_t kLossWaves = 4;
 // torch.sigmoid on a half tensor: fp32 math, half result
 NGP_DEV float sigmoid_h(ngp_half x) { return (float)(ngp_half)(1.0f / (1.0f + expf(-(float)x))); }
 
-NGP_DEV float scan_incl(float v, uint32_t lane) {
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-        const float t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
+// wave-wide prefix sums / sums on DPP lane moves (ngp_dpp.h); every lane of
+// the wave is active wherever these are called
+NGP_DEV float scan_incl(float v, uint32_t) { return ngp_dpp::scan_incl(v); }
 NGP_DEV float wave_sum(float v) {
-#pragma unroll
-    for (uint32_t o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ngp_dpp::scan_incl(v)), 63));
 }
 
 struct LossArgs {

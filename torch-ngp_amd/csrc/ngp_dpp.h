@@ -1,0 +1,61 @@
+// Wave-64 scans on DPP lane moves (row_shr within 16-lane rows, then
+// row_bcast:15 / row_bcast:31 across rows): each step is one VALU
+// instruction with a DPP source instead of a ds_bpermute round trip through
+// the LDS crossbar (__shfl_up), so a 6-step scan is a short dependent chain
+// of ALU ops. Lanes whose source is outside the move (or masked off) take
+// the identity. gfx9-family only (row_bcast does not exist on gfx10+).
+#pragma once
+#include "ngp_common.h"
+
+namespace ngp_dpp {
+
+// DPP controls (GFX9 encoding)
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+
+template <int CTRL, int ROW_MASK>
+NGP_DEV uint32_t mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+template <int CTRL, int ROW_MASK>
+NGP_DEV float movf(float v) {
+    return __builtin_bit_cast(float, mov<CTRL, ROW_MASK>(__builtin_bit_cast(uint32_t, v)));
+}
+
+// one step of the segmented scan: (a, f) <- src (+) mine
+template <int CTRL, int ROW_MASK>
+NGP_DEV void seg_step2(float& a, float& b, uint32_t& f) {
+    const float ta = movf<CTRL, ROW_MASK>(a), tb = movf<CTRL, ROW_MASK>(b);
+    const uint32_t tf = mov<CTRL, ROW_MASK>(f);
+    if (!f) {
+        a += ta;
+        b += tb;
+    }
+    f |= tf;
+}
+
+// Inclusive segmented sum of (a, b) over the wave: a lane with head set
+// starts a new segment. Returns, per lane, the sum from its segment's head
+// up to itself.
+NGP_DEV void seg_scan2(float& a, float& b, bool head) {
+    uint32_t f = head ? 1u : 0u;
+    seg_step2<kRowShr1, 0xf>(a, b, f);
+    seg_step2<kRowShr2, 0xf>(a, b, f);
+    seg_step2<kRowShr4, 0xf>(a, b, f);
+    seg_step2<kRowShr8, 0xf>(a, b, f);
+    seg_step2<kRowBcast15, 0xa>(a, b, f);
+    seg_step2<kRowBcast31, 0xc>(a, b, f);
+}
+
+// Inclusive prefix sum over the wave.
+NGP_DEV float scan_incl(float v) {
+    v += movf<kRowShr1, 0xf>(v);
+    v += movf<kRowShr2, 0xf>(v);
+    v += movf<kRowShr4, 0xf>(v);
+    v += movf<kRowShr8, 0xf>(v);
+    v += movf<kRowBcast15, 0xa>(v);
+    v += movf<kRowBcast31, 0xc>(v);
+    return v;
+}
+
+}  // namespace ngp_dpp
