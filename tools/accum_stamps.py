@@ -26,6 +26,9 @@ ft = FusedTrainer(model, SyntheticLego(dev, num_rays=4096), M=101762)
 stamps = torch.zeros(4096 * 64, dtype=torch.int64, device=dev)
 lib = nat.lib()
 assert lib.ngp_debug_stamps(ctypes.c_void_p(nat.ptr(stamps))) == 0
+ms = torch.zeros(2 * 1024 * 16, dtype=torch.int64, device=dev)  # k_mlp_bwd: set before any step
+if hasattr(lib, "ngp_debug_mlp_stamps"):
+    assert lib.ngp_debug_mlp_stamps(ctypes.c_void_p(nat.ptr(ms))) == 0
 for _ in range(12):
     ft.step()
 torch.cuda.synchronize()
@@ -80,3 +83,29 @@ if nx:
         dd = d[lv * nx:(lv + 1) * nx]
         per[lv] = [int(x) for x in np.median(dd, axis=0)]
     print(json.dumps({"bin_phase_med_by_level": per}))
+
+# k_mlp_bwd (sigma NH=1, colour NH=2): per wave, 16 stamps: entry, after the
+# fragment image copy, after each chunk, after the loop, after the dW fold,
+# after the slab row
+if hasattr(lib, "ngp_debug_mlp_stamps"):
+    ms.zero_()
+    ft.step()
+    torch.cuda.synchronize()
+    mm = ms.view(2, 1024, 16).cpu().numpy().astype(np.int64)
+    out = {}
+    for nh, name in ((0, "sigma"), (1, "colour")):
+        w = mm[nh][mm[nh][:, 0] > 0]
+        chunk_t = []
+        for r in w:
+            prev = r[1]
+            for k in range(2, 12):
+                if r[k] == 0:
+                    break
+                chunk_t.append(r[k] - prev)
+                prev = r[k]
+        out[name] = {"waves": int(len(w)), "frag_copy_med": int(np.median(w[:, 1] - w[:, 0])),
+                     "chunk_med": int(np.median(chunk_t)), "chunk_p90": int(np.percentile(chunk_t, 90)),
+                     "chunks_per_wave_max": int(max(np.count_nonzero(r[2:12]) for r in w)),
+                     "loop_med": int(np.median(w[:, 12] - w[:, 1])), "fold_med": int(np.median(w[:, 13] - w[:, 12])),
+                     "slab_med": int(np.median(w[:, 14] - w[:, 13])), "total_med": int(np.median(w[:, 14] - w[:, 0]))}
+    print(json.dumps({"mlp_bwd": out}))

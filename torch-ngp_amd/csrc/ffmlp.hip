@@ -542,6 +542,13 @@ struct GiPairMajor {
     }
 };
 
+#ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-wave phase clocks
+__device__ unsigned long long* g_mlp_stamps;
+#define MSTAMP(slot) do { if (g_mlp_stamps && (threadIdx.x & 63) == 0) g_mlp_stamps[((size_t)(NH - 1) * 1024 + blockIdx.x * kWaves + (threadIdx.x >> 6)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define MSTAMP(slot) do { } while (0)
+#endif
+
 template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
@@ -556,8 +563,11 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     const half8* fr = lds;
     ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
 
+    MSTAMP(0);
     for (uint32_t t = threadIdx.x; t < (uint32_t)L::FRAGS * 64; t += blockDim.x) lds[t] = image[t];
     __syncthreads();
+    MSTAMP(1);
+    uint32_t nst = 0;
 
     const uint32_t wave = threadIdx.x >> 6;
     ngp_half* dT = tiles + (size_t)wave * 2 * kTileRows * kTileLd;
@@ -622,7 +632,10 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
             dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
             gi_out(row0, B, in_dim, gi);
         }
+        MSTAMP(2 + min(nst, 9u));
+        ++nst;
     }
+    MSTAMP(12);
 
     // fold the waves' register tiles into two LDS dW images (waves 0/1 store,
     // then waves 2/3 add), then publish image0 + image1 as the slab row: a
@@ -643,9 +656,11 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
         add_dw<false>(dw_last, img + fwd_desc<W, IN_KS, NH>(LAST, in_dim).off, W, kOut);
     }
     __syncthreads();
+    MSTAMP(13);
     const float* img0 = reinterpret_cast<const float*>(lds);
     float* slab_row = slab + (size_t)blockIdx.x * nparams;
     for (uint32_t t = threadIdx.x; t < nparams; t += blockDim.x) slab_row[t] = img0[t] + img0[nparams + t];
+    MSTAMP(14);
 }
 
 // grad_weights[p] = sum over workgroup rows of the slab, in a fixed order
@@ -1039,3 +1054,9 @@ extern "C" int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32
 
 extern "C" int ngp_ffmlp_allocate_splitk(size_t size) { (void)size; return NGP_OK; }
 extern "C" int ngp_ffmlp_free_splitk(void) { return NGP_OK; }
+
+#ifdef NGP_STAMPS
+extern "C" int ngp_debug_mlp_stamps(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_mlp_stamps), &buf, sizeof(buf)) == hipSuccess ? NGP_OK : NGP_ERR_HIP;
+}
+#endif

@@ -571,8 +571,8 @@ NGP_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::
 
 #ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-workgroup phase clocks
 __device__ unsigned long long* g_stamps;
-#define STAMP(slot, v) do { if (threadIdx.x == 0) g_stamps[blockIdx.x * 64 + (slot)] = (v); } while (0)
-#define BSTAMP(slot) do { if (threadIdx.x == 0) g_stamps[32768 + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP(slot, v) do { if (g_stamps && threadIdx.x == 0) g_stamps[blockIdx.x * 64 + (slot)] = (v); } while (0)
+#define BSTAMP(slot) do { if (g_stamps && threadIdx.x == 0) g_stamps[32768 + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define STAMP(slot, v) do { } while (0)
 #define BSTAMP(slot) do { } while (0)
