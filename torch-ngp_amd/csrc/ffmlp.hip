@@ -432,9 +432,29 @@ NGP_DEV void pack_delta(const f32x4 (&acc)[kNB][MT], const half8 (&h)[kNB][KS], 
 // Add (FIRST: store) one wave's dW tile sums (C layout) into the workgroup's
 // fp32 dW image in LDS. Waves take turns (see k_mlp_bwd), so the summation
 // order is fixed and the result reproducible.
+// The image's rows are padded to ld = in_w + kFoldPad floats: a tile's four
+// 16-lane groups hold rows 4 apart, which the pad puts on different LDS banks
+// (unpadded, in_w a multiple of 16, they were 4-way conflicted).
+constexpr uint32_t kFoldPad = 4;
 template <bool FIRST, int MO, int MI>
-NGP_DEV void add_dw(const f32x4 (&t)[MO][MI], float* __restrict__ acc, uint32_t in_w, uint32_t out_w) {
+NGP_DEV void add_dw(const f32x4 (&t)[MO][MI], float* __restrict__ acc, uint32_t in_w, uint32_t out_w,
+                    uint32_t ld) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    // all of the matrix's reads are issued before any write (a read-add-write
+    // per element would expose the LDS latency once per element: 176 times
+    // for the colour network)
+    float v[MO][MI][4];
+    if (!FIRST) {
+#pragma unroll
+        for (int m = 0; m < MO; ++m)
+#pragma unroll
+            for (int k = 0; k < MI; ++k)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t o = 16 * m + 4 * g + r, i = 16 * k + c;
+                    v[m][k][r] = (o < out_w && i < in_w) ? acc[o * ld + i] : 0.0f;
+                }
+    }
 #pragma unroll
     for (int m = 0; m < MO; ++m)
 #pragma unroll
@@ -442,10 +462,7 @@ NGP_DEV void add_dw(const f32x4 (&t)[MO][MI], float* __restrict__ acc, uint32_t 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint32_t o = 16 * m + 4 * g + r, i = 16 * k + c;
-                if (o < out_w && i < in_w) {
-                    float* p = &acc[o * in_w + i];
-                    *p = FIRST ? t[m][k][r] : *p + t[m][k][r];
-                }
+                if (o < out_w && i < in_w) acc[o * ld + i] = FIRST ? t[m][k][r] : v[m][k][r] + t[m][k][r];
             }
 }
 
@@ -464,7 +481,8 @@ struct BwdLds {
     static constexpr size_t frag_bytes = (size_t)FRAGS * 64 * 16;
     static constexpr size_t tile_bytes = (size_t)kWaves * 2 * kTileRows * kTileLd * 2;
     static constexpr size_t nparams_max = (size_t)W * (32 * IN_KS) + (size_t)NH * W * W + (size_t)kOut * W;
-    static constexpr size_t acc_bytes = nparams_max * 4;
+    static constexpr size_t acc_bytes =
+        ((size_t)W * (32 * IN_KS + kFoldPad) + (size_t)NH * W * (W + kFoldPad) + (size_t)kOut * (W + kFoldPad)) * 4;
     // the two dW images of the epilogue reuse the fragment + tile space once
     // the chunk loop is done
     static constexpr size_t total =
@@ -564,12 +582,19 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
 
     MSTAMP(0);
+    // the first chunk's inputs and output grads are requested before the
+    // fragment image copy, so the two latencies overlap
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t stride = gridDim.x * kWaves;
+    uint32_t chunk = blockIdx.x * kWaves + wave;
+    half8 xn[kNB][IN_KS], dn[kNB][1];
+    xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
+    load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn);  // output activation ignored (ffmlp.cu:783)
     for (uint32_t t = threadIdx.x; t < (uint32_t)L::FRAGS * 64; t += blockDim.x) lds[t] = image[t];
     __syncthreads();
     MSTAMP(1);
-    uint32_t nst = 0;
+    [[maybe_unused]] uint32_t nst = 0;
 
-    const uint32_t wave = threadIdx.x >> 6;
     ngp_half* dT = tiles + (size_t)wave * 2 * kTileRows * kTileLd;
     ngp_half* hT = dT + (size_t)kTileRows * kTileLd;
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
@@ -582,11 +607,6 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
 
     // inputs and output gradients of the next chunk are prefetched while the
     // current one computes (one wave per SIMD: nothing else hides the latency)
-    const uint32_t stride = gridDim.x * kWaves;
-    uint32_t chunk = blockIdx.x * kWaves + wave;
-    half8 xn[kNB][IN_KS], dn[kNB][1];
-    xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
-    load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn);  // output activation ignored (ffmlp.cu:783)
     for (; chunk < nchunks; chunk += stride) {
         const uint32_t row0 = chunk * 16 * kNB;
         half8 x[kNB][IN_KS], dout[kNB][1];
@@ -640,26 +660,43 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     // fold the waves' register tiles into two LDS dW images (waves 0/1 store,
     // then waves 2/3 add), then publish image0 + image1 as the slab row: a
     // fixed summation order, so dW is bit-reproducible
-    float* img = reinterpret_cast<float*>(lds) + (size_t)(wave & 1) * nparams;
+    // padded image: first [W][in_dim + pad], hidden q [W][W + pad], last [16][W + pad]
+    const uint32_t ld0 = in_dim + kFoldPad, ldw = W + kFoldPad;
+    const uint32_t p_hid = W * ld0, p_last = p_hid + NH * W * ldw, npad = p_last + kOut * ldw;
+    float* img = reinterpret_cast<float*>(lds) + (size_t)(wave & 1) * npad;
     __syncthreads();  // fragments and tiles are dead from here on
     if (wave < 2) {
-        add_dw<true>(dw_first, img, in_dim, W);
+        add_dw<true>(dw_first, img, in_dim, W, ld0);
 #pragma unroll
-        for (int q = 1; q <= NH; ++q) add_dw<true>(dw_hid[q - 1], img + fwd_desc<W, IN_KS, NH>(q, in_dim).off, W, W);
-        add_dw<true>(dw_last, img + fwd_desc<W, IN_KS, NH>(LAST, in_dim).off, W, kOut);
+        for (int q = 1; q <= NH; ++q) add_dw<true>(dw_hid[q - 1], img + p_hid + (q - 1) * W * ldw, W, W, ldw);
+        add_dw<true>(dw_last, img + p_last, W, kOut, ldw);
     }
     __syncthreads();
     if (wave >= 2) {
-        add_dw<false>(dw_first, img, in_dim, W);
+        add_dw<false>(dw_first, img, in_dim, W, ld0);
 #pragma unroll
-        for (int q = 1; q <= NH; ++q) add_dw<false>(dw_hid[q - 1], img + fwd_desc<W, IN_KS, NH>(q, in_dim).off, W, W);
-        add_dw<false>(dw_last, img + fwd_desc<W, IN_KS, NH>(LAST, in_dim).off, W, kOut);
+        for (int q = 1; q <= NH; ++q) add_dw<false>(dw_hid[q - 1], img + p_hid + (q - 1) * W * ldw, W, W, ldw);
+        add_dw<false>(dw_last, img + p_last, W, kOut, ldw);
     }
     __syncthreads();
     MSTAMP(13);
+    // slab row = image0 + image1 in the unpadded [out][in] layout, 16 bytes per access
     const float* img0 = reinterpret_cast<const float*>(lds);
     float* slab_row = slab + (size_t)blockIdx.x * nparams;
-    for (uint32_t t = threadIdx.x; t < nparams; t += blockDim.x) slab_row[t] = img0[t] + img0[nparams + t];
+    auto publish = [&](uint32_t poff, uint32_t ld, uint32_t off, uint32_t in_w, uint32_t out_w) {
+        const uint32_t n4 = out_w * in_w / 4;
+        for (uint32_t t = threadIdx.x; t < n4; t += blockDim.x) {
+            const uint32_t o = 4 * t / in_w, i = 4 * t - o * in_w;
+            const float4 a = *reinterpret_cast<const float4*>(img0 + poff + o * ld + i);
+            const float4 b = *reinterpret_cast<const float4*>(img0 + npad + poff + o * ld + i);
+            *reinterpret_cast<float4*>(slab_row + off + o * in_w + i) = float4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+        }
+    };
+    publish(0, ld0, 0, in_dim, W);
+#pragma unroll
+    for (int q = 1; q <= NH; ++q)
+        publish(p_hid + (q - 1) * W * ldw, ldw, fwd_desc<W, IN_KS, NH>(q, in_dim).off, W, W);
+    publish(p_last, ldw, fwd_desc<W, IN_KS, NH>(LAST, in_dim).off, W, kOut);
     MSTAMP(14);
 }
 
