@@ -865,7 +865,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         if (t == 0) retire[0] = 0;
     }
     STAMP(2, __builtin_amdgcn_s_memtime());
-    uint32_t nstamp = 0;
+    [[maybe_unused]] uint32_t nstamp = 0;
 
     // 3. units. The first item batch of a unit and, for a single-owner unit,
     // its slice of the table are loaded one unit ahead (while the previous
@@ -927,7 +927,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             reinterpret_cast<uint4*>(acc)[i] = uint4{0u, 0u, 0u, 0u};
         if (t == 0) s_bad = 0;
         lds_barrier();
-        const uint32_t sb = 4 + 5 * min(nstamp, 11u);
+        [[maybe_unused]] const uint32_t sb = 4 + 5 * min(nstamp, 11u);
         STAMP(sb, __builtin_amdgcn_s_memtime());
         STAMP(sb + 3, (cur.s1 - cur.s0) | ((uint64_t)cur.owner << 32) | ((uint64_t)cur.level << 40));
         bool bad = false;
