@@ -665,18 +665,51 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         key[idx] = k;
         live[idx] = lv_;
         val[idx] = ngp_half2{(ngp_half)v0, (ngp_half)v1};
-        // rank within the bin: one LDS atomic per wave when the wave shares a bin
-        const uint32_t bin = k >> kBinShift;
-        const uint64_t lm = __ballot(lv_);
-        rank[idx] = 0;
-        if (lm) {
+    }
+    // Rank within the bin. When every live item of the wave (all corners) is
+    // in one bin -- the dense levels' z-slab bins, where all the workgroup's
+    // waves hit the same counter -- the wave takes its whole run with ONE LDS
+    // atomic (same-address LDS atomics serialize: 8 per wave were ~half of
+    // those levels' bin time, tools/accum_stamps.py); otherwise per corner:
+    // one atomic per wave when the wave's items of that corner share a bin,
+    // else one per item.
+    uint64_t lms[NC];
+    uint32_t b0 = 0xffffffffu;
+#pragma unroll
+    for (uint32_t idx = 0; idx < NC; idx++) {
+        lms[idx] = __ballot(live[idx]);
+        if (b0 == 0xffffffffu && lms[idx])
+            b0 = __builtin_amdgcn_readlane(key[idx], __ffsll((unsigned long long)lms[idx]) - 1) >> kBinShift;
+    }
+    bool uni = b0 != 0xffffffffu;
+#pragma unroll
+    for (uint32_t idx = 0; idx < NC; idx++) uni = uni && __ballot(live[idx] && (key[idx] >> kBinShift) != b0) == 0;
+    if (uni) {
+        uint32_t total = 0;
+#pragma unroll
+        for (uint32_t idx = 0; idx < NC; idx++) total += (uint32_t)__popcll(lms[idx]);
+        uint32_t r0 = 0;
+        if (lane == 0) r0 = atomicAdd(&cnt[b0], total);
+        uint32_t run = __builtin_amdgcn_readfirstlane(r0);
+#pragma unroll
+        for (uint32_t idx = 0; idx < NC; idx++) {
+            rank[idx] = run + lanes_below(lms[idx]);
+            run += (uint32_t)__popcll(lms[idx]);
+        }
+    } else {
+#pragma unroll
+        for (uint32_t idx = 0; idx < NC; idx++) {
+            const uint32_t bin = key[idx] >> kBinShift;
+            const uint64_t lm = lms[idx];
+            rank[idx] = 0;
+            if (!lm) continue;
             const int first = __ffsll((unsigned long long)lm) - 1;
-            const uint32_t b0 = __shfl(bin, first, 64);
-            if (__ballot(lv_ && bin != b0) == 0) {
+            const uint32_t bf = __builtin_amdgcn_readlane(bin, first);
+            if (__ballot(live[idx] && bin != bf) == 0) {
                 uint32_t r0 = 0;
-                if (lane == first) r0 = atomicAdd(&cnt[b0], (uint32_t)__popcll(lm));
-                rank[idx] = __shfl(r0, first, 64) + lanes_below(lm);
-            } else if (lv_) {
+                if (lane == first) r0 = atomicAdd(&cnt[bf], (uint32_t)__popcll(lm));
+                rank[idx] = __builtin_amdgcn_readlane(r0, first) + lanes_below(lm);
+            } else if (live[idx]) {
                 rank[idx] = atomicAdd(&cnt[bin], 1u);
             }
         }
