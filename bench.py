@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
     ap.add_argument("--engine", choices=["fused", "autograd"], default="fused")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="collective backend for N > 1: nccl (= RCCL, the measured path) or gloo "
+                         "(host-staged; a rehearsal of the data-parallel step with every rank on the "
+                         "visible GPUs, e.g. 2 ranks on a 1-GPU box)")
     return ap.parse_args()
 
 
@@ -86,7 +90,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and args.backend == "gloo":
+        local = local % torch.cuda.device_count()
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if world > 1 else 0)
