@@ -312,3 +312,44 @@ def test_step_overflow_skips_via_kernel_flags(cuda):
     assert ft.scale == 2.0 ** 38
     for a, b in zip(ft.params, before):
         assert torch.equal(a.detach(), b)
+
+
+def test_checkpoint_roundtrip_and_torch_formats(cuda):
+    """checkpoint() is the reference trainer's checkpoint dict (nerf/utils.py
+    save_checkpoint): torch's Adam / LambdaLR / GradScaler load its optimizer,
+    lr_scheduler and scaler entries, and a trainer restored from it continues
+    bit-identically to the one that saved it."""
+    from nerf.network_ff import NeRFNetwork
+    _, _, _, a = _setup(cuda)
+    for _ in range(3):
+        a.step()
+    ck = a.checkpoint()
+    assert {"epoch", "global_step", "stats", "mean_count", "mean_density", "model", "optimizer",
+            "lr_scheduler", "scaler"} <= set(ck)
+    assert ck["global_step"] == 3 and set(ck["model"]) >= {"encoder.embeddings", "sigma_net.weights",
+                                                           "color_net.weights", "density_bitfield"}
+    m2 = NeRFNetwork(bound=1, cuda_ray=True).to(cuda)
+    opt = torch.optim.Adam(m2.get_params(1e-2), lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+    opt.load_state_dict(ck["optimizer"])
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda it: 0.1 ** min(it / 30000, 1))
+    sched.load_state_dict(ck["lr_scheduler"])
+    scaler = torch.amp.GradScaler("cuda")
+    scaler.load_state_dict(ck["scaler"])
+    assert scaler.get_scale() == a.scale
+    assert torch.equal(opt.state[m2.encoder.embeddings]["exp_avg"], ck["optimizer"]["state"][0]["exp_avg"])
+    # resume: a differently initialised trainer restored from the checkpoint
+    _, _, _, b = _setup(cuda)
+    with torch.no_grad():
+        for p in b.params:
+            p.add_(0.01)
+    b.sync_half()
+    b.load_checkpoint(ck)
+    for _ in range(3):
+        a.step()
+        b.step()
+    a.flush()
+    b.flush()
+    torch.cuda.synchronize()
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+    assert a.optimizer_steps == b.optimizer_steps and a.scale == b.scale

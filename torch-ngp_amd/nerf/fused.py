@@ -123,6 +123,7 @@ class FusedTrainer:
                 view.copy_(p.detach())
                 p.data = view
                 self.flat_half[int(a):int(a) + p.numel()].copy_(view.reshape(-1))
+        self._starts = [int(a) for a in starts[:-1]]
         self.grads = [self.flat_grad[int(a):int(a) + n].view(p.shape)
                       for a, n, p in zip(starts[:-1], sizes, self.params)]
         self.w_half = [self.flat_half[int(a):int(a) + n].view(p.shape)
@@ -487,3 +488,104 @@ class FusedTrainer:
 
     def sample_count(self):
         return int(self.counter[0].item())
+
+    # ------------------------------------------------------ checkpoints
+    # StepState as int32 words: 0 scale (f32), 4 growth tracker, 6 Adam steps,
+    # 7 LambdaLR epoch, 8 finished iterations, 9 sampler draws
+    _S_SCALE, _S_GROWTH, _S_ADAM, _S_EPOCH, _S_ITER, _S_DRAW = 0, 4, 6, 7, 8, 9
+
+    def _moments(self):
+        """Full-length Adam moments (data parallel: all-gathered from the shards)."""
+        if self.world == 1:
+            return self.exp_avg, self.exp_avg_sq
+        full = []
+        for t in (self.exp_avg, self.exp_avg_sq):
+            out = torch.empty(self.total, dtype=t.dtype, device=t.device)
+            if self._nccl:
+                dist.all_gather_into_tensor(out, t)
+            else:
+                host = torch.empty(self.total, dtype=t.dtype)
+                dist.all_gather_into_tensor(host, t.cpu())
+                out.copy_(host)
+            full.append(out)
+        return full
+
+    def checkpoint(self, full=True, epoch=0, stats=None):
+        """The reference trainer's checkpoint dict (nerf/utils.py save_checkpoint
+        :1175-1211): epoch, global_step, stats, mean_count / mean_density, the
+        model's state_dict and, with full, the optimizer / lr_scheduler / scaler
+        state_dicts in torch's own formats (torch.optim.Adam over
+        model.get_params(lr), LambdaLR, GradScaler load them), so checkpoints
+        move between the reference's trainer and this one. `fused` carries the
+        sampler's draw counter (not part of the reference format)."""
+        self.flush()
+        si = self.state.view(torch.int32).cpu()
+        scale = float(self.state.view(torch.float32)[self._S_SCALE].item())
+        adam_steps, ep, it = int(si[self._S_ADAM]), int(si[self._S_EPOCH]), int(si[self._S_ITER])
+        m = self.model
+        state = {"epoch": epoch, "global_step": it,
+                 "stats": stats if stats is not None else {"loss": [], "valid_loss": [], "results": [],
+                                                           "checkpoints": [], "best_result": None},
+                 "mean_count": m.mean_count, "mean_density": m.mean_density,
+                 "model": m.state_dict(),
+                 "fused": {"draw": int(si[self._S_DRAW])}}
+        if full:
+            m1, m2 = self._moments()
+            # param indices follow model.get_params: encoder [0], sigma_net [1], encoder_dir [], color_net [2]
+            opt_state = {}
+            for i, (a, p) in enumerate(zip(self._starts, self.params)):
+                n = p.numel()
+                opt_state[i] = {"step": torch.tensor(float(adam_steps)),
+                                "exp_avg": m1[a:a + n].view(p.shape).clone(),
+                                "exp_avg_sq": m2[a:a + n].view(p.shape).clone()}
+            group = {"lr": self.lr * 0.1 ** min(ep / self.iters, 1), "betas": tuple(self.betas), "eps": self.eps,
+                     "weight_decay": 0, "amsgrad": False, "maximize": False, "foreach": None,
+                     "capturable": False, "differentiable": False, "fused": None, "initial_lr": self.lr}
+            state["optimizer"] = {"state": opt_state,
+                                  "param_groups": [dict(group, params=ids) for ids in ([0], [1], [], [2])]}
+            lr_now = self.lr * 0.1 ** min(ep / self.iters, 1)
+            state["lr_scheduler"] = {"base_lrs": [self.lr] * 4, "last_epoch": ep, "_step_count": ep + 1,
+                                     "_get_lr_called_within_step": False, "_last_lr": [lr_now] * 4,
+                                     "lr_lambdas": [None] * 4}
+            state["scaler"] = {"scale": scale, "growth_factor": 2.0, "backoff_factor": 0.5,
+                               "growth_interval": self.growth_interval, "_growth_tracker": int(si[self._S_GROWTH])}
+        return state
+
+    def load_checkpoint(self, state, model_only=False):
+        """Inverse of checkpoint() (and loader of the reference's checkpoint
+        dicts, nerf/utils.py load_checkpoint :1237-1290): model weights and
+        buffers, mean_count / mean_density, then Adam moments, step counts,
+        LR epoch and GradScaler state."""
+        self.flush()
+        m = self.model
+        if "model" not in state:  # a bare state_dict
+            m.load_state_dict(state)
+            self.sync_half()
+            return
+        m.load_state_dict(state["model"], strict=False)  # copies into the flat buffers' views
+        self.sync_half()
+        m.mean_count = state.get("mean_count", m.mean_count)
+        m.mean_density = state.get("mean_density", m.mean_density)
+        self.refresh_occupancy()
+        if model_only:
+            return
+        si = self.state.view(torch.int32)
+        si[self._S_ITER] = int(state.get("global_step", 0))
+        if "fused" in state:
+            si[self._S_DRAW] = int(state["fused"]["draw"])
+        if "optimizer" in state:
+            st = state["optimizer"]["state"]
+            for i, (a, p) in enumerate(zip(self._starts, self.params)):
+                if i not in st:
+                    continue
+                for key, dst in (("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
+                    full = st[i][key].to(self.dev, torch.float32).reshape(-1)
+                    lo, hi = max(a, self.lo), min(a + full.numel(), self.hi)  # this rank's part
+                    if lo < hi:
+                        dst[lo - self.lo:hi - self.lo].copy_(full[lo - a:hi - a])
+                si[self._S_ADAM] = int(float(st[i]["step"]))
+        if "lr_scheduler" in state:
+            si[self._S_EPOCH] = int(state["lr_scheduler"]["last_epoch"])
+        if "scaler" in state:
+            self.state.view(torch.float32)[self._S_SCALE] = float(state["scaler"]["scale"])
+            si[self._S_GROWTH] = int(state["scaler"]["_growth_tracker"])
