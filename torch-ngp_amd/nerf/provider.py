@@ -120,3 +120,85 @@ class SyntheticLego:
         images = self.target(rays["rays_o"], rays["rays_d"])
         return {"H": self.H, "W": self.W, "rays_o": rays["rays_o"], "rays_d": rays["rays_d"],
                 "images": images}
+
+
+class NeRFDataset:
+    """Real-scene loader for the reference's transforms*.json format
+    (nerf/provider.py:127-440): blender splits (transforms_{train,val,test}.json,
+    'trainval' = train + val) or one colmap-style transforms.json. Poses go
+    through nerf_matrix_to_ngp(scale, offset) (:19-27); images are decoded with
+    PIL (the reference uses cv2, absent here) to float RGB(A) / 255 and
+    area-resized by 1/downscale (cv2.INTER_AREA there, PIL's box filter here);
+    intrinsics come from fl_x/fl_y or camera_angle_x/y, cx/cy defaulting to the
+    image centre (:419-434). sample() is the reference's collate for training
+    (:442-508): num_rays random pixels of one random image, through get_rays,
+    with their ground-truth colours gathered; on the GPU the same batch feeds
+    nerf.train.Trainer exactly like SyntheticLego does."""
+
+    def __init__(self, path, device, type="train", downscale=1, scale=0.33, offset=(0, 0, 0), num_rays=4096):
+        import json
+        import os
+
+        from PIL import Image
+
+        self.device, self.num_rays = device, num_rays
+        if os.path.exists(os.path.join(path, "transforms.json")):
+            self.mode = "colmap"
+            with open(os.path.join(path, "transforms.json")) as f:
+                transform = json.load(f)
+            frames = transform["frames"]
+        elif os.path.exists(os.path.join(path, "transforms_train.json")):
+            self.mode = "blender"
+            splits = ["train", "val"] if type == "trainval" else [type]
+            frames, transform = [], None
+            for sp in splits:
+                with open(os.path.join(path, f"transforms_{sp}.json")) as f:
+                    t = json.load(f)
+                transform = transform or t
+                frames += t["frames"]
+        else:
+            raise FileNotFoundError(f"NeRFDataset: no transforms*.json under {path}")
+        H = W = None
+        if "h" in transform and "w" in transform:
+            H, W = int(transform["h"]) // downscale, int(transform["w"]) // downscale
+        poses, images = [], []
+        for fr in frames:
+            fp = os.path.join(path, fr["file_path"])
+            if self.mode == "blender" and "." not in os.path.basename(fp):
+                fp += ".png"
+            poses.append(nerf_matrix_to_ngp(np.array(fr["transform_matrix"], dtype=np.float32), scale, offset))
+            img = Image.open(fp)
+            img = img.convert("RGBA" if img.mode in ("RGBA", "LA", "P") else "RGB")
+            if H is None:
+                W, H = img.size[0] // downscale, img.size[1] // downscale
+            if img.size != (W, H):
+                img = img.resize((W, H), Image.BOX)
+            images.append(np.asarray(img, dtype=np.float32) / 255.0)
+        self.H, self.W = H, W
+        self.poses = torch.from_numpy(np.stack(poses)).to(device)
+        self.images = torch.from_numpy(np.stack(images)).to(device)
+        if "fl_x" in transform or "fl_y" in transform:
+            fl_x = (transform["fl_x"] if "fl_x" in transform else transform["fl_y"]) / downscale
+            fl_y = (transform["fl_y"] if "fl_y" in transform else transform["fl_x"]) / downscale
+        elif "camera_angle_x" in transform or "camera_angle_y" in transform:
+            fl_x = W / (2 * math.tan(transform["camera_angle_x"] / 2)) if "camera_angle_x" in transform else None
+            fl_y = H / (2 * math.tan(transform["camera_angle_y"] / 2)) if "camera_angle_y" in transform else None
+            fl_x = fl_x if fl_x is not None else fl_y
+            fl_y = fl_y if fl_y is not None else fl_x
+        else:
+            raise RuntimeError("NeRFDataset: no focal length (fl_x/fl_y or camera_angle_x/y) in the transforms")
+        cx = transform["cx"] / downscale if "cx" in transform else W / 2
+        cy = transform["cy"] / downscale if "cy" in transform else H / 2
+        self.intrinsics = np.array([fl_x, fl_y, cx, cy], dtype=np.float32)
+        self.radius = float(self.poses[:, :3, 3].norm(dim=-1).mean())
+
+    def sample(self, index=None, generator=None):
+        if index is None:
+            index = int(torch.randint(0, self.poses.shape[0], (1,), generator=generator).item())
+        poses = self.poses[index:index + 1]
+        rays = get_rays(poses, self.intrinsics, self.H, self.W, self.num_rays, generator=generator)
+        C = self.images.shape[-1]
+        images = torch.gather(self.images[index:index + 1].view(1, -1, C), 1,
+                              rays["inds"].unsqueeze(-1).expand(1, rays["inds"].shape[-1], C))
+        return {"H": self.H, "W": self.W, "rays_o": rays["rays_o"], "rays_d": rays["rays_d"], "images": images,
+                "index": index}
