@@ -15,20 +15,21 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _setup(cuda, num_rays=1024, mean_count=30000):
+def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield
     torch.manual_seed(0)
-    model = NeRFNetwork(bound=1, cuda_ray=True, density_thresh=10).to(cuda)
+    model = NeRFNetwork(bound=bound, cuda_ray=True, density_thresh=10).to(cuda)
     with torch.no_grad():  # a non-trivial field: larger table values than the 1e-4 init
         model.encoder.embeddings.normal_(0, 0.05)
-    model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(cuda))
+    bits = lego_bitfield(cascade=model.cascade, bound=float(bound))
+    model.density_bitfield.copy_(torch.from_numpy(bits).to(cuda))
     ref = copy.deepcopy(model)
     data = SyntheticLego(cuda, num_rays=num_rays)
     M = mean_count + 128 - mean_count % 128  # what run_cuda's align=128 makes of mean_count
     ref.mean_count = mean_count
-    ft = FusedTrainer(model, data, M=M, seed=3)
+    ft = FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma)
     return model, ref, data, ft
 
 
@@ -38,7 +39,7 @@ def _ref_forward_backward(ref, ft, scale):
     ref.train()
     with torch.autocast("cuda", dtype=torch.float16):
         out = ref.render(rays_o[None], rays_d[None], staged=False, bg_color=bg[None], perturb=False,
-                         force_all_rays=False, dt_gamma=0.0, max_steps=1024)
+                         force_all_rays=False, dt_gamma=ft.dt_gamma, max_steps=1024)
         pred = out["image"][0]
         gt = rgba[:, :3] * rgba[:, 3:] + bg * (1 - rgba[:, 3:])
         loss = ((pred - gt) ** 2).mean(-1).mean()
@@ -75,8 +76,12 @@ def test_lego_sampler(cuda):
     assert not torch.equal(r0, ft.rays_d)
 
 
-def test_fused_forward_backward_matches_autograd(cuda):
-    model, ref, data, ft = _setup(cuda)
+# Config 2 (Lego: bound 1, one cascade, dt_gamma 0) and the Fox-like Config 3
+# shape (bound 2, two cascades, dt_gamma 1/128: the serially marched rays)
+@pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
+def test_fused_forward_backward_matches_autograd(cuda, bound, dt_gamma):
+    model, ref, data, ft = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
+    assert model.cascade == (1 if bound == 1 else 2)
     ft._sample()
     ft.noises.zero_()  # the autograd call below marches with perturb=False
     ft._forward_backward()
@@ -164,8 +169,9 @@ def test_pipelined_steps_match_serial_steps(cuda):
     assert torch.equal(a.model.step_counter, b.model.step_counter)
 
 
-def test_fused_training_reduces_loss_and_captures(cuda):
-    model, ref, data, ft = _setup(cuda, num_rays=4096, mean_count=100000)
+@pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
+def test_fused_training_reduces_loss_and_captures(cuda, bound, dt_gamma):
+    model, ref, data, ft = _setup(cuda, num_rays=4096, mean_count=100000, bound=bound, dt_gamma=dt_gamma)
     losses = []
     for _ in range(4):
         ft.step()
