@@ -304,12 +304,15 @@ class FusedTrainer:
         update, and both networks' MLP fragment images, in one launch."""
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         m, d, pk = self.model, self.data, self._pk
+        # data parallel: the fp16 weights are still being all-gathered while
+        # the batch is drawn, so the networks are packed in _network instead
+        nets = 2 if self.world == 1 else 0
         nat.check(lib.ngp_fused_step_head(P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N,
                                           self._boxes, self._nboxes, self._aabb, float(m.min_near), self.seed,
                                           P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
                                           P(self.nears), P(self.fars), P(self.noises), P(self.counter),
                                           P(m.step_counter), 2.0, 0.5, self.growth_interval, 1, P(self.loss_ray),
-                                          2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"],
+                                          nets, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"],
                                           P(self.grid_ws) if self._grid_counter_bytes else None,
                                           self._grid_counter_bytes, s),
                   "fused_step_head")
@@ -342,6 +345,8 @@ class FusedTrainer:
                                               P(self.enc_out), M, cnt, *grid_args[:-1], 0, s), "grid_encode_fused")
         self._tick("grid_encode_forward")
         sn, cn, img, pk = self.sig_net, self.col_net, self.mlp_img, self._pk
+        if self.world > 1:  # after the all-gather of the fp16 forward copy (see _sample)
+            chk(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
         chk(lib.ngp_nerf_sigma_forward(P(self.enc_out), P(self.w_half[1]), P(img[0]), M, cnt, 32, sn.hidden_dim,
                                        sn.num_layers, P(self.h_sigma), P(self.sigma), P(self.color_in),
                                        P(self.dirs), float(m.density_scale), _PAIR, s), "sigma_mlp")
