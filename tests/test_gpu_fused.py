@@ -145,6 +145,25 @@ def test_fused_optimizer_skips_on_inf(cuda):
     assert all(int(torch.isinf(g.float()).sum()) == 0 for g in ft.grads)
 
 
+@pytest.mark.parametrize("deferred", [False, True])
+def test_fused_optimizer_skips_when_unscale_overflows(cuda, deferred):
+    """A scale backed off to 0 makes 1/scale inf: torch's unscale turns every
+    grad (zeros included) into NaN/inf and GradScaler skips. The fp16 grads
+    themselves are finite, so only the optimizer can see it."""
+    model, ref, data, ft = _setup(cuda)
+    ft.grads[1][3] = 0.5
+    before = [p.detach().clone() for p in ft.params]
+    ft._state_f()[0] = 0.0
+    ft._optimizer(defer=deferred)
+    if deferred:  # the bookkeeping runs in the next step head
+        ft._sample()
+    torch.cuda.synchronize()
+    for a, b in zip(ft.params, before):
+        assert torch.equal(a.detach(), b)
+    assert float(ft._state_f()[0]) == 0.0 and int(ft._state_i()[6]) == 0  # backed off, no Adam step
+    assert int(ft._state_i()[5]) == 0  # the flag was consumed by the scaler update
+
+
 def test_pipelined_steps_match_serial_steps(cuda):
     """step() overlaps the previous step's optimizer with sampling + marching
     (and replays a captured graph of that): after flush() the parameters must
@@ -359,3 +378,58 @@ def test_checkpoint_roundtrip_and_torch_formats(cuda):
     for x, y in zip(a.params, b.params):
         assert torch.equal(x.detach(), y.detach())
     assert a.optimizer_steps == b.optimizer_steps and a.scale == b.scale
+
+
+def test_composite_loss_large_densities_match_serial(cuda):
+    """The fused composite's prefix-sum transmittance against the reference's
+    serial loop (raymarching.cu composite_rays_train_forward) at the densities a
+    hard-surfaced scene trains into: sigma * delta far above the running
+    prefix, and sigma = inf (exp overflow of a large density logit). The
+    serial T *= 1 - alpha stays finite there; so must the fused form."""
+    import ctypes
+    import _ngp_native as nat
+    _, _, _, ft = _setup(cuda)
+    rng = np.random.default_rng(5)
+    N, S = 48, 96
+    M = N * S
+    sigma = rng.uniform(0, 30, M).astype(np.float32)
+    for r in range(0, N, 3):  # a huge density a few samples into every third ray
+        sigma[r * S + 2 + r % 7] = [1e9, 3e7, np.inf][r % 3]
+    deltas = np.stack([rng.uniform(0.002, 0.01, M), rng.uniform(0.002, 0.01, M)], -1).astype(np.float32)
+    col = rng.normal(0, 2, (M, 16)).astype(np.float16)
+    h = rng.normal(0, 1, (M, 16)).astype(np.float16)
+    rays = np.stack([np.arange(N), np.arange(N) * S, np.full(N, S)], -1).astype(np.int32)
+    gt = rng.uniform(0, 1, (N, 4)).astype(np.float32)
+    bg = rng.uniform(0, 1, (N, 3)).astype(np.float32)
+    T_thresh = 1e-4
+    # serial reference (fp64 accumulation, fp32 sigma * delta and half sigmoid)
+    rgb = (1 / (1 + np.exp(-col[:, :3].astype(np.float32)))).astype(np.float16).astype(np.float64)
+    want = np.zeros((N, 3))
+    for r in range(N):
+        T, acc, ws = 1.0, np.zeros(3), 0.0
+        for k in range(r * S, r * S + S):
+            with np.errstate(over="ignore", invalid="ignore"):
+                alpha = 1.0 - np.exp(-float(np.float32(sigma[k]) * np.float32(deltas[k, 0])))
+            w = alpha * T
+            acc += w * rgb[k]
+            ws += w
+            T *= 1 - alpha
+            if T < T_thresh:
+                break
+        want[r] = acc + (1 - ws) * bg[r]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    d_sigma, d_col, d_h, d_del, d_rays, d_gt, d_bg = map(t, (sigma, col, h, deltas, rays, gt, bg))
+    g_col = torch.zeros(M, 16, dtype=torch.float16, device=cuda)
+    g_h = torch.zeros(M, 16, dtype=torch.float16, device=cuda)
+    img = torch.zeros(N, 3, device=cuda)
+    ws_out = torch.zeros(N, device=cuda)
+    loss = torch.zeros(N, device=cuda)
+    P = nat.ptr
+    nat.check(nat.lib().ngp_nerf_composite_loss(
+        P(d_sigma), P(d_col), P(d_h), P(d_del), P(d_rays), M, N, T_thresh, 1.0, P(d_gt), 4, P(d_bg),
+        P(ft.state), P(g_col), P(g_h), P(img), P(ws_out), P(loss), nat.stream_of(img)), "composite_loss")
+    torch.cuda.synchronize()
+    got = img.double().cpu().numpy()
+    assert np.isfinite(got).all() and torch.isfinite(loss).all()
+    assert torch.isfinite(g_col.float()).all() and torch.isfinite(g_h.float()).all()
+    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)

@@ -287,8 +287,14 @@ NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __rest
     }
     const float sd = sg * c.d0;
     const float incl = scan_incl(sd, lane);
+    // the exclusive prefix is the previous lane's inclusive one, NOT incl - sd:
+    // once the density is large (sigma * delta >> the prefix, or inf) that
+    // difference cancels to garbage (inf - inf = NaN), where the reference's
+    // serial T *= 1 - alpha stays exact
+    float excl = __shfl_up(incl, 1, 64);
+    if (lane == 0) excl = 0.0f;
     const float alpha = 1.0f - expf(-sd);
-    const float Tbefore = expf(-(S + (incl - sd)));
+    const float Tbefore = expf(-(S + excl));
     c.Tafter = expf(-(S + incl));
     c.w = alpha * Tbefore;
     c.t = tacc + scan_incl(d1, lane);
@@ -493,15 +499,22 @@ struct AdamArgs {
 constexpr uint32_t kAdamThreads = 256, kAdamChunk = kAdamThreads * 8;
 __global__ void __launch_bounds__(kAdamThreads)
 k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa) {
-    const bool skip = st->found_inf != 0;
-    if (aa.defer_end && blockIdx.x == 0 && threadIdx.x == 0) st->end_pending = 1;  // read by k_step_head only
+    // GradScaler checks the UNSCALED grads: once the scale has backed off so far
+    // that 1/scale is inf, every element (0 * inf = NaN) is non-finite and the
+    // step is skipped, which the checks of the scaled fp16 grads cannot see
+    const float inv_scale = (float)(1.0 / (double)st->scale) * aa.grad_mult;
+    const bool inv_bad = !__builtin_isfinite(inv_scale);
+    const bool skip = st->found_inf != 0 || inv_bad;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (inv_bad) st->found_inf = 1;  // the scaler update backs off, as torch's would
+        if (aa.defer_end) st->end_pending = 1;  // read by k_step_head only
+    }
     const int32_t step = st->adam_step + 1;
     const double lr = (double)aa.base_lr * pow(0.1, fmin((double)st->epoch / (double)aa.iters, 1.0));
     const double bc1 = 1.0 - pow((double)aa.beta1, step);
     const double bc2 = 1.0 - pow((double)aa.beta2, step);
     const float step_size = (float)(lr / bc1);
     const float inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
-    const float inv_scale = (float)(1.0 / (double)st->scale) * aa.grad_mult;
     typedef _Float16 half4 __attribute__((ext_vector_type(4)));
     auto adam1 = [&](float& p, float& m, float& v, float gh) {
         const float gk = gh * inv_scale;
