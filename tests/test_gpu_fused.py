@@ -433,3 +433,24 @@ def test_composite_loss_large_densities_match_serial(cuda):
     assert np.isfinite(got).all() and torch.isfinite(loss).all()
     assert torch.isfinite(g_col.float()).all() and torch.isfinite(g_h.float()).all()
     np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+
+
+def test_long_run_stays_finite_without_overflow(cuda):
+    """400 captured steps at the bench configuration: the loss stays finite and
+    GradScaler never backs off (before the composite's exclusive-prefix fix,
+    large trained densities made runs overflow and spiral into NaN losses;
+    tools/stability.py runs the longer multi-seed version)."""
+    from nerf.fused import FusedTrainer
+    from nerf.network_ff import NeRFNetwork
+    from nerf.provider import SyntheticLego, lego_bitfield
+    torch.manual_seed(3)
+    m = NeRFNetwork(bound=1, cuda_ray=True).to(cuda)
+    m.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(cuda))
+    ft = FusedTrainer(m, SyntheticLego(cuda, num_rays=4096), M=101762, seed=3)
+    ft.capture()
+    for _ in range(400):
+        ft.step()
+    torch.cuda.synchronize()
+    assert ft.scale == 65536.0
+    assert np.isfinite(ft.last_loss) and ft.last_loss < 0.01
+    assert torch.isfinite(ft.flat_param).all()

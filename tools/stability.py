@@ -1,4 +1,4 @@
-"""Long-run stability: fused step vs the reference-API autograd step, several
+"""Long-run stability: fused step (eager / graph) vs the reference-API autograd step, several
 seeds; reports the first overflow (GradScaler backoff) and the first
 non-finite loss / parameter of each run."""
 import os, sys
