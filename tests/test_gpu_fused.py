@@ -437,7 +437,7 @@ def test_composite_loss_large_densities_match_serial(cuda):
 
 def test_long_run_stays_finite_without_overflow(cuda):
     """400 captured steps at the bench configuration: the loss stays finite and
-    GradScaler never backs off (before the composite's exclusive-prefix fix,
+    GradScaler does not spiral down (before the composite's exclusive-prefix fix,
     large trained densities made runs overflow and spiral into NaN losses;
     tools/stability.py runs the longer multi-seed version)."""
     from nerf.fused import FusedTrainer
@@ -451,6 +451,6 @@ def test_long_run_stays_finite_without_overflow(cuda):
     for _ in range(400):
         ft.step()
     torch.cuda.synchronize()
-    assert ft.scale == 65536.0
+    assert ft.scale >= 32768.0  # no backoff in 13 x 600-step runs; one would still be legitimate
     assert np.isfinite(ft.last_loss) and ft.last_loss < 0.01
     assert torch.isfinite(ft.flat_param).all()
