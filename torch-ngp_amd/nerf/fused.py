@@ -30,6 +30,7 @@ scan/emit are both memory-bound and slowed each other more than they
 overlapped (profiles/r01u_overlap_trace.txt).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -40,6 +41,7 @@ import _ngp_native as nat
 from .provider import LEGO_BOXES, LEGO_COLORS
 
 _F16 = nat.DTYPE_CODE[torch.float16]
+_F32 = nat.DTYPE_CODE[torch.float32]
 _RELU, _NONE = 0, 6
 _DEFER, _GEO, _PAIR = 1, 2, 4  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO, NGP_FFMLP_PAIR_MAJOR
 _SCAN, _PRECHECKED = 1, 2  # NGP_SCALER_SCAN, NGP_SCALER_PRECHECKED
@@ -169,13 +171,24 @@ class FusedTrainer:
         self._nboxes = len(LEGO_BOXES)
         self._intr = (ctypes.c_float * 4)(*[float(v) for v in dataset.intrinsics])
         self._aabb = (ctypes.c_float * 6)(*model.aabb_train.detach().cpu().tolist())
+        # World 1: the grid forward reads the fp32 table and rounds each value to
+        # half as it loads it (the same values autocast's cast gives), so Adam
+        # does not write an fp16 copy of the table (2 of its 28 B / parameter).
+        # Data parallel: the fp16 copy is what the all-gather moves.
+        self.table32 = W == 1 and os.environ.get("NGP_FUSED_TABLE16") != "1"
+        if self.table32:
+            nt = self._starts[1]  # the table, then the two MLPs
+            sec = [(0, nt, False), (nt, chunk - nt, True)]
+        else:
+            sec = [(0, chunk, True)]
         self._opt = dict(
-            params=_vp_array([nat.ptr(self.flat_param) + 4 * self.lo]),
-            grads=_vp_array([nat.ptr(self.grad_shard)]),
-            m=_vp_array([nat.ptr(self.exp_avg)]),
-            v=_vp_array([nat.ptr(self.exp_avg_sq)]),
-            half=_vp_array([nat.ptr(self.flat_half) + 2 * self.lo]),
-            sizes=(ctypes.c_uint64 * 1)(chunk))
+            params=_vp_array([nat.ptr(self.flat_param) + 4 * (self.lo + a) for a, _, _ in sec]),
+            grads=_vp_array([nat.ptr(self.grad_shard) + 2 * a for a, _, _ in sec]),
+            m=_vp_array([nat.ptr(self.exp_avg) + 4 * a for a, _, _ in sec]),
+            v=_vp_array([nat.ptr(self.exp_avg_sq) + 4 * a for a, _, _ in sec]),
+            half=_vp_array([nat.ptr(self.flat_half) + 2 * (self.lo + a) if hv else None for a, _, hv in sec]),
+            sizes=(ctypes.c_uint64 * len(sec))(*[n for _, n, _ in sec]),
+            n=len(sec))
         self._nccl = W > 1 and dist.get_backend() == "nccl"
         # GradScaler's inf check is made by the kernels that write the grads
         # (grid backward, MLP dW reduce) into this flag: the optimizer's found-inf
@@ -341,7 +354,8 @@ class FusedTrainer:
         pk = self._pk
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
-        chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(self.w_half[0]), _F16, P(e.offsets),
+        table, tdt = (self.params[0], _F32) if self.table32 else (self.w_half[0], _F16)
+        chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets),
                                               P(self.enc_out), M, cnt, *grid_args[:-1], 0, s), "grid_encode_fused")
         self._tick("grid_encode_forward")
         sn, cn, img, pk = self.sig_net, self.col_net, self.mlp_img, self._pk
@@ -390,7 +404,7 @@ class FusedTrainer:
         o, chk, N, cnt = self._opt, nat.check, self.N, P(self.counter)
         # world 1 zeroes the grads here; data parallel: the shard is the reduce-scatter's
         # output and the flat gradient is cleared after the collective read it
-        args = (1, o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
+        args = (o["n"], o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
                 self.betas[1], self.eps, self.iters, int(self.world == 1), 1.0)
         # inside a step (world 1) the found-inf flag was set by the backward's kernels;
         # otherwise (flush, direct calls, the averaged shard) the grads are swept
