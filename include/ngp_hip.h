@@ -124,6 +124,23 @@ int ngp_march_rays_train_prebuilt(const float* rays_o, const float* rays_d, cons
                                   const float* fars, float* xyzs, float* dirs, float* deltas,
                                   int32_t* rays, int32_t* counter, const float* noises,
                                   void* workspace, size_t workspace_bytes, void* stream);
+/* ngp_march_rays_train_prebuilt plus the tail of a fused step whose optimizer
+ * update was launched by ngp_fused_optimizer_update_head: the deferred
+ * GradScaler / LR / loss bookkeeping (scaler arguments as
+ * ngp_fused_optimizer_step; loss_ray: the previous batch's N per-ray losses)
+ * and ngp_ffmlp_pack of n_nets networks, as an extra row of blocks of the
+ * emit launch. */
+int ngp_march_rays_train_prebuilt_tail(const float* rays_o, const float* rays_d, const uint8_t* grid,
+                                       float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
+                                       uint32_t C, uint32_t H, uint32_t M, const float* nears,
+                                       const float* fars, float* xyzs, float* dirs, float* deltas,
+                                       int32_t* rays, int32_t* counter, const float* noises,
+                                       void* workspace, size_t workspace_bytes, void* state,
+                                       float growth_factor, float backoff_factor, int32_t growth_interval,
+                                       int32_t scaler_enabled, const float* loss_ray, int32_t n_nets,
+                                       const void* const* mlp_weights, const uint32_t* in_dims,
+                                       const uint32_t* hidden_dims, const uint32_t* num_layers,
+                                       void* const* images, void* stream);
 
 /* raymarching.h:14, raymarching.cu:580-588 */
 int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs, const float* deltas,
@@ -366,6 +383,21 @@ int ngp_fused_step_head(const float* poses, uint32_t n_poses, const float* intri
                         int32_t n_nets, const void* const* mlp_weights, const uint32_t* in_dims,
                         const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* images,
                         void* clear, uint32_t clear_bytes, void* stream);
+/* ngp_fused_optimizer_update (bookkeeping deferred) and the batch + clear
+ * parts of ngp_fused_step_head (same arguments) as block ranges of one launch;
+ * the deferred bookkeeping and the MLP packs then go to
+ * ngp_march_rays_train_prebuilt_tail. */
+int ngp_fused_optimizer_update_head(int32_t n_tensors, float* const* params, void* const* grads,
+                                    float* const* exp_avg, float* const* exp_avg_sq,
+                                    void* const* half_params, const uint64_t* sizes, float lr, float beta1,
+                                    float beta2, float eps, int32_t iters, int32_t zero_grads,
+                                    float grad_mult, int32_t scaler_enabled, void* state,
+                                    const float* poses, uint32_t n_poses, const float* intrinsics4,
+                                    uint32_t H, uint32_t W, uint32_t N, const float* boxes, int32_t nboxes,
+                                    const float* aabb6, float min_near, uint32_t seed, float* rays_o,
+                                    float* rays_d, float* rgba, float* bg, float* nears, float* fars,
+                                    float* noises, int32_t* counter, int32_t* step_counter, void* clear,
+                                    uint32_t clear_bytes, void* stream);
 
 /* Data-parallel GradScaler guard for the sharded optimizer (nerf/fused.py,
  * world > 1), run on each rank's own fp16 gradient before the averaging

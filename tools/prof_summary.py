@@ -34,7 +34,10 @@ def main(tag, out=None):
     steps = int(os.environ.get("STEPS", "30"))
     spin = next((i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]), len(rows))
     name = lambda i: rows[i]["Kernel_Name"] if i < len(rows) else ""  # noqa: E731
-    starts = [i for i in range(spin) if "k_adam_multi" in name(i) and "k_step_head" in name(i + 1)]
+    # a step starts with k_adam_head (merged optimizer + batch launch) or, with
+    # NGP_FUSED_SPLIT_HEAD=1 / older builds, k_adam_multi followed by k_step_head
+    starts = [i for i in range(spin) if "k_adam_head" in name(i) or
+              ("k_adam_multi" in name(i) and "k_step_head" in name(i + 1))]
     sel = starts[-steps:]
     per = collections.defaultdict(list)
     spans = []

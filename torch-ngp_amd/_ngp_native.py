@@ -40,6 +40,10 @@ SIGNATURES = {
     "ngp_march_occupancy_build": [c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_sz, c_vp],
     "ngp_march_rays_train_prebuilt": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
+    "ngp_march_rays_train_prebuilt_tail": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
+                                           c_vp, c_f32, c_f32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp],
     "ngp_march_rays_train": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_composite_rays_train_forward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_vp, c_vp,
@@ -79,6 +83,10 @@ SIGNATURES = {
     "ngp_fused_step_head": [c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32, c_vp,
                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_i32, c_i32,
                             c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp],
+    "ngp_fused_optimizer_update_head": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
+                                        c_i32, c_i32, c_f32, c_i32, c_vp,
+                                        c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32,
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp],
     "ngp_ffmlp_pack": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_ffmlp_forward_rows": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
                                c_vp, c_vp],

@@ -23,12 +23,17 @@
 #include "ffmlp_pack.h"
 #include "ngp_common.h"
 #include "ngp_dpp.h"
+#include "ngp_step.h"
 #include "sh_basis.h"
 
 #include <algorithm>
 #include <cfloat>
 
 namespace {
+
+using ngp_step::ScalerArgs;
+using ngp_step::StepState;
+using ngp_step::step_end_block;
 
 constexpr int kMaxBoxes = 8;
 constexpr int kMaxTensors = 8;
@@ -38,24 +43,6 @@ NGP_DEV uint32_t clip_rows(uint32_t B, const int32_t* count) {
     const int32_t c = *count;
     return c <= 0 ? 0u : min(B, (uint32_t)c);
 }
-
-// ---- device step state ------------------------------------------------------
-struct StepState {
-    float scale;           // GradScaler scale
-    float loss_sum;        // sum over rays of the per-ray MSE (this step)
-    float last_loss;       // mean loss of the last finished step
-    float pad;
-    int32_t growth_tracker;
-    int32_t found_inf;
-    int32_t adam_step;     // optimizer steps taken (skipped steps excluded)
-    int32_t epoch;         // LambdaLR epoch (every step)
-    int32_t iter;          // finished steps (k_step_end)
-    int32_t draw;          // batches drawn by the sampler (k_lego_rays)
-    int32_t lego_done;     // k_lego_rays' finished-block count (last block bumps draw)
-    int32_t local_inf;     // data parallel: this rank's own grads held an inf/nan (k_guard_*)
-    int32_t end_pending;   // an optimizer update whose GradScaler/LR bookkeeping is deferred to k_step_head
-    int32_t pad3[3];
-};
 
 // counter-based RNG (no state, graph-safe): 32-bit mix of (seed, a, b, c)
 NGP_DEV uint32_t mix32(uint32_t x) {
@@ -497,15 +484,15 @@ struct AdamArgs {
 // groups of each stream in flight. A chunk inside one tensor (all but the few
 // at the seams) takes its pointers from scalar loads.
 constexpr uint32_t kAdamThreads = 256, kAdamChunk = kAdamThreads * 8;
-__global__ void __launch_bounds__(kAdamThreads)
-k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa) {
+NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const AdamArgs& aa, uint32_t blk,
+                        uint32_t nblk) {
     // GradScaler checks the UNSCALED grads: once the scale has backed off so far
     // that 1/scale is inf, every element (0 * inf = NaN) is non-finite and the
     // step is skipped, which the checks of the scaled fp16 grads cannot see
     const float inv_scale = (float)(1.0 / (double)st->scale) * aa.grad_mult;
     const bool inv_bad = !__builtin_isfinite(inv_scale);
     const bool skip = st->found_inf != 0 || inv_bad;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (blk == 0 && threadIdx.x == 0) {
         if (inv_bad) st->found_inf = 1;  // the scaler update backs off, as torch's would
         if (aa.defer_end) st->end_pending = 1;  // read by k_step_head only
     }
@@ -525,7 +512,7 @@ k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa) {
     };
     const uint64_t total = tl.start[tl.n];
     const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
-    for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    for (uint64_t c = blk; c < nchunks; c += nblk) {
         const uint64_t c0 = c * kAdamChunk, c1 = min(c0 + kAdamChunk, total);
         const int k = find_tensor(tl, c0);
         if (find_tensor(tl, c1 - 1) == k && c1 - tl.start[k] <= tl.size[k]) {
@@ -582,6 +569,11 @@ k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa) {
     }
 }
 
+__global__ void __launch_bounds__(kAdamThreads)
+k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa) {
+    adam_sweep(tl, st, aa, blockIdx.x, gridDim.x);
+}
+
 // ---- data-parallel GradScaler guard ----------------------------------------------
 // With the sharded optimizer (nerf/fused.py, world > 1) each rank sees only
 // its shard of the reduced gradient, but GradScaler must skip (and back off)
@@ -612,53 +604,6 @@ k_guard_poison(ngp_half* __restrict__ g, uint64_t chunk, int32_t world, StepStat
     if (threadIdx.x == 0) st->local_inf = 0;
 }
 
-struct ScalerArgs {
-    float growth_factor, backoff_factor;
-    int32_t growth_interval, enabled;
-    float inv_n;
-};
-
-// GradScaler.update, LambdaLR epoch, Adam step count, loss bookkeeping (mean
-// of the per-ray losses, fixed-order tree sum); also records this step's
-// sample count into step_counter[iter % 16]
-NGP_DEV void step_end_block(StepState* __restrict__ st, const ScalerArgs& sa, const int32_t* __restrict__ counter,
-                            int32_t* __restrict__ step_counter, const float* __restrict__ loss_ray, uint32_t n_rays) {
-    __shared__ float part[256];
-    float acc = 0.0f;
-    if (loss_ray)
-        for (uint32_t i = threadIdx.x; i < n_rays; i += 256) acc += loss_ray[i];
-    part[threadIdx.x] = acc;
-    __syncthreads();
-    for (uint32_t o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
-        __syncthreads();
-    }
-    if (threadIdx.x != 0) return;
-    if (loss_ray) st->loss_sum = part[0];
-    const bool inf = st->found_inf != 0;
-    if (sa.enabled) {
-        if (inf) {
-            st->scale *= sa.backoff_factor;
-            st->growth_tracker = 0;
-        } else if (++st->growth_tracker == sa.growth_interval) {
-            st->scale *= sa.growth_factor;
-            st->growth_tracker = 0;
-        }
-    }
-    if (!inf) st->adam_step += 1;
-    st->epoch += 1;
-    if (step_counter) {
-        const int slot = st->iter % 16;
-        step_counter[slot * 2] = counter[0];
-        step_counter[slot * 2 + 1] = counter[1];
-    }
-    st->iter += 1;
-    st->last_loss = st->loss_sum * sa.inv_n;
-    st->loss_sum = 0.0f;
-    st->found_inf = 0;
-    st->end_pending = 0;
-}
-
 __global__ void __launch_bounds__(256)
 k_step_end(StepState* __restrict__ st, ScalerArgs sa, const int32_t* __restrict__ counter,
            int32_t* __restrict__ step_counter, const float* __restrict__ loss_ray, uint32_t n_rays) {
@@ -687,6 +632,36 @@ k_step_head(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState
         ngp_pack::build_frags(j.image, j.w, j.m, j.transposed != 0);
     }
 }
+
+// The fused step's first launch when an optimizer update is pending (world 1):
+// Adam's sweep, the next batch and the grid backward's cursor clear as block
+// ranges of one kernel. The three touch disjoint state (Adam: parameters,
+// moments, grads and the scaler fields it reads; the sampler: draw / lego_done /
+// counter). The bookkeeping and MLP packs, which need Adam finished, ride in
+// the march emit launch (raymarching.hip EmitTail).
+__global__ void __launch_bounds__(kAdamThreads)
+k_adam_head(TensorList tl, StepState* __restrict__ st, AdamArgs aa, uint32_t nadam, const float* __restrict__ poses,
+            LegoScene sc, uint32_t N, LegoOut out, uint32_t nlego, uint4* __restrict__ clear, uint32_t clear16) {
+    if (blockIdx.x < nadam) {
+        adam_sweep(tl, st, aa, blockIdx.x, nadam);
+        return;
+    }
+    const uint32_t b = blockIdx.x - nadam;
+    if (b < nlego) {
+        lego_rays_block(b, nlego, poses, sc, N, st, out);
+    } else {
+        for (uint32_t i = threadIdx.x; i < clear16; i += blockDim.x) clear[i] = uint4{0u, 0u, 0u, 0u};
+    }
+}
+
+struct HeadLaunch {  // the batch + clear parts of k_adam_head
+    const float* poses;
+    LegoScene sc;
+    uint32_t N;
+    LegoOut out;
+    uint4* clear;
+    uint32_t clear16;
+};
 
 TensorList make_list(int n, float* const* p, void* const* g, float* const* m, float* const* v,
                      void* const* ph, const uint64_t* sizes) {
@@ -734,7 +709,7 @@ int optimizer_launch(int32_t n_tensors, float* const* params, void* const* grads
                      float beta1, float beta2, float eps, int32_t iters, int32_t zero_grads, float grad_mult,
                      float growth_factor, float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
                      uint32_t num_rays, const int32_t* counter, int32_t* step_counter, const float* loss_ray,
-                     void* state, void* stream, bool defer_end) {
+                     void* state, void* stream, bool defer_end, const HeadLaunch* head = nullptr) {
     NGP_REQUIRE(n_tensors >= 1 && n_tensors <= kMaxTensors, NGP_ERR_ARG,
                 "fused_optimizer_step: 1..%d tensors", kMaxTensors);
     for (int k = 0; k < n_tensors; ++k)
@@ -754,7 +729,14 @@ int optimizer_launch(int32_t n_tensors, float* const* params, void* const* grads
     AdamArgs aa{lr, beta1, beta2, eps, iters, zero_grads, grad_mult, defer_end ? 1 : 0};
     const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
     const uint64_t adam_blocks = std::min<uint64_t>(nchunks, 16ull * ngp_num_cus());
-    k_adam_multi<<<(uint32_t)(adam_blocks ? adam_blocks : 1), kAdamThreads, 0, s>>>(tl, st, aa);
+    const uint32_t na = (uint32_t)(adam_blocks ? adam_blocks : 1);
+    if (head) {
+        const uint32_t nlego = ngp_div_up(head->N, 256);
+        k_adam_head<<<na + nlego + 1, kAdamThreads, 0, s>>>(tl, st, aa, na, head->poses, head->sc, head->N,
+                                                              head->out, nlego, head->clear, head->clear16);
+    } else {
+        k_adam_multi<<<na, kAdamThreads, 0, s>>>(tl, st, aa);
+    }
     if (!defer_end) {
         ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled,
                       num_rays ? 1.0f / (float)num_rays : 0.0f};
@@ -885,6 +867,31 @@ extern "C" int ngp_fused_step_head(const float* poses, uint32_t n_poses, const f
         poses, sc, N, static_cast<StepState*>(state), out, nlego, sa, loss_ray, jobs, static_cast<uint4*>(clear),
         clear ? clear_bytes / 16 : 0u);
     return ngp_check_launch("fused_step_head");
+}
+
+extern "C" int ngp_fused_optimizer_update_head(
+    int32_t n_tensors, float* const* params, void* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+    void* const* half_params, const uint64_t* sizes, float lr, float beta1, float beta2, float eps, int32_t iters,
+    int32_t zero_grads, float grad_mult, int32_t scaler_enabled, void* state, const float* poses, uint32_t n_poses,
+    const float* intrinsics4, uint32_t H, uint32_t W, uint32_t N, const float* boxes, int32_t nboxes,
+    const float* aabb6, float min_near, uint32_t seed, float* rays_o, float* rays_d, float* rgba, float* bg,
+    float* nears, float* fars, float* noises, int32_t* counter, int32_t* step_counter, void* clear,
+    uint32_t clear_bytes, void* stream) {
+    NGP_REQUIRE(state, NGP_ERR_ARG, "fused_optimizer_update_head: null state");
+    NGP_REQUIRE(nboxes >= 0 && nboxes <= kMaxBoxes, NGP_ERR_ARG, "step_head: at most %d boxes", kMaxBoxes);
+    NGP_REQUIRE(n_poses > 0 && H > 0 && W > 0 && N > 0, NGP_ERR_ARG, "step_head: empty pose set, image or batch");
+    NGP_REQUIRE(clear_bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(clear) & 15) == 0, NGP_ERR_ARG,
+                "step_head: clear must be 16-byte aligned, a multiple of 16 bytes");
+    HeadLaunch hl{};
+    hl.poses = poses;
+    hl.sc = make_scene(n_poses, intrinsics4, H, W, boxes, nboxes, aabb6, min_near, seed);
+    hl.N = N;
+    hl.out = LegoOut{rays_o, rays_d, rgba, bg, nears, fars, noises, counter, step_counter};
+    hl.clear = static_cast<uint4*>(clear);
+    hl.clear16 = clear ? clear_bytes / 16 : 0u;
+    return optimizer_launch(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes, lr, beta1, beta2,
+                            eps, iters, zero_grads, grad_mult, 2.0f, 0.5f, 2000, scaler_enabled, 0, nullptr,
+                            nullptr, nullptr, state, stream, true, &hl);
 }
 
 extern "C" int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, void* state,

@@ -1,0 +1,76 @@
+// Device step state of the fused train step and its GradScaler / LR / loss
+// bookkeeping (shared by nerf_fused.hip and raymarching.hip, whose march
+// emit launch can carry the bookkeeping of a deferred optimizer update).
+#pragma once
+#include "ngp_common.h"
+
+namespace ngp_step {
+
+// ---- device step state ------------------------------------------------------
+struct StepState {
+    float scale;           // GradScaler scale
+    float loss_sum;        // sum over rays of the per-ray MSE (this step)
+    float last_loss;       // mean loss of the last finished step
+    float pad;
+    int32_t growth_tracker;
+    int32_t found_inf;
+    int32_t adam_step;     // optimizer steps taken (skipped steps excluded)
+    int32_t epoch;         // LambdaLR epoch (every step)
+    int32_t iter;          // finished steps (k_step_end)
+    int32_t draw;          // batches drawn by the sampler (k_lego_rays)
+    int32_t lego_done;     // k_lego_rays' finished-block count (last block bumps draw)
+    int32_t local_inf;     // data parallel: this rank's own grads held an inf/nan (k_guard_*)
+    int32_t end_pending;   // an optimizer update whose GradScaler/LR bookkeeping is deferred to k_step_head
+    int32_t pad3[3];
+};
+
+
+struct ScalerArgs {
+    float growth_factor, backoff_factor;
+    int32_t growth_interval, enabled;
+    float inv_n;
+};
+
+// GradScaler.update, LambdaLR epoch, Adam step count, loss bookkeeping (mean
+// of the per-ray losses, fixed-order tree sum); also records this step's
+// sample count into step_counter[iter % 16]
+NGP_DEV void step_end_block(StepState* __restrict__ st, const ScalerArgs& sa, const int32_t* __restrict__ counter,
+                            int32_t* __restrict__ step_counter, const float* __restrict__ loss_ray, uint32_t n_rays) {
+    __shared__ float part[256];
+    float acc = 0.0f;
+    if (loss_ray)
+        for (uint32_t i = threadIdx.x; i < n_rays; i += 256) acc += loss_ray[i];
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    if (loss_ray) st->loss_sum = part[0];
+    const bool inf = st->found_inf != 0;
+    if (sa.enabled) {
+        if (inf) {
+            st->scale *= sa.backoff_factor;
+            st->growth_tracker = 0;
+        } else if (++st->growth_tracker == sa.growth_interval) {
+            st->scale *= sa.growth_factor;
+            st->growth_tracker = 0;
+        }
+    }
+    if (!inf) st->adam_step += 1;
+    st->epoch += 1;
+    if (step_counter) {
+        const int slot = st->iter % 16;
+        step_counter[slot * 2] = counter[0];
+        step_counter[slot * 2 + 1] = counter[1];
+    }
+    st->iter += 1;
+    st->last_loss = st->loss_sum * sa.inv_n;
+    st->loss_sum = 0.0f;
+    st->found_inf = 0;
+    st->end_pending = 0;
+}
+
+
+}  // namespace ngp_step

@@ -21,8 +21,11 @@
 //   * occupancy lookups hit an LDS rank/select image of the bitfield (OccLds)
 //     instead of L2: marching is a serial dependency chain per ray, so the
 //     lookup latency is the step time.
+#include "ffmlp_pack.h"
 #include "ngp_common.h"
+#include "ngp_step.h"
 
+#include <algorithm>
 #include <cfloat>
 
 namespace {
@@ -619,12 +622,35 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
 // last group's the counter (counter[0] = end, counter[1] += N, the
 // reference's two atomics :405-406). Outputs of rays with offset + count > M
 // are skipped (reference :416).
+// Optional tail of the emit launch (the fused step, nerf/fused.py): one extra
+// row of blocks that runs the deferred GradScaler / LR / loss bookkeeping of the
+// optimizer update before this step (block 0) and packs the MLP fragment
+// images from the fp16 weights it wrote (blocks 1..), beside the emit blocks
+// instead of in a latency-bound launch of their own.
+struct EmitTail {
+    ngp_step::StepState* st;  // null: no tail row
+    ngp_step::ScalerArgs sa;
+    const float* loss_ray;
+    uint32_t n_rays, groups;  // groups: emit ray groups (gridDim.x may be wider)
+    ngp_pack::PackJobs jobs;
+};
+
 __global__ void __launch_bounds__(kMarchThreads)
 k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d, MarchConst k,
              uint32_t N, uint32_t M, const float* __restrict__ nears, const float* __restrict__ noises,
              const float* __restrict__ ts, float* __restrict__ xyzs, float* __restrict__ dirs,
              float* __restrict__ deltas, int32_t* __restrict__ rays, const uint32_t* __restrict__ scan,
-             int32_t* __restrict__ counter) {
+             int32_t* __restrict__ counter, EmitTail tail) {
+    if (blockIdx.y == kEmitSplit) {  // the tail row (block-uniform)
+        if (blockIdx.x == 0) {
+            if (tail.st->end_pending) ngp_step::step_end_block(tail.st, tail.sa, nullptr, nullptr, tail.loss_ray, tail.n_rays);
+        } else if (blockIdx.x - 1 < (uint32_t)tail.jobs.n) {
+            const ngp_pack::PackJob& j = tail.jobs.job[blockIdx.x - 1];
+            ngp_pack::build_frags(j.image, j.w, j.m, j.transposed != 0);
+        }
+        return;
+    }
+    if (blockIdx.x >= tail.groups) return;
     __shared__ uint32_t off[kMarchThreads + 1];
     __shared__ uint32_t lds_waves[kMarchThreads / 64];
     const uint32_t* __restrict__ counts = scan + 4;
@@ -642,7 +668,7 @@ k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     if (threadIdx.x == 0) off[kMarchThreads] = total;
     if (blockIdx.y == 0) {
         if (n < N) rays[(size_t)n * 3 + 1] = (int32_t)(base + excl);
-        if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        if (blockIdx.x == tail.groups - 1 && threadIdx.x == 0) {
             counter[0] = (int32_t)(base + total);
             counter[1] += (int32_t)N;
         }
@@ -977,7 +1003,7 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
                              uint32_t H, uint32_t M, const float* nears, const float* fars,
                              float* xyzs, float* dirs, float* deltas, int32_t* rays, int32_t* counter,
                              const float* noises, void* workspace, size_t workspace_bytes,
-                             bool build_image, void* stream) {
+                             bool build_image, void* stream, const EmitTail* tail = nullptr) {
     if (int e = check_cascade(C, H, max_steps)) return e;
     NGP_REQUIRE(rays && counter, NGP_ERR_ARG, "march_rays_train: null rays/counter");
     if (N == 0) return NGP_OK;
@@ -1003,8 +1029,12 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
     }
     k_march_train<<<blocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
         rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan);
-    k_march_emit<<<dim3(groups, kEmitSplit), kMarchThreads, 0, st>>>(rays_o, rays_d, k, N, M, nears, noises,
-                                                                    ts, xyzs, dirs, deltas, rays, scan, counter);
+    EmitTail et{};
+    if (tail) et = *tail;
+    et.groups = groups;
+    const uint32_t gx = tail ? std::max<uint32_t>(groups, 1u + (uint32_t)tail->jobs.n) : groups;
+    k_march_emit<<<dim3(gx, kEmitSplit + (tail ? 1u : 0u)), kMarchThreads, 0, st>>>(
+        rays_o, rays_d, k, N, M, nears, noises, ts, xyzs, dirs, deltas, rays, scan, counter, et);
     return ngp_check_launch("march_rays_train");
 }
 
@@ -1047,6 +1077,33 @@ extern "C" int ngp_march_rays_train_prebuilt(const float* rays_o, const float* r
     return march_train_impl(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, M, nears, fars,
                             xyzs, dirs, deltas, rays, counter, noises, workspace, workspace_bytes, false,
                             stream);
+}
+
+extern "C" int ngp_march_rays_train_prebuilt_tail(const float* rays_o, const float* rays_d,
+                                                  const uint8_t* grid, float bound, float dt_gamma,
+                                                  uint32_t max_steps, uint32_t N, uint32_t C, uint32_t H,
+                                                  uint32_t M, const float* nears, const float* fars,
+                                                  float* xyzs, float* dirs, float* deltas, int32_t* rays,
+                                                  int32_t* counter, const float* noises, void* workspace,
+                                                  size_t workspace_bytes, void* state, float growth_factor,
+                                                  float backoff_factor, int32_t growth_interval,
+                                                  int32_t scaler_enabled, const float* loss_ray, int32_t n_nets,
+                                                  const void* const* mlp_weights, const uint32_t* in_dims,
+                                                  const uint32_t* hidden_dims, const uint32_t* num_layers,
+                                                  void* const* images, void* stream) {
+    NGP_REQUIRE(state && loss_ray, NGP_ERR_ARG, "march_rays_train_prebuilt_tail: null state or loss_ray");
+    EmitTail tail{};
+    tail.st = static_cast<ngp_step::StepState*>(state);
+    tail.sa = ngp_step::ScalerArgs{growth_factor, backoff_factor, growth_interval, scaler_enabled,
+                                   N ? 1.0f / (float)N : 0.0f};
+    tail.loss_ray = loss_ray;
+    tail.n_rays = N;
+    if (n_nets > 0)
+        if (int e = ngp_pack::build_jobs(n_nets, mlp_weights, in_dims, hidden_dims, num_layers, images, tail.jobs))
+            return e;
+    return march_train_impl(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, M, nears, fars,
+                            xyzs, dirs, deltas, rays, counter, noises, workspace, workspace_bytes, false,
+                            stream, &tail);
 }
 
 extern "C" int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs,

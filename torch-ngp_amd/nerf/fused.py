@@ -176,6 +176,7 @@ class FusedTrainer:
         # does not write an fp16 copy of the table (2 of its 28 B / parameter).
         # Data parallel: the fp16 copy is what the all-gather moves.
         self.table32 = W == 1 and os.environ.get("NGP_FUSED_TABLE16") != "1"
+        self._merge_head = W == 1 and os.environ.get("NGP_FUSED_SPLIT_HEAD") != "1"
         if self.table32:
             nt = self._starts[1]  # the table, then the two MLPs
             sec = [(0, nt, False), (nt, chunk - nt, True)]
@@ -252,12 +253,32 @@ class FusedTrainer:
 
     def _body(self, pending):
         """One step's launches (world 1): [optimizer(previous grads)] ->
-        sample -> march -> network forward/backward."""
-        if pending:
-            self._optimizer(defer=True)
-        self._sample()
-        self._march()
+        sample -> march -> network forward/backward. With an update pending,
+        Adam and the batch draw share one launch and the deferred scaler
+        bookkeeping + MLP packs ride in the march's emit launch (12 launches
+        instead of 13; NGP_FUSED_SPLIT_HEAD=1 keeps them apart)."""
+        if pending and self._merge_head:
+            self._optimizer_head()
+            self._march(tail=True)
+        else:
+            if pending:
+                self._optimizer(defer=True)
+            self._sample()
+            self._march()
         self._network()
+
+    def _optimizer_head(self):
+        lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
+        o, m, d = self._opt, self.model, self.data
+        nat.check(lib.ngp_fused_optimizer_update_head(
+            o["n"], o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
+            self.betas[1], self.eps, self.iters, 1, 1.0, _PRECHECKED, P(self.state),
+            P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N, self._boxes, self._nboxes, self._aabb,
+            float(m.min_near), self.seed, P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
+            P(self.nears), P(self.fars), P(self.noises), P(self.counter), P(m.step_counter),
+            P(self.grid_ws) if self._grid_counter_bytes else None, self._grid_counter_bytes, s),
+            "fused_optimizer_update_head")
+        self._tick("optimizer")
 
     # ---- data parallel (world > 1): ZeRO-1 --------------------------------
     # The flat fp16 gradient is guarded (ngp_grad_guard) and averaged with one
@@ -336,14 +357,20 @@ class FusedTrainer:
         self._march()
         self._network()
 
-    def _march(self):
+    def _march(self, tail=False):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         m, M, N, cnt = self.model, self.M, self.N, P(self.counter)
-        nat.check(lib.ngp_march_rays_train_prebuilt(P(self.rays_o), P(self.rays_d), P(m.density_bitfield),
-                                     float(m.bound), self.dt_gamma, self.max_steps, N, m.cascade,
-                                     m.grid_size, M, P(self.nears), P(self.fars), P(self.xyzs),
-                                     P(self.dirs), P(self.deltas), P(self.rays), cnt, P(self.noises),
-                                     P(self.march_ws), self.march_ws.numel(), s), "march_rays_train")
+        args = (P(self.rays_o), P(self.rays_d), P(m.density_bitfield), float(m.bound), self.dt_gamma,
+                self.max_steps, N, m.cascade, m.grid_size, M, P(self.nears), P(self.fars), P(self.xyzs),
+                P(self.dirs), P(self.deltas), P(self.rays), cnt, P(self.noises), P(self.march_ws),
+                self.march_ws.numel())
+        if tail:  # + the deferred scaler bookkeeping and the MLP packs (see _body)
+            pk = self._pk
+            nat.check(lib.ngp_march_rays_train_prebuilt_tail(
+                *args, P(self.state), 2.0, 0.5, self.growth_interval, 1, P(self.loss_ray), 2, pk["w"], pk["ins"],
+                pk["hid"], pk["nl"], pk["img"], s), "march_rays_train_tail")
+        else:
+            nat.check(lib.ngp_march_rays_train_prebuilt(*args, s), "march_rays_train")
         self._tick("march_rays_train")
 
     def _network(self):
