@@ -188,6 +188,9 @@ def test_pipelined_steps_match_serial_steps(cuda):
         assert torch.equal(x.detach(), y.detach())
     assert a.optimizer_steps == b.optimizer_steps
     assert torch.equal(a.model.step_counter, b.model.step_counter)
+    # the scaler / loss bookkeeping (deferred into the march emit launch in world 1)
+    assert a.scale == b.scale and a.last_loss == b.last_loss
+    assert int(a._state_i()[7]) == int(b._state_i()[7])  # LambdaLR epoch
 
 
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
