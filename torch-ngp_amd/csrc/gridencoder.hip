@@ -526,14 +526,27 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 // term, gridencoder.cu:325) and summed in fp32. Items past a bin's capacity
 // fall back to direct atomics. Levels with more than kMaxBinsPerLevel bins
 // use k_grid_bwd.
-constexpr uint32_t kBinShift = 12;
+// The NGP_* macros exist only for same-box A/B builds (tools/variants.sh).
+#ifndef NGP_BIN_SHIFT
+#define NGP_BIN_SHIFT 12
+#endif
+#ifndef NGP_SEG_ITEMS
+#define NGP_SEG_ITEMS 16384
+#endif
+#ifndef NGP_MERGE_MAX_RES
+#define NGP_MERGE_MAX_RES 128
+#endif
+#ifndef NGP_ACC_BATCH
+#define NGP_ACC_BATCH 16
+#endif
+constexpr uint32_t kBinShift = NGP_BIN_SHIFT;
 constexpr uint32_t kBinEntries = 1u << kBinShift;
 constexpr uint32_t kMaxBinsPerLevel = 256;
-constexpr uint32_t kSegItems = 16384;
+constexpr uint32_t kSegItems = NGP_SEG_ITEMS;
 // Levels up to this resolution merge runs of equal corners in-wave: on the
 // Lego step the merge cuts their items 3.5-16x (tools/grid_bwd_micro.py);
 // finer levels gain less than the scan costs.
-constexpr uint32_t kMergeMaxRes = 128;
+constexpr uint32_t kMergeMaxRes = NGP_MERGE_MAX_RES;
 
 struct BinPlan {
     uint32_t nlev;                   // levels [0, nlev) are binned
@@ -803,7 +816,7 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // (inf / NaN: fp16 overflow under the loss scale) cannot be carried by the
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
-constexpr uint32_t kAccThreads = 512, kAccBatch = 16, kRetireGroups = 16;
+constexpr uint32_t kAccThreads = 512, kAccBatch = NGP_ACC_BATCH, kRetireGroups = 16;
 __global__ void __launch_bounds__(kAccThreads)
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
