@@ -85,11 +85,35 @@ class KernelTimer:
         return float(np.mean(ts)) if ts else float("nan")
 
 
+def launch_cmd(gpus, argv, port):
+    """The torch.distributed.run command line that starts `gpus` ranks of this
+    script (one per GPU, rendezvous on 127.0.0.1) with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: start the N ranks as a child
+        # torch.distributed.run (this process has made no GPU call) and exit
+        # with its status; rank 0 of the children prints the JSON line
+        import subprocess
+        sys.exit(subprocess.call(launch_cmd(args.gpus, sys.argv[1:], _free_port())))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if world > 1 and args.backend == "gloo":
         local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
@@ -99,6 +123,10 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
+    # what the collective layer itself reports (the ranks RCCL / gloo joined)
+    comm = {"backend": dist.get_backend() if world > 1 else None,
+            "world_size": dist.get_world_size() if world > 1 else 1}
+    assert comm["world_size"] == args.gpus
     torch.manual_seed(1234 + rank)
     np.random.seed(rank)
 
@@ -116,6 +144,7 @@ def main():
         result = run_fused(args, model, data, bits, world, dev)
     else:
         result = run_autograd(args, model, data, bits, world, dev)
+    result["config"]["collective"] = comm
 
     if rank == 0 and world == 1 and args.cpu:
         result["cpu_baseline"] = cpu_baseline(model, data, args)

@@ -121,6 +121,25 @@ def grid_encode_backward(grad, inputs, offsets, C, per_level_scale, H, gridtype=
     return out
 
 
+def grad_total_variation(inputs, embeddings, offsets, weight, per_level_scale, H, gridtype=0,
+                         align_corners=False):
+    """float64 image of the TV gradient kernel_grad_tv adds (gridencoder.cu:503-607);
+    inputs and embeddings float32 or float64 (the reference's type)."""
+    emb = np.ascontiguousarray(embeddings)
+    x = np.ascontiguousarray(inputs, dtype=emb.dtype)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int32)
+    B, D = x.shape
+    C = emb.shape[1]
+    L = offsets.shape[0] - 1
+    S = np.float32(np.log2(per_level_scale))
+    out = np.zeros((int(offsets[-1]), C), dtype=np.float64)
+    rc = lib().oracle_grad_tv(_p(x), _p(emb), _p(out), _p(offsets), _f(weight), _u(B), _u(D), _u(C), _u(L),
+                              _f(S), _u(H), _u(gridtype), ctypes.c_int(int(align_corners)),
+                              ctypes.c_int(_DT[emb.dtype]))
+    assert rc == 0
+    return out
+
+
 def grid_input_backward(grad, dy_dx, B, D, C, L, grad_layout=1):
     grad = np.ascontiguousarray(grad)
     dy_dx = np.ascontiguousarray(dy_dx, dtype=grad.dtype)

@@ -274,6 +274,72 @@ int oracle_grid_encode_backward(const void* grad, const float* inputs, const int
     return 0;
 }
 
+/* kernel_grad_tv (gridencoder.cu:503-607): float or double table; every
+ * point's per-entry contribution w * results * rsqrt(idelta + 1e-9) is formed
+ * in the table's type (nvcc contracts idelta += v * v to an fma) and summed
+ * into a float64 image (the reference's atomics are unordered). */
+int oracle_grad_tv(const void* inputs, const void* grid, double* grad, const int32_t* offsets, float weight,
+                   uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                   int align_corners, int dt) {
+    if (dt == DT_F16) return -1;
+    for (uint32_t level = 0; level < L; ++level) {
+        const uint32_t off0 = (uint32_t)offsets[level];
+        const uint32_t hs = (uint32_t)offsets[level + 1] - off0;
+        const float scale = level_scale(level, S, H);
+        const uint32_t res = (uint32_t)ceil(scale) + 1u;
+        for (uint32_t b = 0; b < B; ++b) {
+            int oob = 0;
+            for (uint32_t d = 0; d < D; ++d) {
+                const double x = load_v(inputs, (size_t)b * D + d, dt);
+                if (x < 0 || x > 1) oob = 1;
+            }
+            if (oob) continue;
+            uint32_t pg[8];
+            for (uint32_t d = 0; d < D; ++d) {
+                const double x = load_v(inputs, (size_t)b * D + d, dt);
+                /* inputs[d] * scale + 0.5 in scalar_t (fma under nvcc), then floorf */
+                const float pos = dt == DT_F32 ? fmaf((float)x, scale, align_corners ? 0.0f : 0.5f)
+                                               : (float)fma(x, (double)scale, align_corners ? 0.0 : 0.5);
+                pg[d] = (uint32_t)floorf(pos);
+            }
+            const uint32_t index = grid_index(gridtype, align_corners, hs, res, pg, D);
+            for (uint32_t c = 0; c < C; ++c) {
+                double results = 0, idelta = 0;
+                float rf = 0, idf = 0;
+                const double g0 = load_v(grid, ((size_t)off0 + index) * C + c, dt);
+                for (uint32_t d = 0; d < D; ++d) {
+                    const uint32_t cur = pg[d];
+                    for (int side = 0; side < 2; ++side) {
+                        if (side == 0 ? !(cur < res) : !(cur > 0)) continue;
+                        pg[d] = side == 0 ? cur + 1 : cur - 1;
+                        const uint32_t nb = grid_index(gridtype, align_corners, hs, res, pg, D);
+                        const double gv = g0 - load_v(grid, ((size_t)off0 + nb) * C + c, dt);
+                        if (dt == DT_F32) {
+                            const float gf = (float)g0 - (float)load_v(grid, ((size_t)off0 + nb) * C + c, dt);
+                            rf += gf;
+                            idf = fmaf(gf, gf, idf);
+                        } else {
+                            results += gv;
+                            idelta = fma(gv, gv, idelta);
+                        }
+                        pg[d] = cur;
+                    }
+                }
+                double contrib;
+                if (dt == DT_F32) {
+                    const float w = weight / (float)(2 * D);
+                    contrib = (double)(w * rf * (1.0f / sqrtf(idf + 1e-9f)));
+                } else {
+                    const double w = (double)(weight / (float)(2 * D));
+                    contrib = w * results * (double)(1.0f / sqrtf((float)(idelta + (double)1e-9f)));
+                }
+                grad[((size_t)off0 + index) * C + c] += contrib;
+            }
+        }
+    }
+    return 0;
+}
+
 /* kernel_input_backward (gridencoder.cu:340-366) */
 int oracle_grid_input_backward(const void* grad, const void* dy_dx, void* grad_inputs, uint32_t B,
                                uint32_t D, uint32_t C, uint32_t L, int dt, int grad_layout) {

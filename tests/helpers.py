@@ -28,3 +28,22 @@ def lego_rays(N, H=800, W=800, seed=0, radius=4.0311 * 0.8, camera_angle_x=0.691
     d = fwd + dx[:, None] * right - dy[:, None] * upv
     d /= np.linalg.norm(d, axis=-1, keepdims=True)
     return cam.astype(np.float32), d.astype(np.float32)
+
+
+def close16(got, ref, what="", min_equal=0.98, rel_norm=1e-3):
+    """fp16 outputs of an fp32-accumulating kernel against the float64 oracle
+    rounded to fp16: each value bit-identical or within 2 fp16 ulps plus 1e-3
+    of the largest magnitude (sums that cancel), >= min_equal of the values
+    bit-identical, and the whole tensor within rel_norm."""
+    import numpy as np
+    got = np.asarray(got).astype(np.float16)
+    ref = np.asarray(ref).astype(np.float16)
+    assert got.shape == ref.shape, what
+    g, r = got.astype(np.float64), ref.astype(np.float64)
+    assert np.isfinite(g).all(), what
+    tol = 2 * np.spacing(np.abs(ref)).astype(np.float64) + 1e-3 * np.abs(r).max()
+    bad = np.abs(g - r) > tol
+    assert not bad.any(), (what, int(bad.sum()), g[bad][:6], r[bad][:6])
+    same = float((got.view(np.uint16) == ref.view(np.uint16)).mean())
+    assert same >= min_equal, (what, same)
+    assert np.linalg.norm(g - r) <= rel_norm * np.linalg.norm(r), (what, np.linalg.norm(g - r) / np.linalg.norm(r))

@@ -75,11 +75,62 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _run(world):
+def _equiv_worker(rank, world, port, q):
+    """world 2: ONE data-parallel step from the same initial parameters; returns
+    this rank's averaged gradient shard and the parameters after flush().
+    world 1: the same step's gradients of each rank's batch, computed one
+    rank-seed at a time by single-process trainers."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "torch-ngp_amd")]
+    import torch.distributed as dist
+    from nerf.fused import FusedTrainer
+    from nerf.network_ff import NeRFNetwork
+    from nerf.provider import SyntheticLego, lego_bitfield
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+
+    def trainer(distributed, seed=0):
+        torch.manual_seed(0)
+        model = NeRFNetwork(bound=1, cuda_ray=True).to(dev)
+        with torch.no_grad():
+            model.encoder.embeddings.normal_(0, 0.05)
+        model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
+        return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, seed=seed, distributed=distributed)
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ft = trainer(True)
+        ft.step()  # sample -> march -> network -> reduce-scatter (the update stays pending)
+        torch.cuda.synchronize()
+        shard = ft.grad_shard.cpu().numpy()
+        ft.flush()
+        torch.cuda.synchronize()
+        q.put((rank, ft.lo, shard, [p.detach().cpu().numpy() for p in ft.params], ft.total))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    grads = []
+    for r in range(2):  # the data-parallel sampler seeds rank r with seed + 7919 r
+        ft = trainer(False, seed=7919 * r)
+        ft._sample()
+        ft._forward_backward()
+        torch.cuda.synchronize()
+        grads.append(ft.flat_grad.clone())
+    # the gradient of the mean loss over both batches, then the optimizer on it
+    mean = ((grads[0].float() + grads[1].float()).half() / 2)
+    ft.flat_grad.copy_(mean)
+    ft._optimizer()
+    torch.cuda.synchronize()
+    q.put((0, 0, mean.cpu().numpy(), [p.detach().cpu().numpy() for p in ft.params], ft.total))
+
+
+def _run(world, target=_worker):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=600) for _ in range(world)], key=lambda t: t[0])
@@ -98,3 +149,24 @@ def test_fused_data_parallel_two_ranks_stay_in_sync():
     assert all(k0) and all(k1), (k0, k1)  # both ranks skipped the step with rank 0's inf
     (_, ps, _, _), = _run(1)
     assert any(not np.array_equal(a, b) for a, b in zip(p0, ps))  # the other rank's rays mattered
+
+
+def test_zero1_step_equals_single_process_step_on_both_batches():
+    """ZeRO-1 equivalence: the averaged gradient the two ranks' reduce-scatter
+    leaves in their shards is the mean of the two batches' gradients computed
+    by single-process trainers, and the parameters after the sharded update
+    (flush: Adam per shard + all-gather) equal a single-process Adam step on
+    that mean."""
+    two = sorted(_run(2, _equiv_worker), key=lambda t: t[0])
+    (_, _, want, p_ref, total), = _run(1, _equiv_worker)
+    got = np.zeros(total, np.float16)
+    for _, lo, shard, _, _ in two:
+        got[lo:lo + shard.size] = shard
+    g, w = got.astype(np.float64), want.astype(np.float64)
+    assert np.abs(w).max() > 0
+    assert np.linalg.norm(g - w) <= 1e-3 * np.linalg.norm(w)
+    assert (got.view(np.uint16) == want.view(np.uint16)).mean() >= 0.999
+    for p in (two[0][3], two[1][3]):  # both ranks hold the full, identical parameters
+        for a, b in zip(p, p_ref):
+            assert np.abs(a - b).max() <= 2.5e-2  # Adam's first step is lr * sign(g)
+            assert (a == b).mean() >= 0.999

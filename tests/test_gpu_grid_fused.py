@@ -96,7 +96,7 @@ CASES = [
     (20000, 16, 16, LEGO_SCALE, 19, "uniform"),
     (60000, 16, 16, LEGO_SCALE, 19, "rays"),
     (120000, 8, 16, 1.5, 19, "concentrated"),   # heavy bins: several segments per bin
-    (30000, 8, 16, 2.0, 22, "uniform"),          # 512-bin levels: the atomic suffix
+    (30000, 8, 16, 2.0, 22, "uniform"),          # 2^22-entry levels: 1024 bins of 2^12, past kMaxBinsPerLevel: the atomic suffix
     (513, 4, 8, 2.0, 12, "uniform"),
 ]
 

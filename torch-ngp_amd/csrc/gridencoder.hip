@@ -543,6 +543,9 @@ constexpr uint32_t kBinShift = NGP_BIN_SHIFT;
 constexpr uint32_t kBinEntries = 1u << kBinShift;
 constexpr uint32_t kMaxBinsPerLevel = 256;
 constexpr uint32_t kSegItems = NGP_SEG_ITEMS;
+// entries within a bin are packed in 16 bits while staged (| bin << 16)
+static_assert(kBinShift >= 9 && kBinShift <= 16, "NGP_BIN_SHIFT must be in [9, 16]");
+static_assert(kSegItems > 0, "NGP_SEG_ITEMS must be positive");
 // Levels up to this resolution merge runs of equal corners in-wave: on the
 // Lego step the merge cuts their items 3.5-16x (tools/grid_bwd_micro.py);
 // finer levels gain less than the scan costs.
@@ -817,6 +820,10 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
 constexpr uint32_t kAccThreads = 512, kAccBatch = NGP_ACC_BATCH, kRetireGroups = 16;
+static_assert(kAccBatch > 0, "NGP_ACC_BATCH must be positive");
+static_assert(kBinEntries % kAccThreads == 0, "each flush thread owns whole entries (G > 0)");
+// the int64 LDS image of one bin (+ the counts in dynamic LDS) fits a CU's 160 KB
+static_assert(kBinEntries * 2 * sizeof(unsigned long long) <= 128 * 1024, "bin image exceeds LDS");
 __global__ void __launch_bounds__(kAccThreads)
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
@@ -1168,7 +1175,7 @@ k_grid_tv(const T* __restrict__ inputs, const T* __restrict__ grid, T* __restric
             for (uint32_t c = 0; c < C; c++) {
                 const T gv = g[index + c] - g[ir + c];
                 results[c] += gv;
-                idelta[c] += gv * gv;
+                idelta[c] = fma(gv, gv, idelta[c]);  // nvcc contracts the reference's += v * v
             }
         }
         if (cur_d > 0) {
@@ -1178,7 +1185,7 @@ k_grid_tv(const T* __restrict__ inputs, const T* __restrict__ grid, T* __restric
             for (uint32_t c = 0; c < C; c++) {
                 const T gv = g[index + c] - g[il + c];
                 results[c] += gv;
-                idelta[c] += gv * gv;
+                idelta[c] = fma(gv, gv, idelta[c]);
             }
         }
         pg[d] = cur_d;
