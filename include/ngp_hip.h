@@ -412,6 +412,46 @@ int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, v
 /* (n == 0: no scan; the per-rank flag ngp_fused_inf_flag(state, 1) was set by
  * the kernels that wrote the gradient.) */
 
+/* ------------------------------------------------------------------------ */
+/* Density-grid update (replaces the torch glue of NeRFRenderer.             */
+/* update_extra_state, nerf/renderer.py:498-598, and its packbits call,      */
+/* raymarching.h:11)                                                          */
+/* ------------------------------------------------------------------------ */
+
+/* The query points of one update, P = C * ppc ordered by cascade. coords
+ * int32 [P,3] cell coordinates (renderer.py:552-561), or NULL for every cell
+ * of each cascade in meshgrid(x, y, z, 'ij') order (ppc = H^3, :516-523);
+ * noise f32 [P,3] uniform [0,1) (the reference's rand_like, :533 / :569).
+ * Writes xyzs f32 [P,3] = (2c/(H-1) - 1)(bound_c - hgs) + (2 noise - 1) hgs
+ * with the reference's fp32 operations, and indices i32 [P] = cascade * H^3 +
+ * morton3D(c). */
+int ngp_density_grid_points(const int32_t* coords, const float* noise, uint32_t P, uint32_t ppc, uint32_t C,
+                            uint32_t H, float bound, float* xyzs, int32_t* indices, void* stream);
+/* The densities of the points: sigma network forward on their encodings
+ * (pair-major [L][B][2] half, ngp_grid_encode_forward_fused out_layout 0),
+ * density = exp(h[:,0]) * density_scale (renderer.py:535-536), written as a
+ * max into tmp_grid[indices[b]] (tmp_grid f32 [C * H^3], -1 where unset;
+ * a cell drawn twice keeps the larger density). image: ngp_ffmlp_pack image
+ * of the network or NULL. */
+int ngp_nerf_density_forward(const void* inputs, const void* weights, const void* image, uint32_t B,
+                             uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers, float density_scale,
+                             const int32_t* indices, float* tmp_grid, void* stream);
+/* EMA (renderer.py:582-583: where grid >= 0 and tmp >= 0, grid = max(grid *
+ * decay, tmp)), tmp reset to -1, stats[0] = sum(clamp(grid, 0)) as a double
+ * (mean_density = float(stats[0] / (C H^3)), :584), and the bitfield at
+ * min(mean_density, density_thresh) (:589-590), all on the device. */
+int ngp_density_grid_ema_pack(float* grid, float* tmp_grid, uint32_t C, uint32_t H, float decay,
+                              double density_thresh, double* stats, uint8_t* bitfield, void* stream);
+/* Device-side draws of an update (no host sync, graph-capturable): partial=0:
+ * the noise of every cell (coords unused); partial=1: per cascade H^3/4
+ * uniform cells then H^3/4 cells drawn from the cascade's occupied cells
+ * (grid > 0, listed in cell order as torch.nonzero does, :555-558), with
+ * their noise. Counter RNG over (seed, update, point). */
+size_t ngp_density_grid_draw_workspace_bytes(uint32_t C, uint32_t H);
+int ngp_density_grid_draw(const float* grid, uint32_t C, uint32_t H, uint32_t partial, uint32_t seed,
+                          uint32_t update, int32_t* coords, float* noise, void* ws, size_t ws_bytes,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

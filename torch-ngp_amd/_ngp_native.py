@@ -106,6 +106,11 @@ SIGNATURES = {
     "ngp_fused_optimizer_step": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
                                  c_i32, c_i32, c_f32, c_f32, c_f32, c_i32, c_i32, c_u32, c_vp, c_vp,
                                  c_vp, c_vp, c_vp],
+    "ngp_density_grid_points": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_vp, c_vp, c_vp],
+    "ngp_nerf_density_forward": [c_vp, c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_vp, c_vp, c_vp],
+    "ngp_density_grid_ema_pack": [c_vp, c_vp, c_u32, c_u32, c_f32, ctypes.c_double, c_vp, c_vp, c_vp],
+    "ngp_density_grid_draw_workspace_bytes": [c_u32, c_u32],
+    "ngp_density_grid_draw": [c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_sz, c_vp],
 }
 _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,
@@ -116,6 +121,7 @@ _RESTYPES = {
     "ngp_fused_state_bytes": c_sz,
     "ngp_grid_encode_backward_fused_workspace_bytes": c_sz,
     "ngp_ffmlp_image_bytes": c_sz,
+    "ngp_density_grid_draw_workspace_bytes": c_sz,
 }
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}

@@ -1,0 +1,338 @@
+// Density-grid update of the NeRF renderer (reference nerf/renderer.py
+// update_extra_state :498-598) on the device: the query points of an update,
+// the EMA of the grid, its mean and the occupancy bitfield, with no host
+// round trip between them. The densities themselves come from the fused grid
+// forward + the sigma FFMLP's density epilogue (ngp_nerf_density_forward).
+//
+//   k_density_points  cascade-ordered points -> world xyz (the reference's
+//                     float ops, :524-533 / :563-569) + flat cell index
+//                     cascade * H^3 + morton3D (raymarching.cu:56-71)
+//   k_density_ema     valid = grid >= 0 && tmp >= 0: grid = max(grid * decay,
+//                     tmp) (:582-583); tmp reset to -1 for the next update;
+//                     sum of clamp(grid, 0) for mean_density (:584)
+//   k_density_pack    packbits (raymarching.cu:274-300) at min(mean_density,
+//                     density_thresh) (:589-590), read on the device
+//   k_density_occ_*   the partial update's "random occupied cells" draw
+//                     (:555-558) without a host nonzero(): occupied cells of a
+//                     cascade compacted in cell order, then sampled
+//   k_density_draw    counter-based draws (the fused trainer's update): cell
+//                     coordinates and noise
+#include "ngp_common.h"
+
+#include <algorithm>
+#include <cfloat>
+
+namespace {
+
+constexpr uint32_t kMaxCascades = 16;
+
+NGP_DEV uint32_t expand_bits(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+NGP_DEV uint32_t morton3(uint32_t x, uint32_t y, uint32_t z) {
+    return expand_bits(x) | (expand_bits(y) << 1) | (expand_bits(z) << 2);
+}
+NGP_DEV uint32_t compact_bits(uint32_t x) {
+    x &= 0x09249249u;
+    x = (x ^ (x >> 2)) & 0x030C30C3u;
+    x = (x ^ (x >> 4)) & 0x0300F00Fu;
+    x = (x ^ (x >> 8)) & 0xFF0000FFu;
+    x = (x ^ (x >> 16)) & 0x000003FFu;
+    return x;
+}
+
+struct CascadeScales {
+    float s[kMaxCascades];    // float(bound_c - hgs): the world extent of the cascade's cell centres
+    float hgs[kMaxCascades];  // float(bound_c / H): half a cell
+};
+
+// Host side of :528-529: bound_c = min(2^c, bound), hgs = bound_c / H in double
+// (Python floats), each rounded to float where torch multiplies by it.
+static CascadeScales cascade_scales(uint32_t C, uint32_t H, float bound) {
+    CascadeScales cs{};
+    for (uint32_t c = 0; c < C && c < kMaxCascades; ++c) {
+        const double bc = std::min((double)(1u << c), (double)bound);
+        const double hgs = bc / (double)H;
+        cs.s[c] = (float)(bc - hgs);
+        cs.hgs[c] = (float)hgs;
+    }
+    return cs;
+}
+
+// counter-based RNG (as the fused sampler's, nerf_fused.hip)
+NGP_DEV uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du;
+    x ^= x >> 15; x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+NGP_DEV uint32_t rng_u32(uint32_t seed, uint32_t a, uint32_t b, uint32_t c) {
+    return mix32(seed ^ mix32(a + 0x9e3779b9u * mix32(b ^ mix32(c + 0x85ebca6bu))));
+}
+NGP_DEV float rng_unit(uint32_t seed, uint32_t a, uint32_t b, uint32_t c) {
+    return (float)(rng_u32(seed, a, b, c) >> 8) * (1.0f / 16777216.0f);
+}
+
+// Point p of cascade p / ppc. coords: [P, 3] cell coordinates, or null for
+// every cell of each cascade in the reference's meshgrid(x, y, z, 'ij') order
+// (ppc = H^3). noise: [P, 3] uniform [0, 1).
+__global__ void __launch_bounds__(256)
+k_density_points(const int32_t* __restrict__ coords, const float* __restrict__ noise, uint32_t P, uint32_t ppc,
+                 uint32_t H, CascadeScales cs, float* __restrict__ xyzs, int32_t* __restrict__ indices) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const uint32_t cas = p / ppc;
+    uint32_t c[3];
+    if (coords) {
+        c[0] = (uint32_t)coords[(size_t)p * 3];
+        c[1] = (uint32_t)coords[(size_t)p * 3 + 1];
+        c[2] = (uint32_t)coords[(size_t)p * 3 + 2];
+    } else {
+        const uint32_t i = p - cas * ppc;
+        c[0] = i / (H * H);
+        c[1] = (i / H) % H;
+        c[2] = i % H;
+    }
+    // xyzs = 2 * coords.float() / (H - 1) - 1 (tensor / scalar: times the fp32 reciprocal)
+    const float inv = 1.0f / (float)(H - 1);
+    const float s = cs.s[cas], h = cs.hgs[cas];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float x = 2.0f * (float)c[k];
+        x = x * inv;
+        x = x - 1.0f;
+        x = x * s;                                  // cas_xyzs = xyzs * (bound - hgs)
+        const float n = noise[(size_t)p * 3 + k];
+        float j = n * 2.0f;                         // (rand * 2 - 1) * hgs
+        j = j - 1.0f;
+        j = j * h;
+        xyzs[(size_t)p * 3 + k] = x + j;
+    }
+    indices[p] = (int32_t)(cas * H * H * H + morton3(c[0], c[1], c[2]));
+}
+
+NGP_DEV float torch_maximum(float a, float b) {  // torch.maximum: NaN propagates
+    if (__builtin_isnan(a) || __builtin_isnan(b)) return __builtin_nanf("");
+    return a > b ? a : b;
+}
+
+constexpr uint32_t kEmaThreads = 256;
+
+__global__ void __launch_bounds__(kEmaThreads)
+k_density_ema(float* __restrict__ grid, float* __restrict__ tmp, uint32_t n, float decay,
+              double* __restrict__ sum) {
+    __shared__ double wsum[kEmaThreads / 64];
+    double acc = 0.0;
+    for (uint32_t i = blockIdx.x * kEmaThreads + threadIdx.x; i < n; i += gridDim.x * kEmaThreads) {
+        float g = grid[i];
+        const float t = tmp[i];
+        if (g >= 0 && t >= 0) {
+            g = torch_maximum(g * decay, t);
+            grid[i] = g;
+        }
+        tmp[i] = -1.0f;
+        acc += g < 0 ? 0.0 : (double)g;  // clamp(min=0)
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double b = 0.0;
+#pragma unroll
+        for (uint32_t w = 0; w < kEmaThreads / 64; ++w) b += wsum[w];
+        atomicAdd(sum, b);
+    }
+}
+
+// packbits at thresh = min(mean_density, density_thresh): mean_density is
+// torch.mean(...).item() of the fp32 grid (a float32 value), compared with
+// the Python float density_thresh in double; the winner is cast to float.
+__global__ void __launch_bounds__(256)
+k_density_pack(const float* __restrict__ grid, uint32_t nbytes, uint32_t n, const double* __restrict__ sum,
+               double density_thresh, uint8_t* __restrict__ bitfield) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nbytes) return;
+    const double mean = (double)(float)(*sum / (double)n);
+    const float thresh = (float)(mean < density_thresh ? mean : density_thresh);
+    const float4* g = reinterpret_cast<const float4*>(grid + (size_t)b * 8);
+    const float4 a = g[0], c = g[1];
+    uint32_t bits = 0;
+    bits |= (a.x > thresh) ? 1u : 0u;
+    bits |= (a.y > thresh) ? 2u : 0u;
+    bits |= (a.z > thresh) ? 4u : 0u;
+    bits |= (a.w > thresh) ? 8u : 0u;
+    bits |= (c.x > thresh) ? 16u : 0u;
+    bits |= (c.y > thresh) ? 32u : 0u;
+    bits |= (c.z > thresh) ? 64u : 0u;
+    bits |= (c.w > thresh) ? 128u : 0u;
+    bitfield[b] = (uint8_t)bits;
+}
+
+// ---- occupied-cell draw (partial update) ---------------------------------------
+// Cells of a cascade are counted per 1024-cell block, the block counts scanned,
+// and the occupied cells (grid > 0) written in cell order, so occ[k] is the
+// k-th occupied cell of the cascade, as torch.nonzero lists them.
+constexpr uint32_t kOccBlock = 1024;
+
+__global__ void __launch_bounds__(kOccBlock)
+k_density_occ_count(const float* __restrict__ grid, uint32_t H3, uint32_t* __restrict__ bcount) {
+    __shared__ uint32_t wc[kOccBlock / 64];
+    const uint32_t cas = blockIdx.y;
+    const uint32_t i = blockIdx.x * kOccBlock + threadIdx.x;
+    const bool occ = i < H3 && grid[(size_t)cas * H3 + i] > 0.0f;
+    const uint64_t m = __ballot(occ);
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kOccBlock / 64; ++w) s += wc[w];
+        bcount[cas * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+// One workgroup per cascade: exclusive scan of its block counts in place;
+// total[cas] = the cascade's occupied cells.
+__global__ void __launch_bounds__(1024)
+k_density_occ_scan(uint32_t* __restrict__ bcount, uint32_t nblk, uint32_t* __restrict__ total) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const uint32_t cas = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint32_t* bc = bcount + (size_t)cas * nblk;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nblk; base += 1024) {
+        const uint32_t v = base + t < nblk ? bc[base + t] : 0u;
+        uint32_t incl = v;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t before = carry, all = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 16; ++w) {
+            before += w < wv ? wsum[w] : 0u;
+            all += wsum[w];
+        }
+        if (base + t < nblk) bc[base + t] = before + incl - v;
+        __syncthreads();
+        if (t == 0) carry += all;
+        __syncthreads();
+    }
+    if (t == 0) total[cas] = carry;
+}
+
+__global__ void __launch_bounds__(kOccBlock)
+k_density_occ_write(const float* __restrict__ grid, uint32_t H3, const uint32_t* __restrict__ bcount,
+                    uint32_t* __restrict__ occ) {
+    __shared__ uint32_t wc[kOccBlock / 64];
+    const uint32_t cas = blockIdx.y;
+    const uint32_t i = blockIdx.x * kOccBlock + threadIdx.x;
+    const bool o = i < H3 && grid[(size_t)cas * H3 + i] > 0.0f;
+    const uint64_t m = __ballot(o);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) wc[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = bcount[cas * gridDim.x + blockIdx.x];
+    for (uint32_t w = 0; w < wv; ++w) before += wc[w];
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (o) occ[(size_t)cas * H3 + before + below] = i;
+}
+
+// Draws of the fused trainer's update (counter RNG over (seed, update, point,
+// stream)): full mode (occ null) draws only the noise of every cell;
+// partial mode per cascade N = ppc / 2 uniform cells, then N cells drawn from
+// the occupied list (uniform cells again where the cascade has none, as the
+// reference's occ[randint(0, 0)] cannot), each with its noise.
+__global__ void __launch_bounds__(256)
+k_density_draw(uint32_t P, uint32_t ppc, uint32_t H, uint32_t seed, uint32_t update,
+               const uint32_t* __restrict__ occ, const uint32_t* __restrict__ total,
+               int32_t* __restrict__ coords, float* __restrict__ noise) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    if (occ) {
+        const uint32_t cas = p / ppc, k = p - cas * ppc, half = ppc / 2;
+        const uint32_t n_occ = total[cas];
+        uint32_t c[3];
+        if (k >= half && n_occ > 0) {
+            const uint32_t cell = occ[(size_t)cas * H * H * H + rng_u32(seed, update, p, 7) % n_occ];
+            c[0] = compact_bits(cell);
+            c[1] = compact_bits(cell >> 1);
+            c[2] = compact_bits(cell >> 2);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) c[j] = rng_u32(seed, update, p, 8 + j) % H;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) coords[(size_t)p * 3 + j] = (int32_t)c[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) noise[(size_t)p * 3 + j] = rng_unit(seed, update, p, 1 + j);
+}
+
+}  // namespace
+
+extern "C" int ngp_density_grid_points(const int32_t* coords, const float* noise, uint32_t P, uint32_t ppc,
+                                       uint32_t C, uint32_t H, float bound, float* xyzs, int32_t* indices,
+                                       void* stream) {
+    NGP_REQUIRE(noise && xyzs && indices, NGP_ERR_ARG, "density_grid_points: null noise / xyzs / indices");
+    NGP_REQUIRE(C >= 1 && C <= kMaxCascades && H >= 2 && H <= 1024, NGP_ERR_ARG,
+                "density_grid_points: cascade %u / grid size %u out of range", C, H);
+    NGP_REQUIRE(ppc > 0 && P == ppc * C, NGP_ERR_ARG, "density_grid_points: P = %u is not %u points x %u cascades",
+                P, ppc, C);
+    NGP_REQUIRE(coords || ppc == H * H * H, NGP_ERR_ARG, "density_grid_points: all-cell mode needs ppc = H^3");
+    if (P == 0) return NGP_OK;
+    k_density_points<<<ngp_div_up(P, 256), 256, 0, ngp_stream(stream)>>>(coords, noise, P, ppc, H,
+                                                                         cascade_scales(C, H, bound), xyzs, indices);
+    return ngp_check_launch("density_grid_points");
+}
+
+extern "C" int ngp_density_grid_ema_pack(float* grid, float* tmp_grid, uint32_t C, uint32_t H, float decay,
+                                         double density_thresh, double* stats, uint8_t* bitfield, void* stream) {
+    NGP_REQUIRE(grid && tmp_grid && stats && bitfield, NGP_ERR_ARG, "density_grid_ema_pack: null pointer");
+    NGP_REQUIRE(H % 2 == 0 && C >= 1, NGP_ERR_ARG, "density_grid_ema_pack: grid size %u must be even", H);
+    const uint32_t n = C * H * H * H;
+    hipStream_t st = ngp_stream(stream);
+    if (hipMemsetAsync(stats, 0, sizeof(double), st) != hipSuccess)
+        return ngp_set_error(NGP_ERR_HIP, "density_grid_ema_pack: stats clear failed");
+    const uint32_t blocks = std::min<uint32_t>(ngp_div_up(n, kEmaThreads), 4 * ngp_num_cus());
+    k_density_ema<<<blocks, kEmaThreads, 0, st>>>(grid, tmp_grid, n, decay, stats);
+    k_density_pack<<<ngp_div_up(n / 8, 256), 256, 0, st>>>(grid, n / 8, n, stats, density_thresh, bitfield);
+    return ngp_check_launch("density_grid_ema_pack");
+}
+
+extern "C" size_t ngp_density_grid_draw_workspace_bytes(uint32_t C, uint32_t H) {
+    const size_t H3 = (size_t)H * H * H, nblk = (H3 + kOccBlock - 1) / kOccBlock;
+    return ((C * nblk + C) * sizeof(uint32_t) + 255) / 256 * 256 + C * H3 * sizeof(uint32_t);
+}
+
+extern "C" int ngp_density_grid_draw(const float* grid, uint32_t C, uint32_t H, uint32_t partial, uint32_t seed,
+                                     uint32_t update, int32_t* coords, float* noise, void* ws, size_t ws_bytes,
+                                     void* stream) {
+    NGP_REQUIRE(noise && (!partial || (coords && grid && ws)), NGP_ERR_ARG, "density_grid_draw: null pointer");
+    NGP_REQUIRE(!partial || ws_bytes >= ngp_density_grid_draw_workspace_bytes(C, H), NGP_ERR_ARG,
+                "density_grid_draw: workspace too small");
+    const uint32_t H3 = H * H * H;
+    const uint32_t ppc = partial ? 2 * (H3 / 4) : H3, P = C * ppc;
+    hipStream_t st = ngp_stream(stream);
+    uint32_t *bcount = nullptr, *total = nullptr, *occ = nullptr;
+    if (partial) {
+        const uint32_t nblk = ngp_div_up(H3, kOccBlock);
+        bcount = static_cast<uint32_t*>(ws);
+        total = bcount + (size_t)C * nblk;
+        occ = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + ((C * nblk + C) * sizeof(uint32_t) + 255) / 256 * 256);
+        k_density_occ_count<<<dim3(nblk, C), kOccBlock, 0, st>>>(grid, H3, bcount);
+        k_density_occ_scan<<<C, 1024, 0, st>>>(bcount, nblk, total);
+        k_density_occ_write<<<dim3(nblk, C), kOccBlock, 0, st>>>(grid, H3, bcount, occ);
+    }
+    k_density_draw<<<ngp_div_up(P, 256), 256, 0, st>>>(P, ppc, H, seed, update, occ, total, coords, noise);
+    return ngp_check_launch("density_grid_draw");
+}

@@ -307,6 +307,30 @@ struct EpiNerfSigma {
     }
 };
 
+// Density-grid query (renderer.update_extra_state, renderer.py:533-538): the
+// sigma network's density = trunc_exp(h[:, 0]) * density_scale (fp32 exp of
+// the half value), scattered into tmp_grid[index[row]]. The grid is written
+// as a max (float bits as int: densities are >= 0, the grid is reset to -1):
+// a cell queried twice in one partial update keeps its larger density, where
+// the reference's index_put keeps an arbitrary one of them.
+struct EpiDensity {
+    float* tmp_grid;
+    const int32_t* index;
+    float density_scale;
+    template <typename FO>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act) const {
+        const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+        if (g != 0) return;  // column 0 (the log density) lives in lane group 0, register 0
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+            const uint32_t row = row0 + nb * 16 + c;
+            if (row >= B) continue;
+            const float s = expf((float)(ngp_half)out_act.fwd(o[nb][0][0])) * density_scale;
+            atomicMax(reinterpret_cast<int*>(tmp_grid) + index[row], __float_as_int(s));
+        }
+    }
+};
+
 template <int W, int IN_KS, int NH, typename FA, typename FO, typename XL, typename EPI>
 __global__ void __launch_bounds__(kThreads)
 k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weights,
@@ -812,6 +836,13 @@ int launch_fwd_nerf(const void* in, const void* w, const void* image, uint32_t B
     return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActReLU{}, ActNone{}, nullptr, count, epi, st);
 }
 
+template <int W, int IN_KS, int NH>
+int launch_fwd_density(const void* in, const void* w, const void* image, uint32_t B, uint32_t in_dim,
+                       const EpiDensity& epi, hipStream_t st) {
+    return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActReLU{}, ActNone{}, nullptr, nullptr, epi, st,
+                                      InPairMajor{B});
+}
+
 constexpr size_t kImageBytes = 128 * 1024;  // fragment image slot at the head of the workspace
 
 template <int W, int IN_KS, int NH>
@@ -962,6 +993,18 @@ extern "C" int ngp_nerf_sigma_forward(const void* inputs, const void* weights, c
                            density_scale};
     NGP_MLP_DISPATCH(launch_fwd_nerf, inputs, weights, image, B, in_dim, count, epi,
                      (flags & NGP_FFMLP_PAIR_MAJOR) != 0, st);
+}
+
+extern "C" int ngp_nerf_density_forward(const void* inputs, const void* weights, const void* image, uint32_t B,
+                                        uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers,
+                                        float density_scale, const int32_t* indices, float* tmp_grid,
+                                        void* stream) {
+    if (int e = check_shape(B, in_dim, kOut, hidden_dim, num_layers)) return e;
+    NGP_REQUIRE(indices && tmp_grid, NGP_ERR_ARG, "nerf_density_forward: null indices / tmp_grid");
+    if (B == 0) return NGP_OK;
+    hipStream_t st = ngp_stream(stream);
+    const EpiDensity epi{tmp_grid, indices, density_scale};
+    NGP_MLP_DISPATCH(launch_fwd_density, inputs, weights, image, B, in_dim, epi, st);
 }
 
 extern "C" int ngp_ffmlp_inference(const void* inputs, const void* weights, uint32_t B,

@@ -3,6 +3,7 @@ hashgrid(L16, C2, 2048*bound) -> FFMLP 32->64->64->16 -> trunc_exp(sigma) +
 15 geometry features; SH(deg 4) ++ geo ++ 1 pad -> FFMLP 32->64->64->64->16
 -> sigmoid(rgb[:3]). Constructor keywords of the renderer pass through
 (fixes fork break §1.3.4: extra kwargs no longer crash construction)."""
+import numpy as np
 import torch
 
 from activation import trunc_exp
@@ -60,6 +61,31 @@ class NeRFNetwork(NeRFRenderer):
             rgbs[mask] = h.to(rgbs.dtype)
             return rgbs
         return h
+
+    def _query_density(self, xyzs, indices, tmp_grid):
+        """Density-grid query of update_extra_state under autocast (the
+        reference trainer updates inside autocast, nerf/utils.py): the fused
+        grid forward (fp32 table rounded to half on load, as autocast's cast
+        does) and the sigma network with its density-scatter epilogue."""
+        if not (torch.is_autocast_enabled() and self.encoder.level_dim == 2):
+            return super()._query_density(xyzs, indices, tmp_grid)
+        import _ngp_native as nat
+        e, P = self.encoder, xyzs.shape[0]
+        enc = torch.empty(e.num_levels, P, e.level_dim, dtype=torch.float16, device=xyzs.device)
+        st, lib, ptr = nat.stream_of(xyzs), nat.lib(), nat.ptr
+        # autocast's half table (grid.py:52-56): a 2 MiB fp16 slice per hashed
+        # level stays resident in an XCD's 4 MiB L2 (4 MiB in fp32 does not)
+        emb = e.embeddings.detach().half()
+        emb_dt = nat.DTYPE_CODE[emb.dtype]
+        nat.check(lib.ngp_grid_encode_forward_fused(
+            ptr(xyzs), float(self.bound), ptr(emb), emb_dt, ptr(e.offsets), ptr(enc), P, None, e.input_dim,
+            e.level_dim, e.num_levels, float(np.log2(e.per_level_scale)), e.base_resolution, e.gridtype_id,
+            int(e.align_corners), e.interp_id, 0, st), "grid_encode_fused")
+        sn = self.sigma_net
+        w = sn.weights.detach().half()
+        nat.check(lib.ngp_nerf_density_forward(ptr(enc), ptr(w), None, P, sn.input_dim, sn.hidden_dim,
+                                               sn.num_layers, float(self.density_scale), ptr(indices),
+                                               ptr(tmp_grid), st), "nerf_density_forward")
 
     def get_params(self, lr):
         return [{"params": self.encoder.parameters(), "lr": lr},

@@ -265,56 +265,89 @@ class NeRFRenderer(nn.Module):
     @torch.no_grad()
     def update_extra_state(self, decay=0.95, S=128):
         """EMA density-grid update + packbits + mean_count (renderer.py:498-598,
-        upstream cadence: every update_extra_interval steps)."""
+        upstream cadence: every update_extra_interval steps).
+
+        The random draws are the reference's torch ones in its order (per
+        block and cascade: rand_like noise; partial updates: randint cells,
+        nonzero + randint occupied cells), so an update consumes the torch RNG
+        exactly as upstream. Everything after them runs on the device without a
+        host round trip (csrc/density_grid.hip): query points, their densities
+        (`_query_density`), the EMA, the mean and the bitfield. A cell drawn
+        twice in one partial update keeps the larger density (upstream keeps
+        an arbitrary one of them)."""
         if not self.cuda_ray:
             return
-        tmp_grid = -torch.ones_like(self.density_grid)
+        import _ngp_native as nat
         dev = self.density_bitfield.device
+        H, C = self.grid_size, self.cascade
         if self.iter_density < 16:
-            X = torch.arange(self.grid_size, dtype=torch.int32, device=dev).split(S)
-            for xs in X:
-                for ys in X:
-                    for zs in X:
-                        xx, yy, zz = custom_meshgrid(xs, ys, zs)
-                        coords = torch.stack([xx.reshape(-1), yy.reshape(-1), zz.reshape(-1)], -1)
-                        indices = raymarching.morton3D(coords).long()
-                        xyzs = 2 * coords.float() / (self.grid_size - 1) - 1
-                        for cas in range(self.cascade):
-                            bound = min(2 ** cas, self.bound)
-                            hgs = bound / self.grid_size
-                            cas_xyzs = xyzs * (bound - hgs)
-                            cas_xyzs += (torch.rand_like(cas_xyzs) * 2 - 1) * hgs
-                            sigmas = self.density(cas_xyzs)["sigma"].reshape(-1).detach()
-                            tmp_grid[cas, indices] = sigmas.float() * self.density_scale
+            X = torch.arange(H, dtype=torch.int32, device=dev).split(S)
+            blocks = [(xs, ys, zs) for xs in X for ys in X for zs in X]
+            noise = [[None] * len(blocks) for _ in range(C)]
+            for bi, (xs, ys, zs) in enumerate(blocks):
+                n = len(xs) * len(ys) * len(zs)
+                for cas in range(C):  # rand_like(cas_xyzs), :533
+                    noise[cas][bi] = torch.rand(n, 3, device=dev)
+            if len(blocks) == 1:
+                coords = None  # every cell, meshgrid order
+            else:
+                cb = []
+                for xs, ys, zs in blocks:
+                    xx, yy, zz = custom_meshgrid(xs, ys, zs)
+                    cb.append(torch.stack([xx.reshape(-1), yy.reshape(-1), zz.reshape(-1)], -1))
+                coords = torch.cat(cb).repeat(C, 1).contiguous()
+            noise = torch.cat([torch.cat(nc) for nc in noise]).contiguous()
+            ppc = H ** 3
         else:
-            N = self.grid_size ** 3 // 4
-            for cas in range(self.cascade):
-                coords = torch.randint(0, self.grid_size, (N, 3), device=dev)
-                indices = raymarching.morton3D(coords).long()
+            N = H ** 3 // 4
+            cs, ns = [], []
+            for cas in range(C):  # :551-569
+                coords = torch.randint(0, H, (N, 3), device=dev)
                 occ = torch.nonzero(self.density_grid[cas] > 0).squeeze(-1)
                 rand_mask = torch.randint(0, max(occ.shape[0], 1), [N], dtype=torch.long, device=dev)
-                occ_indices = occ[rand_mask] if occ.shape[0] > 0 else indices
-                occ_coords = raymarching.morton3D_invert(occ_indices)
-                indices = torch.cat([indices, occ_indices], dim=0)
-                coords = torch.cat([coords.int(), occ_coords], dim=0)
-                xyzs = 2 * coords.float() / (self.grid_size - 1) - 1
-                bound = min(2 ** cas, self.bound)
-                hgs = bound / self.grid_size
-                cas_xyzs = xyzs * (bound - hgs)
-                cas_xyzs += (torch.rand_like(cas_xyzs) * 2 - 1) * hgs
-                sigmas = self.density(cas_xyzs)["sigma"].reshape(-1).detach()
-                tmp_grid[cas, indices] = sigmas.float() * self.density_scale
-        valid = (self.density_grid >= 0) & (tmp_grid >= 0)
-        self.density_grid[valid] = torch.maximum(self.density_grid[valid] * decay, tmp_grid[valid])
-        self.mean_density = torch.mean(self.density_grid.clamp(min=0)).item()
+                occ_coords = (raymarching.morton3D_invert(occ[rand_mask].int()) if occ.shape[0] > 0
+                              else coords.int())
+                cc = torch.cat([coords.int(), occ_coords], dim=0)
+                cs.append(cc)
+                ns.append(torch.rand(cc.shape, device=dev))
+            coords = torch.cat(cs).contiguous()
+            noise = torch.cat(ns).contiguous()
+            ppc = 2 * N
+        P = ppc * C
+        xyzs = torch.empty(P, 3, device=dev)
+        indices = torch.empty(P, dtype=torch.int32, device=dev)
+        st = nat.stream_of(xyzs)
+        nat.check(nat.lib().ngp_density_grid_points(nat.ptr(coords), nat.ptr(noise), P, ppc, C, H,
+                                                    float(self.bound), nat.ptr(xyzs), nat.ptr(indices), st),
+                  "density_grid_points")
+        tmp = self._density_tmp()
+        self._query_density(xyzs, indices, tmp)
+        stats = torch.empty(1, dtype=torch.float64, device=dev)
+        nat.check(nat.lib().ngp_density_grid_ema_pack(nat.ptr(self.density_grid), nat.ptr(tmp), C, H,
+                                                      float(decay), float(self.density_thresh), nat.ptr(stats),
+                                                      nat.ptr(self.density_bitfield), st),
+                  "density_grid_ema_pack")
+        # mean_density: torch.mean(...).item() of the fp32 grid, :584
+        self.mean_density = float(np.float32(stats.item() / self.density_grid.numel()))
         self.iter_density += 1
-        density_thresh = min(self.mean_density, self.density_thresh)
-        self.density_bitfield = raymarching.packbits(self.density_grid, density_thresh,
-                                                     self.density_bitfield)
         total_step = min(16, self.local_step)
         if total_step > 0:
             self.mean_count = int(self.step_counter[:total_step, 0].sum().item() / total_step)
         self.local_step = 0
+
+    def _density_tmp(self):
+        """The update's scratch grid (-1 = not queried); the EMA pass resets it."""
+        t = getattr(self, "_tmp_grid", None)
+        if t is None or t.shape != self.density_grid.shape or t.device != self.density_grid.device:
+            t = torch.full_like(self.density_grid, -1.0)
+            self._tmp_grid = t
+        return t
+
+    def _query_density(self, xyzs, indices, tmp_grid):
+        """tmp_grid[indices] = max(.., density(xyzs) * density_scale)
+        (renderer.py:535-538). Networks with a fused density kernel override it."""
+        sigmas = self.density(xyzs)["sigma"].reshape(-1).detach().float() * self.density_scale
+        tmp_grid.view(-1).view(torch.int32).scatter_reduce_(0, indices.long(), sigmas.view(torch.int32), "amax")
 
     def render(self, rays_o, rays_d, staged=False, max_ray_batch=4096, **kwargs):
         """rays_o/rays_d [B, N, 3] -> {'image' [B, N, 3], 'depth' [B, N], ...}."""
