@@ -35,6 +35,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (spec)
 
 
+# name -> (description, H, W, log2_hashmap_size, occupancy)
+WORKLOADS = {
+    "lego": ("lego_800x800_train_step (synthetic analytic Lego, bound 1, 1 cascade, 128^3 bitfield fixture, "
+             "hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19, "boxes"),
+    "lego_dense": ("lego_800x800_dense_occupancy_train_step (synthetic Lego, bound 1, ball r=0.7 occupancy, "
+                   "hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19, "ball"),
+    "truck": ("truck_1920x1080_train_step (Config 5 single-GPU leg: synthetic scene at 1920x1080, bound 1, "
+              "hashgrid L16 C2 T2^22 = 39.6M entries, FFMLP 64-wide)", 1080, 1920, 22, "boxes"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -46,6 +57,10 @@ def parse():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
     ap.add_argument("--engine", choices=["fused", "autograd"], default="fused")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="lego",
+                    help="lego: the headline (Config 2, Lego 800x800, box occupancy, ~19 samples/ray); "
+                         "lego_dense: same with a ball occupancy (~80 samples/ray); "
+                         "truck: Config 5 single-GPU leg (1920x1080, log2T 22)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="collective backend for N > 1: nccl (= RCCL, the measured path) or gloo "
                          "(host-staged; a rehearsal of the data-parallel step with every rank on the "
@@ -131,20 +146,26 @@ def main():
     np.random.seed(rank)
 
     from nerf.network_ff import NeRFNetwork
-    from nerf.provider import SyntheticLego, lego_bitfield
+    from nerf.provider import SyntheticLego, lego_bitfield, sphere_bitfield
 
-    model = NeRFNetwork(bound=1, cuda_ray=True, density_thresh=10).to(dev)
+    desc, img_h, img_w, log2T, occ = WORKLOADS[args.workload]
+    model = NeRFNetwork(bound=1, cuda_ray=True, density_thresh=10, log2_hashmap_size=log2T).to(dev)
     if world > 1:  # identical initial parameters on every rank
         for p in model.parameters():
             dist.broadcast(p.data, 0)
-    bits = torch.from_numpy(lego_bitfield()).to(dev)
+    bits = torch.from_numpy(lego_bitfield() if occ == "boxes" else sphere_bitfield()).to(dev)
     model.density_bitfield.copy_(bits)
-    data = SyntheticLego(dev, num_rays=args.num_rays)
+    data = SyntheticLego(dev, H=img_h, W=img_w, num_rays=args.num_rays)
     if args.engine == "fused":
         result = run_fused(args, model, data, bits, world, dev)
     else:
         result = run_autograd(args, model, data, bits, world, dev)
     result["config"]["collective"] = comm
+    result["config"]["workload"] = desc
+    result["config"]["image_hw"] = [img_h, img_w]
+    spr = result["config"]["samples_per_step"] / args.num_rays
+    result["samples_per_ray"] = round(spr, 2)
+    result["samples_per_s"] = round(result["value"] * spr, 1)
 
     if rank == 0 and world == 1 and args.cpu:
         result["cpu_baseline"] = cpu_baseline(model, data, args)
@@ -250,15 +271,7 @@ def run_autograd(args, model, data, bits, world, dev):
     del per_call_calls
 
     # density-grid update cost (reported, not in the timed step)
-    with torch.autocast("cuda", dtype=torch.float16):  # first call pays one-time setup
-        model.update_extra_state()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    with torch.autocast("cuda", dtype=torch.float16):
-        model.update_extra_state()
-    torch.cuda.synchronize()
-    density_update_ms = (time.perf_counter() - t) * 1e3
-    model.density_bitfield.copy_(bits)
+    density = density_update_times(model, bits)
 
     result = {
         "metric": METRIC,
@@ -274,8 +287,6 @@ def run_autograd(args, model, data, bits, world, dev):
         "dtype": "fp16",
         "data": "synthetic",
         "config": {
-            "workload": "lego_800x800_train_step (synthetic analytic Lego, bound 1, 1 cascade, "
-                        "128^3 bitfield fixture, hashgrid L16 C2 T2^19, FFMLP 64-wide)",
             "num_rays_per_gpu": args.num_rays,
             "global_batch_rays": args.num_rays * world,
             "samples_per_step": samples_per_step,
@@ -300,7 +311,7 @@ def run_autograd(args, model, data, bits, world, dev):
         "ffmlp_mfma": {"flops_per_step": ffmlp_flops, "ms": round(mlp_ms, 5),
                         "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
                         "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
-        "density_update_ms": round(density_update_ms, 3),
+        "density_update_ms": density,
         "loss": float(loss.float().item()),
     }
 
@@ -372,15 +383,7 @@ def run_fused(args, model, data, bits, world, dev):
     mlp_ms = sum(v for k, v in kernel_ms.items() if k.startswith("ffmlp"))
     ffmlp_flops = 110592 * rows
 
-    with torch.autocast("cuda", dtype=torch.float16):  # first call pays one-time setup
-        model.update_extra_state()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    with torch.autocast("cuda", dtype=torch.float16):
-        model.update_extra_state()
-    torch.cuda.synchronize()
-    density_update_ms = (time.perf_counter() - t) * 1e3
-    model.density_bitfield.copy_(bits)
+    density = density_update_times(model, bits, ft)
 
     return {
         "metric": METRIC,
@@ -396,8 +399,6 @@ def run_fused(args, model, data, bits, world, dev):
         "dtype": "fp16",
         "data": "synthetic",
         "config": {
-            "workload": "lego_800x800_train_step (synthetic analytic Lego, bound 1, 1 cascade, "
-                        "128^3 bitfield fixture, hashgrid L16 C2 T2^19, FFMLP 64-wide)",
             "num_rays_per_gpu": args.num_rays,
             "global_batch_rays": args.num_rays * world,
             "samples_per_step": samples_per_step,
@@ -423,9 +424,47 @@ def run_fused(args, model, data, bits, world, dev):
         "ffmlp_mfma": {"flops_per_step": ffmlp_flops, "ms": round(mlp_ms, 5),
                         "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
                         "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
-        "density_update_ms": round(density_update_ms, 3),
+        "density_update_ms": density,
         "loss": loss,
     }
+
+
+def density_update_times(model, bits, ft=None, reps=3):
+    """Wall time (ms, best of `reps`, synchronised) of one density-grid update
+    (excluded from the step; upstream runs it every 16 steps):
+    the reference-API update_extra_state (torch draws, device query / EMA /
+    packbits) and, with a fused trainer, its device-draw update_density; full
+    updates (the first 16) and partial ones. The bitfield fixture is restored
+    afterwards."""
+    def best(fn, it0):
+        ts = []
+        for _ in range(reps + 1):
+            model.iter_density = it0
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t) * 1e3)
+        return round(min(ts[1:]), 3)
+
+    def ref_update():
+        with torch.autocast("cuda", dtype=torch.float16):
+            model.update_extra_state()
+
+    grid0 = model.density_grid.clone()
+    out = {}
+    for name, it0 in (("full", 0), ("partial", 16)):
+        model.density_grid.copy_(grid0)
+        out[f"update_extra_state_{name}"] = best(ref_update, it0)
+        if ft is not None:
+            model.density_grid.copy_(grid0)
+            out[f"fused_{name}"] = best(ft.update_density, it0)
+    model.density_grid.copy_(grid0)
+    model.iter_density = 0
+    model.density_bitfield.copy_(bits)
+    if ft is not None:
+        ft.refresh_occupancy()
+    return out
 
 
 _PMC_KERNELS = {"grid_encode_backward": ("k_grid_bwd_bin", "k_grid_bin_accum"),
@@ -458,8 +497,36 @@ def pmc_traffic(kernel):
                                     "write_size": int(write)}
 
 
+def host_threads():
+    """Host threads this process may use: the CPUs it is pinned to, capped by
+    OMP_NUM_THREADS when set (os.cpu_count() counts the whole machine, which on
+    a shared GPU box is many times this process's share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
 def cpu_baseline(model, data, args):
-    """The oracle's CPU restatement of the same train step (kind 'port'),
+    """BASELINE.json configs[0] on the host: the pure-PyTorch Config 1 train
+    step (oracle/torch_nerf.py: run() uniform sampling with 512 steps, torch
+    hash grid + SH, nn.Linear MLPs, Adam; synthetic Lego 200x200, 4096 rays) on
+    all of this process's host threads, kind "pytorch". Beside it (`port`):
+    the oracle's C/numpy restatement of the Config-2 step (the cuda_ray
+    pipeline) on one thread, for a same-shape ratio."""
+    from oracle import torch_nerf
+    threads = host_threads()
+    rps, steps, secs, losses = torch_nerf.time_train_steps(threads, budget_s=args.cpu_budget, warmup=1,
+                                                           max_steps=5, num_rays=args.num_rays)
+    out = {"value": round(rps, 2), "unit": "rays/s", "cores": threads, "kind": "pytorch",
+           "sample": f"{steps} timed Config-1 train steps x {args.num_rays} rays x 512 samples (synthetic Lego "
+                     f"200x200, fp32, after 1 warm-up) in {secs:.1f}s on {threads} threads "
+                     f"(torch.set_num_threads), oracle/torch_nerf.py"}
+    out["port"] = port_baseline(model, data, args)
+    return out
+
+
+def port_baseline(model, data, args):
+    """The oracle's CPU restatement of the Config-2 train step (kind 'port'),
     single-threaded, on a bounded sample of 4096-ray batches."""
     try:
         from threadpoolctl import threadpool_limits
@@ -475,7 +542,7 @@ def cpu_baseline(model, data, args):
                   model.density_bitfield.cpu().numpy())
     oracle.build()
     batches = []
-    for _ in range(16):
+    for _ in range(8):
         b = data.sample()
         ro = b["rays_o"][0].cpu().numpy().astype(np.float32)
         rd = b["rays_d"][0].cpu().numpy().astype(np.float32)
@@ -487,13 +554,13 @@ def cpu_baseline(model, data, args):
     if ctx:
         ctx.__enter__()
     try:
-        rps, steps, rays, secs, m = time_cpu_baseline(cpu, batches, args.cpu_budget)
+        rps, steps, rays, secs, m = time_cpu_baseline(cpu, batches, args.cpu_budget / 2)
     finally:
         if ctx:
             ctx.__exit__(None, None, None)
     return {"value": round(rps, 2), "unit": "rays/s", "cores": 1, "kind": "port",
-            "sample": f"{steps} train steps x {args.num_rays} rays (same synthetic Lego workload, "
-                      f"mean {int(m)} samples/step) in {secs:.1f}s, oracle/pipeline.py, 1 thread"}
+            "sample": f"{steps} train steps x {args.num_rays} rays (the benched workload, mean {int(m)} "
+                      f"samples/step) in {secs:.1f}s, oracle/pipeline.py, 1 thread"}
 
 
 if __name__ == "__main__":

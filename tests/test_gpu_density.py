@@ -178,3 +178,97 @@ def test_mark_untrained_grid_matches_numpy(cuda):
         want[cas, idx] = ~seen
     # fp32 (torch) vs fp64 (here) frustum tests may differ exactly on a frustum plane
     assert (got != want).mean() < 1e-4 and 0 < want.mean() < 1
+
+
+# ---- FusedTrainer.update_density: device-side draws -------------------------------
+
+def _mix32(x):
+    x = np.asarray(x, np.uint32)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint32(16)); x = x * np.uint32(0x7feb352d)
+        x = x ^ (x >> np.uint32(15)); x = x * np.uint32(0x846ca68b)
+        x = x ^ (x >> np.uint32(16))
+    return x
+
+
+def _rng_u32(seed, a, b, c):
+    """csrc/density_grid.hip rng_u32 (counter RNG), restated in numpy uint32."""
+    with np.errstate(over="ignore"):
+        inner = _mix32(np.asarray(b, np.uint32) ^ _mix32(np.uint32(c) + np.uint32(0x85ebca6b)))
+        return _mix32(np.uint32(seed) ^ _mix32(np.uint32(a) + np.uint32(0x9e3779b9) * inner))
+
+
+def _draws(seed, update, P, ppc, H, grid=None):
+    p = np.arange(P, dtype=np.uint32)
+    noise = np.stack([(_rng_u32(seed, update, p, 1 + j) >> np.uint32(8)).astype(np.float32) * np.float32(2 ** -24)
+                      for j in range(3)], -1)
+    if grid is None:
+        return None, noise
+    coords = np.stack([_rng_u32(seed, update, p, 8 + j) % np.uint32(H) for j in range(3)], -1).astype(np.int32)
+    cas, k = p // ppc, p % ppc
+    for c in range(grid.shape[0]):
+        occ = np.nonzero(grid[c] > 0)[0].astype(np.int32)
+        sel = (cas == c) & (k >= ppc // 2)
+        if occ.size:
+            cells = occ[_rng_u32(seed, update, p[sel], 7) % np.uint32(occ.size)]
+            coords[sel] = oracle.morton3D_invert(cells)
+    return coords, noise
+
+
+@torch.no_grad()
+def _torch_update_from(m, coords, noise, ppc, decay=0.95):
+    """The reference update (:524-590) from given cells and noise (torch ops on
+    the model's autograd density path); duplicates keep the larger density."""
+    import raymarching
+    H = m.grid_size
+    tmp_grid = -torch.ones_like(m.density_grid)
+    for cas in range(m.cascade):
+        c = coords[cas * ppc:(cas + 1) * ppc]
+        indices = raymarching.morton3D(c).long()
+        xyzs = 2 * c.float() / (H - 1) - 1
+        bound = min(2 ** cas, m.bound)
+        hgs = bound / H
+        cas_xyzs = xyzs * (bound - hgs)
+        cas_xyzs += (noise[cas * ppc:(cas + 1) * ppc] * 2 - 1) * hgs
+        sig = m.density(cas_xyzs)["sigma"].reshape(-1).detach().float() * m.density_scale
+        tmp_grid[cas].view(torch.int32).scatter_reduce_(0, indices, sig.view(torch.int32), "amax")
+    valid = (m.density_grid >= 0) & (tmp_grid >= 0)
+    m.density_grid[valid] = torch.maximum(m.density_grid[valid] * decay, tmp_grid[valid])
+    m.mean_density = torch.mean(m.density_grid.clamp(min=0)).item()
+    m.density_bitfield = raymarching.packbits(m.density_grid, min(m.mean_density, m.density_thresh),
+                                              m.density_bitfield)
+
+
+@pytest.mark.parametrize("bound", [1, 2])
+def test_fused_update_density_matches_restatement(cuda, bound):
+    from nerf.fused import FusedTrainer
+    from nerf.provider import SyntheticLego
+    a = _model(cuda, bound=bound)
+    b = copy.deepcopy(a)
+    ft = FusedTrainer(a, SyntheticLego(cuda, num_rays=256), M=20000, seed=5)
+    H, C = a.grid_size, a.cascade
+    allc = torch.stack(torch.meshgrid(*[torch.arange(H, dtype=torch.int32, device=cuda)] * 3, indexing="ij"),
+                       -1).reshape(-1, 3).repeat(C, 1)
+    for it in range(4):
+        partial = it >= 2
+        if partial:
+            a.iter_density = b.iter_density = 16
+        pre = b.density_grid.cpu().numpy()
+        ft.update_density()
+        ppc = H ** 3 // 2 if partial else H ** 3
+        coords, noise = _draws(5, a.iter_density - 1, C * ppc, ppc, H, pre if partial else None)
+        d = ft._dens
+        np.testing.assert_array_equal(d["noise"][:C * ppc].cpu().numpy(), noise)
+        if partial:
+            np.testing.assert_array_equal(d["coords"][:C * ppc].cpu().numpy(), coords)
+        with torch.autocast("cuda", dtype=torch.float16):
+            _torch_update_from(b, torch.from_numpy(coords).to(cuda) if partial else allc,
+                               torch.from_numpy(noise).to(cuda), ppc)
+        torch.cuda.synchronize()
+        ga, gb = a.density_grid.cpu().numpy(), b.density_grid.cpu().numpy()
+        np.testing.assert_allclose(ga, gb, rtol=1e-6, atol=0)
+        assert abs(ft.mean_density - b.mean_density) <= 1e-6 * b.mean_density
+        assert torch.equal(a.density_bitfield, b.density_bitfield)
+    # the marcher's occupancy image follows the new bitfield: a step still marches
+    ft.step()
+    assert ft.sample_count() > 0

@@ -170,3 +170,43 @@ def test_zero1_step_equals_single_process_step_on_both_batches():
         for a, b in zip(p, p_ref):
             assert np.abs(a - b).max() <= 2.5e-2  # Adam's first step is lr * sign(g)
             assert (a == b).mean() >= 0.999
+
+
+def _density_worker(rank, world, port, q):
+    """update_density on every rank: same draws, sharded queries, MAX
+    all-reduce of the scratch grid."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "torch-ngp_amd")]
+    import torch.distributed as dist
+    from nerf.fused import FusedTrainer
+    from nerf.network_ff import NeRFNetwork
+    from nerf.provider import SyntheticLego, lego_bitfield
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = NeRFNetwork(bound=1, cuda_ray=True).to(dev)
+    with torch.no_grad():
+        model.encoder.embeddings.normal_(0, 0.3)
+    model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
+    ft = FusedTrainer(model, SyntheticLego(dev, num_rays=256), M=20000, distributed=world > 1)
+    for it in range(3):
+        if it == 2:
+            model.iter_density = 16
+        ft.update_density()
+    torch.cuda.synchronize()
+    q.put((rank, model.density_grid.cpu().numpy(), model.density_bitfield.cpu().numpy()))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_update_density_is_rank_consistent():
+    two = sorted(_run(2, _density_worker), key=lambda t: t[0])
+    (_, g1, b1), = _run(1, _density_worker)
+    for _, g, b in two:
+        assert np.array_equal(b, b1)
+        np.testing.assert_allclose(g, g1, rtol=0, atol=0)

@@ -73,6 +73,7 @@ class FusedTrainer:
         self.max_steps, self.T_thresh, self.dt_gamma = int(max_steps), float(T_thresh), float(dt_gamma)
         self.lr, self.iters, self.betas, self.eps = float(lr), int(iters), betas, float(eps)
         self.growth_interval, self.seed = int(growth_interval), int(seed)
+        self.density_seed = int(seed)  # the density-grid draws are the same on every rank
         self.world = dist.get_world_size() if distributed and dist.is_initialized() else 1
         if self.world > 1:
             self.seed += 7919 * dist.get_rank()
@@ -197,6 +198,7 @@ class FusedTrainer:
         self._inf_flag = nat.lib().ngp_fused_inf_flag(nat.ptr(self.state), int(W > 1))
         self.graph = None
         self._events = None
+        self._dens = None  # density-grid update buffers (update_density)
         self._pending = False  # gradients of the last forward/backward not yet applied
 
     def sync_half(self):
@@ -214,6 +216,76 @@ class FusedTrainer:
             nat.ptr(m.density_bitfield), m.cascade, m.grid_size, self.N, self.max_steps,
             nat.ptr(self.march_ws), self.march_ws.numel(), nat.stream_of(self.march_ws)),
             "march_occupancy_build")
+
+    # ------------------------------------------------------ density grid
+    def update_density(self, decay=0.95):
+        """The density-grid update (update_extra_state, renderer.py:498-598)
+        with device-side draws: no host sync, so it can run inside a training
+        loop at the upstream cadence (every 16 steps). Full updates while
+        iter_density < 16, then partial ones (uniform + occupied cells), as
+        upstream. Data parallel: every rank draws the same cells (the draw
+        seed does not depend on the rank), queries its 1/world of them, and a
+        MAX all-reduce of the scratch grid gives every rank the same grid and
+        bitfield. mean_density stays on the device (`mean_density`)."""
+        self.flush()  # the pending optimizer update first: the query reads the parameters
+        m, lib, P_ = self.model, nat.lib(), nat.ptr
+        H, C = m.grid_size, m.cascade
+        H3 = H ** 3
+        dev, s = self.dev, nat.stream_of(self.rays_o)
+        d = self._dens
+        if d is None:
+            wsb = int(lib.ngp_density_grid_draw_workspace_bytes(C, H))
+            d = self._dens = dict(
+                coords=torch.zeros(C * H3 // 2, 3, dtype=torch.int32, device=dev),
+                noise=torch.zeros(C * H3, 3, device=dev),
+                xyzs=torch.zeros(C * H3, 3, device=dev),
+                idx=torch.zeros(C * H3, dtype=torch.int32, device=dev),
+                enc=torch.zeros(self.enc.num_levels, C * H3 // self.world + 1, 2, dtype=torch.float16, device=dev),
+                tmp=torch.full((C, H3), -1.0, device=dev),
+                stats=torch.zeros(1, dtype=torch.float64, device=dev),
+                ws=torch.zeros(max(wsb, 256), dtype=torch.uint8, device=dev),
+                table=torch.zeros_like(self.params[0], dtype=torch.float16) if self.table32 else None)
+        partial = int(m.iter_density >= 16)
+        ppc = 2 * (H3 // 4) if partial else H3
+        P = C * ppc
+        nat.check(lib.ngp_density_grid_draw(P_(m.density_grid), C, H, partial, self.density_seed, m.iter_density,
+                                            P_(d["coords"]), P_(d["noise"]), P_(d["ws"]), d["ws"].numel(), s),
+                  "density_grid_draw")
+        nat.check(lib.ngp_density_grid_points(P_(d["coords"]) if partial else None, P_(d["noise"]), P, ppc, C, H,
+                                              float(m.bound), P_(d["xyzs"]), P_(d["idx"]), s), "density_grid_points")
+        lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
+        e, n = self.enc, hi - lo
+        if d["table"] is not None:  # world 1 keeps no fp16 table copy: make one for the query
+            d["table"].copy_(self.params[0].detach())
+        table = d["table"] if d["table"] is not None else self.w_half[0]
+        # the encodings are [L][n][2] (pair-major, row stride n) at the buffer's head
+        nat.check(lib.ngp_grid_encode_forward_fused(
+            P_(d["xyzs"]) + 12 * lo, float(m.bound), P_(table), _F16, P_(e.offsets), P_(d["enc"]), n, None,
+            e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id, int(e.align_corners),
+            e.interp_id, 0, s), "grid_encode_fused")
+        sn = self.sig_net
+        nat.check(lib.ngp_nerf_density_forward(P_(d["enc"]), P_(self.w_half[1]), None, n, sn.input_dim, sn.hidden_dim,
+                                               sn.num_layers, float(m.density_scale), P_(d["idx"]) + 4 * lo,
+                                               P_(d["tmp"]), s), "nerf_density_forward")
+        if self.world > 1:
+            if self._nccl:
+                dist.all_reduce(d["tmp"], op=dist.ReduceOp.MAX)
+            else:
+                host = d["tmp"].cpu()
+                dist.all_reduce(host, op=dist.ReduceOp.MAX)
+                d["tmp"].copy_(host)
+        nat.check(lib.ngp_density_grid_ema_pack(P_(m.density_grid), P_(d["tmp"]), C, H, float(decay),
+                                                float(m.density_thresh), P_(d["stats"]), P_(m.density_bitfield), s),
+                  "density_grid_ema_pack")
+        m.iter_density += 1
+        self.refresh_occupancy()
+
+    @property
+    def mean_density(self):
+        """mean_density of the last update_density (torch.mean(...).item(), :584)."""
+        if self._dens is None:
+            return float(self.model.mean_density)
+        return float(np.float32(self._dens["stats"].item() / self.model.density_grid.numel()))
 
     # ------------------------------------------------------------------ step
     def _tick(self, name):

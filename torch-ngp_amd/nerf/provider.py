@@ -63,6 +63,25 @@ def lego_bitfield(cascade=1, H=128, bound=1.0):
     return box_bitfield(LEGO_BOXES, cascade, H, bound)
 
 
+def sphere_bitfield(radius=0.7, cascade=1, H=128, bound=1.0):
+    """Occupancy of the cells whose centre lies in a ball (a conservative,
+    early-training grid around the Lego boxes, which it contains): ~80 samples
+    per ray at the Lego cameras, inside SURVEY §8(d)'s 50-120 estimate."""
+    i = np.arange(H)
+    xx, yy, zz = (a.reshape(-1) for a in np.meshgrid(i, i, i, indexing="ij"))
+    idx = _morton3(xx, yy, zz)
+    grid = np.zeros((cascade, H ** 3), np.float32)
+    for c in range(cascade):
+        b = min(2 ** c, bound)
+        cx, cy, cz = (((a + 0.5) / H * 2 - 1) * b for a in (xx, yy, zz))
+        grid[c, idx] = (cx * cx + cy * cy + cz * cz) <= radius * radius
+    flat = grid.reshape(-1, 8)
+    bits = np.zeros(flat.shape[0], np.uint8)
+    for k in range(8):
+        bits |= (flat[:, k] > 0.5).astype(np.uint8) << k
+    return bits
+
+
 class SyntheticLego:
     """100 ring poses at 800x800, camera_angle_x 0.6911112, radius 4.0311
     (scaled by `scale`, default 0.8 as in readme.md:139)."""
