@@ -26,6 +26,8 @@
 #include "ngp_common.h"
 #include "sh_basis.h"
 
+#include <type_traits>
+
 namespace {
 
 using ngp_pack::half8;
@@ -38,8 +40,19 @@ using ngp_pack::perm_unit;
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kWaves = 4;  // the backward epilogue folds waves pairwise (0+2, 1+3)
+constexpr int kWaves = 4;  // forward: waves per workgroup
 constexpr int kThreads = kWaves * 64;
+// Backward: waves per workgroup sharing one fragment image. The dW tiles
+// live in registers for the whole chunk loop (176 of them for the colour
+// network), which leaves room for one wave per SIMD: at 8 waves per workgroup
+// (two per SIMD, 256 registers each) the compiler spills 362 (colour) / 78
+// (sigma) VGPRs.
+#ifndef NGP_MLP_BWD_WAVES
+#define NGP_MLP_BWD_WAVES 4
+#endif
+constexpr int kBwdWaves = NGP_MLP_BWD_WAVES;
+constexpr int kBwdThreads = kBwdWaves * 64;
+static_assert(kBwdWaves % 2 == 0 && kBwdWaves <= 16, "the dW fold pairs waves (two LDS images)");
 constexpr int kNB = 2;          // 16-sample column blocks per wave step (32 samples)
 constexpr int kOut = 16;        // padded output width (FFMLP pads to 16)
 // Per-wave staging tiles of the dW products: [32 samples][units], row pitch
@@ -51,6 +64,24 @@ constexpr uint32_t kMaxBwdBlocks = 256;
 
 NGP_DEV f32x4 mfma(half8 a, half8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// Fragment image -> LDS with every load of a thread issued before its first
+// store (a load/store pair per iteration exposed the load latency ~12 times).
+template <int FRAGS, int THREADS>
+NGP_DEV void copy_frags(half8* __restrict__ lds, const half8* __restrict__ image) {
+    constexpr int TOTAL = FRAGS * 64, PER = (TOTAL + THREADS - 1) / THREADS;
+    half8 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int t = k * THREADS + (int)threadIdx.x;
+        if (t < TOTAL) v[k] = image[t];
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int t = k * THREADS + (int)threadIdx.x;
+        if (t < TOTAL) lds[t] = v[k];
+    }
 }
 
 // Activation enum of ffmlp.py:89-96 / utils.h:29-37.
@@ -340,7 +371,7 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
     if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);  // rows past the sample count
     extern __shared__ half8 lds[];
     if (image) {  // prepacked (ngp_ffmlp_pack): straight 16-byte copies
-        for (uint32_t t = threadIdx.x; t < (uint32_t)N::FWD_FRAGS * 64; t += blockDim.x) lds[t] = image[t];
+        copy_frags<N::FWD_FRAGS, kThreads>(lds, image);
     } else {
         for (int q = 0; q < N::NMAT; ++q) build_frags(lds, weights, fwd_desc<W, IN_KS, NH>(q, in_dim), false);
     }
@@ -453,41 +484,30 @@ NGP_DEV void pack_delta(const f32x4 (&acc)[kNB][MT], const half8 (&h)[kNB][KS], 
         }
 }
 
-// Add (FIRST: store) one wave's dW tile sums (C layout) into the workgroup's
-// fp32 dW image in LDS. Waves take turns (see k_mlp_bwd), so the summation
-// order is fixed and the result reproducible.
-// The image's rows are padded to ld = in_w + kFoldPad floats: a tile's four
-// 16-lane groups hold rows 4 apart, which the pad puts on different LDS banks
-// (unpadded, in_w a multiple of 16, they were 4-way conflicted).
-constexpr uint32_t kFoldPad = 4;
+// Fold image: tile-major [tile][lane] f32x4 (one 1 KB slot per 16x16 dW
+// tile), so a wave stores / adds a tile with one conflict-free 16-byte LDS
+// access per lane (the [out][in] layout took four scalar accesses per tile
+// element group). FIRST stores; otherwise every read of the wave is issued
+// before its first add.
 template <bool FIRST, int MO, int MI>
-NGP_DEV void add_dw(const f32x4 (&t)[MO][MI], float* __restrict__ acc, uint32_t in_w, uint32_t out_w,
-                    uint32_t ld) {
-    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    // all of the matrix's reads are issued before any write (a read-add-write
-    // per element would expose the LDS latency once per element: 176 times
-    // for the colour network)
-    float v[MO][MI][4];
-    if (!FIRST) {
+NGP_DEV void fold_tiles(const f32x4 (&t)[MO][MI], float* __restrict__ img) {
+    f32x4* p = reinterpret_cast<f32x4*>(img) + (threadIdx.x & 63);
+    if (FIRST) {
 #pragma unroll
         for (int m = 0; m < MO; ++m)
 #pragma unroll
-            for (int k = 0; k < MI; ++k)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const uint32_t o = 16 * m + 4 * g + r, i = 16 * k + c;
-                    v[m][k][r] = (o < out_w && i < in_w) ? acc[o * ld + i] : 0.0f;
-                }
+            for (int k = 0; k < MI; ++k) p[(m * MI + k) * 64] = t[m][k];
+        return;
     }
+    f32x4 v[MO][MI];
 #pragma unroll
     for (int m = 0; m < MO; ++m)
 #pragma unroll
-        for (int k = 0; k < MI; ++k)
+        for (int k = 0; k < MI; ++k) v[m][k] = p[(m * MI + k) * 64];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t o = 16 * m + 4 * g + r, i = 16 * k + c;
-                if (o < out_w && i < in_w) acc[o * ld + i] = FIRST ? t[m][k][r] : v[m][k][r] + t[m][k][r];
-            }
+    for (int m = 0; m < MO; ++m)
+#pragma unroll
+        for (int k = 0; k < MI; ++k) p[(m * MI + k) * 64] = v[m][k] + t[m][k];
 }
 
 template <int MO, int MI>
@@ -503,10 +523,10 @@ struct BwdLds {
     using N = Net<W, IN_KS, NH>;
     static constexpr int FRAGS = N::FWD_FRAGS + N::BWD_FRAGS;
     static constexpr size_t frag_bytes = (size_t)FRAGS * 64 * 16;
-    static constexpr size_t tile_bytes = (size_t)kWaves * 2 * kTileRows * kTileLd * 2;
+    static constexpr size_t tile_bytes = (size_t)kBwdWaves * 2 * kTileRows * kTileLd * 2;
     static constexpr size_t nparams_max = (size_t)W * (32 * IN_KS) + (size_t)NH * W * W + (size_t)kOut * W;
-    static constexpr size_t acc_bytes =
-        ((size_t)W * (32 * IN_KS + kFoldPad) + (size_t)NH * W * (W + kFoldPad) + (size_t)kOut * (W + kFoldPad)) * 4;
+    // one fold image: 1 KB per 16x16 dW tile (see fold_tiles)
+    static constexpr size_t acc_bytes = (size_t)(N::MTW * N::IN_MT + NH * N::MTW * N::MTW + N::MTW) * 1024;
     // the two dW images of the epilogue reuse the fragment + tile space once
     // the chunk loop is done
     static constexpr size_t total =
@@ -586,13 +606,13 @@ struct GiPairMajor {
 
 #ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-wave phase clocks
 __device__ unsigned long long* g_mlp_stamps;
-#define MSTAMP(slot) do { if (g_mlp_stamps && (threadIdx.x & 63) == 0) g_mlp_stamps[((size_t)(NH - 1) * 1024 + blockIdx.x * kWaves + (threadIdx.x >> 6)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define MSTAMP(slot) do { if (g_mlp_stamps && (threadIdx.x & 63) == 0) g_mlp_stamps[((size_t)(NH - 1) * 2048 + blockIdx.x * kBwdWaves + (threadIdx.x >> 6)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define MSTAMP(slot) do { } while (0)
 #endif
 
 template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kBwdThreads)
 k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
           const half8* __restrict__ image, XL xl, GI gi_out, bool want_gi,
           float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, FA act,
@@ -609,12 +629,12 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     // the first chunk's inputs and output grads are requested before the
     // fragment image copy, so the two latencies overlap
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t stride = gridDim.x * kWaves;
-    uint32_t chunk = blockIdx.x * kWaves + wave;
+    const uint32_t stride = gridDim.x * kBwdWaves;
+    uint32_t chunk = blockIdx.x * kBwdWaves + wave;
     half8 xn[kNB][IN_KS], dn[kNB][1];
     xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
     load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn);  // output activation ignored (ffmlp.cu:783)
-    for (uint32_t t = threadIdx.x; t < (uint32_t)L::FRAGS * 64; t += blockDim.x) lds[t] = image[t];
+    copy_frags<L::FRAGS, kBwdThreads>(lds, image);
     __syncthreads();
     MSTAMP(1);
     [[maybe_unused]] uint32_t nst = 0;
@@ -681,46 +701,60 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     }
     MSTAMP(12);
 
-    // fold the waves' register tiles into two LDS dW images (waves 0/1 store,
-    // then waves 2/3 add), then publish image0 + image1 as the slab row: a
-    // fixed summation order, so dW is bit-reproducible
-    // padded image: first [W][in_dim + pad], hidden q [W][W + pad], last [16][W + pad]
-    const uint32_t ld0 = in_dim + kFoldPad, ldw = W + kFoldPad;
-    const uint32_t p_hid = W * ld0, p_last = p_hid + NH * W * ldw, npad = p_last + kOut * ldw;
-    float* img = reinterpret_cast<float*>(lds) + (size_t)(wave & 1) * npad;
-    __syncthreads();  // fragments and tiles are dead from here on
-    if (wave < 2) {
-        add_dw<true>(dw_first, img, in_dim, W, ld0);
+    // fold the waves' register tiles into two LDS dW images (round r: waves
+    // 2r and 2r + 1 store (r = 0) or add into images 0 and 1), then publish
+    // image0 + image1 as the slab row: a fixed summation order, so dW is
+    // bit-reproducible. Images are tile-major (fold_tiles): first layer's
+    // MTW x IN_MT tiles, each hidden layer's MTW x MTW, the last layer's 1 x MTW.
+    constexpr int T_FIRST = N::MTW * N::IN_MT, T_HID = N::MTW * N::MTW, T_LAST = N::MTW;
+    constexpr int NT = T_FIRST + NH * T_HID + T_LAST;
+    static_assert((size_t)2 * NT * 1024 <= L::total, "fold images exceed the workgroup's LDS");
+    float* img = reinterpret_cast<float*>(lds) + (size_t)(wave & 1) * NT * 256;
+    auto fold = [&](auto first) {
+        constexpr bool F = decltype(first)::value;
+        fold_tiles<F>(dw_first, img);
 #pragma unroll
-        for (int q = 1; q <= NH; ++q) add_dw<true>(dw_hid[q - 1], img + p_hid + (q - 1) * W * ldw, W, W, ldw);
-        add_dw<true>(dw_last, img + p_last, W, kOut, ldw);
-    }
-    __syncthreads();
-    if (wave >= 2) {
-        add_dw<false>(dw_first, img, in_dim, W, ld0);
-#pragma unroll
-        for (int q = 1; q <= NH; ++q) add_dw<false>(dw_hid[q - 1], img + p_hid + (q - 1) * W * ldw, W, W, ldw);
-        add_dw<false>(dw_last, img + p_last, W, kOut, ldw);
-    }
-    __syncthreads();
-    MSTAMP(13);
-    // slab row = image0 + image1 in the unpadded [out][in] layout, 16 bytes per access
-    const float* img0 = reinterpret_cast<const float*>(lds);
-    float* slab_row = slab + (size_t)blockIdx.x * nparams;
-    auto publish = [&](uint32_t poff, uint32_t ld, uint32_t off, uint32_t in_w, uint32_t out_w) {
-        const uint32_t n4 = out_w * in_w / 4;
-        for (uint32_t t = threadIdx.x; t < n4; t += blockDim.x) {
-            const uint32_t o = 4 * t / in_w, i = 4 * t - o * in_w;
-            const float4 a = *reinterpret_cast<const float4*>(img0 + poff + o * ld + i);
-            const float4 b = *reinterpret_cast<const float4*>(img0 + npad + poff + o * ld + i);
-            *reinterpret_cast<float4*>(slab_row + off + o * in_w + i) = float4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
-        }
+        for (int q = 1; q <= NH; ++q) fold_tiles<F>(dw_hid[q - 1], img + (T_FIRST + (q - 1) * T_HID) * 256);
+        fold_tiles<F>(dw_last, img + (T_FIRST + NH * T_HID) * 256);
     };
-    publish(0, ld0, 0, in_dim, W);
+    __syncthreads();  // fragments and tiles are dead from here on
+    if (wave < 2) fold(std::true_type{});
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t r = 1; r < (uint32_t)kBwdWaves / 2; ++r) {
+        if ((wave >> 1) == r) fold(std::false_type{});
+        __syncthreads();
+    }
+    MSTAMP(13);
+    // slab row = image0 + image1 in the unpadded [out][in] layout: per tile a
+    // lane adds its two 16-byte slots and stores its 4 outputs (rows 16m + 4g +
+    // r, column 16k + c: 64-byte segments per row)
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const f32x4* i0 = reinterpret_cast<const f32x4*>(lds);
+    const f32x4* i1 = i0 + NT * 64;
+    float* slab_row = slab + (size_t)blockIdx.x * nparams;
+    for (int tt = (int)wave; tt < NT; tt += kBwdWaves) {
+        int local, mi;
+        uint32_t in_w, out_w, off;
+        if (tt < T_FIRST) {
+            local = tt; mi = N::IN_MT; in_w = in_dim; out_w = W; off = 0;
+        } else if (tt < T_FIRST + NH * T_HID) {
+            const int q = (tt - T_FIRST) / T_HID;
+            local = tt - T_FIRST - q * T_HID; mi = N::MTW; in_w = W; out_w = W;
+            off = fwd_desc<W, IN_KS, NH>(q + 1, in_dim).off;
+        } else {
+            local = tt - T_FIRST - NH * T_HID; mi = N::MTW; in_w = W; out_w = kOut;
+            off = fwd_desc<W, IN_KS, NH>(LAST, in_dim).off;
+        }
+        const uint32_t m = (uint32_t)(local / mi), k = (uint32_t)(local % mi);
+        const f32x4 a = i0[tt * 64 + lane], b = i1[tt * 64 + lane];
+        const uint32_t i = 16 * k + c;
 #pragma unroll
-    for (int q = 1; q <= NH; ++q)
-        publish(p_hid + (q - 1) * W * ldw, ldw, fwd_desc<W, IN_KS, NH>(q, in_dim).off, W, W);
-    publish(p_last, ldw, fwd_desc<W, IN_KS, NH>(LAST, in_dim).off, W, kOut);
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t o = 16 * m + 4 * g + r;
+            if (o < out_w && i < in_w) slab_row[off + o * in_w + i] = a[r] + b[r];
+        }
+    }
     MSTAMP(14);
 }
 
@@ -785,7 +819,7 @@ uint32_t num_params(uint32_t in_dim, uint32_t hidden, uint32_t num_layers) {
 
 uint32_t bwd_blocks(uint32_t B) {
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
-    uint32_t nb = ngp_div_up(nchunks, kWaves);
+    uint32_t nb = ngp_div_up(nchunks, kBwdWaves);
     return nb < kMaxBwdBlocks ? nb : kMaxBwdBlocks;
 }
 
@@ -883,7 +917,7 @@ int launch_bwd_t(const void* grad, const void* in, const void* w, const void* im
         hipLaunchKernelGGL(k_mlp_pack_jobs, dim3(jobs.n), dim3(256), 0, st, jobs);
         image = ws;
     }
-    hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH, FA, XL, GI>), dim3(blocks), dim3(kThreads), L::total, st,
+    hipLaunchKernelGGL((k_mlp_bwd<W, IN_KS, NH, FA, XL, GI>), dim3(blocks), dim3(kBwdThreads), L::total, st,
                        (const ngp_half*)grad, (const ngp_half*)in, (const half8*)image, xl, gi, want_gi, slab,
                        np, B, in_dim, act, count);
     if (!defer) {
