@@ -24,6 +24,7 @@
 #include "ngp_common.h"
 #include "ngp_dpp.h"
 #include "ngp_step.h"
+#include "ngp_head.h"
 #include "sh_basis.h"
 
 #include <algorithm>
@@ -34,142 +35,12 @@ namespace {
 using ngp_step::ScalerArgs;
 using ngp_step::StepState;
 using ngp_step::step_end_block;
-
-constexpr int kMaxBoxes = 8;
-constexpr int kMaxTensors = 8;
+using namespace ngp_head;
 
 NGP_DEV uint32_t clip_rows(uint32_t B, const int32_t* count) {
     if (!count) return B;
     const int32_t c = *count;
     return c <= 0 ? 0u : min(B, (uint32_t)c);
-}
-
-// counter-based RNG (no state, graph-safe): 32-bit mix of (seed, a, b, c)
-NGP_DEV uint32_t mix32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352du;
-    x ^= x >> 15; x *= 0x846ca68bu;
-    x ^= x >> 16;
-    return x;
-}
-NGP_DEV uint32_t rng_u32(uint32_t seed, uint32_t a, uint32_t b, uint32_t c) {
-    return mix32(seed ^ mix32(a + 0x9e3779b9u * mix32(b ^ mix32(c + 0x85ebca6bu))));
-}
-NGP_DEV float rng_unit(uint32_t seed, uint32_t a, uint32_t b, uint32_t c) {
-    return (float)(rng_u32(seed, a, b, c) >> 8) * (1.0f / 16777216.0f);
-}
-
-struct LegoScene {
-    float lo[kMaxBoxes][3], hi[kMaxBoxes][3], rgb[kMaxBoxes][3];
-    int nboxes;
-    float fx, fy, cx, cy;
-    uint32_t H, W, n_poses;
-    float aabb[6];
-    float min_near;
-    uint32_t seed;
-};
-
-// near/far against the aabb, reference raymarching.cu:91-145 (same as
-// k_near_far in raymarching.hip)
-NGP_DEV void near_far(const float o[3], const float d[3], const float aabb[6], float min_near,
-                      float& near, float& far) {
-    const float rdx = 1 / d[0], rdy = 1 / d[1], rdz = 1 / d[2];
-    near = (aabb[0] - o[0]) * rdx;
-    far = (aabb[3] - o[0]) * rdx;
-    if (near > far) { float c = near; near = far; far = c; }
-    float ny = (aabb[1] - o[1]) * rdy, fy = (aabb[4] - o[1]) * rdy;
-    if (ny > fy) { float c = ny; ny = fy; fy = c; }
-    if (near > fy || ny > far) { near = far = FLT_MAX; return; }
-    if (ny > near) near = ny;
-    if (fy < far) far = fy;
-    float nz = (aabb[2] - o[2]) * rdz, fz = (aabb[5] - o[2]) * rdz;
-    if (nz > fz) { float c = nz; nz = fz; fz = c; }
-    if (near > fz || nz > far) { near = far = FLT_MAX; return; }
-    if (nz > near) near = nz;
-    if (fz < far) far = fz;
-    if (near < min_near) near = min_near;
-}
-
-struct LegoOut {
-    float *rays_o, *rays_d, *rgba, *bg, *nears, *fars, *noises;
-    int32_t *counter, *step_counter;
-};
-
-// Block `blk` of the `nblk` blocks (256 threads) drawing one batch.
-NGP_DEV void lego_rays_block(uint32_t blk, uint32_t nblk, const float* __restrict__ poses, const LegoScene& sc,
-                             uint32_t N, StepState* __restrict__ st, const LegoOut& out) {
-    float* __restrict__ rays_o = out.rays_o;
-    float* __restrict__ rays_d = out.rays_d;
-    float* __restrict__ rgba = out.rgba;
-    float* __restrict__ bg = out.bg;
-    float* __restrict__ nears = out.nears;
-    float* __restrict__ fars = out.fars;
-    float* __restrict__ noises = out.noises;
-    int32_t* __restrict__ counter = out.counter;
-    int32_t* __restrict__ step_counter = out.step_counter;
-    const uint32_t n = blk * blockDim.x + threadIdx.x;
-    const uint32_t it = (uint32_t)st->draw;
-    // Only this kernel touches draw / lego_done / counter / step_counter, so it
-    // can run beside the previous step's optimizer (nerf/fused.py pipelining).
-    if (n == 0) {
-        if (step_counter && it > 0) {  // the previous batch's counts (mean_count, update_extra_state)
-            const uint32_t slot = (it - 1) & 15u;
-            step_counter[slot * 2] = counter[0];
-            step_counter[slot * 2 + 1] = counter[1];
-        }
-        counter[0] = 0;
-        counter[1] = 0;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // every block has read draw before the last one bumps it
-        __threadfence();
-        if (atomicAdd(&st->lego_done, 1) == (int32_t)nblk - 1) {
-            st->draw = (int32_t)it + 1;
-            st->lego_done = 0;
-        }
-    }
-    if (n >= N) return;
-    const uint32_t pose = rng_u32(sc.seed, it, 0xffffffffu, 0) % sc.n_poses;
-    const float* P = poses + (size_t)pose * 16;
-    const uint32_t pix = rng_u32(sc.seed, it, n, 1) % (sc.H * sc.W);
-    // get_rays (utils.py:52-136): pixel centre, camera direction, normalise, rotate
-    const float i = (float)(pix % sc.W) + 0.5f;
-    const float j = (float)(pix / sc.W) + 0.5f;
-    float xs = (i - sc.cx) / sc.fx, ys = (j - sc.cy) / sc.fy, zs = 1.0f;
-    const float nrm = sqrtf(xs * xs + ys * ys + zs * zs);
-    xs /= nrm; ys /= nrm; zs /= nrm;
-    float o[3], d[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        d[k] = fmaf(zs, P[k * 4 + 2], fmaf(ys, P[k * 4 + 1], xs * P[k * 4 + 0]));
-        o[k] = P[k * 4 + 3];
-        rays_o[n * 3 + k] = o[k];
-        rays_d[n * 3 + k] = d[k];
-    }
-    // analytic RGBA: colour of the nearest box hit (SyntheticLego.target)
-    float best = INFINITY;
-    int arg = -1;
-    for (int b = 0; b < sc.nboxes; ++b) {
-        float tn = -INFINITY, tf = INFINITY;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float inv = 1.0f / d[k];
-            const float t0 = (sc.lo[b][k] - o[k]) * inv, t1 = (sc.hi[b][k] - o[k]) * inv;
-            tn = fmaxf(tn, fminf(t0, t1));
-            tf = fminf(tf, fmaxf(t0, t1));
-        }
-        if (tf >= tn && tf > 0 && tn < best) { best = tn; arg = b; }
-    }
-    rgba[n * 4 + 0] = arg >= 0 ? sc.rgb[arg][0] : 0.0f;
-    rgba[n * 4 + 1] = arg >= 0 ? sc.rgb[arg][1] : 0.0f;
-    rgba[n * 4 + 2] = arg >= 0 ? sc.rgb[arg][2] : 0.0f;
-    rgba[n * 4 + 3] = arg >= 0 ? 1.0f : 0.0f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) bg[n * 3 + k] = rng_unit(sc.seed, it, n, 2 + k);
-    noises[n] = rng_unit(sc.seed, it, n, 5);
-    float nr, fr;
-    near_far(o, d, sc.aabb, sc.min_near, nr, fr);
-    nears[n] = nr;
-    fars[n] = fr;
 }
 
 __global__ void __launch_bounds__(256)
@@ -425,24 +296,6 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     }
 }
 
-// ---- optimizer ------------------------------------------------------------------
-struct TensorList {
-    int n;
-    float* p[kMaxTensors];
-    ngp_half* g[kMaxTensors];
-    float* m[kMaxTensors];
-    float* v[kMaxTensors];
-    ngp_half* ph[kMaxTensors];        // optional fp16 shadow of p (the MLPs' forward weights)
-    uint64_t size[kMaxTensors];
-    uint64_t start[kMaxTensors + 1];  // flat index space; each tensor starts 8-aligned
-};
-
-NGP_DEV int find_tensor(const TensorList& tl, uint64_t i) {
-    int k = 0;
-    while (k + 1 < tl.n && i >= tl.start[k + 1]) ++k;
-    return k;
-}
-
 // GradScaler._unscale_grads_ inf/nan check over every grad (8 halves / lane)
 __global__ void __launch_bounds__(256)
 k_nonfinite(TensorList tl, StepState* __restrict__ st) {
@@ -465,113 +318,9 @@ k_nonfinite(TensorList tl, StepState* __restrict__ st) {
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&st->found_inf, 1);
 }
 
-struct AdamArgs {
-    float base_lr, beta1, beta2, eps;
-    int32_t iters;   // LambdaLR: lr = base_lr * 0.1 ** min(epoch / iters, 1)
-    int32_t zero_grads;
-    float grad_mult; // e.g. 1 / world_size after a data-parallel all-reduce (sum)
-    int32_t defer_end;  // the step's bookkeeping runs in the next k_step_head
-};
-
-// torch.optim.Adam (weight_decay 0) on p, with g = half_grad * (1 / scale);
-// skipped (state untouched) when the check found an inf/nan, like
-// GradScaler.step. Grads are zeroed afterwards either way. (Ending the step
-// in Adam's last block instead of k_step_end was measured: 4096 blocks
-// retiring through one counter cost ~180 us of contended atomics.)
-//
-// Layout: chunks of kAdamChunk elements of the flat (8-aligned per tensor)
-// index space, chunk c to block c mod gridDim; every thread keeps two 16-byte
-// groups of each stream in flight. A chunk inside one tensor (all but the few
-// at the seams) takes its pointers from scalar loads.
-constexpr uint32_t kAdamThreads = 256, kAdamChunk = kAdamThreads * 8;
-NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const AdamArgs& aa, uint32_t blk,
-                        uint32_t nblk) {
-    // GradScaler checks the UNSCALED grads: once the scale has backed off so far
-    // that 1/scale is inf, every element (0 * inf = NaN) is non-finite and the
-    // step is skipped, which the checks of the scaled fp16 grads cannot see
-    const float inv_scale = (float)(1.0 / (double)st->scale) * aa.grad_mult;
-    const bool inv_bad = !__builtin_isfinite(inv_scale);
-    const bool skip = st->found_inf != 0 || inv_bad;
-    if (blk == 0 && threadIdx.x == 0) {
-        if (inv_bad) st->found_inf = 1;  // the scaler update backs off, as torch's would
-        if (aa.defer_end) st->end_pending = 1;  // read by k_step_head only
-    }
-    const int32_t step = st->adam_step + 1;
-    const double lr = (double)aa.base_lr * pow(0.1, fmin((double)st->epoch / (double)aa.iters, 1.0));
-    const double bc1 = 1.0 - pow((double)aa.beta1, step);
-    const double bc2 = 1.0 - pow((double)aa.beta2, step);
-    const float step_size = (float)(lr / bc1);
-    const float inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
-    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-    auto adam1 = [&](float& p, float& m, float& v, float gh) {
-        const float gk = gh * inv_scale;
-        m = m + (1.0f - aa.beta1) * (gk - m);
-        v = v * aa.beta2 + (1.0f - aa.beta2) * gk * gk;
-        const float denom = sqrtf(v) * inv_bc2_sqrt + aa.eps;
-        p = p - step_size * (m / denom);
-    };
-    const uint64_t total = tl.start[tl.n];
-    const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
-    for (uint64_t c = blk; c < nchunks; c += nblk) {
-        const uint64_t c0 = c * kAdamChunk, c1 = min(c0 + kAdamChunk, total);
-        const int k = find_tensor(tl, c0);
-        if (find_tensor(tl, c1 - 1) == k && c1 - tl.start[k] <= tl.size[k]) {
-            // whole chunk inside tensor k: two float4 groups per thread, loads first
-            const uint64_t base = c0 - tl.start[k] + threadIdx.x * 4;
-            float4 pv[2], mv[2], vv[2];
-            half4 gh[2];
-            bool in[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const uint64_t off = base + u * (kAdamChunk / 2);
-                in[u] = c0 + (off - (c0 - tl.start[k])) < c1;
-                if (!in[u]) continue;
-                pv[u] = *reinterpret_cast<const float4*>(tl.p[k] + off);
-                mv[u] = *reinterpret_cast<const float4*>(tl.m[k] + off);
-                vv[u] = *reinterpret_cast<const float4*>(tl.v[k] + off);
-                gh[u] = *reinterpret_cast<const half4*>(tl.g[k] + off);
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                if (!in[u]) continue;
-                const uint64_t off = base + u * (kAdamChunk / 2);
-                if (!skip) {
-                    adam1(pv[u].x, mv[u].x, vv[u].x, (float)gh[u][0]);
-                    adam1(pv[u].y, mv[u].y, vv[u].y, (float)gh[u][1]);
-                    adam1(pv[u].z, mv[u].z, vv[u].z, (float)gh[u][2]);
-                    adam1(pv[u].w, mv[u].w, vv[u].w, (float)gh[u][3]);
-                    *reinterpret_cast<float4*>(tl.p[k] + off) = pv[u];
-                    *reinterpret_cast<float4*>(tl.m[k] + off) = mv[u];
-                    *reinterpret_cast<float4*>(tl.v[k] + off) = vv[u];
-                    if (tl.ph[k])
-                        *reinterpret_cast<half4*>(tl.ph[k] + off) =
-                            half4{(ngp_half)pv[u].x, (ngp_half)pv[u].y, (ngp_half)pv[u].z, (ngp_half)pv[u].w};
-                }
-                if (aa.zero_grads) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
-            }
-            continue;
-        }
-        // a seam chunk: per element
-        for (uint64_t i = c0 + threadIdx.x; i < c1; i += kAdamThreads) {
-            const int kk = find_tensor(tl, i);
-            const uint64_t off = i - tl.start[kk];
-            if (off >= tl.size[kk]) continue;  // alignment padding between tensors
-            if (!skip) {
-                float p = tl.p[kk][off], m = tl.m[kk][off], v = tl.v[kk][off];
-                adam1(p, m, v, (float)tl.g[kk][off]);
-                tl.p[kk][off] = p;
-                tl.m[kk][off] = m;
-                tl.v[kk][off] = v;
-                if (tl.ph[kk]) tl.ph[kk][off] = (ngp_half)p;
-            }
-            if (aa.zero_grads) tl.g[kk][off] = (ngp_half)0.0f;
-        }
-    }
-}
-
 __global__ void __launch_bounds__(kAdamThreads)
 k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa) {
-    adam_sweep(tl, st, aa, blockIdx.x, gridDim.x);
+    adam_sweep(tl, st, aa, blockIdx.x, gridDim.x, threadIdx.x);
 }
 
 // ---- data-parallel GradScaler guard ----------------------------------------------
@@ -643,7 +392,7 @@ __global__ void __launch_bounds__(kAdamThreads)
 k_adam_head(TensorList tl, StepState* __restrict__ st, AdamArgs aa, uint32_t nadam, const float* __restrict__ poses,
             LegoScene sc, uint32_t N, LegoOut out, uint32_t nlego, uint4* __restrict__ clear, uint32_t clear16) {
     if (blockIdx.x < nadam) {
-        adam_sweep(tl, st, aa, blockIdx.x, nadam);
+        adam_sweep(tl, st, aa, blockIdx.x, nadam, threadIdx.x);
         return;
     }
     const uint32_t b = blockIdx.x - nadam;
