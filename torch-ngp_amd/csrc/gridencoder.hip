@@ -605,6 +605,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     static_assert(kMaxBinsPerLevel <= kBinPts, "one bin per thread in the reservation step");
     __shared__ uint32_t cnt[kMaxBinsPerLevel], soff[kMaxBinsPerLevel + 1], wsum[NW];
     __shared__ uint2 binfo[kMaxBinsPerLevel];  // (slot - stage index, end of the bin's in-capacity stage run)
+    __shared__ uint32_t s_over;                // some bin of this workgroup ran past its capacity
     extern __shared__ BinItem stage[];  // kBinPts * NC
     const uint32_t level = blockIdx.y;
     const uint32_t nb = bp.nbins[level];
@@ -615,12 +616,21 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     BSTAMP(0);
 
     const uint32_t b = blockIdx.x * kBinPts + threadIdx.x;
-    bool valid = b < rows_of(B, im);
+    const bool in_rows = b < rows_of(B, im);
+    // the sample's coordinates and this level's grad are loaded together (the
+    // grad of an out-of-bounds sample is discarded below): loads gated on the
+    // previous coordinate's bounds check went out one round trip at a time
+    const uint32_t bl = in_rows ? b : 0u;
     float x[D];
 #pragma unroll
+    for (uint32_t d = 0; d < D; d++) x[d] = inputs[(size_t)bl * D + d];
+    const size_t gi0 = grad_layout == 0 ? (size_t)level * B + bl : (size_t)bl * L + level;
+    const ngp_half2 gv0 = *reinterpret_cast<const ngp_half2*>(grad + gi0 * 2);
+    bool valid = in_rows;
+#pragma unroll
     for (uint32_t d = 0; d < D; d++) {
-        x[d] = valid ? inputs[(size_t)b * D + d] : 0.5f;
-        if (valid && im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
+        if (!in_rows) x[d] = 0.5f;
+        if (in_rows && im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
         if (x[d] < 0 || x[d] > 1) valid = false;
     }
     const uint32_t off0 = (uint32_t)offsets[level];
@@ -637,13 +647,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         pos[d] -= (float)pg[d];
         if (interp == 1) pos[d] = smoothstep(pos[d]);
     }
-    float g0 = 0.0f, g1 = 0.0f;
-    if (valid) {
-        const size_t gi = grad_layout == 0 ? (size_t)level * B + b : (size_t)b * L + level;
-        const ngp_half2 gv = *reinterpret_cast<const ngp_half2*>(grad + gi * C);
-        g0 = (float)gv[0];
-        g1 = (float)gv[1];
-    }
+    const float g0 = valid ? (float)gv0[0] : 0.0f, g1 = valid ? (float)gv0[1] : 0.0f;
     if (g0 == 0.0f && g1 == 0.0f) valid = false;  // nothing to add (e.g. samples past the early stop)
 
     uint32_t key[NC], rank[NC];
@@ -769,22 +773,31 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         const uint32_t bin = key[idx] >> kBinShift;
         stage[soff[bin] + rank[idx]] = BinItem{(key[idx] & (kBinEntries - 1)) | (bin << 16), val[idx]};
     }
+    if (threadIdx.x == 0) s_over = 0;
+    lds_barrier();
     if (threadIdx.x < nb) {
         const uint32_t t = threadIdx.x, lim = bs_mine >= cap ? 0u : min(c_mine, cap - bs_mine);
         binfo[t] = uint2{t * cap + bs_mine - soff[t], soff[t] + lim};
+        if (lim < c_mine) s_over = 1;  // benign race: every writer stores 1
     }
     lds_barrier();
     BSTAMP(3);
     const uint32_t total = soff[nb];
     BinItem* lvl_items = items + bp.item0[level];
     ngp_half* gg = grad_grid + (size_t)off0 * C;
+    // in-capacity items: plain stores, back to back (with the overflow path's
+    // returning atomics in the same loop the compiler waited for every
+    // store's completion before the next)
     for (uint32_t k = threadIdx.x; k < total; k += kBinPts) {
+        const BinItem it = stage[k];
+        const uint2 bi = binfo[it.e >> 16];
+        if (k < bi.y) lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
+    }
+    for (uint32_t k = threadIdx.x; s_over && k < total; k += kBinPts) {
         const BinItem it = stage[k];
         const uint32_t bin = it.e >> 16;
         const uint2 bi = binfo[bin];
-        if (k < bi.y) {
-            lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
-        } else {  // past the bin's capacity
+        if (k >= bi.y) {  // past the bin's capacity
             const size_t e = (size_t)bin * kBinEntries + (it.e & 0xffffu);
             ngp_half2* p = reinterpret_cast<ngp_half2*>(gg + e * C);
             if (nonfinite) {  // the returning atomic: the entry's new value is checked
@@ -1013,7 +1026,27 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         lds_barrier();
         const float q24 = 1.0f / 16777216.0f;
         bool inf_out = false;  // a stored grad is inf/nan (GradScaler's check, when `nonfinite` is given)
-        if (cur.owner) {
+        if (cur.owner && cur.fresh) {
+            // the common case: the unit owns its slice of a cleared grad. All of
+            // the lane's LDS reads first, then the stores. Nothing here consumes
+            // a global load, so no wait on the next unit's prefetched items (with
+            // the old values in the loop below, the compiler waited vmcnt(0) --
+            // every outstanding load and store -- before each entry).
+            ulonglong2 xs[G];
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j) {
+                const uint32_t e = j * kAccThreads + t;
+                xs[j] = e < cur.ne ? reinterpret_cast<const ulonglong2*>(acc)[e] : ulonglong2{0ull, 0ull};
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j) {
+                const int64_t x0 = (int64_t)xs[j].x, x1 = (int64_t)xs[j].y;
+                if (x0 == 0 && x1 == 0) continue;  // also every e >= ne
+                const ngp_half2 n{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
+                inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
+                cur.tbl[j * kAccThreads + t] = n;
+            }
+        } else if (cur.owner) {
             // one entry per lane per step: a lane reads its entry's two 8-byte
             // sums as one 16-byte LDS read (consecutive lanes, consecutive 16 B:
             // conflict-free; the former 4-entry groups per lane read at a 64-B
