@@ -46,13 +46,15 @@ units = []
 for i in range(nwg):
     prev = st[i, 2]
     for u in range(int(min(st[i, 3], 11))):
-        a, b, c, info = st[i, 4 + 5 * u: 8 + 5 * u]
-        units.append((a - prev, b - a, c - b, info & 0xffffffff, (info >> 32) & 0xff, (info >> 40) & 0xff))
+        a, b, c, info, d = st[i, 4 + 5 * u: 9 + 5 * u]
+        # d: after the barrier that drains the adds (0 in builds without that stamp)
+        dr, fl = (d - b, c - d) if d else (0, c - b)
+        units.append((a - prev, b - a, c - b, info & 0xffffffff, (info >> 32) & 0xff, (info >> 40) & 0xff, dr, fl))
         prev = c
 u = np.array(units, dtype=np.int64)
 res["units"] = len(u)
 res["units_per_wg_max"] = int(st[:, 3].max())
-for k, name in enumerate(["gap_to_start", "adds", "flush"]):
+for k, name in ((0, "gap_to_start"), (1, "adds"), (2, "drain_and_flush"), (6, "drain"), (7, "flush")):
     res[name + "_med"] = int(np.median(u[:, k]))
     res[name + "_p90"] = int(np.percentile(u[:, k], 90))
     res[name + "_sum_per_wg"] = int(u[:, k].sum() / nwg)
@@ -62,7 +64,8 @@ by_level = {}
 for lv in np.unique(u[:, 5]):
     m = u[:, 5] == lv
     by_level[int(lv)] = {"units": int(m.sum()), "items_med": int(np.median(u[m, 3])),
-                         "adds_med": int(np.median(u[m, 1])), "flush_med": int(np.median(u[m, 2]))}
+                         "adds_med": int(np.median(u[m, 1])), "drain_med": int(np.median(u[m, 6])),
+                         "flush_med": int(np.median(u[m, 7]))}
 res["by_level"] = by_level
 print(json.dumps(res, indent=1))
 

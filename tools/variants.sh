@@ -13,7 +13,7 @@ while [ $# -ge 2 ]; do
     mkdir -p "$out"
     /opt/rocm/bin/hipcc $FLAGS $defs -c "$R/torch-ngp_amd/csrc/gridencoder.hip" -o "$out/gridencoder.o"
     objs=""
-    for o in ngp_lib raymarching shencoder ffmlp adam nerf_fused; do objs="$objs $OBJ/$o.o"; done
+    for o in ngp_lib raymarching shencoder ffmlp adam nerf_fused density_grid; do objs="$objs $OBJ/$o.o"; done
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libngp_hip.so" $objs "$out/gridencoder.o"
     rm -f "$out/gridencoder.o"
     echo "built $out/libngp_hip.so ($defs)"

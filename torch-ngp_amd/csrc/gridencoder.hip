@@ -539,6 +539,9 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #ifndef NGP_ACC_BATCH
 #define NGP_ACC_BATCH 16
 #endif
+#ifndef NGP_MATCH_MAX_BINS
+#define NGP_MATCH_MAX_BINS 64
+#endif
 constexpr uint32_t kBinShift = NGP_BIN_SHIFT;
 constexpr uint32_t kBinEntries = 1u << kBinShift;
 constexpr uint32_t kMaxBinsPerLevel = 256;
@@ -693,45 +696,57 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // those levels' bin time, tools/accum_stamps.py); otherwise per corner:
     // one atomic per wave when the wave's items of that corner share a bin,
     // else one per item.
-    uint64_t lms[NC];
-    uint32_t b0 = 0xffffffffu;
+    // On levels with few bins (dense levels: z-slab bins) a wave's items fall
+    // in a handful of bins: one LDS atomic per distinct bin over all corners
+    // (up to kMatchIters bins). Per-item atomics there were 2-3 counters hit by
+    // every lane, serialized (corners + rank: 15-29 K cycles on levels 0-4
+    // against 8 K on the hashed ones, tools/accum_stamps.py). Items left over
+    // (and every item of a many-bin level) take the per-corner path.
+    constexpr uint32_t kMatchIters = 8, kMatchMaxBins = NGP_MATCH_MAX_BINS;
+    uint64_t pend[NC];
 #pragma unroll
     for (uint32_t idx = 0; idx < NC; idx++) {
-        lms[idx] = __ballot(live[idx]);
-        if (b0 == 0xffffffffu && lms[idx])
-            b0 = __builtin_amdgcn_readlane(key[idx], __ffsll((unsigned long long)lms[idx]) - 1) >> kBinShift;
+        pend[idx] = __ballot(live[idx]);
+        rank[idx] = 0;
     }
-    bool uni = b0 != 0xffffffffu;
+    for (uint32_t it = 0; nb <= kMatchMaxBins && it < kMatchIters; ++it) {
+        uint32_t bf = 0xffffffffu;
 #pragma unroll
-    for (uint32_t idx = 0; idx < NC; idx++) uni = uni && __ballot(live[idx] && (key[idx] >> kBinShift) != b0) == 0;
-    if (uni) {
+        for (uint32_t idx = 0; idx < NC; idx++)
+            if (bf == 0xffffffffu && pend[idx])
+                bf = __builtin_amdgcn_readlane(key[idx], __ffsll((unsigned long long)pend[idx]) - 1) >> kBinShift;
+        if (bf == 0xffffffffu) break;
+        uint64_t m[NC];
         uint32_t total = 0;
 #pragma unroll
-        for (uint32_t idx = 0; idx < NC; idx++) total += (uint32_t)__popcll(lms[idx]);
+        for (uint32_t idx = 0; idx < NC; idx++) {
+            m[idx] = __ballot(live[idx] && (key[idx] >> kBinShift) == bf);
+            total += (uint32_t)__popcll(m[idx]);
+        }
         uint32_t r0 = 0;
-        if (lane == 0) r0 = atomicAdd(&cnt[b0], total);
+        if (lane == 0) r0 = atomicAdd(&cnt[bf], total);
         uint32_t run = __builtin_amdgcn_readfirstlane(r0);
 #pragma unroll
         for (uint32_t idx = 0; idx < NC; idx++) {
-            rank[idx] = run + lanes_below(lms[idx]);
-            run += (uint32_t)__popcll(lms[idx]);
+            if ((m[idx] >> lane) & 1ull) rank[idx] = run + lanes_below(m[idx]);
+            run += (uint32_t)__popcll(m[idx]);
+            pend[idx] &= ~m[idx];
         }
-    } else {
+    }
 #pragma unroll
-        for (uint32_t idx = 0; idx < NC; idx++) {
-            const uint32_t bin = key[idx] >> kBinShift;
-            const uint64_t lm = lms[idx];
-            rank[idx] = 0;
-            if (!lm) continue;
-            const int first = __ffsll((unsigned long long)lm) - 1;
-            const uint32_t bf = __builtin_amdgcn_readlane(bin, first);
-            if (__ballot(live[idx] && bin != bf) == 0) {
-                uint32_t r0 = 0;
-                if (lane == first) r0 = atomicAdd(&cnt[bf], (uint32_t)__popcll(lm));
-                rank[idx] = __builtin_amdgcn_readlane(r0, first) + lanes_below(lm);
-            } else if (live[idx]) {
-                rank[idx] = atomicAdd(&cnt[bin], 1u);
-            }
+    for (uint32_t idx = 0; idx < NC; idx++) {
+        const uint64_t lm = pend[idx];
+        if (!lm) continue;
+        const bool mine = (lm >> lane) & 1ull;
+        const uint32_t bin = key[idx] >> kBinShift;
+        const int first = __ffsll((unsigned long long)lm) - 1;
+        const uint32_t bf = __builtin_amdgcn_readlane(bin, first);
+        if (__ballot(mine && bin != bf) == 0) {
+            uint32_t r0 = 0;
+            if (lane == first) r0 = atomicAdd(&cnt[bf], (uint32_t)__popcll(lm));
+            if (mine) rank[idx] = __builtin_amdgcn_readlane(r0, first) + lanes_below(lm);
+        } else if (mine) {
+            rank[idx] = atomicAdd(&cnt[bin], 1u);
         }
     }
     lds_barrier();
@@ -834,6 +849,7 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // first entry, which is what GradScaler's inf check looks for.
 constexpr uint32_t kAccThreads = 512, kAccBatch = NGP_ACC_BATCH, kRetireGroups = 16;
 static_assert(kAccBatch > 0, "NGP_ACC_BATCH must be positive");
+static_assert(kMaxLevels <= 64, "the accumulate finds a bin's level with one wave ballot");
 static_assert(kBinEntries % kAccThreads == 0, "each flush thread owns whole entries (G > 0)");
 // the int64 LDS image of one bin (+ the counts in dynamic LDS) fits a CU's 160 KB
 static_assert(kBinEntries * 2 * sizeof(unsigned long long) <= 128 * 1024, "bin image exceeds LDS");
@@ -865,24 +881,39 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         }
     }
     lds_barrier();
-    auto level_of = [&](uint32_t b) {
+    auto level_of = [&](uint32_t b) {  // last level whose first bin is <= b (binary lifting)
         uint32_t l = 0;
-        while (l + 1 < nlev && b >= s_bin0[l + 1]) ++l;
+#pragma unroll
+        for (uint32_t s = kMaxLevels / 2; s; s >>= 1)
+            if (l + s < nlev && b >= s_bin0[l + s]) l += s;
         return l;
     };
 
-    // 1. units per bin, exclusive prefix (thread t owns bins [t*per, t*per + per))
+    // 1. units per bin, exclusive prefix (thread t owns bins [t*per, t*per + per)).
+    // The counts are loaded kStep1Loads at a time, all before their use (one
+    // round trip per group instead of one per bin).
+    constexpr uint32_t kStep1Loads = 4;
     const uint32_t per = (nbins + kAccThreads - 1) / kAccThreads;
     uint32_t mine = 0;
     uint32_t level = t * per < nbins ? level_of(t * per) : 0;
-    for (uint32_t j = 0; j < per; ++j) {
-        const uint32_t b = t * per + j;
-        if (b >= nbins) break;
-        while (level + 1 < nlev && b >= s_bin0[level + 1]) ++level;
-        const uint32_t n = min(cursor[b], s_cap[level]);
-        bn[b] = n | (cursor[b] > s_cap[level] ? 0x80000000u : 0u);  // top bit: items went atomic
-        upre[b] = (n + kSegItems - 1) / kSegItems;  // n: the clipped count
-        mine += upre[b];
+    for (uint32_t j0 = 0; j0 < per; j0 += kStep1Loads) {
+        uint32_t cv[kStep1Loads];
+#pragma unroll
+        for (uint32_t j = 0; j < kStep1Loads; ++j) {
+            const uint32_t b = t * per + j0 + j;
+            cv[j] = j0 + j < per && b < nbins ? cursor[b] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kStep1Loads; ++j) {
+            const uint32_t b = t * per + j0 + j;
+            if (j0 + j >= per || b >= nbins) break;
+            while (level + 1 < nlev && b >= s_bin0[level + 1]) ++level;
+            const uint32_t n = min(cv[j], s_cap[level]);
+            bn[b] = n | (cv[j] > s_cap[level] ? 0x80000000u : 0u);  // top bit: items went atomic
+            const uint32_t nu = (n + kSegItems - 1) / kSegItems;      // n: the clipped count
+            upre[b] = nu;
+            mine += nu;
+        }
     }
     uint32_t incl = mine;
 #pragma unroll
@@ -936,24 +967,31 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // 3. units. The first item batch of a unit and, for a single-owner unit,
     // its slice of the table are loaded one unit ahead (while the previous
     // unit does its LDS adds and writes), hiding the memory latency.
+    // No bool members: with them the struct lived in scratch memory (a
+    // private-segment load and store per unit, waited on like any other).
+    constexpr uint32_t kOwner = 1, kFresh = 2;  // flags; fresh: the table slice is known to be zero
     struct Unit {
-        uint32_t level, lbin, s0, s1;
-        bool owner, fresh;  // fresh: the table slice is known to be zero (no read-modify-write)
+        uint32_t level, lbin, s0, s1, ne, flags;
         const uint64_t* src;
         ngp_half2* tbl;
-        uint32_t ne;
     };
+    // The unit's bin: the last bin whose first unit is <= u, found 64 ways
+    // per round (two dependent LDS reads for up to 4096 bins; a binary
+    // search took ~11), and its level by one ballot over the level starts.
     auto locate = [&](uint32_t u) {
-        uint32_t lo = 0, hi = nbins - 1;  // last bin whose first unit <= u
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (upre[mid] <= u) lo = mid; else hi = mid - 1;
+        uint32_t lo = 0, n = nbins;
+        while (n > 1) {
+            const uint32_t stride = (n + 63) / 64, k = lane * stride;
+            const uint64_t mk = __ballot(k < n && upre[lo + k] <= u);  // lane 0 always qualifies
+            const uint32_t L = 63u - (uint32_t)__builtin_clzll(mk);
+            lo += L * stride;
+            n = min(stride, n - L * stride);
         }
         Unit r;
         const uint32_t gb = lo, seg = u - upre[gb];
-        r.owner = upre[gb + 1] - upre[gb] == 1;
-        r.fresh = r.owner && zeroed && (bn[gb] >> 31) == 0;
-        r.level = level_of(gb);
+        const bool owner = upre[gb + 1] - upre[gb] == 1;
+        r.flags = (owner ? kOwner : 0u) | (owner && zeroed && (bn[gb] >> 31) == 0 ? kFresh : 0u);
+        r.level = 63u - (uint32_t)__builtin_clzll(__ballot(lane < nlev && s_bin0[lane] <= gb));
         r.lbin = gb - s_bin0[r.level];
         r.s0 = seg * kSegItems;
         r.s1 = min(bn[gb] & 0x7fffffffu, r.s0 + kSegItems);
@@ -973,15 +1011,20 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             it[q] = k < w.s1 ? __builtin_nontemporal_load(w.src + k) : ~0ull;
         }
     };
+    // Only a non-fresh owner reads its slice back. No select on the loaded
+    // value here: consuming it (a `fresh ? 0 : load` select) made the compiler
+    // wait vmcnt(0) -- for the whole item prefetch issued just before -- right
+    // after issuing it (phase clocks: ~6 K cycles per unit, tools/accum_stamps.py).
     auto load_old = [&](const Unit& w, uint32_t (&old)[G]) {
+        if ((w.flags & (kOwner | kFresh)) != kOwner) return;
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
             const uint32_t e = j * kAccThreads + t;
-            if (w.owner && e < w.ne) old[j] = w.fresh ? 0u : reinterpret_cast<const uint32_t*>(w.tbl)[e];
+            if (e < w.ne) old[j] = reinterpret_cast<const uint32_t*>(w.tbl)[e];
         }
     };
     uint64_t it[kAccBatch];
-    uint32_t old[G];
+    uint32_t old[G] = {};
     Unit cur{};
     if (blockIdx.x < total) {
         cur = locate(blockIdx.x);
@@ -995,7 +1038,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         lds_barrier();
         [[maybe_unused]] const uint32_t sb = 4 + 5 * min(nstamp, 11u);
         STAMP(sb, __builtin_amdgcn_s_memtime());
-        STAMP(sb + 3, (cur.s1 - cur.s0) | ((uint64_t)cur.owner << 32) | ((uint64_t)cur.level << 40));
+        STAMP(sb + 3, (cur.s1 - cur.s0) | ((uint64_t)(cur.flags & kOwner) << 32) | ((uint64_t)cur.level << 40));
         bool bad = false;
         for (uint32_t k0 = cur.s0;;) {
 #pragma unroll
@@ -1024,9 +1067,10 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         }
         if (__ballot(bad)) s_bad = 1;  // benign race: every writer stores 1
         lds_barrier();
+        STAMP(sb + 4, __builtin_amdgcn_s_memtime());
         const float q24 = 1.0f / 16777216.0f;
         bool inf_out = false;  // a stored grad is inf/nan (GradScaler's check, when `nonfinite` is given)
-        if (cur.owner && cur.fresh) {
+        if (cur.flags & kFresh) {
             // the common case: the unit owns its slice of a cleared grad. All of
             // the lane's LDS reads first, then the stores. Nothing here consumes
             // a global load, so no wait on the next unit's prefetched items (with
@@ -1046,7 +1090,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                 inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
                 cur.tbl[j * kAccThreads + t] = n;
             }
-        } else if (cur.owner) {
+        } else if (cur.flags & kOwner) {
             // one entry per lane per step: a lane reads its entry's two 8-byte
             // sums as one 16-byte LDS read (consecutive lanes, consecutive 16 B:
             // conflict-free; the former 4-entry groups per lane read at a 64-B
