@@ -73,19 +73,22 @@ print(json.dumps(res, indent=1))
 # counter init, after corners + ranks, after reservation + scan, after
 # staging, end
 b = stamps[32768:32768 + 8 * 4096].view(-1, 8).cpu().numpy().astype(np.int64)
+gx = (ft.M + 511) // 512  # bin-kernel workgroups per level (kBinPts samples each)
+blevel = np.arange(len(b)) // gx
+blevel = blevel[b[:, 0] > 0]  # workgroups past the sample count leave before stamping
 b = b[b[:, 0] > 0]
 d = np.diff(b[:, :5], axis=1)
+if (b[:, 5] > 0).all():  # builds with the in-phase stamps: loads | corners + merge | rank
+    d = np.concatenate([np.stack([b[:, 5] - b[:, 0], b[:, 6] - b[:, 5], b[:, 1] - b[:, 6]], 1), d[:, 1:]], 1)
 print(json.dumps({"bin_workgroups": int(len(b)),
                   "bin_phase_med": [int(x) for x in np.median(d, axis=0)],
                   "bin_phase_p90": [int(x) for x in np.percentile(d, 90, axis=0)],
-                  "bin_phases": ["corners+rank", "reserve+scan", "stage", "write-out"]}))
-nx = len(b) // 16 if len(b) % 16 == 0 else None
-if nx:
-    per = {}
-    for lv in range(16):
-        dd = d[lv * nx:(lv + 1) * nx]
-        per[lv] = [int(x) for x in np.median(dd, axis=0)]
-    print(json.dumps({"bin_phase_med_by_level": per}))
+                  "bin_phases": (["loads", "corners+merge", "rank"] if d.shape[1] == 6 else ["corners+rank"])
+                  + ["reserve+scan", "stage", "write-out"]}))
+per = {}
+for lv in np.unique(blevel):
+    per[int(lv)] = [int(x) for x in np.median(d[blevel == lv], axis=0)]
+print(json.dumps({"bin_phase_med_by_level": per}))
 
 # k_mlp_bwd (sigma NH=1, colour NH=2): per wave, 16 stamps: entry, after the
 # fragment image copy, after each chunk, after the loop, after the dW fold,

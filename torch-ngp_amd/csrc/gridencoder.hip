@@ -592,7 +592,10 @@ NGP_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::
 __device__ unsigned long long* g_stamps;
 #define STAMP(slot, v) do { if (g_stamps && threadIdx.x == 0) g_stamps[blockIdx.x * 64 + (slot)] = (v); } while (0)
 #define BSTAMP(slot) do { if (g_stamps && threadIdx.x == 0) g_stamps[32768 + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+// after the wave's outstanding loads have arrived
+#define BSTAMPW(slot) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); BSTAMP(slot); } while (0)
 #else
+#define BSTAMPW(slot) do { } while (0)
 #define STAMP(slot, v) do { } while (0)
 #define BSTAMP(slot) do { } while (0)
 #endif
@@ -610,6 +613,10 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     __shared__ uint2 binfo[kMaxBinsPerLevel];  // (slot - stage index, end of the bin's in-capacity stage run)
     __shared__ uint32_t s_over;                // some bin of this workgroup ran past its capacity
     extern __shared__ BinItem stage[];  // kBinPts * NC
+    // the grid covers the row capacity; workgroups past the marched sample
+    // count (about a fifth of them on the Lego step) leave before any work
+    const uint32_t rows = rows_of(B, im);
+    if (blockIdx.x * kBinPts >= rows) return;
     const uint32_t level = blockIdx.y;
     const uint32_t nb = bp.nbins[level];
     const bool merge = (bp.merge_mask >> level) & 1u;
@@ -619,7 +626,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     BSTAMP(0);
 
     const uint32_t b = blockIdx.x * kBinPts + threadIdx.x;
-    const bool in_rows = b < rows_of(B, im);
+    const bool in_rows = b < rows;
     // the sample's coordinates and this level's grad are loaded together (the
     // grad of an out-of-bounds sample is discarded below): loads gated on the
     // previous coordinate's bounds check went out one round trip at a time
@@ -652,6 +659,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     }
     const float g0 = valid ? (float)gv0[0] : 0.0f, g1 = valid ? (float)gv0[1] : 0.0f;
     if (g0 == 0.0f && g1 == 0.0f) valid = false;  // nothing to add (e.g. samples past the early stop)
+    BSTAMPW(5);
 
     uint32_t key[NC], rank[NC];
     ngp_half2 val[NC];
@@ -675,7 +683,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         float v0 = w * g0, v1 = w * g1;
         bool lv_ = valid;
         if (merge) {
-            const uint32_t kprev = __shfl_up(k, 1, 64);
+            const uint32_t kprev = ngp_dpp::prev_lane(k);
             const bool same = valid && lane > 0 && kprev == k;
             const uint64_t sm = __ballot(same);
             if (sm) {
@@ -703,6 +711,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // against 8 K on the hashed ones, tools/accum_stamps.py). Items left over
     // (and every item of a many-bin level) take the per-corner path.
     constexpr uint32_t kMatchIters = 8, kMatchMaxBins = NGP_MATCH_MAX_BINS;
+    BSTAMP(6);
     uint64_t pend[NC];
 #pragma unroll
     for (uint32_t idx = 0; idx < NC; idx++) {
@@ -763,12 +772,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     }
     {   // block-wide exclusive scan of cnt[0..nb)
         const uint32_t t = threadIdx.x, wv = t >> 6;
-        uint32_t incl = c_mine;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(incl, o, 64);
-            if ((uint32_t)lane >= o) incl += u;
-        }
+        const uint32_t incl = ngp_dpp::scan_incl_u32(c_mine);
         if (lane == 63) wsum[wv] = incl;
         lds_barrier();
         uint32_t before = 0, all = 0;
@@ -915,12 +919,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             mine += nu;
         }
     }
-    uint32_t incl = mine;
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += u;
-    }
+    const uint32_t incl = ngp_dpp::scan_incl_u32(mine);
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
     uint32_t run = incl - mine, total = 0;
@@ -1032,6 +1031,9 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         load_old(cur, old);
     }
     for (uint32_t u = blockIdx.x; u < total; u += gridDim.x) {
+        // (clearing each entry in the flush after reading it instead -- no
+        // zeroing pass -- gave wrong sums on the GPU for reasons not found;
+        // measured and dropped)
         for (uint32_t i = t; i < kBinEntries * C / 2; i += kAccThreads)
             reinterpret_cast<uint4*>(acc)[i] = uint4{0u, 0u, 0u, 0u};
         if (t == 0) s_bad = 0;
@@ -1068,6 +1070,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         if (__ballot(bad)) s_bad = 1;  // benign race: every writer stores 1
         lds_barrier();
         STAMP(sb + 4, __builtin_amdgcn_s_memtime());
+        const bool unit_bad = s_bad != 0;
         const float q24 = 1.0f / 16777216.0f;
         bool inf_out = false;  // a stored grad is inf/nan (GradScaler's check, when `nonfinite` is given)
         if (cur.flags & kFresh) {
@@ -1122,8 +1125,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                 }
             }
         }
-        if (s_bad && t == 0) cur.tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
-        if (nonfinite && (__ballot(inf_out) != 0 || s_bad) && (t & 63) == 0) atomicOr(nonfinite, 1);
+        if (unit_bad && t == 0) cur.tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
+        if (nonfinite && (__ballot(inf_out) != 0 || unit_bad) && (t & 63) == 0) atomicOr(nonfinite, 1);
         lds_barrier();  // the image is rezeroed by the next unit
         STAMP(sb + 2, __builtin_amdgcn_s_memtime());
         ++nstamp;

@@ -12,6 +12,7 @@ namespace ngp_dpp {
 // DPP controls (GFX9 encoding)
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
 constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+constexpr int kWaveShr1 = 0x138;
 
 template <int CTRL, int ROW_MASK>
 NGP_DEV uint32_t mov(uint32_t v) {
@@ -57,5 +58,20 @@ NGP_DEV float scan_incl(float v) {
     v += movf<kRowBcast31, 0xc>(v);
     return v;
 }
+
+// Inclusive prefix sum over the wave (integers).
+NGP_DEV uint32_t scan_incl_u32(uint32_t v) {
+    v += mov<kRowShr1, 0xf>(v);
+    v += mov<kRowShr2, 0xf>(v);
+    v += mov<kRowShr4, 0xf>(v);
+    v += mov<kRowShr8, 0xf>(v);
+    v += mov<kRowBcast15, 0xa>(v);
+    v += mov<kRowBcast31, 0xc>(v);
+    return v;
+}
+
+// The previous lane's value (lane 0 gets 0): __shfl_up(v, 1) without the
+// LDS crossbar.
+NGP_DEV uint32_t prev_lane(uint32_t v) { return mov<kWaveShr1, 0xf>(v); }
 
 }  // namespace ngp_dpp
