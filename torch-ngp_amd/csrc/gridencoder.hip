@@ -705,41 +705,56 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // one atomic per wave when the wave's items of that corner share a bin,
     // else one per item.
     // On levels with few bins (dense levels: z-slab bins) a wave's items fall
-    // in a handful of bins: one LDS atomic per distinct bin over all corners
-    // (up to kMatchIters bins). Per-item atomics there were 2-3 counters hit by
-    // every lane, serialized (corners + rank: 15-29 K cycles on levels 0-4
-    // against 8 K on the hashed ones, tools/accum_stamps.py). Items left over
-    // (and every item of a many-bin level) take the per-corner path.
+    // in a handful of bins: up to kMatchIters distinct bins over all corners
+    // are matched first (per-item atomics there were 2-3 counters hit by every
+    // lane, serialized: corners + rank 15-29 K cycles on levels 0-4 against
+    // 8 K on the hashed ones, tools/accum_stamps.py). Lane i keeps match i's
+    // bin and item count, and ONE LDS atomic instruction reserves every
+    // matched bin's run at once; each item then adds its match's base (one
+    // lane permute). Items left over (and every item of a many-bin level)
+    // take the per-corner path.
     constexpr uint32_t kMatchIters = 8, kMatchMaxBins = NGP_MATCH_MAX_BINS;
+    static_assert(kMatchIters <= 64, "one lane per match");
     BSTAMP(6);
     uint64_t pend[NC];
+    uint32_t mit[NC];  // the item's match, or kMatchIters (none)
 #pragma unroll
     for (uint32_t idx = 0; idx < NC; idx++) {
         pend[idx] = __ballot(live[idx]);
         rank[idx] = 0;
+        mit[idx] = kMatchIters;
     }
-    for (uint32_t it = 0; nb <= kMatchMaxBins && it < kMatchIters; ++it) {
+    uint32_t nmatch = 0, m_bin = 0, m_total = 0;
+    for (; nb <= kMatchMaxBins && nmatch < kMatchIters; ++nmatch) {
         uint32_t bf = 0xffffffffu;
 #pragma unroll
         for (uint32_t idx = 0; idx < NC; idx++)
             if (bf == 0xffffffffu && pend[idx])
                 bf = __builtin_amdgcn_readlane(key[idx], __ffsll((unsigned long long)pend[idx]) - 1) >> kBinShift;
         if (bf == 0xffffffffu) break;
-        uint64_t m[NC];
-        uint32_t total = 0;
+        uint32_t run = 0;
 #pragma unroll
         for (uint32_t idx = 0; idx < NC; idx++) {
-            m[idx] = __ballot(live[idx] && (key[idx] >> kBinShift) == bf);
-            total += (uint32_t)__popcll(m[idx]);
+            const uint64_t m = __ballot(live[idx] && (key[idx] >> kBinShift) == bf);
+            if ((m >> lane) & 1ull) {
+                rank[idx] = run + lanes_below(m);
+                mit[idx] = nmatch;
+            }
+            run += (uint32_t)__popcll(m);
+            pend[idx] &= ~m;
         }
-        uint32_t r0 = 0;
-        if (lane == 0) r0 = atomicAdd(&cnt[bf], total);
-        uint32_t run = __builtin_amdgcn_readfirstlane(r0);
+        if ((uint32_t)lane == nmatch) {
+            m_bin = bf;
+            m_total = run;
+        }
+    }
+    if (nmatch) {
+        uint32_t base = 0;
+        if ((uint32_t)lane < nmatch) base = atomicAdd(&cnt[m_bin], m_total);
 #pragma unroll
         for (uint32_t idx = 0; idx < NC; idx++) {
-            if ((m[idx] >> lane) & 1ull) rank[idx] = run + lanes_below(m[idx]);
-            run += (uint32_t)__popcll(m[idx]);
-            pend[idx] &= ~m[idx];
+            const uint32_t bm = __shfl(base, (int)(mit[idx] & 63u), 64);
+            if (mit[idx] < kMatchIters) rank[idx] += bm;
         }
     }
 #pragma unroll
