@@ -32,6 +32,10 @@ if hasattr(lib, "ngp_debug_mlp_stamps"):
 for _ in range(12):
     ft.step()
 torch.cuda.synchronize()
+stamps.zero_()  # one more step on a clean buffer: no stale stamps of workgroups that exited early
+ms.zero_()
+ft.step()
+torch.cuda.synchronize()
 st = stamps[:32768].view(-1, 64).cpu().numpy().astype(np.int64)  # accumulate: 2 workgroups per CU
 nwg = int((st[:, 0] > 0).sum())
 st = st[:nwg]
@@ -72,11 +76,14 @@ print(json.dumps(res, indent=1))
 # k_grid_bwd_bin: per (point block, level) workgroup, 5 stamps: after the
 # counter init, after corners + ranks, after reservation + scan, after
 # staging, end
-b = stamps[32768:32768 + 8 * 4096].view(-1, 8).cpu().numpy().astype(np.int64)
+b = stamps[32768:32768 + 16 * 4096].view(-1, 16).cpu().numpy().astype(np.int64)
 gx = (ft.M + 511) // 512  # bin-kernel workgroups per level (kBinPts samples each)
 blevel = np.arange(len(b)) // gx
+bidx = np.arange(len(b))[b[:, 0] > 0]  # linear workgroup id: XCD = id % 8 (each XCD has its own clock)
 blevel = blevel[b[:, 0] > 0]  # workgroups past the sample count leave before stamping
 b = b[b[:, 0] > 0]
+np.savez_compressed(os.path.join(ROOT, "gpurun_out", "bin_stamps.npz"), b=b, level=blevel, bidx=bidx,
+                    acc=st)  # raw clocks for offline timelines
 d = np.diff(b[:, :5], axis=1)
 if (b[:, 5] > 0).all():  # builds with the in-phase stamps: loads | corners + merge | rank
     d = np.concatenate([np.stack([b[:, 5] - b[:, 0], b[:, 6] - b[:, 5], b[:, 1] - b[:, 6]], 1), d[:, 1:]], 1)

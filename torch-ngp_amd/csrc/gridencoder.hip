@@ -539,6 +539,9 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #ifndef NGP_ACC_BATCH
 #define NGP_ACC_BATCH 16
 #endif
+#ifndef NGP_JOINT_MERGE
+#define NGP_JOINT_MERGE 1
+#endif
 #ifndef NGP_MATCH_MAX_BINS
 #define NGP_MATCH_MAX_BINS 64
 #endif
@@ -591,17 +594,23 @@ NGP_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::
 #ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-workgroup phase clocks
 __device__ unsigned long long* g_stamps;
 #define STAMP(slot, v) do { if (g_stamps && threadIdx.x == 0) g_stamps[blockIdx.x * 64 + (slot)] = (v); } while (0)
-#define BSTAMP(slot) do { if (g_stamps && threadIdx.x == 0) g_stamps[32768 + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define BSTAMP(slot) do { if (g_stamps && threadIdx.x == 0) g_stamps[32768 + (size_t)stamp_id * 16 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
+// the chip-wide 100 MHz clock (s_memtime counts per shader engine / CU and
+// cannot order workgroups against each other)
+#define BRSTAMP(slot) do { if (g_stamps && threadIdx.x == 0) g_stamps[32768 + (size_t)stamp_id * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RSTAMP(slot) STAMP(slot, __builtin_amdgcn_s_memrealtime())
 // after the wave's outstanding loads have arrived
 #define BSTAMPW(slot) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); BSTAMP(slot); } while (0)
 #else
 #define BSTAMPW(slot) do { } while (0)
+#define BRSTAMP(slot) do { } while (0)
+#define RSTAMP(slot) do { } while (0)
 #define STAMP(slot, v) do { } while (0)
 #define BSTAMP(slot) do { } while (0)
 #endif
 
 template <uint32_t D>
-__global__ void __launch_bounds__(kBinPts)
+__global__ void __launch_bounds__(kBinPts, 8)  // 4 workgroups per CU: <= 64 VGPRs
 k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
                const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
@@ -615,17 +624,24 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     extern __shared__ BinItem stage[];  // kBinPts * NC
     // the grid covers the row capacity; workgroups past the marched sample
     // count (about a fifth of them on the Lego step) leave before any work
+    // grid (level, point block): consecutive workgroups take different levels
+    // of one block, so the coarse levels' VALU-heavy merging (dispatched
+    // first and alone when the grid was level-major: 9-16 us per workgroup
+    // against 6-8 us on the fine levels) shares the CUs with the fine levels'
+    // latency-bound work
+    const uint32_t level = blockIdx.x, chunk = blockIdx.y;
+    [[maybe_unused]] const uint32_t stamp_id = level * gridDim.y + chunk;
     const uint32_t rows = rows_of(B, im);
-    if (blockIdx.x * kBinPts >= rows) return;
-    const uint32_t level = blockIdx.y;
+    if (chunk * kBinPts >= rows) return;
     const uint32_t nb = bp.nbins[level];
     const bool merge = (bp.merge_mask >> level) & 1u;
     const int lane = (int)(threadIdx.x & 63);
     if (threadIdx.x < nb) cnt[threadIdx.x] = 0;
     lds_barrier();
     BSTAMP(0);
+    BRSTAMP(8);
 
-    const uint32_t b = blockIdx.x * kBinPts + threadIdx.x;
+    const uint32_t b = chunk * kBinPts + threadIdx.x;
     const bool in_rows = b < rows;
     // the sample's coordinates and this level's grad are loaded together (the
     // grad of an out-of-bounds sample is discarded below): loads gated on the
@@ -664,6 +680,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     uint32_t key[NC], rank[NC];
     ngp_half2 val[NC];
     bool live[NC];
+    float vv[NC][2];
 #pragma unroll
     for (uint32_t idx = 0; idx < NC; idx++) {
         float w = 1;
@@ -680,23 +697,51 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         }
         const uint32_t k = valid ? grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl)
                                  : 0xffffffffu;
-        float v0 = w * g0, v1 = w * g1;
-        bool lv_ = valid;
+        key[idx] = k;
+        live[idx] = valid;
+        vv[idx][0] = w * g0;
+        vv[idx][1] = w * g1;
+#if !NGP_JOINT_MERGE
         if (merge) {
             const uint32_t kprev = ngp_dpp::prev_lane(k);
             const bool same = valid && lane > 0 && kprev == k;
             const uint64_t sm = __ballot(same);
             if (sm) {
                 // runs of equal keys: segmented DPP scan, the run's last lane keeps the sum
-                ngp_dpp::seg_scan2(v0, v1, !same);
+                ngp_dpp::seg_scan2(vv[idx][0], vv[idx][1], !same);
                 const bool next_same = lane < 63 && ((sm >> (lane + 1)) & 1ull);
-                lv_ = valid && !next_same;
+                live[idx] = valid && !next_same;
             }
         }
-        key[idx] = k;
-        live[idx] = lv_;
-        val[idx] = ngp_half2{(ngp_half)v0, (ngp_half)v1};
+#endif
     }
+#if NGP_JOINT_MERGE
+    if (merge) {
+        // Consecutive samples in one cell share all 2^D corners: one run
+        // structure (cell equality with the previous lane) and one segmented
+        // DPP scan carrying every corner's pair, the run's last lane keeping
+        // the sums. Per corner (a key compare, a ballot and a scan each) this
+        // was the coarse levels' VALU bottleneck.
+        // (every lane moves its values: a DPP move reading a lane that is off
+        // in EXEC -- as under a short-circuited condition -- yields 0)
+        const uint32_t vprev = ngp_dpp::prev_lane(valid ? 1u : 0u);
+        uint32_t pprev[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; d++) pprev[d] = ngp_dpp::prev_lane(pg[d]);
+        bool same = valid && lane > 0 && vprev != 0;
+#pragma unroll
+        for (uint32_t d = 0; d < D; d++) same = same && pprev[d] == pg[d];
+        const uint64_t sm = __ballot(same);
+        if (sm) {
+            ngp_dpp::seg_scan_pairs<NC>(vv, !same);
+            const bool next_same = lane < 63 && ((sm >> (lane + 1)) & 1ull);
+#pragma unroll
+            for (uint32_t idx = 0; idx < NC; idx++) live[idx] = valid && !next_same;
+        }
+    }
+#endif
+#pragma unroll
+    for (uint32_t idx = 0; idx < NC; idx++) val[idx] = ngp_half2{(ngp_half)vv[idx][0], (ngp_half)vv[idx][1]};
     // Rank within the bin. When every live item of the wave (all corners) is
     // in one bin -- the dense levels' z-slab bins, where all the workgroup's
     // waves hit the same counter -- the wave takes its whole run with ONE LDS
@@ -843,6 +888,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         }
     }
     BSTAMP(4);
+    BRSTAMP(9);
 }
 
 // An fp16 value as a signed count of 2^-24 (every finite fp16 is one:
@@ -878,12 +924,16 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                  const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite, bool zeroed,
                  bool external) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
+    // [entry][channel]; a channel-planar image (8-byte lane stride for the
+    // 64-bit atomics instead of 16) measured the same
     __shared__ __attribute__((aligned(16))) unsigned long long acc[kBinEntries * C];
+    auto acc_entry = [&](uint32_t e) { return reinterpret_cast<const ulonglong2*>(acc)[e]; };
     __shared__ uint32_t wsum[NW];
     __shared__ uint32_t s_last, s_bad;
     extern __shared__ uint32_t dyn[];
     const uint32_t nbins = bp.total_bins;
     STAMP(0, __builtin_amdgcn_s_memtime());
+    RSTAMP(60);
     uint32_t* upre = dyn;              // [nbins + 1] first unit of each bin
     uint32_t* bn = dyn + nbins + 1;    // [nbins] items of each bin (clipped at its capacity)
     // the plan's per-level arrays, indexed per lane below: kernel arguments
@@ -891,6 +941,16 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     __shared__ uint32_t s_bin0[kMaxLevels + 1], s_cap[kMaxLevels], s_item0[kMaxLevels], s_off[kMaxLevels + 1];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t nlev = bp.nlev;
+    // the first group of this thread's bin counts (step 1 below) is loaded
+    // before anything else: its round trip overlaps the plan's LDS copy
+    constexpr uint32_t kStep1Loads = 4;
+    const uint32_t per = (nbins + kAccThreads - 1) / kAccThreads;
+    uint32_t cv0[kStep1Loads];
+#pragma unroll
+    for (uint32_t j = 0; j < kStep1Loads; ++j) {
+        const uint32_t b = t * per + j;
+        cv0[j] = j < per && b < nbins ? cursor[b] : 0u;
+    }
     if (t <= nlev) {
         s_bin0[t] = t < nlev ? bp.bin0[t] : nbins;
         s_off[t] = (uint32_t)offsets[t];
@@ -911,8 +971,6 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // 1. units per bin, exclusive prefix (thread t owns bins [t*per, t*per + per)).
     // The counts are loaded kStep1Loads at a time, all before their use (one
     // round trip per group instead of one per bin).
-    constexpr uint32_t kStep1Loads = 4;
-    const uint32_t per = (nbins + kAccThreads - 1) / kAccThreads;
     uint32_t mine = 0;
     uint32_t level = t * per < nbins ? level_of(t * per) : 0;
     for (uint32_t j0 = 0; j0 < per; j0 += kStep1Loads) {
@@ -920,7 +978,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
         for (uint32_t j = 0; j < kStep1Loads; ++j) {
             const uint32_t b = t * per + j0 + j;
-            cv[j] = j0 + j < per && b < nbins ? cursor[b] : 0u;
+            cv[j] = j0 == 0 ? cv0[j] : j0 + j < per && b < nbins ? cursor[b] : 0u;
         }
 #pragma unroll
         for (uint32_t j = 0; j < kStep1Loads; ++j) {
@@ -1040,12 +1098,23 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     uint64_t it[kAccBatch];
     uint32_t old[G] = {};
     Unit cur{};
-    if (blockIdx.x < total) {
-        cur = locate(blockIdx.x);
+    // Unit order: round k gives unit k * grid + blockIdx.x, except the last,
+    // partial round, which is dealt in reverse (grid - 1 - blockIdx.x). The
+    // units run in bin order, so round 0's first workgroups hold the coarse
+    // levels' long units (up to 4x the items of a fine-level unit); dealt
+    // forward they also got a round-2 unit and finished last.
+    const uint32_t ngr = gridDim.x, full = total / ngr;
+    auto unit_at = [&](uint32_t k) {  // this workgroup's k-th unit, or total (none)
+        const uint32_t uk = k < full ? k * ngr + blockIdx.x : full * ngr + (ngr - 1 - blockIdx.x);
+        return k <= full && uk < total ? uk : total;
+    };
+    uint32_t u = unit_at(0);
+    if (u < total) {
+        cur = locate(u);
         load_batch(cur, cur.s0, it);
         load_old(cur, old);
     }
-    for (uint32_t u = blockIdx.x; u < total; u += gridDim.x) {
+    for (uint32_t k = 0; u < total; ++k) {
         // (clearing each entry in the flush after reading it instead -- no
         // zeroing pass -- gave wrong sums on the GPU for reasons not found;
         // measured and dropped)
@@ -1075,7 +1144,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) old_cur[j] = old[j];
         // prefetch the next unit
-        const uint32_t un = u + gridDim.x;
+        const uint32_t un = unit_at(k + 1);
         Unit nxt = cur;
         if (un < total) {
             nxt = locate(un);
@@ -1098,7 +1167,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j) {
                 const uint32_t e = j * kAccThreads + t;
-                xs[j] = e < cur.ne ? reinterpret_cast<const ulonglong2*>(acc)[e] : ulonglong2{0ull, 0ull};
+                xs[j] = e < cur.ne ? acc_entry(e) : ulonglong2{0ull, 0ull};
             }
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j) {
@@ -1111,14 +1180,12 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         } else if (cur.flags & kOwner) {
             // one entry per lane per step: a lane reads its entry's two 8-byte
             // sums as one 16-byte LDS read (consecutive lanes, consecutive 16 B:
-            // conflict-free; the former 4-entry groups per lane read at a 64-B
-            // lane stride, 4-16-way conflicted) and stores the entry's half2
-            // (256 B per wave)
+            // conflict-free) and stores the entry's half2 (256 B per wave)
 #pragma unroll
             for (uint32_t j = 0; j < G; ++j) {
                 const uint32_t e = j * kAccThreads + t;
                 if (e >= cur.ne) continue;
-                const ulonglong2 xx = reinterpret_cast<const ulonglong2*>(acc)[e];
+                const ulonglong2 xx = acc_entry(e);
                 const int64_t x0 = (int64_t)xx.x, x1 = (int64_t)xx.y;
                 if (x0 == 0 && x1 == 0) continue;
                 const ngp_half2 o = __builtin_bit_cast(ngp_half2, old_cur[j]);
@@ -1128,7 +1195,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             }
         } else {
             for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
-                const ulonglong2 xx = reinterpret_cast<const ulonglong2*>(acc)[e];
+                const ulonglong2 xx = acc_entry(e);
                 const int64_t x0 = (int64_t)xx.x, x1 = (int64_t)xx.y;
                 if (x0 == 0 && x1 == 0) continue;
                 const ngp_half2 v{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
@@ -1147,7 +1214,9 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         ++nstamp;
         STAMP(3, nstamp);
         cur = nxt;
+        u = un;
     }
+    RSTAMP(61);
 }
 
 // GradScaler's inf/nan check over a grad range (levels the binned path does
@@ -1564,7 +1633,7 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
         uint32_t* cursor = static_cast<uint32_t*>(workspace);
         uint32_t* retire = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_counters_bytes(bp));
         BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) + bin_counters_bytes(bp) + 256);
-        const dim3 grid(ngp_div_up(B, kBinPts), bp.nlev);
+        const dim3 grid(bp.nlev, ngp_div_up(B, kBinPts));
         k_grid_bwd_bin<3><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
             (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, im,
             bp, cursor, items, grad_layout, nonfinite);

@@ -48,6 +48,38 @@ NGP_DEV void seg_scan2(float& a, float& b, bool head) {
     seg_step2<kRowBcast31, 0xc>(a, b, f);
 }
 
+// seg_scan2 for N value pairs sharing one segment structure (one flag move
+// per step instead of one per pair).
+template <int CTRL, int ROW_MASK, int N>
+NGP_DEV void seg_stepn(float (&a)[N][2], uint32_t& f) {
+    float t[N][2];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        t[i][0] = movf<CTRL, ROW_MASK>(a[i][0]);
+        t[i][1] = movf<CTRL, ROW_MASK>(a[i][1]);
+    }
+    const uint32_t tf = mov<CTRL, ROW_MASK>(f);
+    if (!f) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            a[i][0] += t[i][0];
+            a[i][1] += t[i][1];
+        }
+    }
+    f |= tf;
+}
+
+template <int N>
+NGP_DEV void seg_scan_pairs(float (&a)[N][2], bool head) {
+    uint32_t f = head ? 1u : 0u;
+    seg_stepn<kRowShr1, 0xf, N>(a, f);
+    seg_stepn<kRowShr2, 0xf, N>(a, f);
+    seg_stepn<kRowShr4, 0xf, N>(a, f);
+    seg_stepn<kRowShr8, 0xf, N>(a, f);
+    seg_stepn<kRowBcast15, 0xa, N>(a, f);
+    seg_stepn<kRowBcast31, 0xc, N>(a, f);
+}
+
 // Inclusive prefix sum over the wave.
 NGP_DEV float scan_incl(float v) {
     v += movf<kRowShr1, 0xf>(v);
