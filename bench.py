@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--num_rays", type=int, default=4096)
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--kernel-steps", type=int, default=10, help="instrumented steps for kernel timing")
+    ap.add_argument("--settle-steps", type=int, default=1000,
+                    help="untimed steps after the warmup that bring the GPU to its sustained clock")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
     ap.add_argument("--engine", choices=["fused", "autograd"], default="fused")
@@ -350,6 +352,16 @@ def run_fused(args, model, data, bits, world, dev):
             print(f"[bench] graph capture failed, running eager: {e!r}", file=sys.stderr)
             ft.graph = None
     torch.cuda.synchronize()
+    # clock settle: the GPU raises its clocks only under sustained load. A
+    # 20-step run right after 5 warmup steps measured 15.0M rays/s against
+    # 17.3M for 200 steps on the same box (profiles/r02zl_settle.txt), so a
+    # fixed number of untimed steps (same on every rank: they hold
+    # collectives) runs before the timed region.
+    for i in range(args.settle_steps):
+        ft.step()
+        if i % 64 == 63:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
 
     # ---------------- timed region ----------------
     if world > 1:
@@ -405,6 +417,7 @@ def run_fused(args, model, data, bits, world, dev):
             "mean_count_M": mean_count,
             "parallelism": f"dp{world}",
             "hipgraph": used_graph,
+            "settle_steps": args.settle_steps,
             "engine": "fused",
             "baseline_ref": "V100 97 it/s x 4096 rays (readme.md:211)",
         },

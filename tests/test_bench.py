@@ -32,7 +32,8 @@ def test_bench_gpus2_gloo_runs_two_ranks():
     """`bench.py --gpus 2 --backend gloo` on the one-GPU box: both ranks run the
     data-parallel step and rank 0 reports n_gpus 2 and the 2 ranks gloo joined."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
-                        "--steps", "3", "--warmup", "2", "--kernel-steps", "1", "--no-cpu", "--no-graph"],
+                        "--steps", "3", "--warmup", "2", "--kernel-steps", "1", "--no-cpu", "--no-graph",
+                        "--settle-steps", "2"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
