@@ -110,6 +110,7 @@ NGP_DEV float sigmoid_h(ngp_half x) { return (float)(ngp_half)(1.0f / (1.0f + ex
 // wave-wide prefix sums / sums on DPP lane moves (ngp_dpp.h); every lane of
 // the wave is active wherever these are called
 NGP_DEV float scan_incl(float v, uint32_t) { return ngp_dpp::scan_incl(v); }
+NGP_DEV float lane63(float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63)); }
 NGP_DEV float wave_sum(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ngp_dpp::scan_incl(v)), 63));
 }
@@ -133,8 +134,9 @@ NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __rest
     const uint32_t i = offset + base + lane;
     c.ok = base + lane < num_steps;
     const float sg = c.ok ? sigma[i] : 0.0f;
-    c.d0 = c.ok ? deltas[(size_t)i * 2] : 0.0f;
-    const float d1 = c.ok ? deltas[(size_t)i * 2 + 1] : 0.0f;
+    const float2 dd = c.ok ? *reinterpret_cast<const float2*>(deltas + (size_t)i * 2) : float2{0.0f, 0.0f};
+    c.d0 = dd.x;
+    const float d1 = dd.y;
     c.c0 = c.c1 = c.c2 = 0.0f;
     if (c.ok) {
         typedef _Float16 half4 __attribute__((ext_vector_type(4)));
@@ -149,8 +151,7 @@ NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __rest
     // once the density is large (sigma * delta >> the prefix, or inf) that
     // difference cancels to garbage (inf - inf = NaN), where the reference's
     // serial T *= 1 - alpha stays exact
-    float excl = __shfl_up(incl, 1, 64);
-    if (lane == 0) excl = 0.0f;
+    const float excl = __builtin_bit_cast(float, ngp_dpp::prev_lane(__builtin_bit_cast(uint32_t, incl)));  // lane 0: 0
     const float alpha = 1.0f - expf(-sd);
     const float Tbefore = expf(-(S + excl));
     c.Tafter = expf(-(S + incl));
@@ -161,8 +162,8 @@ NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __rest
     c.active = c.ok && lane <= last;
     if (!c.active) c.w = 0.0f;
     stop = below != 0;
-    S += __shfl(incl, 63, 64);
-    tacc = __shfl(c.t, 63, 64);
+    S += lane63(incl);
+    tacc = lane63(c.t);
     return c;
 }
 
@@ -182,6 +183,19 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     const uint32_t offset = (uint32_t)rays[n * 3 + 1];
     const uint32_t num_steps = (uint32_t)rays[n * 3 + 2];
     const bool valid = num_steps != 0 && offset + num_steps <= M;
+    // everything that only needs the ray's row is requested now, with the
+    // first chunk: the background, the target and the first chunk's h0 (each
+    // was a dependent round trip after the forward's scans)
+    const float bg0 = bg[index * 3], bg1 = bg[index * 3 + 1], bg2 = bg[index * 3 + 2];
+    float gt4[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    if (la.gt_channels == 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gt4[k] = gt[(size_t)index * 4 + k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) gt4[k] = gt[(size_t)index * 3 + k];
+    }
+    const float h0_first = valid && lane < num_steps ? (float)h_sigma[(size_t)(offset + lane) * 16] : 0.0f;
 
     // ---- forward (composite_rays_train_forward)
     // The first 64-sample chunk (all of most rays) is kept for the backward
@@ -211,19 +225,16 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
         }
     }
     // ---- background blend + MSE (utils.py train_step) and its gradient
-    const float bg0 = bg[index * 3], bg1 = bg[index * 3 + 1], bg2 = bg[index * 3 + 2];
     const float one_m_ws = 1.0f - ws;
     const float p0 = r + one_m_ws * bg0, p1 = g + one_m_ws * bg1, p2 = b + one_m_ws * bg2;
     float q0, q1, q2;
     if (la.gt_channels == 4) {
-        const float* gp = gt + (size_t)index * 4;
-        const float a = gp[3], om = 1.0f - a;
-        q0 = gp[0] * a + bg0 * om;
-        q1 = gp[1] * a + bg1 * om;
-        q2 = gp[2] * a + bg2 * om;
+        const float a = gt4[3], om = 1.0f - a;
+        q0 = gt4[0] * a + bg0 * om;
+        q1 = gt4[1] * a + bg1 * om;
+        q2 = gt4[2] * a + bg2 * om;
     } else {
-        const float* gp = gt + (size_t)index * 3;
-        q0 = gp[0]; q1 = gp[1]; q2 = gp[2];
+        q0 = gt4[0]; q1 = gt4[1]; q2 = gt4[2];
     }
     const float e0 = p0 - q0, e1 = p1 - q1, e2 = p2 - q2;
     if (lane == 0) {
@@ -270,7 +281,7 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
         const float pg = rg + scan_incl(c.w * c.c1, lane);
         const float pb = rb + scan_incl(c.w * c.c2, lane);
         const float pd = rd + scan_incl(c.w * c.t, lane);
-        rr = __shfl(pr, 63, 64); rg = __shfl(pg, 63, 64); rb = __shfl(pb, 63, 64); rd = __shfl(pd, 63, 64);
+        rr = lane63(pr); rg = lane63(pg); rb = lane63(pb); rd = lane63(pd);
         if (c.ok) {
             const uint32_t i = offset + base + lane;
             float gc0 = 0, gc1 = 0, gc2 = 0, gs = 0;
@@ -289,7 +300,7 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
             go[0] = o0;
             go[1] = o1;
             // sigmas = ds * trunc_exp(h0): grad_h0 = (gs * ds) * exp(clamp(h0, -15, 15)), -> half
-            const float h0 = (float)h_sigma[(size_t)i * 16];
+            const float h0 = base == 0 ? h0_first : (float)h_sigma[(size_t)i * 16];
             grad_h[(size_t)i * 16] = ngp_f2h((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
         }
         stopped = stopped || stop;
