@@ -23,6 +23,7 @@
 //     lookup latency is the step time.
 #include "ffmlp_pack.h"
 #include "ngp_common.h"
+#include "ngp_dpp.h"
 #include "ngp_step.h"
 
 #include <algorithm>
@@ -271,12 +272,7 @@ template <uint32_t BLOCK>
 NGP_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds_waves, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
-    uint32_t incl = v;
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += u;
-    }
+    const uint32_t incl = ngp_dpp::scan_incl_u32(v);  // DPP: no LDS-crossbar round trips
     if (lane == 63) lds_waves[wave] = incl;
     __syncthreads();
     uint32_t wave_base = 0;
@@ -518,9 +514,11 @@ NGP_DEV uint32_t march_ray_segmented(const Ray& r, const MarchConst& k, const OC
     for (;;) {
         // stitch: in_s = first index >= a_s the true walk visits
         uint32_t cur = 0;
+        // segment exits by v_readlane (uniform lane index): a __shfl here was
+        // an LDS-crossbar round trip per segment, 64 in a row
         for (uint32_t sg = 0; sg < 64; ++sg) {
             if (lane == sg) in = cur;
-            const uint32_t Xs = __shfl(X, sg, 64);
+            const uint32_t Xs = (uint32_t)__builtin_amdgcn_readlane((int)X, (int)sg);
             if (cur < (sg + 1) * L) cur = Xs;
         }
         const bool inside = in < b && !(ended && in >= kend);
@@ -537,13 +535,8 @@ NGP_DEV uint32_t march_ray_segmented(const Ray& r, const MarchConst& k, const OC
     const bool inside = in < b && !(ended && in >= kend);
     const uint64_t mine = inside ? occm & ~((1ull << (in - a)) - 1ull) : 0ull;
     const uint32_t cnt = __popcll(mine);
-    uint32_t incl = cnt;
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += u;
-    }
-    const uint32_t total = __shfl(incl, 63, 64);
+    const uint32_t incl = ngp_dpp::scan_incl_u32(cnt);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     uint32_t off = incl - cnt;
     if (mine && off < k.max_steps) {
         float tj = ta;
@@ -575,7 +568,7 @@ NGP_DEV uint32_t march_ray_wave(const Ray& r, const MarchConst& k, const OCC& oc
     }
     uint32_t n = 0;
     if ((threadIdx.x & 63) == 0) n = march_ray_train<ONE_LEVEL>(r, k, occ, t0, far, ts);
-    return __shfl(n, 0, 64);
+    return (uint32_t)__builtin_amdgcn_readlane((int)n, 0);
 }
 
 __global__ void __launch_bounds__(kSegThreads)
