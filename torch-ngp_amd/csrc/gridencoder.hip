@@ -524,7 +524,7 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 //                    (coalesced, one per entry per unit).
 // Contributions are rounded to half once per run (the reference rounds each
 // term, gridencoder.cu:325) and summed in fp32. Items past a bin's capacity
-// fall back to direct atomics. Levels with more than kMaxBinsPerLevel bins
+// fall back to direct atomics. Levels with more than kMaxBinsPerLevelBig bins
 // use k_grid_bwd.
 // The NGP_* macros exist only for same-box A/B builds (tools/variants.sh).
 #ifndef NGP_BIN_SHIFT
@@ -547,7 +547,10 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #endif
 constexpr uint32_t kBinShift = NGP_BIN_SHIFT;
 constexpr uint32_t kBinEntries = 1u << kBinShift;
-constexpr uint32_t kMaxBinsPerLevel = 256;
+constexpr uint32_t kMaxBinsPerLevel = 256;       // the bin kernel's small instantiation
+constexpr uint32_t kMaxBinsPerLevelBig = 1024;   // ... and the large one (2^22-entry levels)
+// the accumulate keeps two words per bin in LDS beside its 64 KiB image
+constexpr uint32_t kMaxTotalBins = 11776;
 constexpr uint32_t kSegItems = NGP_SEG_ITEMS;
 // entries within a bin are packed in 16 bits while staged (| bin << 16)
 static_assert(kBinShift >= 9 && kBinShift <= 16, "NGP_BIN_SHIFT must be in [9, 16]");
@@ -609,7 +612,7 @@ __device__ unsigned long long* g_stamps;
 #define BSTAMP(slot) do { } while (0)
 #endif
 
-template <uint32_t D>
+template <uint32_t D, uint32_t NBMAX>
 __global__ void __launch_bounds__(kBinPts, 8)  // 4 workgroups per CU: <= 64 VGPRs
 k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
                const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
@@ -617,9 +620,9 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
                InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
                int32_t grad_layout, int32_t* __restrict__ nonfinite) {
     constexpr uint32_t C = 2, NC = 1u << D, NW = kBinPts / 64;
-    static_assert(kMaxBinsPerLevel <= kBinPts, "one bin per thread in the reservation step");
-    __shared__ uint32_t cnt[kMaxBinsPerLevel], soff[kMaxBinsPerLevel + 1], wsum[NW];
-    __shared__ uint2 binfo[kMaxBinsPerLevel];  // (slot - stage index, end of the bin's in-capacity stage run)
+    constexpr uint32_t BPT = (NBMAX + kBinPts - 1) / kBinPts;  // bins per thread in the reservation step
+    __shared__ uint32_t cnt[NBMAX], soff[NBMAX + 1], wsum[NW];
+    __shared__ uint2 binfo[NBMAX];  // (slot - stage index, end of the bin's in-capacity stage run)
     __shared__ uint32_t s_over;                // some bin of this workgroup ran past its capacity
     extern __shared__ BinItem stage[];  // kBinPts * NC
     // the grid covers the row capacity; workgroups past the marched sample
@@ -636,7 +639,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     const uint32_t nb = bp.nbins[level];
     const bool merge = (bp.merge_mask >> level) & 1u;
     const int lane = (int)(threadIdx.x & 63);
-    if (threadIdx.x < nb) cnt[threadIdx.x] = 0;
+    for (uint32_t j = threadIdx.x; j < nb; j += kBinPts) cnt[j] = 0;
     lds_barrier();
     BSTAMP(0);
     BRSTAMP(8);
@@ -825,14 +828,19 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // The part of a run past the bin's capacity goes atomic, so slots
     // [0, min(cursor, cap)) are always all written.
     const uint32_t cap = bp.cap[level];
-    uint32_t c_mine = 0, bs_mine = 0;
-    if (threadIdx.x < nb) {
-        c_mine = cnt[threadIdx.x];
-        if (c_mine) bs_mine = atomicAdd(&cursor[bp.bin0[level] + threadIdx.x], c_mine);
+    // thread t owns bins t*BPT .. t*BPT + BPT - 1 (contiguous, in scan order)
+    uint32_t c_mine[BPT], bs_mine[BPT], c_sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < BPT; ++j) {
+        const uint32_t bj = threadIdx.x * BPT + j;
+        c_mine[j] = bj < nb ? cnt[bj] : 0u;
+        bs_mine[j] = 0;
+        if (c_mine[j]) bs_mine[j] = atomicAdd(&cursor[bp.bin0[level] + bj], c_mine[j]);
+        c_sum += c_mine[j];
     }
     {   // block-wide exclusive scan of cnt[0..nb)
         const uint32_t t = threadIdx.x, wv = t >> 6;
-        const uint32_t incl = ngp_dpp::scan_incl_u32(c_mine);
+        const uint32_t incl = ngp_dpp::scan_incl_u32(c_sum);
         if (lane == 63) wsum[wv] = incl;
         lds_barrier();
         uint32_t before = 0, all = 0;
@@ -841,7 +849,13 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
             before += w < wv ? wsum[w] : 0u;
             all += wsum[w];
         }
-        if (t < nb) soff[t] = before + incl - c_mine;
+        uint32_t run = before + incl - c_sum;
+#pragma unroll
+        for (uint32_t j = 0; j < BPT; ++j) {
+            const uint32_t bj = t * BPT + j;
+            if (bj < nb) soff[bj] = run;
+            run += c_mine[j];
+        }
         if (t == 0) soff[nb] = all;
     }
     lds_barrier();
@@ -854,10 +868,13 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     }
     if (threadIdx.x == 0) s_over = 0;
     lds_barrier();
-    if (threadIdx.x < nb) {
-        const uint32_t t = threadIdx.x, lim = bs_mine >= cap ? 0u : min(c_mine, cap - bs_mine);
-        binfo[t] = uint2{t * cap + bs_mine - soff[t], soff[t] + lim};
-        if (lim < c_mine) s_over = 1;  // benign race: every writer stores 1
+#pragma unroll
+    for (uint32_t j = 0; j < BPT; ++j) {
+        const uint32_t bj = threadIdx.x * BPT + j;
+        if (bj >= nb) break;
+        const uint32_t lim = bs_mine[j] >= cap ? 0u : min(c_mine[j], cap - bs_mine[j]);
+        binfo[bj] = uint2{bj * cap + bs_mine[j] - soff[bj], soff[bj] + lim};
+        if (lim < c_mine[j]) s_over = 1;  // benign race: every writer stores 1
     }
     lds_barrier();
     BSTAMP(3);
@@ -913,6 +930,8 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
 constexpr uint32_t kAccThreads = 512, kAccBatch = NGP_ACC_BATCH, kRetireGroups = 16;
+// the accumulate's static LDS (the 64 KiB image and its small arrays), for the launch's occupancy choice
+constexpr size_t kAccStaticLds = 66 * 1024 + 1024;
 static_assert(kAccBatch > 0, "NGP_ACC_BATCH must be positive");
 static_assert(kMaxLevels <= 64, "the accumulate finds a bin's level with one wave ballot");
 static_assert(kBinEntries % kAccThreads == 0, "each flush thread owns whole entries (G > 0)");
@@ -1242,7 +1261,7 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
     for (uint32_t l = 0; l < L; ++l) {
         const uint32_t hs = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
         const uint32_t nb = (hs + kBinEntries - 1) / kBinEntries;
-        if (nb > kMaxBinsPerLevel) break;
+        if (nb > kMaxBinsPerLevelBig || bins + nb > kMaxTotalBins) break;
         const double side = (double)(align_corners ? lv.res[l] : lv.res[l] + 1);
         const bool hashed = std::pow(side, (double)D) > (double)hs;
         const uint64_t cap = hashed ? std::min<uint64_t>(items_all, 2 * ((items_all + nb - 1) / nb) + 2048)
@@ -1634,10 +1653,21 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
         uint32_t* retire = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_counters_bytes(bp));
         BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) + bin_counters_bytes(bp) + 256);
         const dim3 grid(bp.nlev, ngp_div_up(B, kBinPts));
-        k_grid_bwd_bin<3><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
-            (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp, im,
-            bp, cursor, items, grad_layout, nonfinite);
-        k_grid_bin_accum<<<2 * ngp_num_cus(), kAccThreads, (2 * bp.total_bins + 1) * sizeof(uint32_t), st>>>(
+        uint32_t nbmax = 0;
+        for (uint32_t l = 0; l < bp.nlev; ++l) nbmax = std::max(nbmax, bp.nbins[l]);
+        if (nbmax <= kMaxBinsPerLevel)
+            k_grid_bwd_bin<3, kMaxBinsPerLevel><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
+                (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
+                im, bp, cursor, items, grad_layout, nonfinite);
+        else
+            k_grid_bwd_bin<3, kMaxBinsPerLevelBig><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
+                (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
+                im, bp, cursor, items, grad_layout, nonfinite);
+        // two persistent workgroups per CU while both fit the CU's LDS (the
+        // 64 KiB image + two words per bin), else one
+        const size_t dyn = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
+        const uint32_t per_cu = 2 * (dyn + kAccStaticLds) <= 160 * 1024 ? 2u : 1u;
+        k_grid_bin_accum<<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
             offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, zeroed, external);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
