@@ -1133,14 +1133,25 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         load_batch(cur, cur.s0, it);
         load_old(cur, old);
     }
+    // Sparse units (a cleared grad's owner with at most kSparseMax items: the
+    // 2^22-entry levels' bins, the Lego's levels 5-6) flush per ITEM instead
+    // of per entry: each lane reads its items' sums, stores them (items of
+    // one entry store the same value) and, after a barrier, clears just
+    // those entries -- no 4096-entry flush and no zeroing pass for the next
+    // unit. The entries are kept in ent[] (the prefetch overwrites it[]).
+    constexpr uint32_t kSparseQ = 4, kSparseMax = kSparseQ * kAccThreads;
+    static_assert(kSparseQ <= kAccBatch, "a sparse unit is one item batch");
+    bool need_zero = true;  // the image holds entries no flush cleared (initially: all of it)
     for (uint32_t k = 0; u < total; ++k) {
-        // (clearing each entry in the flush after reading it instead -- no
-        // zeroing pass -- gave wrong sums on the GPU for reasons not found;
-        // measured and dropped)
-        for (uint32_t i = t; i < kBinEntries * C / 2; i += kAccThreads)
-            reinterpret_cast<uint4*>(acc)[i] = uint4{0u, 0u, 0u, 0u};
-        if (t == 0) s_bad = 0;
-        lds_barrier();
+        // (clearing each entry in the flush right after reading it, by the
+        // same lane -- no zeroing pass -- gave wrong sums on the GPU; the
+        // sparse flush below clears only after a barrier)
+        if (need_zero) {
+            for (uint32_t i = t; i < kBinEntries * C / 2; i += kAccThreads)
+                reinterpret_cast<uint4*>(acc)[i] = uint4{0u, 0u, 0u, 0u};
+            if (t == 0) s_bad = 0;
+            lds_barrier();
+        }
         [[maybe_unused]] const uint32_t sb = 4 + 5 * min(nstamp, 11u);
         STAMP(sb, __builtin_amdgcn_s_memtime());
         STAMP(sb + 3, (cur.s1 - cur.s0) | ((uint64_t)(cur.flags & kOwner) << 32) | ((uint64_t)cur.level << 40));
@@ -1159,6 +1170,10 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             load_batch(cur, k0, it);
         }
         STAMP(sb + 1, __builtin_amdgcn_s_memtime());
+        const bool sparse = (cur.flags & kFresh) && cur.s1 - cur.s0 <= kSparseMax;
+        uint32_t ent[kSparseQ];  // sparse: this lane's items' entries (0xffffffff: none)
+#pragma unroll
+        for (uint32_t q = 0; q < kSparseQ; ++q) ent[q] = it[q] == ~0ull ? 0xffffffffu : (uint32_t)it[q];
         uint32_t old_cur[G];
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) old_cur[j] = old[j];
@@ -1176,7 +1191,29 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         const bool unit_bad = s_bad != 0;
         const float q24 = 1.0f / 16777216.0f;
         bool inf_out = false;  // a stored grad is inf/nan (GradScaler's check, when `nonfinite` is given)
-        if (cur.flags & kFresh) {
+        if (sparse) {
+            ulonglong2 xs[kSparseQ];
+#pragma unroll
+            for (uint32_t q = 0; q < kSparseQ; ++q)
+                xs[q] = ent[q] != 0xffffffffu ? acc_entry(ent[q]) : ulonglong2{0ull, 0ull};
+#pragma unroll
+            for (uint32_t q = 0; q < kSparseQ; ++q) {
+                const int64_t x0 = (int64_t)xs[q].x, x1 = (int64_t)xs[q].y;
+                // (a bad unit stores only its NaN marker below: an item store
+                // to entry 0 from another lane would race with it)
+                if (unit_bad || ent[q] == 0xffffffffu || (x0 == 0 && x1 == 0)) continue;
+                const ngp_half2 n{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
+                inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
+                cur.tbl[ent[q]] = n;
+            }
+            lds_barrier();  // every lane's reads are done before any entry is cleared
+#pragma unroll
+            for (uint32_t q = 0; q < kSparseQ; ++q)
+                if (ent[q] != 0xffffffffu) reinterpret_cast<ulonglong2*>(acc)[ent[q]] = ulonglong2{0ull, 0ull};
+            if (t == 0) s_bad = 0;  // read above, before the barrier
+            need_zero = false;
+        } else if (cur.flags & kFresh) {
+            need_zero = true;
             // the common case: the unit owns its slice of a cleared grad. All of
             // the lane's LDS reads first, then the stores. Nothing here consumes
             // a global load, so no wait on the next unit's prefetched items (with
@@ -1197,6 +1234,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                 cur.tbl[j * kAccThreads + t] = n;
             }
         } else if (cur.flags & kOwner) {
+            need_zero = true;
             // one entry per lane per step: a lane reads its entry's two 8-byte
             // sums as one 16-byte LDS read (consecutive lanes, consecutive 16 B:
             // conflict-free) and stores the entry's half2 (256 B per wave)
@@ -1213,6 +1251,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                 cur.tbl[e] = n;
             }
         } else {
+            need_zero = true;
             for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
                 const ulonglong2 xx = acc_entry(e);
                 const int64_t x0 = (int64_t)xx.x, x1 = (int64_t)xx.y;
