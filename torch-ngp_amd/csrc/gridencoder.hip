@@ -336,7 +336,7 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
             const uint32_t rest = idx >> 1;
 #pragma unroll
             for (uint32_t c = 0; c < C; ++c) {
-                const F other = (F)__shfl_xor((float)mine[q][rest][c], 1, 64);
+                const F other = (F)ngp_dpp::pair_swap((float)mine[q][rest][c]);  // DPP, every lane active
                 const F v = ((idx & 1u) == xbit) ? mine[q][rest][c] : other;
                 res[c] = A::mac(res[c], (F)w, v);
             }
@@ -541,6 +541,9 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #endif
 #ifndef NGP_JOINT_MERGE
 #define NGP_JOINT_MERGE 1
+#endif
+#ifndef NGP_SPARSE_Q
+#define NGP_SPARSE_Q 4
 #endif
 #ifndef NGP_MATCH_MAX_BINS
 #define NGP_MATCH_MAX_BINS 64
@@ -1139,7 +1142,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // one entry store the same value) and, after a barrier, clears just
     // those entries -- no 4096-entry flush and no zeroing pass for the next
     // unit. The entries are kept in ent[] (the prefetch overwrites it[]).
-    constexpr uint32_t kSparseQ = 4, kSparseMax = kSparseQ * kAccThreads;
+    constexpr uint32_t kSparseQ = NGP_SPARSE_Q, kSparseMax = kSparseQ * kAccThreads;
     static_assert(kSparseQ <= kAccBatch, "a sparse unit is one item batch");
     bool need_zero = true;  // the image holds entries no flush cleared (initially: all of it)
     for (uint32_t k = 0; u < total; ++k) {

@@ -13,6 +13,7 @@ namespace ngp_dpp {
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
 constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
 constexpr int kWaveShr1 = 0x138;
+constexpr int kQuadXor1 = 0xB1;  // quad_perm [1, 0, 3, 2]: the lane pair partner
 
 template <int CTRL, int ROW_MASK>
 NGP_DEV uint32_t mov(uint32_t v) {
@@ -101,6 +102,10 @@ NGP_DEV uint32_t scan_incl_u32(uint32_t v) {
     v += mov<kRowBcast31, 0xc>(v);
     return v;
 }
+
+// The value of the lane pair partner (lane ^ 1): __shfl_xor(v, 1) without
+// the LDS crossbar.
+NGP_DEV float pair_swap(float v) { return movf<kQuadXor1, 0xf>(v); }
 
 // The previous lane's value (lane 0 gets 0): __shfl_up(v, 1) without the
 // LDS crossbar.
