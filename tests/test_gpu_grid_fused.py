@@ -96,7 +96,8 @@ CASES = [
     (20000, 16, 16, LEGO_SCALE, 19, "uniform"),
     (60000, 16, 16, LEGO_SCALE, 19, "rays"),
     (120000, 8, 16, 1.5, 19, "concentrated"),   # heavy bins: several segments per bin
-    (30000, 8, 16, 2.0, 22, "uniform"),          # 2^22-entry levels: 1024 bins of 2^12, past kMaxBinsPerLevel: the atomic suffix
+    (30000, 8, 16, 2.0, 22, "uniform"),          # 2^22-entry levels: 1024 bins of 2^12 (the large bin kernel, sparse flushes)
+    (30000, 6, 16, 2.0, 23, "uniform"),          # 2^23-entry levels: 2048 bins, past kMaxBinsPerLevelBig: the atomic suffix
     (513, 4, 8, 2.0, 12, "uniform"),
 ]
 
@@ -174,12 +175,13 @@ def test_grid_forward_fused_bit_exact(cuda, table, layout):
     assert np.all(got[n:] == 7.0)  # rows past the sample count untouched
 
 
-@pytest.mark.parametrize("log2T", [19, 22])
-def test_grid_backward_fused_flags_nonfinite(cuda, log2T):
+@pytest.mark.parametrize("log2T,zeroed", [(19, False), (19, True), (22, True), (23, False)])
+def test_grid_backward_fused_flags_nonfinite(cuda, log2T, zeroed):
     """The nonfinite flag is GradScaler's inf check made by the kernels that
     write the grads: an inf output grad, or finite terms whose fp16 sum
-    overflows, must set it, on the binned levels and (T = 2^22: levels past
-    the binned prefix) the scanned ones."""
+    overflows, must set it, on the binned levels (read-modify-write, fresh
+    per-entry and per-item flushes) and (T = 2^23: levels past the binned
+    prefix) the scanned ones."""
     nat = _lib()
     B, L, H, scale = 20000, 16, 16, LEGO_SCALE
     offs = oracle.grid_offsets(3, L, 2, H, scale, log2T)
@@ -189,9 +191,9 @@ def test_grid_backward_fused_flags_nonfinite(cuda, log2T):
         g = g16.copy()
         g[B // 2, 2 * lvl] = np.float16(np.inf)
         flag = torch.zeros(1, dtype=torch.int32, device=cuda)
-        _bwd(nat, cuda, g, w, offs, L, H, scale, 1.0, flag=flag)
+        _bwd(nat, cuda, g, w, offs, L, H, scale, 1.0, flag=flag, zeroed=zeroed)
         assert int(flag.item()) == 1, ("inf grad", lvl)
     big = np.full((B, L * 2), 60000.0, np.float16)  # finite terms, their fp16 sums overflow
     flag = torch.zeros(1, dtype=torch.int32, device=cuda)
-    _bwd(nat, cuda, big, w, offs, L, H, scale, 1.0, flag=flag)
+    _bwd(nat, cuda, big, w, offs, L, H, scale, 1.0, flag=flag, zeroed=zeroed)
     assert int(flag.item()) == 1, "sum overflow"

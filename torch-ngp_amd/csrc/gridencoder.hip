@@ -507,25 +507,28 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 // Scattered atomics cost one memory-side request per (point, corner pair)
 // whatever is done, and the coarse levels' few entries turn them into hot
 // spots. Instead every level's corner contributions are sorted into bins of
-// 2^13 table entries:
-//   k_grid_bwd_bin   one workgroup = 1024 consecutive samples of one level.
+// 2^kBinShift table entries (NGP_BIN_SHIFT, default 2^12 = 4096):
+//   k_grid_bwd_bin   one workgroup = kBinPts (512) consecutive samples of one
+//                    level; the grid is (level, block), levels interleaved.
 //                    Consecutive samples walk along a ray, so on coarse
-//                    levels neighbouring lanes hit the same corner: per
-//                    corner, runs of equal keys are summed in-wave (segmented
-//                    shuffle scan) and only the run's last lane keeps an item.
-//                    Items are ranked per bin in LDS (one LDS atomic per wave
-//                    when the whole wave lands in one bin), each bin's run is
-//                    reserved with one global atomic and written contiguously.
+//                    levels neighbouring lanes sit in one cell: runs of
+//                    samples in one cell are summed in-wave (one segmented DPP
+//                    scan carrying all corners) and only the run's last lane
+//                    keeps the items. Items are ranked per bin in LDS (few-bin
+//                    levels: one LDS atomic instruction for up to 8 bins of
+//                    the wave), each bin's run is reserved with one global
+//                    atomic and written contiguously.
 //   k_grid_bin_accum persistent; a work unit = up to kSegItems items of one
-//                    bin, summed in an LDS fp32 image of the bin's entries.
-//                    A bin with one unit is added to the fp16 table with
-//                    plain 16-byte loads and stores (single owner); larger
-//                    bins flush each unit's image with packed fp16 atomics
-//                    (coalesced, one per entry per unit).
+//                    bin, summed exactly in an LDS image of int64 fixed-point
+//                    counts of the bin's entries. A unit that owns its bin
+//                    stores the slice (per entry, or per item for small units
+//                    of a cleared grad); bins with several units flush each
+//                    image with packed fp16 atomics (coalesced, one per entry
+//                    per unit).
 // Contributions are rounded to half once per run (the reference rounds each
-// term, gridencoder.cu:325) and summed in fp32. Items past a bin's capacity
+// term, gridencoder.cu:325) and summed exactly. Items past a bin's capacity
 // fall back to direct atomics. Levels with more than kMaxBinsPerLevelBig bins
-// use k_grid_bwd.
+// (or past the plan's kMaxTotalBins) use k_grid_bwd.
 // The NGP_* macros exist only for same-box A/B builds (tools/variants.sh).
 #ifndef NGP_BIN_SHIFT
 #define NGP_BIN_SHIFT 12
