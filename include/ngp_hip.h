@@ -295,6 +295,16 @@ int ngp_nerf_sigma_forward(const void* inputs, const void* weights, const void* 
                            const int32_t* count, uint32_t in_dim, uint32_t hidden_dim,
                            uint32_t num_layers, void* h_out, float* sigma, void* color_in,
                            const float* dirs, float density_scale, uint32_t flags, void* stream);
+/* The whole NeRF forward in one launch (network_ff.py:51-74): the sigma
+ * network on pair-major encodings enc [16][B][2] (rows < *count), the
+ * ngp_nerf_sigma_forward epilogue (h_out, sigma, color_in, same values), and
+ * the colour network on color_in, rgb logits color_out [B,16] half. Images:
+ * the two networks' ngp_ffmlp_pack images. 64-wide networks with 32 inputs. */
+int ngp_nerf_forward(const void* enc, const void* sigma_image, const void* color_image, uint32_t B,
+                     const int32_t* count, uint32_t hidden_dim, uint32_t num_layers,
+                     uint32_t hidden_dim_color, uint32_t num_layers_color, void* h_out, float* sigma,
+                     void* color_in, const float* dirs, float density_scale, void* color_out,
+                     void* stream);
 #define NGP_FFMLP_DEFER_REDUCE 1u /* leave dW partials for ngp_ffmlp_reduce */
 #define NGP_FFMLP_NERF_GEO 2u     /* grad_inputs [B,16]: input-grad cols 16..30 -> cols 1..15 */
 #define NGP_FFMLP_PAIR_MAJOR 4u   /* inputs and grad_inputs as [in_dim/2][B][2] (the grid's [L,B,2]) */

@@ -484,3 +484,32 @@ def test_grid_forward_fp32_table_equals_fp16_copy(cuda):
     outs = [o.view(e.num_levels, ft.M, e.level_dim)[:, :n] for o in outs]
     assert n > 0 and torch.isfinite(outs[0].float()).all()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
+def test_one_launch_forward_equals_split_forward(cuda, monkeypatch, bound, dt_gamma):
+    """ngp_nerf_forward (sigma + colour networks in one launch) against the
+    two launches (ngp_nerf_sigma_forward + ngp_ffmlp_forward_rows) on the same
+    batch: h, sigma, color_in, rgb logits, loss and the MLP gradients
+    bit-identical."""
+    outs = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("NGP_FUSED_SPLIT_FWD", split)
+        model, ref, data, ft = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
+        assert ft._one_fwd == (split == "0")
+        ft._sample()
+        ft._forward_backward()
+        torch.cuda.synchronize()
+        n = int(ft.counter[0])
+        assert n > 0
+        outs.append((n, ft.h_sigma[:n].clone(), ft.sigma[:n].clone(), ft.color_in[:n].clone(),
+                     ft.color_out[:n].clone(), [g.clone() for g in ft.grads], ft.loss_ray.clone()))
+    (n0, *a), (n1, *b) = outs
+    assert n0 == n1
+    for name, x, y in zip(["h", "sigma", "color_in", "color_out"], a[:4], b[:4]):
+        assert torch.equal(x, y), name
+    # MLP grads: fixed-order slab reduce; the table grad's shared bins add by
+    # fp16 atomics in arrival order
+    assert torch.equal(a[4][1], b[4][1]) and torch.equal(a[4][2], b[4][2])
+    assert _rel(a[4][0], b[4][0]) < 1e-3
+    assert torch.equal(a[5], b[5])

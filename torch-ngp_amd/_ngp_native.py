@@ -92,6 +92,8 @@ SIGNATURES = {
                                c_vp, c_vp],
     "ngp_nerf_sigma_forward": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp,
                                c_f32, c_u32, c_vp],
+    "ngp_nerf_forward": [c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp,
+                         c_f32, c_vp, c_vp],
     "ngp_ffmlp_backward_rows": [c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32,
                                 c_vp, c_vp, c_i32, c_u32, c_vp, c_sz, c_vp],
     "ngp_ffmlp_reduce": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],

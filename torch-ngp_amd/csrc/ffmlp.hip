@@ -312,6 +312,14 @@ struct EpiNerfSigma {
     float density_scale;
     template <typename FO>
     NGP_DEV void operator()(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act) const {
+        half8 unused[kNB][1];
+        run<false>(row0, B, o, out_act, unused);
+    }
+    // OPERAND: also hand back color_in's rows as the colour network's
+    // first-layer B operand (load_rows' layout: lane (g, c) holds columns
+    // 8g .. 8g+7 of row c), the same fp16 values the store writes.
+    template <bool OPERAND, typename FO>
+    NGP_DEV void run(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act, half8 (&xc)[kNB][1]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
         for (int nb = 0; nb < kNB; ++nb) {
@@ -322,11 +330,21 @@ struct EpiNerfSigma {
             // h[row][4g+4] from the next lane group (color_in shifts h by one column)
             const uint32_t nx = __shfl((uint32_t)__builtin_bit_cast(uint16_t, v[0]), lane + 16, 64);
             const ngp_half next = g < 3 ? __builtin_bit_cast(ngp_half, (uint16_t)nx) : (ngp_half)0.0f;
+            const half4 q = half4{v[1], v[2], v[3], next};  // color_in[row][16 + 4g .. 16 + 4g + 3]
+            uint2 qq[2];  // lane groups 2 and 3 take color_in columns 16..23 / 24..31 from groups 0,1 / 2,3
+            if constexpr (OPERAND) {
+                const uint2 qm = __builtin_bit_cast(uint2, q);
+                const int src = (g >= 2 ? 2 * (g - 2) : 0) * 16 + c;
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+                    qq[k] = uint2{(uint32_t)__shfl((int)qm.x, src + 16 * k, 64), (uint32_t)__shfl((int)qm.y, src + 16 * k, 64)};
+                xc[nb][0] = half8{0, 0, 0, 0, 0, 0, 0, 0};
+            }
             if (row >= B) continue;
             *reinterpret_cast<half4*>(h + (size_t)row * kOut + 4 * g) = v;
             if (g == 0) sigma[row] = density_scale * expf((float)v[0]);
             ngp_half* ci = color_in + (size_t)row * 32;
-            *reinterpret_cast<half4*>(ci + 16 + 4 * g) = half4{v[1], v[2], v[3], next};
+            *reinterpret_cast<half4*>(ci + 16 + 4 * g) = q;
             float sh[16];
             ngp_sh::sh_basis<float>(dirs[(size_t)row * 3], dirs[(size_t)row * 3 + 1], dirs[(size_t)row * 3 + 2],
                                     4u, [&](uint32_t k, float x) { sh[k] = x; });
@@ -334,6 +352,17 @@ struct EpiNerfSigma {
 #pragma unroll
             for (int k = 0; k < 4; ++k) s4[k] = ngp_f2h(sh[4 * g + k]);
             *reinterpret_cast<half4*>(ci + 4 * g) = s4;
+            if constexpr (OPERAND) {
+                half8 x;
+                if (g < 2) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) x[k] = ngp_f2h(g == 0 ? sh[k] : sh[8 + k]);
+                } else {
+                    const half4 a = __builtin_bit_cast(half4, qq[0]), b = __builtin_bit_cast(half4, qq[1]);
+                    x = half8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+                }
+                xc[nb][0] = x;
+            }
         }
     }
 };
@@ -398,6 +427,57 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
         f32x4 o[kNB][1];
         dense<1, N::KSW>(lds, fwd_desc<W, IN_KS, NH>(NH + 1, in_dim).frag0, h, o);
         epi(row0, B, o, out_act);
+    }
+}
+
+// The NeRF forward in one launch (network_ff.py:51-74): per 32-sample chunk
+// the sigma network on the pair-major encodings, its epilogue (h, sigma,
+// color_in stored for the composite and the backward), then the colour network
+// on color_in's rows straight from registers, rgb logits stored [B, 16]. Each
+// row's values are the two launches' bit for bit; the colour launch's
+// color_in read and its fragment copy and launch tail go away. Both networks
+// are W wide with 32 inputs; the images are the ngp_ffmlp_pack ones.
+template <int W, int NHS, int NHC>
+__global__ void __launch_bounds__(kThreads)
+k_nerf_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img_s, const half8* __restrict__ img_c,
+           uint32_t B, const int32_t* __restrict__ count, EpiNerfSigma es, ngp_half* __restrict__ color_out) {
+    using NS = Net<W, 1, NHS>;
+    using NC = Net<W, 1, NHC>;
+    const InPairMajor xl{B};  // the encodings' allocated rows
+    if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);
+    extern __shared__ half8 lds[];
+    half8* lds_c = lds + NS::FWD_FRAGS * 64;
+    copy_frags<NS::FWD_FRAGS, kThreads>(lds, img_s);
+    copy_frags<NC::FWD_FRAGS, kThreads>(lds_c, img_c);
+    __syncthreads();
+    const ActReLU act;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
+    for (uint32_t chunk = blockIdx.x * kWaves + wave; chunk < nchunks; chunk += gridDim.x * kWaves) {
+        const uint32_t row0 = chunk * 16 * kNB;
+        half8 x[kNB][1];
+        xl.template operator()<1>(enc, 32u, row0, B, x);
+        f32x4 acc[kNB][NS::MTW];
+        half8 h[kNB][NS::KSW];
+        dense<NS::MTW, 1>(lds, fwd_desc<W, 1, NHS>(0, 32u).frag0, x, acc);
+        pack_act<NS::MTW, NS::KSW>(acc, act, h);
+#pragma unroll
+        for (int q = 1; q <= NHS; ++q) {
+            dense<NS::MTW, NS::KSW>(lds, fwd_desc<W, 1, NHS>(q, 32u).frag0, h, acc);
+            pack_act<NS::MTW, NS::KSW>(acc, act, h);
+        }
+        f32x4 o[kNB][1];
+        dense<1, NS::KSW>(lds, fwd_desc<W, 1, NHS>(NHS + 1, 32u).frag0, h, o);
+        es.template run<true>(row0, B, o, ActNone{}, x);
+        dense<NC::MTW, 1>(lds_c, fwd_desc<W, 1, NHC>(0, 32u).frag0, x, acc);
+        pack_act<NC::MTW, NC::KSW>(acc, act, h);
+#pragma unroll
+        for (int q = 1; q <= NHC; ++q) {
+            dense<NC::MTW, NC::KSW>(lds_c, fwd_desc<W, 1, NHC>(q, 32u).frag0, h, acc);
+            pack_act<NC::MTW, NC::KSW>(acc, act, h);
+        }
+        dense<1, NC::KSW>(lds_c, fwd_desc<W, 1, NHC>(NHC + 1, 32u).frag0, h, o);
+        store_tiles<1>(color_out, kOut, row0, B, o, ActNone{});
     }
 }
 
@@ -877,6 +957,19 @@ int launch_fwd_density(const void* in, const void* w, const void* image, uint32_
                                       InPairMajor{B});
 }
 
+template <int W, int NHS, int NHC>
+int launch_nerf_fwd(const void* enc, const void* img_s, const void* img_c, uint32_t B, const int32_t* count,
+                    const EpiNerfSigma& es, void* color_out, hipStream_t st) {
+    const size_t lds = (size_t)(Net<W, 1, NHS>::FWD_FRAGS + Net<W, 1, NHC>::FWD_FRAGS) * 64 * 16;
+    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
+    uint32_t blocks = ngp_div_up(nchunks, kWaves);
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) return NGP_OK;
+    hipLaunchKernelGGL((k_nerf_fwd<W, NHS, NHC>), dim3(blocks), dim3(kThreads), lds, st, (const ngp_half*)enc,
+                       (const half8*)img_s, (const half8*)img_c, B, count, es, (ngp_half*)color_out);
+    return ngp_check_launch("nerf_forward");
+}
+
 constexpr size_t kImageBytes = 128 * 1024;  // fragment image slot at the head of the workspace
 
 template <int W, int IN_KS, int NH>
@@ -1027,6 +1120,33 @@ extern "C" int ngp_nerf_sigma_forward(const void* inputs, const void* weights, c
                            density_scale};
     NGP_MLP_DISPATCH(launch_fwd_nerf, inputs, weights, image, B, in_dim, count, epi,
                      (flags & NGP_FFMLP_PAIR_MAJOR) != 0, st);
+}
+
+extern "C" int ngp_nerf_forward(const void* enc, const void* sigma_image, const void* color_image, uint32_t B,
+                                const int32_t* count, uint32_t hidden_dim, uint32_t num_layers,
+                                uint32_t hidden_dim_color, uint32_t num_layers_color, void* h_out, float* sigma,
+                                void* color_in, const float* dirs, float density_scale, void* color_out,
+                                void* stream) {
+    NGP_REQUIRE(hidden_dim == 64 && hidden_dim_color == 64, NGP_ERR_UNSUPPORTED,
+                "nerf_forward: 64-wide networks only on this build, got %u / %u", hidden_dim, hidden_dim_color);
+    NGP_REQUIRE(num_layers >= 2 && num_layers <= 3 && num_layers_color >= 2 && num_layers_color <= 4,
+                NGP_ERR_UNSUPPORTED, "nerf_forward: num_layers in [2, 3] (sigma) / [2, 4] (color), got %u / %u",
+                num_layers, num_layers_color);
+    NGP_REQUIRE(enc && sigma_image && color_image && h_out && sigma && color_in && dirs && color_out, NGP_ERR_ARG,
+                "nerf_forward: null pointer");
+    if (B == 0) return NGP_OK;
+    hipStream_t st = ngp_stream(stream);
+    const EpiNerfSigma es{static_cast<ngp_half*>(h_out), sigma, static_cast<ngp_half*>(color_in), dirs,
+                          density_scale};
+    const uint32_t key = (num_layers - 1) * 8 + (num_layers_color - 1);
+    switch (key) {
+        case 1 * 8 + 1: return launch_nerf_fwd<64, 1, 1>(enc, sigma_image, color_image, B, count, es, color_out, st);
+        case 1 * 8 + 2: return launch_nerf_fwd<64, 1, 2>(enc, sigma_image, color_image, B, count, es, color_out, st);
+        case 1 * 8 + 3: return launch_nerf_fwd<64, 1, 3>(enc, sigma_image, color_image, B, count, es, color_out, st);
+        case 2 * 8 + 1: return launch_nerf_fwd<64, 2, 1>(enc, sigma_image, color_image, B, count, es, color_out, st);
+        case 2 * 8 + 2: return launch_nerf_fwd<64, 2, 2>(enc, sigma_image, color_image, B, count, es, color_out, st);
+        default: return launch_nerf_fwd<64, 2, 3>(enc, sigma_image, color_image, B, count, es, color_out, st);
+    }
 }
 
 extern "C" int ngp_nerf_density_forward(const void* inputs, const void* weights, const void* image, uint32_t B,

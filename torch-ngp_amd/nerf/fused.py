@@ -178,6 +178,12 @@ class FusedTrainer:
         # Data parallel: the fp16 copy is what the all-gather moves.
         self.table32 = W == 1 and os.environ.get("NGP_FUSED_TABLE16") != "1"
         self._merge_head = W == 1 and os.environ.get("NGP_FUSED_SPLIT_HEAD") != "1"
+        # one launch for the sigma + colour forwards where ngp_nerf_forward covers
+        # the shapes (NGP_FUSED_SPLIT_FWD=1 keeps two launches, for A/B and tests)
+        sn_, cn_ = self.sig_net, self.col_net
+        self._one_fwd = (os.environ.get("NGP_FUSED_SPLIT_FWD") != "1" and sn_.hidden_dim == 64
+                         and cn_.hidden_dim == 64 and sn_.input_dim == 32 and cn_.input_dim == 32
+                         and 2 <= sn_.num_layers <= 3 and 2 <= cn_.num_layers <= 4)
         if self.table32:
             nt = self._starts[1]  # the table, then the two MLPs
             sec = [(0, nt, False), (nt, chunk - nt, True)]
@@ -460,14 +466,21 @@ class FusedTrainer:
         sn, cn, img, pk = self.sig_net, self.col_net, self.mlp_img, self._pk
         if self.world > 1:  # after the all-gather of the fp16 forward copy (see _sample)
             chk(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
-        chk(lib.ngp_nerf_sigma_forward(P(self.enc_out), P(self.w_half[1]), P(img[0]), M, cnt, 32, sn.hidden_dim,
-                                       sn.num_layers, P(self.h_sigma), P(self.sigma), P(self.color_in),
-                                       P(self.dirs), float(m.density_scale), _PAIR, s), "sigma_mlp")
-        self._tick("ffmlp_forward_sigma")
-        chk(lib.ngp_ffmlp_forward_rows(P(self.color_in), P(self.w_half[2]), P(img[1]), M, cnt, 32, 16,
-                                       cn.hidden_dim, cn.num_layers, _RELU, _NONE, P(self.color_out), s),
-            "color_mlp")
-        self._tick("ffmlp_forward_color")
+        if self._one_fwd:  # both networks in one launch (ngp_nerf_forward)
+            chk(lib.ngp_nerf_forward(P(self.enc_out), P(img[0]), P(img[1]), M, cnt, sn.hidden_dim, sn.num_layers,
+                                     cn.hidden_dim, cn.num_layers, P(self.h_sigma), P(self.sigma),
+                                     P(self.color_in), P(self.dirs), float(m.density_scale), P(self.color_out), s),
+                "nerf_forward")
+            self._tick("ffmlp_forward")
+        else:
+            chk(lib.ngp_nerf_sigma_forward(P(self.enc_out), P(self.w_half[1]), P(img[0]), M, cnt, 32, sn.hidden_dim,
+                                           sn.num_layers, P(self.h_sigma), P(self.sigma), P(self.color_in),
+                                           P(self.dirs), float(m.density_scale), _PAIR, s), "sigma_mlp")
+            self._tick("ffmlp_forward_sigma")
+            chk(lib.ngp_ffmlp_forward_rows(P(self.color_in), P(self.w_half[2]), P(img[1]), M, cnt, 32, 16,
+                                           cn.hidden_dim, cn.num_layers, _RELU, _NONE, P(self.color_out), s),
+                "color_mlp")
+            self._tick("ffmlp_forward_color")
         chk(lib.ngp_nerf_composite_loss(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
                                         P(self.rays), M, N, self.T_thresh, float(m.density_scale),
                                         P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
