@@ -394,6 +394,8 @@ def run_fused(args, model, data, bits, world, dev):
     achieved = dom_bytes / (kernel_ms[dominant] * 1e-3) / 1e9
     mlp_ms = sum(v for k, v in kernel_ms.items() if k.startswith("ffmlp"))
     ffmlp_flops = 110592 * rows
+    step_bytes = whole_step_bytes(rows, args.num_rays, sum(p.numel() for p in model.parameters()),
+                                  int(model.encoder.embeddings.numel()))
 
     density = density_update_times(model, bits, ft)
 
@@ -437,6 +439,10 @@ def run_fused(args, model, data, bits, world, dev):
         "ffmlp_mfma": {"flops_per_step": ffmlp_flops, "ms": round(mlp_ms, 5),
                         "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
                         "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
+        # SURVEY §8(d)'s secondary figure: the step's algorithmic bytes over the
+        # whole step time (per rank) against the HBM peak
+        "step_roofline": {"algorithmic_bytes": int(step_bytes),
+                          "frac": round(step_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)},
         "density_update_ms": density,
         "loss": loss,
     }
@@ -482,6 +488,16 @@ def density_update_times(model, bits, ft=None, reps=3):
 
 _PMC_KERNELS = {"grid_encode_backward": ("k_grid_bwd_bin", "k_grid_bin_accum"),
                 "grid_encode_forward": ("k_grid_fwd_pair",)}
+
+
+def whole_step_bytes(samples, rays, n_params, n_table):
+    """Algorithmic HBM bytes of one step per SURVEY §8(d): grid forward 588 B and
+    backward 1,100 B per sample (+ the fp16 table grad's zero fill, 2 B per table
+    value), march 48 B/ray + 32 B/sample, composite forward 32 B/ray + 24
+    B/sample and backward 52 B/ray + 40 B/sample, SH 76 B/direction, dense Adam
+    28 B/parameter."""
+    return (588 * samples + 1100 * samples + 2 * n_table + 48 * rays + 32 * samples + 32 * rays + 24 * samples
+            + 52 * rays + 40 * samples + 76 * samples + 28 * n_params)
 
 
 def pmc_traffic(kernel):
