@@ -40,7 +40,10 @@ using ngp_pack::perm_unit;
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kWaves = 4;  // forward: waves per workgroup
+#ifndef NGP_MLP_FWD_WAVES  // same-box A/B builds only (tools/variants.sh)
+#define NGP_MLP_FWD_WAVES 4
+#endif
+constexpr int kWaves = NGP_MLP_FWD_WAVES;  // forward: waves per workgroup (sharing one fragment copy)
 constexpr int kThreads = kWaves * 64;
 // Backward: waves per workgroup sharing one fragment image. The dW tiles
 // live in registers for the whole chunk loop (176 of them for the colour
@@ -68,6 +71,10 @@ NGP_DEV f32x4 mfma(half8 a, half8 b, f32x4 c) {
 
 // Fragment image -> LDS with every load of a thread issued before its first
 // store (a load/store pair per iteration exposed the load latency ~12 times).
+// The loads are unconditional (a partial last round reads a clamped index):
+// a load under a divergent branch leaves the compiler unsure how many memory
+// operations are outstanding, so it waited vmcnt(0) after each one and the
+// copy took one round trip per load (~9 K cycles, tools/fwd_stamps.py).
 template <int FRAGS, int THREADS>
 NGP_DEV void copy_frags(half8* __restrict__ lds, const half8* __restrict__ image) {
     constexpr int TOTAL = FRAGS * 64, PER = (TOTAL + THREADS - 1) / THREADS;
@@ -75,14 +82,18 @@ NGP_DEV void copy_frags(half8* __restrict__ lds, const half8* __restrict__ image
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int t = k * THREADS + (int)threadIdx.x;
-        if (t < TOTAL) v[k] = image[t];
+        v[k] = image[(k + 1) * THREADS <= TOTAL ? t : min(t, TOTAL - 1)];
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int t = k * THREADS + (int)threadIdx.x;
-        if (t < TOTAL) lds[t] = v[k];
+        if ((k + 1) * THREADS <= TOTAL || t < TOTAL) lds[t] = v[k];
     }
 }
+
+// a row index that is always readable (rows past B read row B - 1 and the
+// caller zeroes the value): loads without branches, see copy_frags
+NGP_DEV uint32_t clamp_row(uint32_t row, uint32_t B) { return row < B ? row : (B ? B - 1 : 0u); }
 
 // Activation enum of ffmlp.py:89-96 / utils.h:29-37.
 enum Act : uint32_t { kReLU = 0, kExp = 1, kSine = 2, kSigmoid = 3, kSquareplus = 4, kSoftplus = 5, kNone = 6 };
@@ -224,9 +235,11 @@ NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const uint32_t col = 32 * s + 8 * g;
-            half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (row < B && col < width) v = *reinterpret_cast<const half8*>(src + (size_t)row * width + col);
-            out[nb][s] = v;
+            const bool ok = row < B && col < width;
+            const half8 v = *reinterpret_cast<const half8*>(src + (size_t)clamp_row(row, B) * width +
+                                                            (col < width ? col : 0u));
+            const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+            out[nb][s] = ok ? v : z;
         }
     }
 }
@@ -255,14 +268,14 @@ struct InPairMajor {
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const uint32_t col = 32 * s + 8 * g;
-                half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (row < B && col < width) {
+                const bool ok = row < B && col < width;
+                const uint32_t rr = clamp_row(row, B), cc = col < width ? col : 0u;
+                half8 v;
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        const ngp_half2 h = *reinterpret_cast<const ngp_half2*>(src + ((size_t)(col / 2 + p) * ld + row) * 2);
-                        v[2 * p] = h[0];
-                        v[2 * p + 1] = h[1];
-                    }
+                for (int p = 0; p < 4; ++p) {
+                    const ngp_half2 h = *reinterpret_cast<const ngp_half2*>(src + ((size_t)(cc / 2 + p) * ld + rr) * 2);
+                    v[2 * p] = ok ? h[0] : (ngp_half)0.0f;
+                    v[2 * p + 1] = ok ? h[1] : (ngp_half)0.0f;
                 }
                 out[nb][s] = v;
             }
@@ -304,6 +317,19 @@ struct EpiStore {
     }
 };
 
+#ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py, tools/fwd_stamps.py): per-wave phase clocks
+__device__ unsigned long long* g_mlp_stamps;
+// k_nerf_fwd: 16 slots per wave after the backward's 2 x 2048 waves; W-suffixed
+// stamps first wait for the wave's outstanding memory operations
+#define FSTAMP(slot, v) do { if (g_mlp_stamps && (threadIdx.x & 63) == 0) g_mlp_stamps[(size_t)2 * 2048 * 16 + ((size_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 16 + (slot)] = (v); } while (0)
+#define FSTAMPW(slot) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); FSTAMP(slot, __builtin_amdgcn_s_memtime()); } while (0)
+#define FRSTAMP(slot) FSTAMP(slot, __builtin_amdgcn_s_memrealtime())
+#else
+#define FSTAMPW(slot) do { } while (0)
+#define FRSTAMP(slot) do { } while (0)
+#endif
+// (kWaves: the forward's waves per workgroup)
+
 struct EpiNerfSigma {
     ngp_half* h;
     float* sigma;
@@ -313,13 +339,30 @@ struct EpiNerfSigma {
     template <typename FO>
     NGP_DEV void operator()(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act) const {
         half8 unused[kNB][1];
-        run<false>(row0, B, o, out_act, unused);
+        float dv[kNB][3];
+        load_dirs(row0, B, dv);
+        run<false>(row0, B, o, out_act, unused, dv);
+    }
+    // the chunk's view directions (row c of lane group g: every group loads
+    // its row's), issued early so the SH does not wait a memory round trip
+    NGP_DEV void load_dirs(uint32_t row0, uint32_t B, float (&dv)[kNB][3]) const {
+        const int c = threadIdx.x & 15;
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+            const uint32_t row = row0 + nb * 16 + c;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float d = dirs[(size_t)clamp_row(row, B) * 3 + k];
+                dv[nb][k] = row < B ? d : 0.0f;
+            }
+        }
     }
     // OPERAND: also hand back color_in's rows as the colour network's
     // first-layer B operand (load_rows' layout: lane (g, c) holds columns
     // 8g .. 8g+7 of row c), the same fp16 values the store writes.
     template <bool OPERAND, typename FO>
-    NGP_DEV void run(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act, half8 (&xc)[kNB][1]) const {
+    NGP_DEV void run(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act, half8 (&xc)[kNB][1],
+                     const float (&dv)[kNB][3]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
         for (int nb = 0; nb < kNB; ++nb) {
@@ -339,18 +382,22 @@ struct EpiNerfSigma {
                 for (int k = 0; k < 2; ++k)
                     qq[k] = uint2{(uint32_t)__shfl((int)qm.x, src + 16 * k, 64), (uint32_t)__shfl((int)qm.y, src + 16 * k, 64)};
                 xc[nb][0] = half8{0, 0, 0, 0, 0, 0, 0, 0};
+                if (nb == 0) FSTAMPW(10);
             }
             if (row >= B) continue;
             *reinterpret_cast<half4*>(h + (size_t)row * kOut + 4 * g) = v;
             if (g == 0) sigma[row] = density_scale * expf((float)v[0]);
             ngp_half* ci = color_in + (size_t)row * 32;
             *reinterpret_cast<half4*>(ci + 16 + 4 * g) = q;
+            if (OPERAND && nb == 0) FSTAMPW(11);
             float sh[16];
-            ngp_sh::sh_basis<float>(dirs[(size_t)row * 3], dirs[(size_t)row * 3 + 1], dirs[(size_t)row * 3 + 2],
-                                    4u, [&](uint32_t k, float x) { sh[k] = x; });
+            ngp_sh::sh_basis<float>(dv[nb][0], dv[nb][1], dv[nb][2], 4u, [&](uint32_t k, float x) { sh[k] = x; });
+            // static indices only: sh[4 * g + k] put the array in scratch memory
+            // (a store and a dependent load round trip per value)
             half4 s4;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) s4[k] = ngp_f2h(sh[4 * g + k]);
+            for (int k = 0; k < 4; ++k)
+                s4[k] = ngp_f2h(g == 0 ? sh[k] : g == 1 ? sh[4 + k] : g == 2 ? sh[8 + k] : sh[12 + k]);
             *reinterpret_cast<half4*>(ci + 4 * g) = s4;
             if constexpr (OPERAND) {
                 half8 x;
@@ -362,6 +409,7 @@ struct EpiNerfSigma {
                     x = half8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
                 }
                 xc[nb][0] = x;
+                if (nb == 0) FSTAMPW(12);
             }
         }
     }
@@ -430,6 +478,7 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
     }
 }
 
+
 // The NeRF forward in one launch (network_ff.py:51-74): per 32-sample chunk
 // the sigma network on the pair-major encodings, its epilogue (h, sigma,
 // color_in stored for the composite and the backward), then the colour network
@@ -444,19 +493,36 @@ k_nerf_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img_s, co
     using NS = Net<W, 1, NHS>;
     using NC = Net<W, 1, NHC>;
     const InPairMajor xl{B};  // the encodings' allocated rows
+    FRSTAMP(8);
+    FSTAMPW(0);
     if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);
     extern __shared__ half8 lds[];
     half8* lds_c = lds + NS::FWD_FRAGS * 64;
+    const ActReLU act;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t nchunks = ngp_div_up(B, 16 * kNB), stride = gridDim.x * kWaves;
+    // the first chunk's encodings and directions are requested before the
+    // fragment copy, each later chunk's at the end of the previous one
+    uint32_t chunk = blockIdx.x * kWaves + wave;
+    half8 xn[kNB][1];
+    float dn[kNB][3];
+    xl.template operator()<1>(enc, 32u, chunk * 16 * kNB, B, xn);
+    es.load_dirs(chunk * 16 * kNB, B, dn);
     copy_frags<NS::FWD_FRAGS, kThreads>(lds, img_s);
     copy_frags<NC::FWD_FRAGS, kThreads>(lds_c, img_c);
     __syncthreads();
-    const ActReLU act;
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
-    for (uint32_t chunk = blockIdx.x * kWaves + wave; chunk < nchunks; chunk += gridDim.x * kWaves) {
+    FSTAMPW(1);
+    for (; chunk < nchunks; chunk += stride) {
         const uint32_t row0 = chunk * 16 * kNB;
         half8 x[kNB][1];
-        xl.template operator()<1>(enc, 32u, row0, B, x);
+        float dv[kNB][3];
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+            x[nb][0] = xn[nb][0];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) dv[nb][k] = dn[nb][k];
+        }
+        FSTAMPW(2);
         f32x4 acc[kNB][NS::MTW];
         half8 h[kNB][NS::KSW];
         dense<NS::MTW, 1>(lds, fwd_desc<W, 1, NHS>(0, 32u).frag0, x, acc);
@@ -468,7 +534,9 @@ k_nerf_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img_s, co
         }
         f32x4 o[kNB][1];
         dense<1, NS::KSW>(lds, fwd_desc<W, 1, NHS>(NHS + 1, 32u).frag0, h, o);
-        es.template run<true>(row0, B, o, ActNone{}, x);
+        FSTAMPW(3);
+        es.template run<true>(row0, B, o, ActNone{}, x, dv);
+        FSTAMPW(4);
         dense<NC::MTW, 1>(lds_c, fwd_desc<W, 1, NHC>(0, 32u).frag0, x, acc);
         pack_act<NC::MTW, NC::KSW>(acc, act, h);
 #pragma unroll
@@ -477,8 +545,14 @@ k_nerf_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img_s, co
             pack_act<NC::MTW, NC::KSW>(acc, act, h);
         }
         dense<1, NC::KSW>(lds_c, fwd_desc<W, 1, NHC>(NHC + 1, 32u).frag0, h, o);
+        FSTAMPW(5);
         store_tiles<1>(color_out, kOut, row0, B, o, ActNone{});
+        FSTAMPW(6);
+        // the next chunk's inputs (clamped rows: no branch, see copy_frags)
+        xl.template operator()<1>(enc, 32u, row0 + stride * 16 * kNB, B, xn);
+        es.load_dirs(row0 + stride * 16 * kNB, B, dn);
     }
+    FRSTAMP(9);
 }
 
 // ---- backward ---------------------------------------------------------------
@@ -685,7 +759,6 @@ struct GiPairMajor {
 };
 
 #ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-wave phase clocks
-__device__ unsigned long long* g_mlp_stamps;
 #define MSTAMP(slot) do { if (g_mlp_stamps && (threadIdx.x & 63) == 0) g_mlp_stamps[((size_t)(NH - 1) * 2048 + blockIdx.x * kBwdWaves + (threadIdx.x >> 6)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define MSTAMP(slot) do { } while (0)
