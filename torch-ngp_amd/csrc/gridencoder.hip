@@ -275,11 +275,17 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
     const bool live = b < rows_of(B, im);
     if (__ballot(live) == 0) return;  // wave-uniform exit; pairs stay together below
 
+    // Every load below is unconditional (dead lanes read a valid clamped
+    // address and discard the value): a load under a divergent branch made the
+    // compiler wait vmcnt(0) right after it, so the 2 x 4 gathers of a lane
+    // went out one round trip at a time.
+    const uint32_t bl = live ? b : 0u;  // some lane of the wave is live, so rows >= 1
     float x[D];
     bool oob = !live;
 #pragma unroll
     for (uint32_t d = 0; d < D; d++) {
-        x[d] = live ? inputs[(size_t)b * D + d] : 0.5f;
+        const float xi = inputs[(size_t)bl * D + d];
+        x[d] = live ? xi : 0.5f;
         if (im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
         if (x[d] < 0 || x[d] > 1) oob = true;
     }
@@ -312,13 +318,12 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
             uint32_t pl[D];
 #pragma unroll
             for (uint32_t d = 0; d < D; d++) pl[d] = (idx & (1u << d)) ? pg[d] + 1 : pg[d];
-            if (!oob) {
-                const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
-                load_entry_as<T, E, C>(g + (size_t)e * C, mine[q][rest]);
-            } else {
+            // grid_index is < hs for any pl (mask / modulo), so an out-of-bounds
+            // point's address is valid too
+            const uint32_t e = grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl);
+            load_entry_as<T, E, C>(g + (size_t)e * C, mine[q][rest]);
 #pragma unroll
-                for (uint32_t c = 0; c < C; ++c) mine[q][rest][c] = 0;
-            }
+            for (uint32_t c = 0; c < C; ++c) mine[q][rest][c] = oob ? (F)0 : mine[q][rest][c];
         }
     }
 #pragma unroll
