@@ -133,18 +133,19 @@ NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __rest
     Chunk c;
     const uint32_t i = offset + base + lane;
     c.ok = base + lane < num_steps;
-    const float sg = c.ok ? sigma[i] : 0.0f;
-    const float2 dd = c.ok ? *reinterpret_cast<const float2*>(deltas + (size_t)i * 2) : float2{0.0f, 0.0f};
-    c.d0 = dd.x;
-    const float d1 = dd.y;
-    c.c0 = c.c1 = c.c2 = 0.0f;
-    if (c.ok) {
-        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-        const half4 co = *reinterpret_cast<const half4*>(color_out + (size_t)i * 16);
-        c.c0 = sigmoid_h(co[0]);
-        c.c1 = sigmoid_h(co[1]);
-        c.c2 = sigmoid_h(co[2]);
-    }
+    // unconditional loads (lanes past the ray read row 0 and drop the value):
+    // a load under a divergent branch makes the compiler wait for it on the spot
+    const uint32_t ic = c.ok ? i : 0u;
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    const float sgl = sigma[ic];
+    const float2 ddl = *reinterpret_cast<const float2*>(deltas + (size_t)ic * 2);
+    const half4 co = *reinterpret_cast<const half4*>(color_out + (size_t)ic * 16);
+    const float sg = c.ok ? sgl : 0.0f;
+    c.d0 = c.ok ? ddl.x : 0.0f;
+    const float d1 = c.ok ? ddl.y : 0.0f;
+    c.c0 = c.ok ? sigmoid_h(co[0]) : 0.0f;
+    c.c1 = c.ok ? sigmoid_h(co[1]) : 0.0f;
+    c.c2 = c.ok ? sigmoid_h(co[2]) : 0.0f;
     const float sd = sg * c.d0;
     const float incl = scan_incl(sd, lane);
     // the exclusive prefix is the previous lane's inclusive one, NOT incl - sd:
@@ -187,15 +188,17 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     // first chunk: the background, the target and the first chunk's h0 (each
     // was a dependent round trip after the forward's scans)
     const float bg0 = bg[index * 3], bg1 = bg[index * 3 + 1], bg2 = bg[index * 3 + 2];
-    float gt4[4] = {0.0f, 0.0f, 0.0f, 1.0f};
-    if (la.gt_channels == 4) {
+    // (RGB targets: alpha 1; loads without branches, see load_chunk)
+    const uint32_t gch = la.gt_channels;
+    float gt4[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) gt4[k] = gt[(size_t)index * 4 + k];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) gt4[k] = gt[(size_t)index * 3 + k];
+    for (int k = 0; k < 4; ++k) {
+        const float v = gt[(size_t)index * gch + min((uint32_t)k, gch - 1u)];
+        gt4[k] = (uint32_t)k < gch ? v : 1.0f;
     }
-    const float h0_first = valid && lane < num_steps ? (float)h_sigma[(size_t)(offset + lane) * 16] : 0.0f;
+    const bool h_ok = valid && lane < num_steps;
+    const float h0l = (float)h_sigma[(size_t)(h_ok ? offset + lane : 0u) * 16];
+    const float h0_first = h_ok ? h0l : 0.0f;
 
     // ---- forward (composite_rays_train_forward)
     // The first 64-sample chunk (all of most rays) is kept for the backward
