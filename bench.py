@@ -507,8 +507,10 @@ def pmc_traffic(kernel):
     over this same bench). FETCH_SIZE doubled per MI355X_MICROARCH.md's HBM
     section (gfx950 tallies wide streaming reads at half); WRITE_SIZE as read."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_step_kernels.json")),
-                   key=lambda f: (len(os.path.basename(f)), os.path.basename(f)))  # r01z < r01ab
+    def order(f):  # rNN then the tag: r01z < r01ab < r02a
+        tag = os.path.basename(f).split("_")[0]
+        return (int(tag[1:3]) if tag[1:3].isdigit() else 0, len(tag), tag)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_step_kernels.json")), key=order)
     if not files:
         return None, None
     pmc = json.load(open(files[-1])).get("pmc_per_launch", {})
