@@ -123,15 +123,23 @@ def test_grid_backward_fused_bin_overflow(cuda):
     """Points in a 0.03-wide cube: on the hashed levels a few entries take all
     corners, bins overflow their capacity and the excess goes through per-item
     fp16 atomics (the reference's own accumulation, gridencoder.cu:325), whose
-    rounding grows with the thousands of terms per entry: 2e-2 here."""
+    rounding grows with the thousands of terms per entry and depends on their
+    arrival order: 2e-2 rel-norm per level, and per entry the bound of
+    test_grid_backward_fp16 (2^-8 of the entry's sum of |contributions|; a
+    max-error test against the level's largest value failed at 4.2e-2 on one
+    run and passed on others)."""
     nat = _lib()
     B, L, H, scale = 40000, 12, 16, 1.5
     offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
     w = _world(B, 1.0, seed=4, concentrated=0.03)
     g16 = (np.random.default_rng(9).standard_normal((B, L * 2)) * 0.5).astype(np.float16)
     got = _bwd(nat, cuda, g16, w, offs, L, H, scale, 1.0, zeroed=True)  # overflowed bins still read back
-    ref = oracle.grid_encode_backward(g16, _normalise(w, 1.0), offs, 2, scale, H)
-    _check_levels(got, ref, offs, "overflow", rtol=2e-2, mtol=4e-2)
+    x = _normalise(w, 1.0)
+    ref = oracle.grid_encode_backward(g16, x, offs, 2, scale, H)
+    _check_levels(got, ref, offs, "overflow", rtol=2e-2, mtol=np.inf)
+    mag = oracle.grid_encode_backward(np.abs(g16.astype(np.float64)), x, offs, 2, scale, H)
+    err = np.abs(got - ref)
+    assert (err <= 2.0 ** -8 * mag + 1e-7).all(), float((err / np.maximum(mag, 1e-30)).max())
 
 
 @pytest.mark.parametrize("layout", [1, 0])
