@@ -26,7 +26,9 @@ ft = FusedTrainer(model, SyntheticLego(dev, num_rays=4096), M=101762)
 stamps = torch.zeros(4096 * 64, dtype=torch.int64, device=dev)
 lib = nat.lib()
 assert lib.ngp_debug_stamps(ctypes.c_void_p(nat.ptr(stamps))) == 0
-ms = torch.zeros(2 * 1024 * 16, dtype=torch.int64, device=dev)  # k_mlp_bwd: set before any step
+# k_mlp_bwd: (NH - 1) * 2048 + wave rows of 16 (ffmlp.hip MSTAMP), then the
+# one-launch forward's rows (FSTAMP); set before any step
+ms = torch.zeros(2 * 2048 * 16 + 4096 * 16, dtype=torch.int64, device=dev)
 if hasattr(lib, "ngp_debug_mlp_stamps"):
     assert lib.ngp_debug_mlp_stamps(ctypes.c_void_p(nat.ptr(ms))) == 0
 for _ in range(12):
@@ -104,7 +106,7 @@ if hasattr(lib, "ngp_debug_mlp_stamps"):
     ms.zero_()
     ft.step()
     torch.cuda.synchronize()
-    mm = ms.view(2, 1024, 16).cpu().numpy().astype(np.int64)
+    mm = ms[:2 * 2048 * 16].view(2, 2048, 16).cpu().numpy().astype(np.int64)
     out = {}
     for nh, name in ((0, "sigma"), (1, "colour")):
         w = mm[nh][mm[nh][:, 0] > 0]
