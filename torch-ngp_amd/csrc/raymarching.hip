@@ -648,8 +648,20 @@ k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     __shared__ uint32_t lds_waves[kMarchThreads / 64];
     const uint32_t* __restrict__ counts = scan + 4;
     const uint32_t n0 = blockIdx.x * kMarchThreads;
+    // the counts of all earlier rays, 8 loads in flight per thread (one load
+    // per iteration waited out an L2 round trip each: 15 of them for the last
+    // group of a 4096-ray batch); indices past n0 read count 0's slot and drop it
     uint32_t part = 0;
-    for (uint32_t i = threadIdx.x; i < n0; i += kMarchThreads) part += counts[i];
+    for (uint32_t i0 = threadIdx.x; i0 < n0; i0 += 8 * kMarchThreads) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t i = i0 + u * kMarchThreads;
+            v[u] = counts[i < n0 ? i : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) part += i0 + u * kMarchThreads < n0 ? v[u] : 0u;
+    }
     uint32_t before;
     block_exclusive_scan<kMarchThreads>(part, lds_waves, before);
     const uint32_t base = scan[0] + before;
@@ -680,13 +692,11 @@ k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
         if (base + off[lo + 1] > M) continue;  // whole ray dropped, like the reference
         const float* row = ts + (size_t)rn * k.max_steps;
         const float t = row[kk];
-        float prev;
-        if (kk == 0) {
-            prev = ray_t0(nears[rn], noises[rn], k);
-        } else {
-            const float tp = row[kk - 1];
-            prev = tp + clampf(tp * k.dt_gamma, k.dt_min, k.dt_max);
-        }
+        // all loads unconditional (a load under the kk == 0 branch made the
+        // compiler wait for each one on the spot)
+        const float tp = row[kk ? kk - 1 : 0u];
+        const float nr = nears[rn], nz = noises[rn];
+        const float prev = kk == 0 ? ray_t0(nr, nz, k) : tp + clampf(tp * k.dt_gamma, k.dt_min, k.dt_max);
         const float ox = rays_o[rn * 3], oy = rays_o[rn * 3 + 1], oz = rays_o[rn * 3 + 2];
         const float dx = rays_d[rn * 3], dy = rays_d[rn * 3 + 1], dz = rays_d[rn * 3 + 2];
         const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
