@@ -253,9 +253,15 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
 // holds at most ceil(L / 8) level tables), and one block does KL of them for
 // its 128 points: the point is loaded once and the KL levels' gathers are all
 // in flight together.
+//
+// Large batches (the density-grid update's 1-2M query points, B >= kFwdGroupMajorMin)
+// run level-group-major with one level per block instead: an XCD then works
+// through all points of level j before level j + 8, and its L2 holds one level
+// table at a time (two hashed fp16 tables are its whole 4 MiB). Same values.
 constexpr uint32_t kFwdLevelsPerBlock = 2;
+constexpr uint32_t kFwdGroupMajorMin = 1u << 19;
 
-template <typename T, typename E, uint32_t D, uint32_t C>
+template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL = kFwdLevelsPerBlock>
 __global__ void __launch_bounds__(256)
 k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
                 const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
@@ -263,11 +269,13 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
                 int32_t out_layout, InMap im) {
     using A = Acc<T>;
     using F = typename A::F;
-    constexpr uint32_t KL = kFwdLevelsPerBlock, NR = 1u << (D - 1);
+    constexpr uint32_t NR = 1u << (D - 1);
+    constexpr bool kGroupMajor = KL == 1;
     const uint32_t lpx = (L + 7) / 8;                       // levels per XCD
     const uint32_t gpx = (lpx + KL - 1) / KL;               // level groups per XCD
     const uint32_t k = blockIdx.x >> 3;
-    const uint32_t grp = k % gpx, chunk = k / gpx;
+    const uint32_t nch = (B + 127) / 128;                   // point chunks (grid sized on B)
+    const uint32_t grp = kGroupMajor ? k / nch : k % gpx, chunk = kGroupMajor ? k % nch : k / gpx;
     const uint32_t level0 = (blockIdx.x & 7) + 8 * KL * grp;  // this block: level0, level0 + 8, ...
     if (level0 >= L) return;
     const uint32_t b = chunk * (blockDim.x / 2) + (threadIdx.x >> 1);
@@ -1439,15 +1447,23 @@ int fwd_c(const float* inputs, const void* emb, const int32_t* offsets, void* ou
     T* dd = (T*)dy_dx;
     if (!dd && (sizeof(T) <= 4)) {
         // XCD-aware 1-D grid (see the kernel): 8 XCDs x level groups x point chunks
-        const uint32_t gpx = ((L + 7) / 8 + kFwdLevelsPerBlock - 1) / kFwdLevelsPerBlock;
+        const bool gm = B >= kFwdGroupMajorMin;
+        const uint32_t kl = gm ? 1u : kFwdLevelsPerBlock;
+        const uint32_t gpx = ((L + 7) / 8 + kl - 1) / kl;
         const dim3 gp(8 * gpx * ngp_div_up(B, 128));
+#define NGP_FWD_PAIR(CC)                                                                                     \
+    (gm ? k_grid_fwd_pair<T, E, D, CC, 1><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, \
+                                                             interp, layout, im)                              \
+        : k_grid_fwd_pair<T, E, D, CC><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac,     \
+                                                          interp, layout, im))
         switch (C) {
-            case 1: k_grid_fwd_pair<T, E, D, 1><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
-            case 2: k_grid_fwd_pair<T, E, D, 2><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
-            case 4: k_grid_fwd_pair<T, E, D, 4><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
-            case 8: k_grid_fwd_pair<T, E, D, 8><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im); break;
+            case 1: NGP_FWD_PAIR(1); break;
+            case 2: NGP_FWD_PAIR(2); break;
+            case 4: NGP_FWD_PAIR(4); break;
+            case 8: NGP_FWD_PAIR(8); break;
             default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: C must be 1, 2, 4, or 8.");
         }
+#undef NGP_FWD_PAIR
         return ngp_check_launch("grid_encode_forward");
     }
     switch (C) {
