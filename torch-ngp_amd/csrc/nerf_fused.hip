@@ -405,15 +405,15 @@ k_step_head(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState
 __global__ void __launch_bounds__(kAdamThreads)
 k_adam_head(TensorList tl, StepState* __restrict__ st, AdamArgs aa, uint32_t nadam, const float* __restrict__ poses,
             LegoScene sc, uint32_t N, LegoOut out, uint32_t nlego, uint4* __restrict__ clear, uint32_t clear16) {
-    if (blockIdx.x < nadam) {
-        adam_sweep(tl, st, aa, blockIdx.x, nadam, threadIdx.x);
-        return;
-    }
-    const uint32_t b = blockIdx.x - nadam;
-    if (b < nlego) {
-        lego_rays_block(b, nlego, poses, sc, N, st, out);
-    } else {
+    // the batch and clear blocks come first: workgroups are dispatched in
+    // index order, and behind Adam's thousands of blocks the sampler's
+    // dependent chain (draw -> pose -> rays -> target) ran in the launch's tail
+    if (blockIdx.x < nlego) {
+        lego_rays_block(blockIdx.x, nlego, poses, sc, N, st, out);
+    } else if (blockIdx.x == nlego) {
         for (uint32_t i = threadIdx.x; i < clear16; i += blockDim.x) clear[i] = uint4{0u, 0u, 0u, 0u};
+    } else {
+        adam_sweep(tl, st, aa, blockIdx.x - nlego - 1, nadam, threadIdx.x);
     }
 }
 
