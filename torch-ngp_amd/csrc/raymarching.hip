@@ -634,7 +634,11 @@ k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
              const float* __restrict__ ts, float* __restrict__ xyzs, float* __restrict__ dirs,
              float* __restrict__ deltas, int32_t* __restrict__ rays, const uint32_t* __restrict__ scan,
              int32_t* __restrict__ counter, EmitTail tail) {
-    if (blockIdx.y == kEmitSplit) {  // the tail row (block-uniform)
+    // the tail row is row 0 (dispatched first: behind the emit rows its
+    // dependent chains, the bookkeeping and the fragment packs, ran in the
+    // launch's tail); the emit rows follow
+    const bool has_tail = tail.st != nullptr;
+    if (has_tail && blockIdx.y == 0) {  // the tail row (block-uniform)
         if (blockIdx.x == 0) {
             if (tail.st->end_pending) ngp_step::step_end_block(tail.st, tail.sa, nullptr, nullptr, tail.loss_ray, tail.n_rays);
         } else if (blockIdx.x - 1 < (uint32_t)tail.jobs.n) {
@@ -671,7 +675,8 @@ k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     const uint32_t excl = block_exclusive_scan<kMarchThreads>(c, lds_waves, total);
     off[threadIdx.x] = excl;
     if (threadIdx.x == 0) off[kMarchThreads] = total;
-    if (blockIdx.y == 0) {
+    const uint32_t ey = blockIdx.y - (has_tail ? 1u : 0u);  // emit row
+    if (ey == 0) {
         if (n < N) rays[(size_t)n * 3 + 1] = (int32_t)(base + excl);
         if (blockIdx.x == tail.groups - 1 && threadIdx.x == 0) {
             counter[0] = (int32_t)(base + total);
@@ -681,7 +686,7 @@ k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     __syncthreads();
 
     const uint32_t chunk = ngp_div_up(total, kEmitSplit);
-    const uint32_t j0 = blockIdx.y * chunk, j1 = min(total, j0 + chunk);
+    const uint32_t j0 = ey * chunk, j1 = min(total, j0 + chunk);
     for (uint32_t j = j0 + threadIdx.x; j < j1; j += kMarchThreads) {
         uint32_t lo = 0, hi = kMarchThreads;  // largest ray r with off[r] <= j
         while (hi - lo > 1) {
