@@ -259,7 +259,10 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
 // through all points of level j before level j + 8, and its L2 holds one level
 // table at a time (two hashed fp16 tables are its whole 4 MiB). Same values.
 constexpr uint32_t kFwdLevelsPerBlock = 2;
-constexpr uint32_t kFwdGroupMajorMin = 1u << 19;
+#ifndef NGP_FWD_GROUP_MAJOR_MIN  // same-box A/B builds only (tools/variants.sh)
+#define NGP_FWD_GROUP_MAJOR_MIN (1u << 19)
+#endif
+constexpr uint32_t kFwdGroupMajorMin = NGP_FWD_GROUP_MAJOR_MIN;
 
 template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL = kFwdLevelsPerBlock>
 __global__ void __launch_bounds__(256)
