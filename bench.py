@@ -6,9 +6,12 @@
 One step = sample 4096 rays of a random training pose -> near/far ->
 march_rays_train -> hash-grid encode -> sigma FFMLP -> trunc_exp -> SH ->
 colour FFMLP -> composite -> MSE -> full backward -> Adam.
---engine fused (default): nerf/fused.py, the step as ~22 fused launches in
+--engine fused (default): nerf/fused.py, the step as 11 fused launches in
 one hipGraph; --engine autograd: nerf/train.py, the same step through the
 reference-API autograd Functions (torch glue ops between them).
+Per-launch device times (the roofline) come from HIP event-record nodes
+inside the graphs replayed in the timed region (a ring of --ring copies of
+the step graph), with the sample counts of those same steps.
 The density bitfield is the analytic Lego-like fixture (density-grid update
 excluded from the timed step as SURVEY §8(d) defines it; its cost is reported
 separately as `density_update_ms`). Rank 0 prints ONE JSON line.
@@ -35,14 +38,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (spec)
 
 
-# name -> (description, H, W, log2_hashmap_size, occupancy)
+# name -> (description, H, W, log2_hashmap_size, occupancy, bound, dt_gamma)
 WORKLOADS = {
     "lego": ("lego_800x800_train_step (synthetic analytic Lego, bound 1, 1 cascade, 128^3 bitfield fixture, "
-             "hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19, "boxes"),
+             "hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19, "boxes", 1, 0.0),
     "lego_dense": ("lego_800x800_dense_occupancy_train_step (synthetic Lego, bound 1, ball r=0.7 occupancy, "
-                   "hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19, "ball"),
+                   "hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19, "ball", 1, 0.0),
     "truck": ("truck_1920x1080_train_step (Config 5 single-GPU leg: synthetic scene at 1920x1080, bound 1, "
-              "hashgrid L16 C2 T2^22 = 39.6M entries, FFMLP 64-wide)", 1080, 1920, 22, "boxes"),
+              "hashgrid L16 C2 T2^22 = 39.6M entries, FFMLP 64-wide)", 1080, 1920, 22, "boxes", 1, 0.0),
+    "fox": ("fox_shaped_800x800_train_step (Config 3 shapes on the synthetic scene: bound 2, 2 cascades, "
+            "dt_gamma 1/128, desired_resolution 4096, hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19,
+            "boxes", 2, 1.0 / 128),
 }
 
 
@@ -53,7 +59,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--num_rays", type=int, default=4096)
     ap.add_argument("--no-graph", dest="graph", action="store_false")
-    ap.add_argument("--kernel-steps", type=int, default=10, help="instrumented steps for kernel timing")
+    ap.add_argument("--kernel-steps", type=int, default=10,
+                    help="eager instrumented steps for kernel timing (only without --ring / hipGraphs)")
+    ap.add_argument("--ring", type=int, default=16,
+                    help="copies of the step graph with event-record nodes, replayed in turn in the timed "
+                         "region; per-launch times are read from the last min(steps, ring) of them (0: plain "
+                         "graph, per-launch times from eager steps after the timed region)")
     ap.add_argument("--settle-steps", type=int, default=1000,
                     help="untimed steps after the warmup that bring the GPU to its sustained clock")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
@@ -62,7 +73,8 @@ def parse():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="lego",
                     help="lego: the headline (Config 2, Lego 800x800, box occupancy, ~19 samples/ray); "
                          "lego_dense: same with a ball occupancy (~80 samples/ray); "
-                         "truck: Config 5 single-GPU leg (1920x1080, log2T 22)")
+                         "truck: Config 5 single-GPU leg (1920x1080, log2T 22); "
+                         "fox: Config 3 shapes (bound 2, 2 cascades, dt_gamma 1/128)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="collective backend for N > 1: nccl (= RCCL, the measured path) or gloo "
                          "(host-staged; a rehearsal of the data-parallel step with every rank on the "
@@ -150,14 +162,17 @@ def main():
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield, sphere_bitfield
 
-    desc, img_h, img_w, log2T, occ = WORKLOADS[args.workload]
-    model = NeRFNetwork(bound=1, cuda_ray=True, density_thresh=10, log2_hashmap_size=log2T).to(dev)
+    desc, img_h, img_w, log2T, occ, bound, dt_gamma = WORKLOADS[args.workload]
+    model = NeRFNetwork(bound=bound, cuda_ray=True, density_thresh=10, log2_hashmap_size=log2T).to(dev)
     if world > 1:  # identical initial parameters on every rank
         for p in model.parameters():
             dist.broadcast(p.data, 0)
-    bits = torch.from_numpy(lego_bitfield() if occ == "boxes" else sphere_bitfield()).to(dev)
+    bits = (lego_bitfield(cascade=model.cascade, bound=float(bound)) if occ == "boxes"
+            else sphere_bitfield(cascade=model.cascade, bound=float(bound)))
+    bits = torch.from_numpy(bits).to(dev)
     model.density_bitfield.copy_(bits)
     data = SyntheticLego(dev, H=img_h, W=img_w, num_rays=args.num_rays)
+    args.dt_gamma = dt_gamma
     if args.engine == "fused":
         result = run_fused(args, model, data, bits, world, dev)
     else:
@@ -186,7 +201,7 @@ def run_autograd(args, model, data, bits, world, dev):
     from nerf.train import Trainer
 
     trainer = Trainer(model, data, lr=1e-2, iters=30000, fp16=True, update_density=False,
-                      distributed=world > 1)
+                      distributed=world > 1, dt_gamma=args.dt_gamma)
 
     # warm-up: first step sizes the sample buffer with a D2H sync (mean_count = 0
     # path of raymarching.py); afterwards mean_count is fixed from the measured
@@ -304,8 +319,8 @@ def run_autograd(args, model, data, bits, world, dev):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(dominant)[0],
-            "traffic_source": pmc_traffic(dominant)[1],
+            "traffic": pmc_traffic(dominant, args.workload)[0],
+            "traffic_source": pmc_traffic(dominant, args.workload)[1],
             "algorithmic_bytes_per_launch": int(dom_bytes),
             "avg_launch_ms": round(kernel_ms[dominant], 5),
         },
@@ -325,7 +340,7 @@ def run_fused(args, model, data, bits, world, dev):
     from nerf.fused import FusedTrainer
 
     # sample-buffer size: measured counts x 1.25 (mean_count, update_extra_state)
-    probe = FusedTrainer(model, data, M=args.num_rays * 64, distributed=world > 1)
+    probe = FusedTrainer(model, data, M=args.num_rays * 64, distributed=world > 1, dt_gamma=args.dt_gamma)
     counts = []
     for _ in range(4):
         probe.step()
@@ -338,10 +353,11 @@ def run_fused(args, model, data, bits, world, dev):
     probe.flush()  # data parallel: every rank's shard of the masters gathered back
     del probe
     torch.cuda.empty_cache()
-    ft = FusedTrainer(model, data, M=mean_count, distributed=world > 1)
+    ft = FusedTrainer(model, data, M=mean_count, distributed=world > 1, dt_gamma=args.dt_gamma)
     for _ in range(max(1, args.warmup)):
         ft.step()
     used_graph = False
+    timing = "eager"
     if args.graph:
         try:
             ft.capture()
@@ -351,6 +367,13 @@ def run_fused(args, model, data, bits, world, dev):
         except Exception as e:  # eager launches are the same kernels; record why
             print(f"[bench] graph capture failed, running eager: {e!r}", file=sys.stderr)
             ft.graph = None
+    if used_graph and args.ring > 0 and not ft.dp:
+        try:  # the timed region replays graphs that carry event-record nodes
+            ft.capture(warmup=1, ring=min(args.ring, 16))
+            timing = "graph_events"
+        except Exception as e:
+            print(f"[bench] timing-ring capture failed, per-launch times from eager steps: {e!r}",
+                  file=sys.stderr)
     torch.cuda.synchronize()
     # clock settle: the GPU raises its clocks only under sustained load. A
     # 20-step run right after 5 warmup steps measured 15.0M rays/s against
@@ -385,13 +408,21 @@ def run_fused(args, model, data, bits, world, dev):
     loss = ft.last_loss
 
     # ---------------- per-kernel device time (roofline) ----------------
-    # in-step device time of each launch (eager steps with events between launches)
-    kernel_ms = ft.timed_steps(args.kernel_steps)
-    rows = min(ft.sample_count(), ft.M)
-    grid_fwd_bytes, grid_bwd_bytes = 588 * rows, 1100 * rows  # SURVEY §8(d), per sample
-    dominant = max(("grid_encode_backward", "grid_encode_forward"), key=lambda k: kernel_ms[k])
-    dom_bytes = grid_bwd_bytes if dominant == "grid_encode_backward" else grid_fwd_bytes
-    achieved = dom_bytes / (kernel_ms[dominant] * 1e-3) / 1e9
+    # timing "graph_events": the event nodes of the last min(steps, ring) graph
+    # replays of the timed region, with those steps' own sample counts;
+    # "eager": eager steps after the timed region, events between launches
+    if timing == "graph_events":
+        kernel_ms, per_replay, counts = ft.ring_times(last=args.steps)
+    else:
+        ft.flush()
+        kernel_ms, per_replay, counts = ft.timed_steps(args.kernel_steps, with_counts=True)
+    counts = [min(int(c), ft.M) for c in counts]
+    rows = float(np.mean(counts))  # mean samples per step of the timed launches
+    # SURVEY §8(d) per-sample bytes; achieved = sum of bytes / sum of times
+    per_sample = {"grid_encode_backward": 1100, "grid_encode_forward": 588}
+    dominant = max(per_sample, key=lambda k: kernel_ms[k])
+    dom_bytes = per_sample[dominant] * rows
+    achieved = per_sample[dominant] * sum(counts) / (sum(per_replay[dominant]) * 1e-3) / 1e9
     mlp_ms = sum(v for k, v in kernel_ms.items() if k.startswith("ffmlp"))
     ffmlp_flops = 110592 * rows
     step_bytes = whole_step_bytes(rows, args.num_rays, sum(p.numel() for p in model.parameters()),
@@ -421,6 +452,9 @@ def run_fused(args, model, data, bits, world, dev):
             "hipgraph": used_graph,
             "settle_steps": args.settle_steps,
             "engine": "fused",
+            "dt_gamma": args.dt_gamma,
+            "cascade": int(model.cascade),
+            "bound": float(model.bound),
             "baseline_ref": "V100 97 it/s x 4096 rays (readme.md:211)",
         },
         "roofline": {
@@ -430,13 +464,17 @@ def run_fused(args, model, data, bits, world, dev):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(dominant)[0],
-            "traffic_source": pmc_traffic(dominant)[1],
+            "traffic": pmc_traffic(dominant, args.workload)[0],
+            "traffic_source": pmc_traffic(dominant, args.workload)[1],
             "algorithmic_bytes_per_launch": int(dom_bytes),
             "avg_launch_ms": round(kernel_ms[dominant], 5),
+            "timing": timing,
+            "launches_timed": len(counts),
+            "samples_per_timed_launch": counts,
+            "launch_ms_per_timed_step": [round(v, 5) for v in per_replay[dominant]],
         },
         "kernels_ms": {k: round(v, 5) for k, v in kernel_ms.items()},
-        "ffmlp_mfma": {"flops_per_step": ffmlp_flops, "ms": round(mlp_ms, 5),
+        "ffmlp_mfma": {"flops_per_step": int(ffmlp_flops), "ms": round(mlp_ms, 5),
                         "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
                         "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
         # SURVEY §8(d)'s secondary figure: the step's algorithmic bytes over the
@@ -500,20 +538,30 @@ def whole_step_bytes(samples, rays, n_params, n_table):
             + 52 * rays + 40 * samples + 76 * samples + 28 * n_params)
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, workload="lego"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/r*_step_kernels.json, written by tools/prof.sh +
-    tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes
-    over this same bench). FETCH_SIZE doubled per MI355X_MICROARCH.md's HBM
-    section (gfx950 tallies wide streaming reads at half); WRITE_SIZE as read."""
+    of the SAME workload (profiles/r*_step_kernels.json with its "workload"
+    key; summaries without one are the default Lego bench), written by
+    tools/prof.sh + tools/prof_summary.py from separate --pmc FETCH_SIZE /
+    WRITE_SIZE passes over this bench. FETCH_SIZE doubled per
+    MI355X_MICROARCH.md's HBM section (gfx950 tallies wide streaming reads at
+    half); WRITE_SIZE as read. None when no summary of this workload exists."""
     import glob
     def order(f):  # rNN then the tag: r01z < r01ab < r02a
         tag = os.path.basename(f).split("_")[0]
         return (int(tag[1:3]) if tag[1:3].isdigit() else 0, len(tag), tag)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_step_kernels.json")), key=order)
+    files = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_step_kernels*.json")), key=order):
+        try:
+            doc = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if doc.get("workload", "lego") == workload and doc.get("pmc_per_launch"):
+            files.append((f, doc))
     if not files:
         return None, None
-    pmc = json.load(open(files[-1])).get("pmc_per_launch", {})
+    pmc = files[-1][1]["pmc_per_launch"]
+    files = [files[-1][0]]
     fetch = write = 0
     found = False
     for pre in _PMC_KERNELS.get(kernel, ()):

@@ -456,7 +456,8 @@ int ngp_density_grid_ema_pack(float* grid, float* tmp_grid, uint32_t C, uint32_t
  * the noise of every cell (coords unused); partial=1: per cascade H^3/4
  * uniform cells then H^3/4 cells drawn from the cascade's occupied cells
  * (grid > 0, listed in cell order as torch.nonzero does, :555-558), with
- * their noise. Counter RNG over (seed, update, point). */
+ * their noise. Counter RNG over (seed ^ 0xd3a5b1c7, update, point): its own
+ * domain, apart from the training sampler's draws of the same seed. */
 size_t ngp_density_grid_draw_workspace_bytes(uint32_t C, uint32_t H);
 int ngp_density_grid_draw(const float* grid, uint32_t C, uint32_t H, uint32_t partial, uint32_t seed,
                           uint32_t update, int32_t* coords, float* noise, void* ws, size_t ws_bytes,

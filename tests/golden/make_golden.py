@@ -7,6 +7,16 @@ not):
   * MLP              — testing/test_ffmlp.py:11-43 (bias-free nn.Linear stack,
                        FFMLP layer semantics)
   * trunc_exp        — activation.py:5-18
+  * NeRFRenderer.run — nerf/renderer.py:126-254 (the pure-torch sampler and
+                       compositing: uniform samples, alphas, cumprod weights,
+                       weights_sum, depth, image with the white background),
+                       called with upsample_steps=0, perturb=False, on a stub
+                       `self` whose near/far is a torch slab test and whose
+                       density / colour are an analytic field; the samples the
+                       field saw and its outputs are recorded with the result
+  * get_rays         — nerf/utils.py:52-136 (+ custom_meshgrid :45-49): whole
+                       images (N=-1) and random pixel batches (N>0, seeded)
+  * nerf_matrix_to_ngp — nerf/provider.py:19-27
 
 Only the class / function definitions are extracted (ast) and executed; the
 scripts' module-level CUDA code never runs. Usage:
@@ -34,9 +44,23 @@ def extract(path, names):
     mod = ast.Module(body=keep, type_ignores=[])
     ns = {"torch": torch, "nn": nn, "F": F, "np": np, "math": __import__("math"),
           "Function": Function, "custom_fwd": torch.cuda.amp.custom_fwd,
-          "custom_bwd": torch.cuda.amp.custom_bwd}
+          "custom_bwd": torch.cuda.amp.custom_bwd, "pver": __import__("packaging.version").version}
     exec(compile(mod, path, "exec"), ns)
     return ns
+
+
+def extract_method(path, cls, name, ns_extra=None):
+    """Exec one method of a reference class as a plain function."""
+    src = open(path).read()
+    tree = ast.parse(src)
+    klass = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == cls)
+    fn = next(n for n in klass.body if isinstance(n, ast.FunctionDef) and n.name == name)
+    fn.decorator_list = []
+    mod = ast.Module(body=[fn], type_ignores=[])
+    ns = {"torch": torch, "np": np, "F": F}
+    ns.update(ns_extra or {})
+    exec(compile(mod, path, "exec"), ns)
+    return ns[name]
 
 
 def sh_fixture():
@@ -84,8 +108,94 @@ def trunc_exp_fixture():
                         y=y.detach().numpy(), gx=x.grad.numpy())
 
 
+def _slab_near_far(rays_o, rays_d, aabb, min_near):
+    """Stub raymarching.near_far_from_aabb for run() (torch, CPU): slab test,
+    near clamped to min_near (raymarching.cu:91-145)."""
+    inv = 1.0 / rays_d
+    t0 = (aabb[:3] - rays_o) * inv
+    t1 = (aabb[3:] - rays_o) * inv
+    near = torch.minimum(t0, t1).amax(-1).clamp(min=min_near)
+    far = torch.maximum(t0, t1).amin(-1)
+    return near, far
+
+
+def renderer_run_fixture():
+    """NeRFRenderer.run (renderer.py:126-254) on an analytic field: a Gaussian
+    density blob (sigma up to 40) and a position / direction dependent colour."""
+    import types
+    run = extract_method(os.path.join(REF, "nerf/renderer.py"), "NeRFRenderer", "run",
+                         {"raymarching": types.SimpleNamespace(near_far_from_aabb=_slab_near_far)})
+    rec = {}
+
+    def density(x):
+        rec["xyzs"] = x.detach().clone()
+        sigma = 40.0 * torch.exp(-((x - torch.tensor([0.1, -0.05, 0.0])) ** 2).sum(-1) / 0.18)
+        rec["sigma"] = sigma.detach().clone()
+        return {"sigma": sigma, "geo_feat": torch.zeros(x.shape[0], 15)}
+
+    def color(x, d, mask=None, geo_feat=None, **kw):
+        rgb = torch.sigmoid(torch.stack([3 * x[:, 0] + d[:, 1], 2 * x[:, 1] - d[:, 0], x[:, 2] + 0.5 * d[:, 2]], -1))
+        rec["rgb"] = rgb.detach().clone()
+        return rgb
+
+    bound = 1.0
+    stub = types.SimpleNamespace(
+        aabb_train=torch.tensor([-bound] * 3 + [bound] * 3), aabb_infer=torch.tensor([-bound] * 3 + [bound] * 3),
+        training=True, min_near=0.2, density_scale=1.0, bg_radius=-1, density=density, color=color)
+    g = torch.Generator().manual_seed(5)
+    N, T = 96, 128
+    cam = torch.tensor([0.3, -3.0, 0.8])
+    tgt = (torch.rand(N, 3, generator=g) - 0.5) * 1.2
+    rays_d = tgt - cam
+    rays_d = rays_d / rays_d.norm(dim=-1, keepdim=True)
+    rays_o = cam.expand(N, 3).contiguous()
+    with torch.no_grad():
+        out = run(stub, rays_o[None], rays_d[None], num_steps=T, upsample_steps=0, bg_color=None, perturb=False)
+    nears, fars = _slab_near_far(rays_o, rays_d, stub.aabb_train, stub.min_near)
+    np.savez_compressed(os.path.join(HERE, "renderer_run_reference.npz"), rays_o=rays_o.numpy(),
+                        rays_d=rays_d.numpy(), nears=nears.numpy(), fars=fars.numpy(), num_steps=np.int32(T),
+                        density_scale=np.float32(stub.density_scale), xyzs=rec["xyzs"].numpy(),
+                        sigma=rec["sigma"].numpy(), rgb=rec["rgb"].numpy(), image=out["image"][0].numpy(),
+                        weights_sum=out["weights_sum"].reshape(-1).numpy(), depth=out["depth"].reshape(-1).numpy())
+
+
+def get_rays_fixture():
+    ns = extract(os.path.join(REF, "nerf/utils.py"), {"get_rays", "custom_meshgrid"})
+    rng = np.random.default_rng(11)
+    poses = []
+    for _ in range(3):  # random rotations + translations, cam2world
+        q = np.linalg.qr(rng.standard_normal((3, 3)))[0]
+        p = np.eye(4)
+        p[:3, :3], p[:3, 3] = q, rng.standard_normal(3) * 2
+        poses.append(p)
+    poses = torch.from_numpy(np.stack(poses).astype(np.float32))
+    H, W = 24, 40
+    intr = np.array([37.5, 36.0, 20.3, 11.7], np.float32)
+    full = ns["get_rays"](poses, intr, H, W, -1)
+    torch.manual_seed(21)
+    part = ns["get_rays"](poses[:1], intr, H, W, 256)
+    np.savez_compressed(os.path.join(HERE, "get_rays_reference.npz"), poses=poses.numpy(), intrinsics=intr,
+                        H=np.int32(H), W=np.int32(W), rays_o=full["rays_o"].numpy(), rays_d=full["rays_d"].numpy(),
+                        seed=np.int32(21), N=np.int32(256), inds_part=part["inds"].numpy(),
+                        rays_o_part=part["rays_o"].numpy(), rays_d_part=part["rays_d"].numpy())
+
+
+def nerf_matrix_fixture():
+    ns = extract(os.path.join(REF, "nerf/provider.py"), {"nerf_matrix_to_ngp"})
+    rng = np.random.default_rng(12)
+    poses = rng.standard_normal((6, 4, 4)).astype(np.float32)
+    args = [(0.33, [0, 0, 0]), (0.8, [0, 0, 0]), (0.33, [0.1, -0.2, 0.3])]
+    out = np.stack([np.stack([ns["nerf_matrix_to_ngp"](p, scale=s, offset=o) for p in poses]) for s, o in args])
+    np.savez_compressed(os.path.join(HERE, "nerf_matrix_reference.npz"), poses=poses,
+                        scales=np.array([a[0] for a in args], np.float32),
+                        offsets=np.array([a[1] for a in args], np.float32), out=out)
+
+
 if __name__ == "__main__":
     sh_fixture()
     mlp_fixture()
     trunc_exp_fixture()
+    renderer_run_fixture()
+    get_rays_fixture()
+    nerf_matrix_fixture()
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

@@ -1,0 +1,159 @@
+"""Parity against fixtures produced by the reference's own Python
+(tests/golden/make_golden.py, run where /root/reference exists; the fixtures
+are data and travel, the reference does not):
+
+* renderer_run_reference.npz — NeRFRenderer.run (nerf/renderer.py:126-254) on
+  an analytic field, upsample_steps=0, perturb=False: the samples the field
+  saw, its sigma / rgb, and run()'s image, weights_sum and depth. The same
+  samples go through the oracle's and the HIP composite_rays_train_forward
+  (raymarching.cu:500-577) with T_thresh = 0 (no early stop, as run() has
+  none): image (+ the white background run() mixes in) and weights_sum
+  within 1e-5 of run()'s cumprod compositing, depth within 1e-5.
+* get_rays_reference.npz — get_rays (nerf/utils.py:52-136) for whole images
+  and a seeded random batch: this repo's torch get_rays (nerf/utils.py) and
+  the device sampler of the fused step (ngp_lego_rays, csrc/ngp_head.h
+  lego_ray) on the same poses / intrinsics / pixels.
+* nerf_matrix_reference.npz — nerf_matrix_to_ngp (nerf/provider.py:19-27).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLDEN, name)))
+
+
+def _run_samples(f):
+    """run()'s uniform samples (renderer.py:148-160, 206-207) restated with the
+    same torch ops: z_vals, clipped xyzs, deltas, and the normalised depths
+    (:226) as the composite kernel's accumulated real deltas."""
+    ro, rd = torch.from_numpy(f["rays_o"]), torch.from_numpy(f["rays_d"])
+    nears, fars = torch.from_numpy(f["nears"])[:, None], torch.from_numpy(f["fars"])[:, None]
+    T, N = int(f["num_steps"]), ro.shape[0]
+    z = torch.linspace(0.0, 1.0, T).unsqueeze(0).expand((N, T))
+    z_vals = nears + (fars - nears) * z
+    sample_dist = (fars - nears) / T
+    xyzs = ro.unsqueeze(-2) + rd.unsqueeze(-2) * z_vals.unsqueeze(-1)
+    aabb = torch.tensor([-1.0] * 3 + [1.0] * 3)
+    xyzs = torch.min(torch.max(xyzs, aabb[:3]), aabb[3:])
+    deltas = z_vals[..., 1:] - z_vals[..., :-1]
+    deltas = torch.cat([deltas, sample_dist * torch.ones_like(deltas[..., :1])], dim=-1)
+    ori = ((z_vals - nears) / (fars - nears)).clamp(0, 1)
+    real = torch.cat([ori[:, :1], ori[:, 1:] - ori[:, :-1]], -1)
+    d2 = torch.stack([deltas, real], -1).reshape(-1, 2).numpy().astype(np.float32)
+    rays = np.stack([np.arange(N), np.arange(N) * T, np.full(N, T)], -1).astype(np.int32)
+    return xyzs.reshape(-1, 3).numpy(), d2, rays
+
+
+def test_run_samples_restated_bit_exact():
+    f = _load("renderer_run_reference.npz")
+    xyzs, _, _ = _run_samples(f)
+    assert np.array_equal(xyzs.view(np.uint32), f["xyzs"].view(np.uint32))
+
+
+def _check_composite(f, ws, depth, image):
+    img = image + (1 - ws)[:, None]  # bg_color = 1 (renderer.py:237-240)
+    assert f["weights_sum"].max() > 0.5 and f["weights_sum"].min() < 0.5  # opaque and see-through rays
+    np.testing.assert_allclose(ws, f["weights_sum"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(img, f["image"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(depth, f["depth"], rtol=1e-5, atol=1e-5)
+
+
+def test_oracle_composite_matches_reference_run():
+    f = _load("renderer_run_reference.npz")
+    _, deltas, rays = _run_samples(f)
+    sigma = (f["sigma"] * f["density_scale"]).astype(np.float32)
+    ws, depth, image = oracle.composite_rays_train_forward(sigma, f["rgb"], deltas, rays, 0.0)
+    _check_composite(f, ws, depth, image)
+
+
+@pytest.mark.gpu
+def test_hip_composite_matches_reference_run(cuda):
+    import raymarching
+    f = _load("renderer_run_reference.npz")
+    _, deltas, rays = _run_samples(f)
+    sigma = torch.from_numpy((f["sigma"] * f["density_scale"]).astype(np.float32)).to(cuda)
+    rgbs = torch.from_numpy(f["rgb"]).to(cuda)
+    ws, depth, image = raymarching.composite_rays_train(sigma, rgbs, torch.from_numpy(deltas).to(cuda),
+                                                       torch.from_numpy(rays).to(cuda), 0.0)
+    _check_composite(f, ws.cpu().numpy(), depth.cpu().numpy(), image.cpu().numpy())
+
+
+def test_torch_get_rays_matches_reference():
+    from nerf.utils import get_rays
+    f = _load("get_rays_reference.npz")
+    poses = torch.from_numpy(f["poses"])
+    H, W = int(f["H"]), int(f["W"])
+    out = get_rays(poses, f["intrinsics"], H, W, -1)
+    np.testing.assert_array_equal(out["rays_o"].numpy(), f["rays_o"])
+    np.testing.assert_allclose(out["rays_d"].numpy(), f["rays_d"], rtol=0, atol=1e-6)
+    torch.manual_seed(int(f["seed"]))
+    part = get_rays(poses[:1], f["intrinsics"], H, W, int(f["N"]))
+    np.testing.assert_array_equal(part["inds"].numpy(), f["inds_part"])
+    np.testing.assert_allclose(part["rays_d"].numpy(), f["rays_d_part"], rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(part["rays_o"].numpy(), f["rays_o_part"])
+
+
+def test_nerf_matrix_to_ngp_matches_reference():
+    from nerf.provider import nerf_matrix_to_ngp
+    f = _load("nerf_matrix_reference.npz")
+    for k, (s, o) in enumerate(zip(f["scales"], f["offsets"])):
+        for j, p in enumerate(f["poses"]):
+            got = nerf_matrix_to_ngp(p, scale=float(s), offset=[float(v) for v in o])
+            np.testing.assert_array_equal(got, f["out"][k, j])
+
+
+def _mix32(x):
+    with np.errstate(over="ignore"):
+        x = np.asarray(x, np.uint32)
+        x = x ^ (x >> np.uint32(16)); x = x * np.uint32(0x7feb352d)
+        x = x ^ (x >> np.uint32(15)); x = x * np.uint32(0x846ca68b)
+        return x ^ (x >> np.uint32(16))
+
+
+def _rng_u32(seed, a, b, c):
+    """csrc/ngp_head.h rng_u32, restated in numpy uint32."""
+    with np.errstate(over="ignore"):
+        inner = _mix32(np.asarray(b, np.uint32) ^ _mix32(np.uint32(c) + np.uint32(0x85ebca6b)))
+        return _mix32(np.uint32(seed) ^ _mix32(np.uint32(a) + np.uint32(0x9e3779b9) * inner))
+
+
+@pytest.mark.gpu
+def test_device_sampler_matches_reference_get_rays(cuda):
+    """The fused step's sampler on the fixture's poses and intrinsics: each
+    ray equals the reference get_rays ray of the pixel and pose the counter
+    RNG picked (pose = rng(seed, draw, ~0, 0) % n_poses, pixel = rng(seed,
+    draw, ray, 1) % (H W))."""
+    import ctypes
+
+    import _ngp_native as nat
+    f = _load("get_rays_reference.npz")
+    H, W, n_poses = int(f["H"]), int(f["W"]), f["poses"].shape[0]
+    N, seed = 2048, 17
+    poses = torch.from_numpy(f["poses"]).to(cuda)
+    z = lambda *s: torch.zeros(*s, device=cuda)  # noqa: E731
+    rays_o, rays_d, rgba, bg = z(N, 3), z(N, 3), z(N, 4), z(N, 3)
+    nears, fars, noises = z(N), z(N), z(N)
+    counter = torch.zeros(2, dtype=torch.int32, device=cuda)
+    state = torch.zeros(nat.lib().ngp_fused_state_bytes(), dtype=torch.uint8, device=cuda)
+    nat.check(nat.lib().ngp_fused_state_init(nat.ptr(state), 1.0, nat.stream_of(state)), "state_init")
+    intr = (ctypes.c_float * 4)(*[float(v) for v in f["intrinsics"]])
+    box = (ctypes.c_float * 9)(-0.1, -0.1, -0.1, 0.1, 0.1, 0.1, 1, 1, 1)
+    aabb = (ctypes.c_float * 6)(-1, -1, -1, 1, 1, 1)
+    P = nat.ptr
+    for draw in range(3):
+        nat.check(nat.lib().ngp_lego_rays(P(poses), n_poses, intr, H, W, N, box, 1, aabb, 0.2, seed, P(state),
+                                          P(rays_o), P(rays_d), P(rgba), P(bg), P(nears), P(fars), P(noises),
+                                          P(counter), None, nat.stream_of(poses)), "lego_rays")
+        torch.cuda.synchronize()
+        pose = int(_rng_u32(seed, draw, 0xFFFFFFFF, 0) % np.uint32(n_poses))
+        pix = (_rng_u32(seed, draw, np.arange(N, dtype=np.uint32), 1) % np.uint32(H * W)).astype(np.int64)
+        np.testing.assert_array_equal(rays_o.cpu().numpy(), f["rays_o"][pose][pix])
+        np.testing.assert_allclose(rays_d.cpu().numpy(), f["rays_d"][pose][pix], rtol=0, atol=2e-6)

@@ -198,7 +198,11 @@ def _rng_u32(seed, a, b, c):
         return _mix32(np.uint32(seed) ^ _mix32(np.uint32(a) + np.uint32(0x9e3779b9) * inner))
 
 
+DENSITY_RNG_DOMAIN = 0xd3a5b1c7  # csrc/density_grid.hip kDensityRngDomain
+
+
 def _draws(seed, update, P, ppc, H, grid=None):
+    seed = np.uint32(seed ^ DENSITY_RNG_DOMAIN)
     p = np.arange(P, dtype=np.uint32)
     noise = np.stack([(_rng_u32(seed, update, p, 1 + j) >> np.uint32(8)).astype(np.float32) * np.float32(2 ** -24)
                       for j in range(3)], -1)

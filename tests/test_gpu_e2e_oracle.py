@@ -13,8 +13,10 @@ autocast casts restated). Two comparisons:
   per-sample sigma and RGB, the rendered image, the loss (north_star: 1e-3 rel)
   and the three parameter gradients.
 
-Configs: Config 2 (Lego, bound 1, one cascade, dt_gamma 0) and the Fox-shaped
-Config 3 (bound 2, two cascades, dt_gamma 1/128).
+Configs: Config 2 (Lego, bound 1, one cascade, dt_gamma 0), the Fox-shaped
+Config 3 (bound 2, two cascades, dt_gamma 1/128) and Config 5's single-GPU
+shapes (Truck: 1920x1080 images, L16 log2T 22 = 39,625,280 table entries, the
+binned backward's 1,024-bin levels with per-item flushes; bound 1).
 
 Tolerances: HIP matmuls accumulate in fp32 (MFMA) and the oracle in float64;
 both round every layer's output to fp16, so an output either matches bit for
@@ -33,17 +35,17 @@ from oracle.pipeline import amp_train_step
 pytestmark = pytest.mark.gpu
 
 
-def _setup(cuda, bound, dt_gamma, num_rays=1024, mean_count=30000):
+def _setup(cuda, bound, dt_gamma, log2T=19, hw=(800, 800), num_rays=1024, mean_count=30000):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield
     torch.manual_seed(0)
-    model = NeRFNetwork(bound=bound, cuda_ray=True, density_thresh=10).to(cuda)
+    model = NeRFNetwork(bound=bound, cuda_ray=True, density_thresh=10, log2_hashmap_size=log2T).to(cuda)
     with torch.no_grad():  # a non-trivial field: larger table values than the 1e-4 init
         model.encoder.embeddings.normal_(0, 0.05)
     bits = lego_bitfield(cascade=model.cascade, bound=float(bound))
     model.density_bitfield.copy_(torch.from_numpy(bits).to(cuda))
-    data = SyntheticLego(cuda, num_rays=num_rays)
+    data = SyntheticLego(cuda, H=hw[0], W=hw[1], num_rays=num_rays)
     M = mean_count + 128 - mean_count % 128
     return FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma)
 
@@ -109,12 +111,15 @@ def _oracle_inputs(ft):
                 T_thresh=ft.T_thresh, min_near=float(m.min_near), loss_scale=ft.scale)
 
 
-CONFIGS = [(1, 0.0), (2, 1 / 128)]
+# (bound, dt_gamma, log2T, (H, W)): Config 2, Config 3 (Fox-shaped), Config 5 (Truck)
+CONFIGS = [(1, 0.0, 19, (800, 800)), (2, 1 / 128, 19, (800, 800)), (1, 0.0, 22, (1080, 1920))]
+IDS = ["lego", "fox", "truck"]
 
 
-@pytest.mark.parametrize("bound,dt_gamma", CONFIGS)
-def test_fused_step_stages_match_oracle(cuda, bound, dt_gamma):
-    ft = _setup(cuda, bound, dt_gamma)
+@pytest.mark.parametrize("bound,dt_gamma,log2T,hw", CONFIGS, ids=IDS)
+def test_fused_step_stages_match_oracle(cuda, bound, dt_gamma, log2T, hw):
+    ft = _setup(cuda, bound, dt_gamma, log2T, hw)
+    assert ft.enc.embeddings.shape[0] == (39625280 if log2T == 22 else 6119864)
     n = _fused_batch(ft)
     assert n > 1000
     inp = _oracle_inputs(ft)
@@ -204,11 +209,11 @@ def test_fused_step_stages_match_oracle(cuda, bound, dt_gamma):
     assert np.all(gemb[gemb_ref == 0] == 0)  # nothing lands where no sample contributed
 
 
-@pytest.mark.parametrize("bound,dt_gamma", CONFIGS)
-def test_fused_step_end_to_end_matches_oracle(cuda, bound, dt_gamma):
+@pytest.mark.parametrize("bound,dt_gamma,log2T,hw", CONFIGS, ids=IDS)
+def test_fused_step_end_to_end_matches_oracle(cuda, bound, dt_gamma, log2T, hw):
     """north_star: rendered RGB / sigma within 1e-3 rel of the reference,
     sample counts / indices bit-exact; the oracle runs from the batch alone."""
-    ft = _setup(cuda, bound, dt_gamma)
+    ft = _setup(cuda, bound, dt_gamma, log2T, hw)
     n = _fused_batch(ft)
     ref = amp_train_step(**_oracle_inputs(ft))
     assert int(ref["counter"][0]) == n and np.array_equal(_np(ft.rays), ref["rays"])
@@ -239,4 +244,4 @@ def test_fused_step_end_to_end_matches_oracle(cuda, bound, dt_gamma):
         assert np.isfinite(g).all() and np.abs(want).max() > 0, what
         report[f"grad_{what}_rel"] = _rel(g, want)
         assert _rel(g, want) <= 5e-3, (what, _rel(g, want))
-    print(f"e2e vs oracle (bound {bound}):", report)
+    print(f"e2e vs oracle (bound {bound}, log2T {log2T}, {hw[1]}x{hw[0]}):", report)

@@ -385,6 +385,34 @@ def test_checkpoint_roundtrip_and_torch_formats(cuda):
     assert a.optimizer_steps == b.optimizer_steps and a.scale == b.scale
 
 
+def test_checkpoint_after_update_density_has_reference_bookkeeping(cuda):
+    """update_density does update_extra_state's bookkeeping (renderer.py:584,
+    593-596): mean_density = mean(clamp(grid, 0)), mean_count = int(mean of the
+    last min(16, local_step) batches' sample counts), local_step = 0; the
+    checkpoint carries those values, and a loaded checkpoint's values are kept."""
+    model, _, _, ft = _setup(cuda)
+    counts = []
+    for _ in range(5):
+        ft.step()
+        counts.append(ft.sample_count())
+    assert model.local_step == 5
+    ft.update_density()
+    assert model.local_step == 0
+    want_density = float(torch.mean(model.density_grid.clamp(min=0)).item())
+    ck = ft.checkpoint()
+    assert abs(ck["mean_density"] - want_density) <= 1e-6 * want_density and want_density > 0
+    assert ck["mean_count"] == int(sum(counts) / len(counts)), (ck["mean_count"], counts)
+    for _ in range(20):  # more than 16 batches since the update: the last 16 count
+        ft.step()
+        counts.append(ft.sample_count())
+    ft.update_density()
+    assert ft.mean_count == int(sum(counts[-16:]) / 16)
+    ck2 = ft.checkpoint()
+    ck2["mean_density"], ck2["mean_count"] = 12.5, 777
+    ft.load_checkpoint(ck2)
+    assert ft.mean_density == 12.5 and ft.mean_count == 777 and ft.checkpoint()["mean_count"] == 777
+
+
 def test_composite_loss_large_densities_match_serial(cuda):
     """The fused composite's prefix-sum transmittance against the reference's
     serial loop (raymarching.cu composite_rays_train_forward) at the densities a

@@ -1,0 +1,105 @@
+"""GPU, RCCL: the fused engine's data-parallel step over a one-rank `nccl`
+(= RCCL on ROCm) process group, in a spawned child process.
+
+FusedTrainer(distributed=True) takes the ZeRO-1 path at any world size: three
+hipGraphs, ngp_grad_guard, `reduce_scatter_tensor(op=AVG)` of the flat fp16
+gradient on RCCL's stream, the sharded Adam, the async
+`all_gather_into_tensor` of the fp16 forward copy overlapped with the next
+batch's sample + march, flush()'s all-gather of the fp32 masters, and the
+density update's MAX all-reduce. With one rank every collective is an
+identity, so the run must equal the single-process (non data-parallel) step
+bit for bit: parameters, Adam moments, GradScaler state, density grid and
+bitfield (reference hook: nerf/utils.py:325-327, the DDP wrap this replaces).
+This is the code path the driver's 8-GPU bench runs; here it executes RCCL on
+the one GPU of the box.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _trainer(dev, distributed):
+    from nerf.fused import FusedTrainer
+    from nerf.network_ff import NeRFNetwork
+    from nerf.provider import SyntheticLego, lego_bitfield
+    torch.manual_seed(0)
+    model = NeRFNetwork(bound=1, cuda_ray=True).to(dev)
+    with torch.no_grad():
+        model.encoder.embeddings.normal_(0, 0.05)
+    model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
+    return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, distributed=distributed)
+
+
+def _run_steps(ft):
+    for _ in range(3):  # eager
+        ft.step()
+    ft.capture(warmup=1)
+    for _ in range(4):  # graph replays (+ the collectives between them)
+        ft.step()
+    ft.update_density()  # flushes, then the density update (MAX all-reduce in dp)
+    for _ in range(2):
+        ft.step()
+    ft.flush()
+    torch.cuda.synchronize()
+    m1, m2 = ft._moments()
+    return dict(params=[p.detach().cpu().numpy() for p in ft.params],
+                m=m1[:ft._starts[-1] + ft.params[-1].numel()].cpu().numpy(),
+                v=m2[:ft._starts[-1] + ft.params[-1].numel()].cpu().numpy(),
+                steps=ft.optimizer_steps, scale=ft.scale, loss=ft.last_loss,
+                grid=ft.model.density_grid.cpu().numpy(), bits=ft.model.density_bitfield.cpu().numpy(),
+                mean_density=ft.mean_density, dp=ft.dp, nccl=ft._nccl)
+
+
+def _worker(port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "torch-ngp_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    try:
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        backend = dist.get_backend()
+        dp = _run_steps(_trainer(dev, True))
+        single = _run_steps(_trainer(dev, False))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put(("ok", backend, dp, single))
+    except Exception as e:  # report the failure to the parent instead of hanging it
+        import traceback
+        q.put(("error", repr(e), traceback.format_exc(), None))
+
+
+def test_rccl_world1_data_parallel_step_equals_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_free_port(), q))
+    p.start()
+    status, backend, dp, single = q.get(timeout=300)
+    p.join(timeout=60)
+    assert status == "ok", (backend, dp)
+    assert p.exitcode == 0
+    assert backend == "nccl" and dp["dp"] and dp["nccl"] and not single["dp"]
+    assert dp["steps"] == single["steps"] >= 8 and dp["scale"] == single["scale"]
+    assert np.isfinite(dp["loss"]) and dp["loss"] == single["loss"]
+    for a, b in zip(dp["params"], single["params"]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(dp["m"].view(np.uint32), single["m"].view(np.uint32))
+    assert np.array_equal(dp["v"].view(np.uint32), single["v"].view(np.uint32))
+    assert np.array_equal(dp["grid"].view(np.uint32), single["grid"].view(np.uint32))
+    assert np.array_equal(dp["bits"], single["bits"]) and dp["mean_density"] == single["mean_density"]

@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, smoke, the bench line (+ the dense-occupancy
-# and Config-5 truck workloads), rocprof stats + PMC.
+# One GPU-box pass: parity tests, smoke, the bench line (+ the dense-occupancy,
+# Config-5 truck and Config-3 fox workloads), rocprof stats + PMC.
 # usage (on the box): bash tools/gpu_round.sh TAG [noprof]
 set -eo pipefail
 TAG=${1:-r01}
@@ -17,4 +17,6 @@ timeout -k 10 200 python -u bench.py --no-cpu --workload lego_dense > gpurun_out
     2> gpurun_out/$TAG/bench_dense.err
 timeout -k 10 200 python -u bench.py --no-cpu --workload truck > gpurun_out/$TAG/bench_truck.json \
     2> gpurun_out/$TAG/bench_truck.err
+timeout -k 10 200 python -u bench.py --no-cpu --workload fox > gpurun_out/$TAG/bench_fox.json \
+    2> gpurun_out/$TAG/bench_fox.err
 if [ "$2" != "noprof" ]; then bash tools/prof.sh $TAG/prof; fi

@@ -41,11 +41,15 @@ def main(tag, out=None):
     sel = starts[-steps:]
     per = collections.defaultdict(list)
     spans = []
+    bwd_spans = []  # grid backward: start of k_grid_bwd_bin to end of k_grid_bin_accum (what the bench's events bracket)
     for i in sel:
         j = next(k for k in range(i, len(rows)) if "k_grid_bin_accum" in name(k)) + 1
         seg = rows[i:j]
         t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
         spans.append((t1 - t0) / 1e3)
+        b0 = next((r for r in seg if "k_grid_bwd_bin" in r["Kernel_Name"]), None)
+        if b0 is not None:
+            bwd_spans.append((int(seg[-1]["End_Timestamp"]) - int(b0["Start_Timestamp"])) / 1e3)
         cnt = collections.Counter()
         for r in seg:
             key = short(r["Kernel_Name"])
@@ -67,13 +71,39 @@ def main(tag, out=None):
             # forward (2M points), a few outliers among the step's launches
             v = sorted(v)
             pmc.setdefault(k, {})[which + "_bytes"] = round(v[len(v) // 2])
+    # the bench line printed by the profiled command (samples of its timed steps)
+    bench = None
+    try:
+        for line in open(os.path.join(tag, "trace.log")):
+            if line.startswith("{") and '"metric"' in line:
+                bench = json.loads(line)
+    except OSError:
+        pass
+    bwd_kernels = sum(v for k, v in kern.items() if k.startswith(("k_grid_bwd_bin", "k_grid_bin_accum")))
     res = {
+        "workload": os.environ.get("WORKLOAD", "lego"),
         "steps": len(sel),
         "step_span_us_mean": round(sum(spans) / len(spans), 1),
         "kernel_busy_us_per_step": round(busy, 1),
         "kernels_us_per_step": dict(sorted(kern.items(), key=lambda t: -t[1])),
         "pmc_per_launch": pmc,
     }
+    if bwd_spans:
+        res["grid_backward_us"] = {"kernels_sum": round(bwd_kernels, 2),
+                                   "span_bin_start_to_accum_end": round(sum(bwd_spans) / len(bwd_spans), 2)}
+    if bench is not None and bwd_spans:
+        # the roofline recomputed from this trace: SURVEY 8(d) 1100 B per sample
+        # x the mean samples of the bench's timed steps / the trace's time
+        r = bench.get("roofline", {})
+        counts = r.get("samples_per_timed_launch") or [bench["config"]["samples_per_step"]]
+        samples = sum(counts) / len(counts)
+        res["roofline_recomputed"] = {
+            "samples_per_step": round(samples, 1),
+            "frac_from_kernels_sum": round(1100 * samples / (bwd_kernels * 1e-6) / 8e12, 4),
+            "frac_from_span": round(1100 * samples / (res["grid_backward_us"]["span_bin_start_to_accum_end"] * 1e-6)
+                                    / 8e12, 4),
+            "bench_frac": r.get("frac"), "bench_avg_launch_ms": r.get("avg_launch_ms"),
+            "bench_timing": r.get("timing")}
     txt = json.dumps(res, indent=1)
     print(txt)
     if out:

@@ -247,8 +247,14 @@ k_density_occ_write(const float* __restrict__ grid, uint32_t H3, const uint32_t*
     if (o) occ[(size_t)cas * H3 + before + below] = i;
 }
 
-// Draws of the fused trainer's update (counter RNG over (seed, update, point,
-// stream)): full mode (occ null) draws only the noise of every cell;
+// The density draws' own RNG domain: the seed is XORed with this tag, so an
+// update's draws are not functions of the same 32-bit values as the training
+// sampler's (ngp_head.h lego_ray: rng_u32(seed, draw, ray, 0..5) with the same
+// seed on rank 0).
+constexpr uint32_t kDensityRngDomain = 0xd3a5b1c7u;
+
+// Draws of the fused trainer's update (counter RNG over (seed ^ domain, update,
+// point, stream)): full mode (occ null) draws only the noise of every cell;
 // partial mode per cascade N = ppc / 2 uniform cells, then N cells drawn from
 // the occupied list (uniform cells again where the cascade has none, as the
 // reference's occ[randint(0, 0)] cannot), each with its noise.
@@ -333,6 +339,6 @@ extern "C" int ngp_density_grid_draw(const float* grid, uint32_t C, uint32_t H, 
         k_density_occ_scan<<<C, 1024, 0, st>>>(bcount, nblk, total);
         k_density_occ_write<<<dim3(nblk, C), kOccBlock, 0, st>>>(grid, H3, bcount, occ);
     }
-    k_density_draw<<<ngp_div_up(P, 256), 256, 0, st>>>(P, ppc, H, seed, update, occ, total, coords, noise);
+    k_density_draw<<<ngp_div_up(P, 256), 256, 0, st>>>(P, ppc, H, seed ^ kDensityRngDomain, update, occ, total, coords, noise);
     return ngp_check_launch("density_grid_draw");
 }

@@ -27,8 +27,12 @@ class _grid_encode(Function):
     @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, inputs, embeddings, offsets, per_level_scale, base_resolution,
                 calc_grad_inputs=False, gridtype=0, align_corners=False, interpolation=0):
-        # inputs: [B, D] float in [0, 1]; embeddings: [sO, C]; offsets: [L + 1] int
-        inputs = inputs.contiguous()
+        # inputs: [B, D] float in [0, 1]; embeddings: [sO, C]; offsets: [L + 1] int.
+        # The kernel reads float coordinates (gridencoder.cu:466); float64 inputs
+        # (testing/test_hashgrid_grad.py:51, which the reference kernel rejects)
+        # are read as float32 here, and their gradient is returned as float64.
+        in_dtype = inputs.dtype
+        inputs = inputs.contiguous() if in_dtype == torch.float32 else inputs.float().contiguous()
         B, D = inputs.shape
         L = offsets.shape[0] - 1
         C = embeddings.shape[1]
@@ -49,6 +53,7 @@ class _grid_encode(Function):
         ctx.save_for_backward(inputs, embeddings, offsets, dy_dx)
         ctx.dims = [B, D, C, L, S, H, gridtype, interpolation]
         ctx.align_corners = align_corners
+        ctx.in_dtype = in_dtype
         return outputs
 
     @staticmethod
@@ -69,7 +74,7 @@ class _grid_encode(Function):
                                          C, L, S, H, dy_dx, grad_inputs, gridtype, align_corners,
                                          interpolation)
         if dy_dx is not None:
-            grad_inputs = grad_inputs.to(inputs.dtype)
+            grad_inputs = grad_inputs.to(ctx.in_dtype)
         return grad_inputs, grad_embeddings, None, None, None, None, None, None, None
 
 

@@ -74,7 +74,10 @@ class FusedTrainer:
         self.lr, self.iters, self.betas, self.eps = float(lr), int(iters), betas, float(eps)
         self.growth_interval, self.seed = int(growth_interval), int(seed)
         self.density_seed = int(seed)  # the density-grid draws are the same on every rank
-        self.world = dist.get_world_size() if distributed and dist.is_initialized() else 1
+        # dp: the data-parallel (ZeRO-1) step with its collectives, also at
+        # world size 1 (a one-rank group runs the same RCCL calls)
+        self.dp = bool(distributed and dist.is_initialized())
+        self.world = dist.get_world_size() if self.dp else 1
         if self.world > 1:
             self.seed += 7919 * dist.get_rank()
         self.enc = enc
@@ -115,7 +118,7 @@ class FusedTrainer:
         # shard: 64-element aligned chunk per rank (world * chunk >= the layout)
         self.chunk = chunk = int(-(-int(starts[-1]) // (64 * W)) * 64)
         self.total = total = chunk * W
-        self.rank = dist.get_rank() if W > 1 else 0
+        self.rank = dist.get_rank() if self.dp else 0
         self.lo, self.hi = self.rank * chunk, (self.rank + 1) * chunk
         self.flat_param = z(total)
         self.flat_grad = z(total, dtype=h)
@@ -134,7 +137,7 @@ class FusedTrainer:
         # Adam moments of this rank's shard only (ZeRO-1); world 1: everything
         self.exp_avg, self.exp_avg_sq = z(chunk), z(chunk)
         # the averaged gradient shard (reduce-scatter output); world 1: the flat grad itself
-        self.grad_shard = self.flat_grad if W == 1 else z(chunk, dtype=h)
+        self.grad_shard = z(chunk, dtype=h) if self.dp else self.flat_grad
         self._offsets_host = (ctypes.c_int32 * enc.offsets.numel())(*enc.offsets.cpu().tolist())
         gb = nat.lib().ngp_grid_encode_backward_fused_workspace_bytes(
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
@@ -176,8 +179,8 @@ class FusedTrainer:
         # half as it loads it (the same values autocast's cast gives), so Adam
         # does not write an fp16 copy of the table (2 of its 28 B / parameter).
         # Data parallel: the fp16 copy is what the all-gather moves.
-        self.table32 = W == 1 and os.environ.get("NGP_FUSED_TABLE16") != "1"
-        self._merge_head = W == 1 and os.environ.get("NGP_FUSED_SPLIT_HEAD") != "1"
+        self.table32 = not self.dp and os.environ.get("NGP_FUSED_TABLE16") != "1"
+        self._merge_head = not self.dp and os.environ.get("NGP_FUSED_SPLIT_HEAD") != "1"
         # one launch for the sigma + colour forwards where ngp_nerf_forward covers
         # the shapes (NGP_FUSED_SPLIT_FWD=1 keeps two launches, for A/B and tests)
         sn_, cn_ = self.sig_net, self.col_net
@@ -197,13 +200,14 @@ class FusedTrainer:
             half=_vp_array([nat.ptr(self.flat_half) + 2 * (self.lo + a) if hv else None for a, _, hv in sec]),
             sizes=(ctypes.c_uint64 * len(sec))(*[n for _, n, _ in sec]),
             n=len(sec))
-        self._nccl = W > 1 and dist.get_backend() == "nccl"
+        self._nccl = self.dp and dist.get_backend() == "nccl"
         # GradScaler's inf check is made by the kernels that write the grads
         # (grid backward, MLP dW reduce) into this flag: the optimizer's found-inf
         # flag (world 1) or the data-parallel guard's per-rank flag
-        self._inf_flag = nat.lib().ngp_fused_inf_flag(nat.ptr(self.state), int(W > 1))
+        self._inf_flag = nat.lib().ngp_fused_inf_flag(nat.ptr(self.state), int(self.dp))
         self.graph = None
-        self._events = None
+        self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
+        self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
         self._pending = False  # gradients of the last forward/backward not yet applied
 
@@ -273,7 +277,7 @@ class FusedTrainer:
         nat.check(lib.ngp_nerf_density_forward(P_(d["enc"]), P_(self.w_half[1]), None, n, sn.input_dim, sn.hidden_dim,
                                                sn.num_layers, float(m.density_scale), P_(d["idx"]) + 4 * lo,
                                                P_(d["tmp"]), s), "nerf_density_forward")
-        if self.world > 1:
+        if self.dp:
             if self._nccl:
                 dist.all_reduce(d["tmp"], op=dist.ReduceOp.MAX)
             else:
@@ -285,32 +289,89 @@ class FusedTrainer:
                   "density_grid_ema_pack")
         m.iter_density += 1
         self.refresh_occupancy()
+        # the reference's bookkeeping after an update (renderer.py:584, 593-596),
+        # kept on the device (no host sync) and resolved on read: mean_density
+        # from the update's stats, mean_count from the last min(16, local_step)
+        # batches' sample counts, then local_step = 0
+        self._mean_density_pending = True
+        total = min(16, int(m.local_step))
+        if total > 0:
+            self._mean_count_pending = self._recent_count_mean(total)
+        m.local_step = 0
+
+    def _recent_count_mean(self, total):
+        """int(mean) of the sample counts of the last `total` batches, as a
+        device scalar (no host sync)."""
+        return torch.div(self._recent_counts(total).sum(), total, rounding_mode="floor")
 
     @property
     def mean_density(self):
-        """mean_density of the last update_density (torch.mean(...).item(), :584)."""
-        if self._dens is None:
-            return float(self.model.mean_density)
-        return float(np.float32(self._dens["stats"].item() / self.model.density_grid.numel()))
+        """model.mean_density, after the last update_density's value
+        (torch.mean(...).item(), :584) has been read back from the device."""
+        if getattr(self, "_mean_density_pending", False):
+            self.model.mean_density = float(np.float32(self._dens["stats"].item() / self.model.density_grid.numel()))
+            self._mean_density_pending = False
+        return float(self.model.mean_density)
+
+    @property
+    def mean_count(self):
+        """model.mean_count, after the last update_density's value (:593-595)."""
+        mc = getattr(self, "_mean_count_pending", None)
+        if mc is not None:
+            self.model.mean_count = int(mc.item())
+            self._mean_count_pending = None
+        return int(self.model.mean_count)
 
     # ------------------------------------------------------------------ step
     def _tick(self, name):
-        """Event after each launch while `timed_steps` instruments eager steps."""
+        """Event after each launch while `timed_steps` instruments eager steps
+        or `capture(ring=...)` records a timing graph (inside a capture the
+        event is an event-record node of the graph: `external`)."""
         if self._events is not None:
-            ev = torch.cuda.Event(enable_timing=True)
+            ev = torch.cuda.Event(enable_timing=True, external=self._capturing)
             ev.record()
             self._events.append((name, ev))
 
-    def timed_steps(self, k):
+    def _recent_counts(self, n):
+        """Sample counts of the last n batches (oldest first) as a device
+        tensor: the newest is still in `counter`, batch `it` was recorded in
+        step_counter slot it % 16 when batch it + 1 was drawn (n <= 16)."""
+        assert 1 <= n <= 16
+        draw = self.state.view(torch.int32)[self._S_DRAW].long()
+        k = torch.arange(n - 1, 0, -1, device=self.dev)
+        old = self.model.step_counter[(draw - 1 - k) & 15, 0].long()
+        return torch.cat([old, self.counter[:1].long()])
+
+    def ring_times(self, last=None):
+        """Per-phase device time of the last replays of the timing ring
+        (`capture(ring=R)`; the events are nodes of the replayed graphs, so
+        these are the steps of the timed region themselves), with the sample
+        count of each of those steps. Returns (per-phase mean ms, per-replay
+        ms of each phase, per-replay sample counts), oldest replay first."""
+        n = min(self._ring_i, len(self._ring), last or len(self._ring))
+        assert n > 0, "no ring replays yet"
+        torch.cuda.synchronize()
+        order = [(self._ring_i - n + j) % len(self._ring) for j in range(n)]
+        per = {}
+        for r in order:
+            ev = self._ring[r][1]
+            for (_, a), (name, b) in zip(ev[:-1], ev[1:]):
+                per.setdefault(name, []).append(a.elapsed_time(b))
+        counts = self._recent_counts(n).cpu().tolist()
+        return {k: float(np.mean(v)) for k, v in per.items()}, per, counts
+
+    def timed_steps(self, k, with_counts=False):
         """Device time per phase (ms, mean over k eager steps), measured with
         events on the launch stream between consecutive launches: each phase's
         kernels run in the cache state of a real step (the previous step's
         optimizer has streamed the parameters through), unlike back-to-back
         repeats of one kernel. A spin kernel ahead of each step lets the host
         queue every launch first, so no phase includes host launch gaps. The
-        phases run serially here (the all-gather is waited for right away)."""
+        phases run serially here (the all-gather is waited for right away).
+        with_counts: also the per-step times of each phase and the steps'
+        sample counts (mean, per-step, counts)."""
         self.flush()
-        acc = {}
+        acc, per, counts = {}, {}, []
         for i in range(k):
             torch.cuda.synchronize()
             torch.cuda._sleep(4_000_000)  # keep the GPU busy while the host queues the step
@@ -325,9 +386,12 @@ class FusedTrainer:
             self.model.local_step += 1
             torch.cuda.synchronize()
             ev, self._events = self._events, None
+            counts.append(self.sample_count())
             for (_, a), (name, b) in zip(ev[:-1], ev[1:]):
                 acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
-        return {n: v / k for n, v in acc.items()}
+                per.setdefault(name, []).append(a.elapsed_time(b))
+        mean = {n: v / k for n, v in acc.items()}
+        return (mean, per, counts) if with_counts else mean
 
     def _body(self, pending):
         """One step's launches (world 1): [optimizer(previous grads)] ->
@@ -367,7 +431,7 @@ class FusedTrainer:
     # gradient once and the forward copy once (what one all-reduce moves) and
     # sweeps 1/world of the Adam state.
     def _reduce(self):
-        if self.world == 1:
+        if not self.dp:
             return
         # the backward's kernels set the per-rank flag: no scan (n = 0)
         nat.check(nat.lib().ngp_grad_guard(nat.ptr(self.flat_grad), 0, self.chunk, self.world,
@@ -383,7 +447,7 @@ class FusedTrainer:
 
     def _gather_half(self, wait):
         """All-gather of the fp16 forward copy; returns the pending work."""
-        if self.world == 1:
+        if not self.dp:
             return None
         shard = self.flat_half[self.lo:self.hi]
         work = None
@@ -400,7 +464,7 @@ class FusedTrainer:
         return work
 
     def _gather_masters(self):
-        if self.world == 1:
+        if not self.dp:
             return
         shard = self.flat_param[self.lo:self.hi]
         if self._nccl:
@@ -418,7 +482,7 @@ class FusedTrainer:
         m, d, pk = self.model, self.data, self._pk
         # data parallel: the fp16 weights are still being all-gathered while
         # the batch is drawn, so the networks are packed in _network instead
-        nets = 2 if self.world == 1 else 0
+        nets = 0 if self.dp else 2
         nat.check(lib.ngp_fused_step_head(P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N,
                                           self._boxes, self._nboxes, self._aabb, float(m.min_near), self.seed,
                                           P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
@@ -464,7 +528,7 @@ class FusedTrainer:
                                               P(self.enc_out), M, cnt, *grid_args[:-1], 0, s), "grid_encode_fused")
         self._tick("grid_encode_forward")
         sn, cn, img, pk = self.sig_net, self.col_net, self.mlp_img, self._pk
-        if self.world > 1:  # after the all-gather of the fp16 forward copy (see _sample)
+        if self.dp:  # after the all-gather of the fp16 forward copy (see _sample)
             chk(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
         if self._one_fwd:  # both networks in one launch (ngp_nerf_forward)
             chk(lib.ngp_nerf_forward(P(self.enc_out), P(img[0]), P(img[1]), M, cnt, sn.hidden_dim, sn.num_layers,
@@ -517,10 +581,10 @@ class FusedTrainer:
         # world 1 zeroes the grads here; data parallel: the shard is the reduce-scatter's
         # output and the flat gradient is cleared after the collective read it
         args = (o["n"], o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
-                self.betas[1], self.eps, self.iters, int(self.world == 1), 1.0)
+                self.betas[1], self.eps, self.iters, int(not self.dp), 1.0)
         # inside a step (world 1) the found-inf flag was set by the backward's kernels;
         # otherwise (flush, direct calls, the averaged shard) the grads are swept
-        mode = _PRECHECKED if defer and self.world == 1 else _SCAN
+        mode = _PRECHECKED if defer and not self.dp else _SCAN
         if defer:
             chk(lib.ngp_fused_optimizer_update(*args, mode, P(self.state), s), "fused_optimizer_update")
         else:
@@ -531,8 +595,11 @@ class FusedTrainer:
     def step(self):
         """One training iteration (the optimizer half lags by one step, see
         the module docstring)."""
-        if self.world == 1:
-            if self.graph is not None and self._pending:
+        if not self.dp:
+            if self._ring and self._pending:  # timing ring: graphs with event nodes
+                self._ring[self._ring_i % len(self._ring)][0].replay()
+                self._ring_i += 1
+            elif self.graph is not None and self._pending:
                 self.graph.replay()
             else:
                 self._body(self._pending)
@@ -570,15 +637,34 @@ class FusedTrainer:
             self._gather_masters()
             self._pending = False
 
-    def capture(self, warmup=2):
+    def capture(self, warmup=2, ring=0):
         """hipGraph(s) of the step body. World 1: one graph (optimizer of the
         previous gradients, sample, march, network). Data parallel: three
         (optimizer | sample + march | network); the collectives between them
-        stay outside."""
+        stay outside. ring=R (world 1): R further copies of the body graph
+        with an event-record node after each launch; step() then replays
+        them in turn (instead of the plain graph) and `ring_times` reads the
+        per-launch device times of the last R replays."""
         for _ in range(max(1, warmup)):
             self.step()
         torch.cuda.synchronize()
-        if self.world == 1:
+        if ring and not self.dp:
+            self._ring, self._ring_i = [], 0
+            try:
+                for _ in range(ring):
+                    g = torch.cuda.CUDAGraph()
+                    self._events, self._capturing = [], True
+                    with torch.cuda.graph(g):
+                        self._tick("start")
+                        self._body(True)
+                    self._ring.append((g, self._events))
+            except Exception:
+                self._ring = []
+                raise
+            finally:
+                self._events, self._capturing = None, False
+            return
+        if not self.dp:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._body(True)
@@ -627,7 +713,7 @@ class FusedTrainer:
 
     def _moments(self):
         """Full-length Adam moments (data parallel: all-gathered from the shards)."""
-        if self.world == 1:
+        if not self.dp:
             return self.exp_avg, self.exp_avg_sq
         full = []
         for t in (self.exp_avg, self.exp_avg_sq):
@@ -657,7 +743,7 @@ class FusedTrainer:
         state = {"epoch": epoch, "global_step": it,
                  "stats": stats if stats is not None else {"loss": [], "valid_loss": [], "results": [],
                                                            "checkpoints": [], "best_result": None},
-                 "mean_count": m.mean_count, "mean_density": m.mean_density,
+                 "mean_count": self.mean_count, "mean_density": self.mean_density,
                  "model": m.state_dict(),
                  "fused": {"draw": int(si[self._S_DRAW])}}
         if full:
@@ -695,6 +781,7 @@ class FusedTrainer:
             return
         m.load_state_dict(state["model"], strict=False)  # copies into the flat buffers' views
         self.sync_half()
+        self._mean_count_pending, self._mean_density_pending = None, False
         m.mean_count = state.get("mean_count", m.mean_count)
         m.mean_density = state.get("mean_density", m.mean_density)
         self.refresh_occupancy()

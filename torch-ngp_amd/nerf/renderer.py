@@ -321,7 +321,12 @@ class NeRFRenderer(nn.Module):
                                                     float(self.bound), nat.ptr(xyzs), nat.ptr(indices), st),
                   "density_grid_points")
         tmp = self._density_tmp()
-        self._query_density(xyzs, indices, tmp)
+        # one cascade's worth of points per query at most (the reference queries
+        # one block of one cascade at a time, :535): the scatter-max into tmp is
+        # order-independent, so the slices give the same grid
+        step = H ** 3
+        for a in range(0, P, step):
+            self._query_density(xyzs[a:a + step], indices[a:a + step], tmp)
         stats = torch.empty(1, dtype=torch.float64, device=dev)
         nat.check(nat.lib().ngp_density_grid_ema_pack(nat.ptr(self.density_grid), nat.ptr(tmp), C, H,
                                                       float(decay), float(self.density_thresh), nat.ptr(stats),
