@@ -35,7 +35,7 @@ from oracle.pipeline import amp_train_step
 pytestmark = pytest.mark.gpu
 
 
-def _setup(cuda, bound, dt_gamma, log2T=19, hw=(800, 800), num_rays=1024, mean_count=30000):
+def _setup(cuda, bound, dt_gamma, log2T=19, hw=(800, 800), num_rays=1024, mean_count=80000):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield
@@ -79,7 +79,9 @@ def _fused_batch(ft):
     ft.noises.zero_()
     ft._forward_backward()
     torch.cuda.synchronize()
-    return int(ft.counter[0])
+    n = int(ft.counter[0])
+    assert n <= ft.M, (n, ft.M)  # every sample fits the buffer (none dropped)
+    return n
 
 
 def _composite_image(ft):
