@@ -449,6 +449,24 @@ def mlp_backward(grad, x, weights, input_dim, output_dim, hidden_dim, num_layers
     return grad_inputs, np.concatenate([g.reshape(-1) for g in gws])
 
 
+def mlp_backward_magnitude(grad, x, weights, input_dim, output_dim, hidden_dim, num_layers, act=0):
+    """The absolute-value twin of mlp_backward's grad_inputs: |grad| pushed
+    back through |W| with the fp16 forward's activation masks. Entry (b, i)
+    is the sum of the absolute terms grad_inputs[b, i] is made of, the scale
+    of its rounding error: an fp16 rounding of any delta on the way moves the
+    result by at most 2^-11 of this (per rounded layer). ReLU / None only."""
+    assert act in (0, 6)
+    mats = mlp_layers(np.abs(np.asarray(weights, np.float16).astype(np.float64)), input_dim, output_dim,
+                      hidden_dim, num_layers)
+    _, hs = mlp_forward(x, weights, input_dim, output_dim, hidden_dim, num_layers, act)
+    d = np.abs(np.asarray(grad, np.float16).astype(np.float64))
+    for li in range(len(mats) - 1, -1, -1):
+        g_in = d @ mats[li]
+        if li == 0:
+            return g_in
+        d = g_in * (hs[li - 1] > 0) if act == 0 else g_in
+
+
 def trunc_exp(x):
     return np.exp(np.asarray(x, np.float32))
 
