@@ -276,6 +276,52 @@ int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bou
                                    uint32_t interp, const int32_t* offsets_host, void* workspace,
                                    size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
                                    void* stream);
+/* Fused Adam over the hash table (world 1; torch.optim.Adam + GradScaler of
+ * nerf/utils.py:975-978 / main_nerf.py:194 on the table, inside the grid
+ * backward). The table's fp32 parameters and Adam moments are double
+ * buffered: buffers [state cur] are current, an update writes the other ones
+ * and the step's GradScaler bookkeeping makes them current unless the step is
+ * skipped (an inf/nan anywhere), so a skip leaves the table untouched as
+ * torch's does. The accumulate applies Adam to every slice it owns (one work
+ * unit per bin of a zeroed grad: the slice's exact sums, rounded to the fp16
+ * grad torch would see, unscaled) and tags the bin in `done`; the optimizer
+ * entries (*_db) then update the other slices from the fp16 grad buffer.
+ * slices: nslices x (first entry, entries, bin or 0xffffffff) covering the
+ * table (ngp_grid_table_slices); done: one word per bin (zero-filled once). */
+typedef struct ngp_adam_table {
+    float* params[2];
+    float* exp_avg[2];
+    float* exp_avg_sq[2];
+    void* grad;               /* fp16 [sum_T * C] */
+    uint32_t* done;
+    const uint32_t* slices;   /* device */
+    uint32_t nslices;
+    uint32_t channels;        /* C (2) */
+    float lr, beta1, beta2, eps;
+    int32_t iters;            /* LambdaLR: lr * 0.1 ** min(epoch / iters, 1) */
+} ngp_adam_table;
+/* The table's slices (host array of 3 * max_slices words): the binned
+ * backward's bins in bin order, then the levels it does not bin in slices of
+ * <= 4096 entries (bin 0xffffffff). Returns their number, or < 0. */
+int ngp_grid_table_slices(const int32_t* offsets_host, uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S,
+                          uint32_t H, int32_t align_corners, uint32_t* slices_host, uint32_t max_slices);
+/* ngp_grid_encode_forward_fused reading table[*sel] (sel: ngp_fused_table_select). */
+int ngp_grid_encode_forward_fused_sel(const float* xyz, float bound, const void* table0, const void* table1,
+                                      const int32_t* sel, int32_t emb_dtype, const int32_t* offsets,
+                                      void* outputs, uint32_t B, const int32_t* count, uint32_t D, uint32_t C,
+                                      uint32_t L, float S, uint32_t H, uint32_t gridtype, int32_t align_corners,
+                                      uint32_t interp, int32_t out_layout, void* stream);
+/* ngp_grid_encode_backward_fused (grad_layout must carry NGP_GRID_GRAD_ZEROED)
+ * with Adam applied by the accumulate to the slices it owns (see
+ * ngp_adam_table); grad_embeddings == at->grad receives only the other
+ * slices' grads. state: the fused step's StepState. */
+int ngp_grid_encode_backward_fused_adam(const void* grad, const float* xyz, float bound,
+                                        const int32_t* offsets, void* grad_embeddings, uint32_t B,
+                                        const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
+                                        uint32_t H, uint32_t gridtype, int32_t align_corners,
+                                        uint32_t interp, const int32_t* offsets_host, void* workspace,
+                                        size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
+                                        const ngp_adam_table* at, void* state, void* stream);
 /* Weight-fragment images (forward + transposed, per matmul) of n networks in
  * one launch; image k needs ngp_ffmlp_image_bytes of its network. The
  * forward/backward *_rows calls below take the image (nullable: the weights
@@ -354,6 +400,13 @@ int ngp_nerf_composite_loss(const float* sigma, const void* color_out, const voi
  * reads; local != 0: the data-parallel guard's per-rank flag), for the
  * nonfinite arguments of the grid backward and the MLP reduce. */
 int32_t* ngp_fused_inf_flag(void* state, int32_t local);
+/* The state's current-table word (ngp_adam_table double buffer). */
+int32_t* ngp_fused_table_select(void* state);
+/* out fp16 [entries * C] = half(params[cur]) of the double-buffered table. */
+int ngp_fused_table_to_half(const ngp_adam_table* at, const void* state, void* out, uint64_t n, void* stream);
+/* Make buffer 0 current (copy buffer 1's params / moments over it when it is
+ * the current one) and set cur = 0: host read-outs then see buffer 0. */
+int ngp_fused_table_normalize(const ngp_adam_table* at, void* state, uint64_t n, void* stream);
 /* Adam (+ GradScaler inf check/unscale/update, LambdaLR 0.1^(epoch/iters))
  * over n_tensors fp32 params with fp16 grads; half_params[k] (nullable) is
  * refreshed with half(p) after the update; grads are zeroed when zero_grads;
@@ -408,6 +461,32 @@ int ngp_fused_optimizer_update_head(int32_t n_tensors, float* const* params, voi
                                     float* rays_d, float* rgba, float* bg, float* nears, float* fars,
                                     float* noises, int32_t* counter, int32_t* step_counter, void* clear,
                                     uint32_t clear_bytes, void* stream);
+
+/* The three optimizer entries above with the hash table double buffered and
+ * updated by the grid backward (ngp_adam_table): the tensor lists hold the
+ * other parameters (the MLPs, updated in place as before); the table's slices
+ * the accumulate did not update are updated here, from at->grad, into the
+ * other buffer, which the bookkeeping then makes current (skipped steps: not). */
+int ngp_fused_optimizer_step_db(int32_t n_tensors, float* const* params, void* const* grads,
+                                float* const* exp_avg, float* const* exp_avg_sq, void* const* half_params,
+                                const uint64_t* sizes, float lr, float beta1, float beta2, float eps,
+                                int32_t iters, int32_t zero_grads, float grad_mult, float growth_factor,
+                                float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
+                                uint32_t num_rays, const int32_t* counter, int32_t* step_counter,
+                                const float* loss_ray, void* state, const ngp_adam_table* at, void* stream);
+int ngp_fused_optimizer_update_db(int32_t n_tensors, float* const* params, void* const* grads,
+                                  float* const* exp_avg, float* const* exp_avg_sq, void* const* half_params,
+                                  const uint64_t* sizes, float lr, float beta1, float beta2, float eps,
+                                  int32_t iters, int32_t zero_grads, float grad_mult, int32_t scaler_enabled,
+                                  void* state, const ngp_adam_table* at, void* stream);
+int ngp_fused_optimizer_update_head_db(
+    int32_t n_tensors, float* const* params, void* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+    void* const* half_params, const uint64_t* sizes, float lr, float beta1, float beta2, float eps, int32_t iters,
+    int32_t zero_grads, float grad_mult, int32_t scaler_enabled, void* state, const float* poses, uint32_t n_poses,
+    const float* intrinsics4, uint32_t H, uint32_t W, uint32_t N, const float* boxes, int32_t nboxes,
+    const float* aabb6, float min_near, uint32_t seed, float* rays_o, float* rays_d, float* rgba, float* bg,
+    float* nears, float* fars, float* noises, int32_t* counter, int32_t* step_counter, void* clear,
+    uint32_t clear_bytes, const ngp_adam_table* at, void* stream);
 
 /* Data-parallel GradScaler guard for the sharded optimizer (nerf/fused.py,
  * world > 1), run on each rank's own fp16 gradient before the averaging

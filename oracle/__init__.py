@@ -449,22 +449,39 @@ def mlp_backward(grad, x, weights, input_dim, output_dim, hidden_dim, num_layers
     return grad_inputs, np.concatenate([g.reshape(-1) for g in gws])
 
 
-def mlp_backward_magnitude(grad, x, weights, input_dim, output_dim, hidden_dim, num_layers, act=0):
-    """The absolute-value twin of mlp_backward's grad_inputs: |grad| pushed
-    back through |W| with the fp16 forward's activation masks. Entry (b, i)
-    is the sum of the absolute terms grad_inputs[b, i] is made of, the scale
-    of its rounding error: an fp16 rounding of any delta on the way moves the
-    result by at most 2^-11 of this (per rounded layer). ReLU / None only."""
-    assert act in (0, 6)
-    mats = mlp_layers(np.abs(np.asarray(weights, np.float16).astype(np.float64)), input_dim, output_dim,
-                      hidden_dim, num_layers)
-    _, hs = mlp_forward(x, weights, input_dim, output_dim, hidden_dim, num_layers, act)
-    d = np.abs(np.asarray(grad, np.float16).astype(np.float64))
-    for li in range(len(mats) - 1, -1, -1):
-        g_in = d @ mats[li]
+def mlp_backward_error_bound(grad, x, weights, input_dim, output_dim, hidden_dim, num_layers):
+    """Per-element error scale of mlp_backward's grad_inputs for a kernel that
+    accumulates in fp32 instead of float64 (ReLU hidden layers). Returns
+    (mag, flip):
+      * mag: |grad| pushed back through |W| with the fp16 forward's ReLU masks,
+        the sum of the absolute terms each grad_input is made of; an fp16
+        rounding of a delta on the way moves the result by at most 2^-11 of it
+        per rounded layer;
+      * flip: what ReLU units whose pre-activation sits within the accumulation
+        error of zero (|z| <= 2^-14 sum|terms| + 2^-24: fp32 vs float64 sums,
+        and fp16's flush of tiny positives to zero) can add when their mask
+        differs -- their whole delta, pushed back through |W|.
+    A grad_input within  layers * 2^-11 * mag + flip  (+ the fp16 ulps of the
+    value) of the oracle is consistent with it."""
+    st = np.float16
+    W = mlp_layers(np.asarray(weights, st).astype(np.float64), input_dim, output_dim, hidden_dim, num_layers)
+    A = [np.abs(w) for w in W]
+    h = np.asarray(x, st).astype(np.float64)
+    hs, amb = [], []
+    for li in range(len(W) - 1):
+        z, za = h @ W[li].T, np.abs(h) @ A[li].T
+        amb.append(np.abs(z) <= 2.0 ** -14 * za + 2.0 ** -24)
+        h = np.maximum(z, 0).astype(st).astype(np.float64)
+        hs.append(h)
+    D = np.abs(np.asarray(grad, st).astype(np.float64))
+    F = np.zeros_like(D)
+    for li in range(len(W) - 1, -1, -1):
+        G, FG = D @ A[li], F @ A[li]
         if li == 0:
-            return g_in
-        d = g_in * (hs[li - 1] > 0) if act == 0 else g_in
+            return G, FG
+        opened = (hs[li - 1] > 0) | amb[li - 1]
+        F = FG * opened + G * amb[li - 1]
+        D = G * opened
 
 
 def trunc_exp(x):

@@ -60,10 +60,9 @@ def _rel(a, b):
 
 
 def _close16(got, ref, what, min_equal=0.98, mag=None):
-    """mag (backward input grads): oracle.mlp_backward_magnitude, the sum of
-    |terms| of each value; every fp16 rounding of a delta on the way (one per
-    layer) may move the value by 2^-11 of it, so 2^-11 x layers x mag is
-    added to the tolerance (sums that cancel to far below their terms)."""
+    """mag (backward input grads): the error scale of oracle.mlp_backward_error_bound
+    (fp16 roundings of the deltas and ReLU units at the edge of zero), added
+    to the tolerance."""
     got = np.asarray(got, np.float16)
     ref = np.asarray(ref, np.float16)
     assert got.shape == ref.shape, what
@@ -194,14 +193,16 @@ def test_fused_step_stages_match_oracle(cuda, bound, dt_gamma, log2T, hw):
     # ---- colour MLP backward: geo-feature grads into g_h[:, 1:16], dW
     gh_full = _np(ft.g_h)[:n]
     gcin_ref, gwc_ref = oracle.mlp_backward(gc[:n], cin, inp["w_color16"], 32, 16, 64, 3)
-    mag_c = 4 * 2.0 ** -11 * oracle.mlp_backward_magnitude(gc[:n], cin, inp["w_color16"], 32, 16, 64, 3)
+    mag_c, flip_c = oracle.mlp_backward_error_bound(gc[:n], cin, inp["w_color16"], 32, 16, 64, 3)
+    mag_c = 4 * 2.0 ** -11 * mag_c + flip_c
     _close16(gh_full[:, 1:16], gcin_ref[:, 16:31], "color mlp grad_inputs", mag=mag_c[:, 16:31])
     gw_color = _np(ft.grads[2]).astype(np.float64)
     assert _rel(gw_color, gwc_ref) <= 1e-3, _rel(gw_color, gwc_ref)
     # ---- sigma MLP backward: encoding grads ([L, M, 2]) and dW
     genc = _np(ft.g_enc).reshape(16, ft.M, 2)[:, :n].transpose(1, 0, 2).reshape(n, 32)
     genc_ref, gws_ref = oracle.mlp_backward(gh_full, enc, inp["w_sigma16"], 32, 16, 64, 2)
-    mag_s = 3 * 2.0 ** -11 * oracle.mlp_backward_magnitude(gh_full, enc, inp["w_sigma16"], 32, 16, 64, 2)
+    mag_s, flip_s = oracle.mlp_backward_error_bound(gh_full, enc, inp["w_sigma16"], 32, 16, 64, 2)
+    mag_s = 3 * 2.0 ** -11 * mag_s + flip_s
     _close16(genc, genc_ref, "sigma mlp grad_inputs", mag=mag_s)
     gw_sigma = _np(ft.grads[1]).astype(np.float64)
     assert _rel(gw_sigma, gws_ref) <= 1e-3, _rel(gw_sigma, gws_ref)

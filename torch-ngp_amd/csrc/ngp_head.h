@@ -191,29 +191,16 @@ struct AdamArgs {
 constexpr uint32_t kAdamThreads = 256, kAdamChunk = kAdamThreads * 8;
 NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const AdamArgs& aa, uint32_t blk,
                         uint32_t nblk, uint32_t tid) {
-    // GradScaler checks the UNSCALED grads: once the scale has backed off so far
-    // that 1/scale is inf, every element (0 * inf = NaN) is non-finite and the
-    // step is skipped, which the checks of the scaled fp16 grads cannot see
-    const float inv_scale = (float)(1.0 / (double)st->scale) * aa.grad_mult;
-    const bool inv_bad = !__builtin_isfinite(inv_scale);
-    const bool skip = st->found_inf != 0 || inv_bad;
+    const ngp_step::AdamConsts ac = ngp_step::adam_consts(st, aa.base_lr, aa.beta1, aa.beta2, aa.iters,
+                                                          aa.grad_mult);
+    const bool skip = st->found_inf != 0 || ac.inv_bad;
     if (blk == 0 && tid == 0) {
-        if (inv_bad) st->found_inf = 1;  // the scaler update backs off, as torch's would
+        if (ac.inv_bad) st->found_inf = 1;  // the scaler update backs off, as torch's would
         if (aa.defer_end) st->end_pending = 1;  // read by k_step_head only
     }
-    const int32_t step = st->adam_step + 1;
-    const double lr = (double)aa.base_lr * pow(0.1, fmin((double)st->epoch / (double)aa.iters, 1.0));
-    const double bc1 = 1.0 - pow((double)aa.beta1, step);
-    const double bc2 = 1.0 - pow((double)aa.beta2, step);
-    const float step_size = (float)(lr / bc1);
-    const float inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
     typedef _Float16 half4 __attribute__((ext_vector_type(4)));
     auto adam1 = [&](float& p, float& m, float& v, float gh) {
-        const float gk = gh * inv_scale;
-        m = m + (1.0f - aa.beta1) * (gk - m);
-        v = v * aa.beta2 + (1.0f - aa.beta2) * gk * gk;
-        const float denom = sqrtf(v) * inv_bc2_sqrt + aa.eps;
-        p = p - step_size * (m / denom);
+        ngp_step::adam_update(p, m, v, gh, ac, aa.beta1, aa.beta2, aa.eps);
     };
     const uint64_t total = tl.start[tl.n];
     const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;

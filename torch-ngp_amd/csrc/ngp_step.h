@@ -21,9 +21,46 @@ struct StepState {
     int32_t lego_done;     // k_lego_rays' finished-block count (last block bumps draw)
     int32_t local_inf;     // data parallel: this rank's own grads held an inf/nan (k_guard_*)
     int32_t end_pending;   // an optimizer update whose GradScaler/LR bookkeeping is deferred to k_step_head
-    int32_t pad3[3];
+    int32_t cur;           // double-buffered table (fused Adam): which of the two p/m/v buffers is current
+    int32_t flip_pending;  // the pending update wrote the other buffer: step_end makes it current unless skipped
+    int32_t pad3;
 };
 
+
+// ---- Adam (torch.optim.Adam, weight_decay 0) on an unscaled fp16 grad -------
+// Shared by the optimizer sweeps (ngp_head.h) and the grid backward's fused
+// Adam (gridencoder.hip), so both compute bit-identical updates.
+struct AdamConsts {
+    float inv_scale;     // 1 / GradScaler scale (x grad_mult)
+    float step_size;     // lr_t / bias_correction1
+    float inv_bc2_sqrt;  // 1 / sqrt(bias_correction2)
+    bool inv_bad;        // 1 / scale is not finite: GradScaler skips
+};
+// step = adam_step + 1, LambdaLR lr = base_lr * 0.1 ** min(epoch / iters, 1)
+NGP_DEV AdamConsts adam_consts(const StepState* __restrict__ st, float base_lr, float beta1, float beta2,
+                               int32_t iters, float grad_mult) {
+    AdamConsts c;
+    // GradScaler checks the UNSCALED grads: once the scale has backed off so far
+    // that 1/scale is inf, every element (0 * inf = NaN) is non-finite and the
+    // step is skipped, which the checks of the scaled fp16 grads cannot see
+    c.inv_scale = (float)(1.0 / (double)st->scale) * grad_mult;
+    c.inv_bad = !__builtin_isfinite(c.inv_scale);
+    const int32_t step = st->adam_step + 1;
+    const double lr = (double)base_lr * pow(0.1, fmin((double)st->epoch / (double)iters, 1.0));
+    const double bc1 = 1.0 - pow((double)beta1, step);
+    const double bc2 = 1.0 - pow((double)beta2, step);
+    c.step_size = (float)(lr / bc1);
+    c.inv_bc2_sqrt = 1.0f / (float)sqrt(bc2);
+    return c;
+}
+NGP_DEV void adam_update(float& p, float& m, float& v, float gh, const AdamConsts& c, float beta1, float beta2,
+                         float eps) {
+    const float gk = gh * c.inv_scale;
+    m = m + (1.0f - beta1) * (gk - m);
+    v = v * beta2 + (1.0f - beta2) * gk * gk;
+    const float denom = sqrtf(v) * c.inv_bc2_sqrt + eps;
+    p = p - c.step_size * (m / denom);
+}
 
 struct ScalerArgs {
     float growth_factor, backoff_factor;
@@ -59,6 +96,10 @@ NGP_DEV void step_end_block(StepState* __restrict__ st, const ScalerArgs& sa, co
         }
     }
     if (!inf) st->adam_step += 1;
+    // fused Adam (double-buffered table): the update went to the other buffer,
+    // which becomes current; a skipped step keeps the current one untouched
+    if (st->flip_pending && !inf) st->cur ^= 1;
+    st->flip_pending = 0;
     st->epoch += 1;
     if (step_counter) {
         const int slot = st->iter % 16;
