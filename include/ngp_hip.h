@@ -293,6 +293,7 @@ typedef struct ngp_adam_table {
     float* exp_avg[2];
     float* exp_avg_sq[2];
     void* grad;               /* fp16 [sum_T * C] */
+    uint64_t size;            /* sum_T * C: values per buffer */
     uint32_t* done;
     const uint32_t* slices;   /* device */
     uint32_t nslices;

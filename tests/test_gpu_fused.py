@@ -15,21 +15,21 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0):
+def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0, fused_adam=None, occ="boxes"):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
-    from nerf.provider import SyntheticLego, lego_bitfield
+    from nerf.provider import SyntheticLego, lego_bitfield, sphere_bitfield
     torch.manual_seed(0)
     model = NeRFNetwork(bound=bound, cuda_ray=True, density_thresh=10).to(cuda)
     with torch.no_grad():  # a non-trivial field: larger table values than the 1e-4 init
         model.encoder.embeddings.normal_(0, 0.05)
-    bits = lego_bitfield(cascade=model.cascade, bound=float(bound))
+    bits = (lego_bitfield if occ == "boxes" else sphere_bitfield)(cascade=model.cascade, bound=float(bound))
     model.density_bitfield.copy_(torch.from_numpy(bits).to(cuda))
     ref = copy.deepcopy(model)
     data = SyntheticLego(cuda, num_rays=num_rays)
     M = mean_count + 128 - mean_count % 128  # what run_cuda's align=128 makes of mean_count
     ref.mean_count = mean_count
-    ft = FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma)
+    ft = FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma, fused_adam=fused_adam)
     return model, ref, data, ft
 
 
@@ -80,7 +80,8 @@ def test_lego_sampler(cuda):
 # shape (bound 2, two cascades, dt_gamma 1/128: the serially marched rays)
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
 def test_fused_forward_backward_matches_autograd(cuda, bound, dt_gamma):
-    model, ref, data, ft = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
+    # fused_adam off: every table grad is materialised (test_fused_adam_* checks the fused update)
+    model, ref, data, ft = _setup(cuda, bound=bound, dt_gamma=dt_gamma, fused_adam=False)
     assert model.cascade == (1 if bound == 1 else 2)
     ft._sample()
     ft.noises.zero_()  # the autograd call below marches with perturb=False
@@ -103,7 +104,7 @@ def test_fused_forward_backward_matches_autograd(cuda, bound, dt_gamma):
 
 
 def test_fused_optimizer_matches_torch_adam_and_scaler(cuda):
-    model, ref, data, ft = _setup(cuda)
+    model, ref, data, ft = _setup(cuda, fused_adam=False)
     ft._sample()
     ft._forward_backward()
     torch.cuda.synchronize()
@@ -183,6 +184,7 @@ def test_pipelined_steps_match_serial_steps(cuda):
         b._sample()
         b._forward_backward()
         b._optimizer()
+    b.flush()  # (the current buffer of the fused-Adam table made buffer 0, as a.flush() did)
     torch.cuda.synchronize()
     for x, y in zip(a.params, b.params):
         assert torch.equal(x.detach(), y.detach())
@@ -411,6 +413,76 @@ def test_checkpoint_after_update_density_has_reference_bookkeeping(cuda):
     ck2["mean_density"], ck2["mean_count"] = 12.5, 777
     ft.load_checkpoint(ck2)
     assert ft.mean_density == 12.5 and ft.mean_count == 777 and ft.checkpoint()["mean_count"] == 777
+
+
+def _fused_adam_run(ft):
+    for _ in range(3):  # eager
+        ft.step()
+    ft.capture(warmup=1)
+    for _ in range(5):  # graph replays
+        ft.step()
+    ft.flush()
+    ft.state.view(torch.float32)[0] = 2.0 ** 40  # the next two steps overflow: skipped, scale backs off
+    ft.step()
+    ft.step()
+    ft.flush()
+    assert ft.scale == 2.0 ** 38
+    ft.state.view(torch.float32)[0] = 4096.0
+    ft.update_density()
+    for _ in range(4):
+        ft.step()
+    ft.flush()
+    torch.cuda.synchronize()
+    m1, m2 = ft._moments()
+    return ([p.detach().clone() for p in ft.params], m1.clone(), m2.clone(), ft.optimizer_steps, ft.scale,
+            ft.last_loss, ft.model.density_bitfield.clone())
+
+
+@pytest.mark.parametrize("bound,dt_gamma,num_rays,occ", [(1, 0.0, 1024, "boxes"), (2, 1 / 128, 1024, "boxes"),
+                                                         (1, 0.0, 4096, "ball")], ids=["lego", "fox", "dense"])
+def test_fused_adam_equals_unfused(cuda, bound, dt_gamma, num_rays, occ):
+    """The table's Adam inside the grid backward (fused_adam: double-buffered
+    p / m / v, the accumulate updates the slices it owns, the step's optimizer
+    launch the rest, the bookkeeping makes the new buffer current) against the
+    unfused optimizer over materialised fp16 table grads: bit-identical
+    parameters, Adam moments, scaler state and loss, through eager steps, graph
+    replays, two overflowing (skipped) steps, a density update and more steps.
+    The dense case (4096 rays through a ball: bins of the coarse levels hold
+    several work units) covers the bins finished through their int64 slot."""
+    mc = 400000 if occ == "ball" else 30000
+    _, _, _, a = _setup(cuda, num_rays=num_rays, mean_count=mc, bound=bound, dt_gamma=dt_gamma, fused_adam=True,
+                        occ=occ)
+    _, _, _, b = _setup(cuda, num_rays=num_rays, mean_count=mc, bound=bound, dt_gamma=dt_gamma, fused_adam=False,
+                        occ=occ)
+    assert a.fused_adam and not b.fused_adam
+    ra, rb = _fused_adam_run(a), _fused_adam_run(b)
+    assert ra[3] == rb[3] >= 10 and ra[4] == rb[4] and ra[5] == rb[5]
+    for x, y, what in zip(ra[0], rb[0], ("table", "sigma", "color")):
+        ne = (x.view(torch.int32) != y.view(torch.int32))
+        assert not ne.any(), (what, int(ne.sum()), float((x - y).abs().max()))
+    for x, y, what in ((ra[1], rb[1], "exp_avg"), (ra[2], rb[2], "exp_avg_sq")):
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32)), what
+    assert torch.equal(ra[6], rb[6])
+    assert int(a.grads[0].abs().sum()) == 0  # every table grad left cleared for the next step
+    if occ == "ball":  # ~330K samples: level 0's two bins get ~35K items each (3 work units)
+        assert a.sample_count() > 250000
+
+
+def test_grid_backward_is_deterministic(cuda):
+    """The binned backward sums every bin exactly (int64 fixed point), also
+    the bins several work units share (their partial sums meet in an int64
+    slot): two backward passes of one batch give bit-identical table grads."""
+    _, _, _, ft = _setup(cuda, num_rays=4096, mean_count=400000, fused_adam=False, occ="ball")
+    ft._sample()
+    ft._forward_backward()
+    g1 = ft.grads[0].clone()
+    n = ft.sample_count()
+    ft.flat_grad.zero_()
+    ft.grid_ws[:ft._grid_counter_bytes].zero_()  # the bin cursors (the step head clears them in a step)
+    ft._network()
+    torch.cuda.synchronize()
+    assert n > 250000 and g1.abs().sum() > 0
+    assert torch.equal(g1.view(torch.int16), ft.grads[0].view(torch.int16))
 
 
 def test_composite_loss_large_densities_match_serial(cuda):

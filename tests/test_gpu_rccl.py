@@ -44,19 +44,30 @@ def _trainer(dev, distributed):
     return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, distributed=distributed)
 
 
+def _snap(ft):
+    ft.flush()
+    torch.cuda.synchronize()
+    return [p.detach().cpu().numpy().copy() for p in ft.params]
+
+
 def _run_steps(ft):
-    for _ in range(3):  # eager
+    phases = {}
+    ft.step()
+    phases["step1"] = _snap(ft)
+    for _ in range(2):  # eager
         ft.step()
+    phases["eager3"] = _snap(ft)
     ft.capture(warmup=1)
     for _ in range(4):  # graph replays (+ the collectives between them)
         ft.step()
+    phases["graphs"] = _snap(ft)
     ft.update_density()  # flushes, then the density update (MAX all-reduce in dp)
     for _ in range(2):
         ft.step()
     ft.flush()
     torch.cuda.synchronize()
     m1, m2 = ft._moments()
-    return dict(params=[p.detach().cpu().numpy() for p in ft.params],
+    return dict(phases=phases, params=[p.detach().cpu().numpy() for p in ft.params],
                 m=m1[:ft._starts[-1] + ft.params[-1].numel()].cpu().numpy(),
                 v=m2[:ft._starts[-1] + ft.params[-1].numel()].cpu().numpy(),
                 steps=ft.optimizer_steps, scale=ft.scale, loss=ft.last_loss,
@@ -97,9 +108,17 @@ def test_rccl_world1_data_parallel_step_equals_single_process():
     assert backend == "nccl" and dp["dp"] and dp["nccl"] and not single["dp"]
     assert dp["steps"] == single["steps"] >= 8 and dp["scale"] == single["scale"]
     assert np.isfinite(dp["loss"]) and dp["loss"] == single["loss"]
-    for a, b in zip(dp["params"], single["params"]):
-        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    for ph in dp["phases"]:  # first phase where the runs part, and by how much
+        for k, (a, b) in enumerate(zip(dp["phases"][ph], single["phases"][ph])):
+            ne = a.view(np.uint32) != b.view(np.uint32)
+            assert not ne.any(), (ph, ["table", "sigma", "color"][k], int(ne.sum()),
+                                  float(np.abs(a - b).max()), np.argwhere(ne)[:4].tolist())
+    ng = dp["grid"].view(np.uint32) != single["grid"].view(np.uint32)
+    assert not ng.any(), ("density grid", int(ng.sum()), float(np.abs(dp["grid"] - single["grid"]).max()))
+    assert np.array_equal(dp["bits"], single["bits"]) and dp["mean_density"] == single["mean_density"]
+    for k, (a, b) in enumerate(zip(dp["params"], single["params"])):
+        ne = a.view(np.uint32) != b.view(np.uint32)
+        assert not ne.any(), ("final", ["table", "sigma", "color"][k], int(ne.sum()), float(np.abs(a - b).max()),
+                              np.argwhere(ne)[:4].tolist())
     assert np.array_equal(dp["m"].view(np.uint32), single["m"].view(np.uint32))
     assert np.array_equal(dp["v"].view(np.uint32), single["v"].view(np.uint32))
-    assert np.array_equal(dp["grid"].view(np.uint32), single["grid"].view(np.uint32))
-    assert np.array_equal(dp["bits"], single["bits"]) and dp["mean_density"] == single["mean_density"]

@@ -113,10 +113,31 @@ SIGNATURES = {
     "ngp_density_grid_ema_pack": [c_vp, c_vp, c_u32, c_u32, c_f32, ctypes.c_double, c_vp, c_vp, c_vp],
     "ngp_density_grid_draw_workspace_bytes": [c_u32, c_u32],
     "ngp_density_grid_draw": [c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_sz, c_vp],
+    # fused table Adam (ngp_adam_table, double-buffered hash table)
+    "ngp_grid_table_slices": [c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32, c_vp, c_u32],
+    "ngp_grid_encode_forward_fused_sel": [c_vp, c_f32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32,
+                                          c_u32, c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_i32, c_vp],
+    "ngp_grid_encode_backward_fused_adam": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
+                                            c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_i32, c_vp,
+                                            c_vp, c_vp, c_vp],
+    "ngp_fused_table_select": [c_vp],
+    "ngp_fused_table_to_half": [c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp],
+    "ngp_fused_table_normalize": [c_vp, c_vp, ctypes.c_uint64, c_vp],
+    "ngp_fused_optimizer_step_db": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
+                                    c_i32, c_i32, c_f32, c_f32, c_f32, c_i32, c_i32, c_u32, c_vp, c_vp,
+                                    c_vp, c_vp, c_vp, c_vp],
+    "ngp_fused_optimizer_update_db": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
+                                      c_i32, c_i32, c_f32, c_i32, c_vp, c_vp, c_vp],
+    "ngp_fused_optimizer_update_head_db": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
+                                           c_i32, c_i32, c_f32, c_i32, c_vp,
+                                           c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp,
+                                           c_vp],
 }
 _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,
     "ngp_fused_inf_flag": c_vp,
+    "ngp_fused_table_select": c_vp,
     "ngp_grid_encode_backward_fused_counter_bytes": c_sz,
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
     "ngp_march_rays_train_workspace_bytes": c_sz,
@@ -127,6 +148,15 @@ _RESTYPES = {
 }
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}
+
+
+class AdamTable(ctypes.Structure):
+    """ngp_adam_table (include/ngp_hip.h): the double-buffered hash table of
+    the fused Adam."""
+    _fields_ = [("params", c_vp * 2), ("exp_avg", c_vp * 2), ("exp_avg_sq", c_vp * 2), ("grad", c_vp),
+                ("size", ctypes.c_uint64), ("done", c_vp), ("slices", c_vp), ("nslices", c_u32),
+                ("channels", c_u32), ("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32),
+                ("iters", c_i32)]
 
 _lib = None
 

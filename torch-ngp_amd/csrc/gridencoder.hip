@@ -22,6 +22,7 @@
 //   * a hashed level's size is a power of two: the modulo becomes a mask.
 #include "ngp_common.h"
 #include "ngp_dpp.h"
+#include "ngp_step.h"
 #include <stdlib.h>
 
 #include <cmath>
@@ -102,7 +103,14 @@ NGP_DEV void load_entry_as(const E* __restrict__ p, typename Acc<T>::F out[C]) {
 struct InMap {
     float shift, scale;  // scale == 0: inputs are used as given
     const int32_t* count;
+    // double-buffered table (fused Adam): grid = *sel ? alt : grid
+    const void* alt = nullptr;
+    const int32_t* sel = nullptr;
 };
+template <typename E>
+NGP_DEV const E* select_table(const E* grid, const InMap& m) {
+    return m.sel && *m.sel ? static_cast<const E*>(m.alt) : grid;
+}
 NGP_DEV uint32_t rows_of(uint32_t B, const InMap& m) {
     if (!m.count) return B;
     const int32_t c = *m.count;
@@ -129,6 +137,7 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= rows_of(B, im)) return;
     const uint32_t level = blockIdx.y;
+    grid = select_table(grid, im);
 
     T* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C
                              : outputs + ((size_t)b * L + level) * C;
@@ -285,6 +294,7 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
     const uint32_t xbit = threadIdx.x & 1;
     const bool live = b < rows_of(B, im);
     if (__ballot(live) == 0) return;  // wave-uniform exit; pairs stay together below
+    grid = select_table(grid, im);
 
     // Every load below is unconditional (dead lanes read a valid clamped
     // address and discard the value): a load under a divergent branch made the
@@ -556,13 +566,16 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #define NGP_MERGE_MAX_RES 128
 #endif
 #ifndef NGP_ACC_BATCH
-#define NGP_ACC_BATCH 16
+#define NGP_ACC_BATCH 8
 #endif
 #ifndef NGP_JOINT_MERGE
 #define NGP_JOINT_MERGE 1
 #endif
 #ifndef NGP_SPARSE_Q
 #define NGP_SPARSE_Q 4
+#endif
+#ifndef NGP_MULTI_UNITS  // 0: bins of several units flush with fp16 atomics (order-dependent rounding)
+#define NGP_MULTI_UNITS 1
 #endif
 #ifndef NGP_MATCH_MAX_BINS
 #define NGP_MATCH_MAX_BINS 64
@@ -590,7 +603,14 @@ struct BinPlan {
     uint32_t bin0[kMaxLevels];       // first global bin of the level
     uint32_t cap[kMaxLevels];        // item capacity per bin
     uint32_t item0[kMaxLevels];      // first item slot of the level; bin b at item0 + b * cap
+    // bins that may hold more than one work unit (cap > kSegItems: the dense
+    // levels) get a slot of int64 sums + an arrival counter: the units add
+    // their exact partial sums there and the last one to arrive finishes the
+    // bin, so its result does not depend on the units' order
+    uint32_t mslot0[kMaxLevels];     // first slot of the level's bins, or kNoSlot
+    uint32_t nmslots;
 };
+constexpr uint32_t kNoSlot = 0xffffffffu;
 
 struct BinItem {  // 8 bytes: the accumulate kernel reads items as one dword pair
     uint32_t e;                      // entry within the bin (| bin << 16 while staged)
@@ -951,6 +971,23 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // (inf / NaN: fp16 overflow under the loss scale) cannot be carried by the
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
+// Fused Adam (ngp_adam_table, world 1): with `st` set, every unit that owns
+// its slice of the zeroed grad updates the whole slice with Adam from its
+// exact sums -- rounded to the fp16 grad torch would hold, unscaled: the
+// arithmetic of the optimizer sweep (ngp_step::adam_update) -- reading the
+// current p / m / v buffers and writing the other ones, and tags its bin in
+// `done` with iter + 1; the step's optimizer launch updates the untagged
+// slices. The slice's grads are never written.
+struct AccAdam {
+    float* p[2];
+    float* m[2];
+    float* v[2];
+    uint32_t* done;
+    const ngp_step::StepState* st;  // null: no fused Adam
+    float lr, beta1, beta2, eps;
+    int32_t iters;
+};
+
 constexpr uint32_t kAccThreads = 512, kAccBatch = NGP_ACC_BATCH, kRetireGroups = 16;
 // the accumulate's static LDS (the 64 KiB image and its small arrays), for the launch's occupancy choice
 constexpr size_t kAccStaticLds = 66 * 1024 + 1024;
@@ -959,11 +996,16 @@ static_assert(kMaxLevels <= 64, "the accumulate finds a bin's level with one wav
 static_assert(kBinEntries % kAccThreads == 0, "each flush thread owns whole entries (G > 0)");
 // the int64 LDS image of one bin (+ the counts in dynamic LDS) fits a CU's 160 KB
 static_assert(kBinEntries * 2 * sizeof(unsigned long long) <= 128 * 1024, "bin image exceeds LDS");
-__global__ void __launch_bounds__(kAccThreads)
+// ZEROED (the fused step: NGP_GRID_GRAD_ZEROED) drops the read-back of owned
+// slices (non-fresh owners occur only with a grad that was not zeroed) and the
+// registers it holds.
+template <bool ZEROED>
+__global__ void __launch_bounds__(kAccThreads, 4)  // 2 workgroups per CU: <= 128 VGPRs
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
-                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite, bool zeroed,
-                 bool external) {
+                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
+                 bool external, AccAdam ad, unsigned long long* __restrict__ msums,
+                 uint32_t* __restrict__ marrive) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     // [entry][channel]; a channel-planar image (8-byte lane stride for the
     // 64-bit atomics instead of 16) measured the same
@@ -980,6 +1022,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // the plan's per-level arrays, indexed per lane below: kernel arguments
     // indexed by a varying value are memory loads, so keep a copy in LDS
     __shared__ uint32_t s_bin0[kMaxLevels + 1], s_cap[kMaxLevels], s_item0[kMaxLevels], s_off[kMaxLevels + 1];
+    __shared__ uint32_t s_mslot0[kMaxLevels];
+    __shared__ uint32_t s_lastunit;
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t nlev = bp.nlev;
     // the first group of this thread's bin counts (step 1 below) is loaded
@@ -998,9 +1042,29 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         if (t < nlev) {
             s_cap[t] = bp.cap[t];
             s_item0[t] = bp.item0[t];
+            s_mslot0[t] = bp.mslot0[t];
         }
     }
     lds_barrier();
+    // fused Adam: the constants of this update (the state the next step head's
+    // optimizer reads: scale, Adam step, LR epoch, current buffer)
+    bool adam_on = false;
+    ngp_step::AdamConsts ac{};
+    const float2 *a_sp = nullptr, *a_sm = nullptr, *a_sv = nullptr;
+    float2 *a_dp = nullptr, *a_dm = nullptr, *a_dv = nullptr;
+    uint32_t tag = 0;
+    if (ad.st) {
+        ac = ngp_step::adam_consts(ad.st, ad.lr, ad.beta1, ad.beta2, ad.iters, 1.0f);
+        adam_on = !ac.inv_bad;  // 1/scale inf: the step is skipped (the optimizer launch flags it)
+        const int src = ad.st->cur & 1;
+        a_sp = reinterpret_cast<const float2*>(ad.p[src]);
+        a_sm = reinterpret_cast<const float2*>(ad.m[src]);
+        a_sv = reinterpret_cast<const float2*>(ad.v[src]);
+        a_dp = reinterpret_cast<float2*>(ad.p[src ^ 1]);
+        a_dm = reinterpret_cast<float2*>(ad.m[src ^ 1]);
+        a_dv = reinterpret_cast<float2*>(ad.v[src ^ 1]);
+        tag = (uint32_t)ad.st->iter + 1u;
+    }
     auto level_of = [&](uint32_t b) {  // last level whose first bin is <= b (binary lifting)
         uint32_t l = 0;
 #pragma unroll
@@ -1082,9 +1146,11 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // unit does its LDS adds and writes), hiding the memory latency.
     // No bool members: with them the struct lived in scratch memory (a
     // private-segment load and store per unit, waited on like any other).
-    constexpr uint32_t kOwner = 1, kFresh = 2;  // flags; fresh: the table slice is known to be zero
+    // flags; fresh: the table slice is known to be zero; multi: one of several
+    // units of a bin of a zeroed grad, finished through the bin's int64 slot
+    constexpr uint32_t kOwner = 1, kFresh = 2, kMulti = 4;
     struct Unit {
-        uint32_t level, lbin, s0, s1, ne, flags;
+        uint32_t level, lbin, gb, s0, s1, ne, flags, slot, nunits;
         const uint64_t* src;
         ngp_half2* tbl;
     };
@@ -1102,10 +1168,15 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         }
         Unit r;
         const uint32_t gb = lo, seg = u - upre[gb];
-        const bool owner = upre[gb + 1] - upre[gb] == 1;
-        r.flags = (owner ? kOwner : 0u) | (owner && zeroed && (bn[gb] >> 31) == 0 ? kFresh : 0u);
+        r.nunits = upre[gb + 1] - upre[gb];
+        const bool owner = r.nunits == 1;
         r.level = 63u - (uint32_t)__builtin_clzll(__ballot(lane < nlev && s_bin0[lane] <= gb));
         r.lbin = gb - s_bin0[r.level];
+        const bool clean = ZEROED && (bn[gb] >> 31) == 0;  // zeroed grad, no items went atomic
+        r.slot = s_mslot0[r.level] == kNoSlot ? kNoSlot : s_mslot0[r.level] + r.lbin;
+        r.flags = (owner ? kOwner : 0u) | (owner && clean ? kFresh : 0u) |
+                  (NGP_MULTI_UNITS && !owner && clean && r.slot != kNoSlot ? kMulti : 0u);
+        r.gb = gb;
         r.s0 = seg * kSegItems;
         r.s1 = min(bn[gb] & 0x7fffffffu, r.s0 + kSegItems);
         r.src = reinterpret_cast<const uint64_t*>(items + s_item0[r.level] + (size_t)r.lbin * s_cap[r.level]);
@@ -1129,7 +1200,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // wait vmcnt(0) -- for the whole item prefetch issued just before -- right
     // after issuing it (phase clocks: ~6 K cycles per unit, tools/accum_stamps.py).
     auto load_old = [&](const Unit& w, uint32_t (&old)[G]) {
-        if ((w.flags & (kOwner | kFresh)) != kOwner) return;
+        if (ZEROED || (w.flags & (kOwner | kFresh)) != kOwner) return;
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
             const uint32_t e = j * kAccThreads + t;
@@ -1176,6 +1247,9 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         }
         [[maybe_unused]] const uint32_t sb = 4 + 5 * min(nstamp, 11u);
         STAMP(sb, __builtin_amdgcn_s_memtime());
+        // fused Adam of the slice this unit owns (whole slice, see the flush)
+        const bool adam_unit = adam_on && (cur.flags & kFresh);
+        const size_t ebase = (size_t)s_off[cur.level] + (size_t)cur.lbin * kBinEntries;
         STAMP(sb + 3, (cur.s1 - cur.s0) | ((uint64_t)(cur.flags & kOwner) << 32) | ((uint64_t)cur.level << 40));
         bool bad = false;
         for (uint32_t k0 = cur.s0;;) {
@@ -1213,7 +1287,52 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         const bool unit_bad = s_bad != 0;
         const float q24 = 1.0f / 16777216.0f;
         bool inf_out = false;  // a stored grad is inf/nan (GradScaler's check, when `nonfinite` is given)
-        if (sparse) {
+        if (adam_unit) {
+            // every entry of the slice (zero where no item landed): the fp16
+            // grad torch would hold, then Adam into the other buffer. A quarter
+            // of the lane's entries at a time, each quarter's p / m / v loads
+            // issued together (unconditional, clamped), so the accumulate keeps
+            // its register budget (2 workgroups of 8 waves per CU)
+            constexpr uint32_t GH = G / 4;
+#pragma unroll
+            for (uint32_t h = 0; h < G / GH; ++h) {
+                float2 ap[GH], am[GH], av[GH];
+                ulonglong2 xs[GH];
+#pragma unroll
+                for (uint32_t j = 0; j < GH; ++j) {
+                    const uint32_t e = (h * GH + j) * kAccThreads + t;
+                    const size_t i = ebase + (e < cur.ne ? e : 0u);
+                    ap[j] = a_sp[i];
+                    am[j] = a_sm[i];
+                    av[j] = a_sv[i];
+                    xs[j] = e < cur.ne ? acc_entry(e) : ulonglong2{0ull, 0ull};
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < GH; ++j) {
+                    const uint32_t e = (h * GH + j) * kAccThreads + t;
+                    if (e >= cur.ne) continue;
+                    const int64_t x0 = (int64_t)xs[j].x, x1 = (int64_t)xs[j].y;
+                    const ngp_half2 n{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
+                    inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
+                    ngp_step::adam_update(ap[j].x, am[j].x, av[j].x, (float)n[0], ac, ad.beta1, ad.beta2, ad.eps);
+                    ngp_step::adam_update(ap[j].y, am[j].y, av[j].y, (float)n[1], ac, ad.beta1, ad.beta2, ad.eps);
+                    a_dp[ebase + e] = ap[j];
+                    a_dm[ebase + e] = am[j];
+                    a_dv[ebase + e] = av[j];
+                }
+            }
+            if (sparse) {  // few items: clear just their entries
+                lds_barrier();  // every lane's reads are done before any entry is cleared
+#pragma unroll
+                for (uint32_t q = 0; q < kSparseQ; ++q)
+                    if (ent[q] != 0xffffffffu) reinterpret_cast<ulonglong2*>(acc)[ent[q]] = ulonglong2{0ull, 0ull};
+                if (t == 0) s_bad = 0;
+                need_zero = false;
+            } else {
+                need_zero = true;
+            }
+            if (t == 0) ad.done[cur.gb] = tag;
+        } else if (sparse) {
             ulonglong2 xs[kSparseQ];
 #pragma unroll
             for (uint32_t q = 0; q < kSparseQ; ++q)
@@ -1255,7 +1374,48 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                 inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
                 cur.tbl[j * kAccThreads + t] = n;
             }
-        } else if (cur.flags & kOwner) {
+        } else if (cur.flags & kMulti) {
+            need_zero = true;
+            // one of several units of a bin: its exact partial sums go into the
+            // bin's int64 slot (integer adds: the total does not depend on the
+            // units' order), then the last unit to arrive takes the totals
+            // (clearing the slot for the next call) and finishes the bin as an
+            // owner would: the fp16 grads, or Adam
+            unsigned long long* sums = msums + (size_t)cur.slot * kBinEntries * C;
+#pragma unroll 1
+            for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
+                const ulonglong2 xx = acc_entry(e);
+                if (xx.x) atomicAdd(sums + 2 * e, xx.x);
+                if (xx.y) atomicAdd(sums + 2 * e + 1, xx.y);
+            }
+            __threadfence();  // this thread's adds are done before the workgroup arrives
+            __syncthreads();
+            if (t == 0) s_lastunit = atomicAdd(marrive + cur.slot, 1u) == cur.nunits - 1 ? 1u : 0u;
+            __syncthreads();
+            if (s_lastunit) {
+                __threadfence();
+                if (t == 0) marrive[cur.slot] = 0;
+                const bool adam_bin = adam_on;
+#pragma unroll 1
+                for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
+                    const int64_t x0 = (int64_t)atomicExch(sums + 2 * e, 0ull);
+                    const int64_t x1 = (int64_t)atomicExch(sums + 2 * e + 1, 0ull);
+                    const ngp_half2 n{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
+                    inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
+                    if (adam_bin) {
+                        float2 pp = a_sp[ebase + e], mm = a_sm[ebase + e], vv = a_sv[ebase + e];
+                        ngp_step::adam_update(pp.x, mm.x, vv.x, (float)n[0], ac, ad.beta1, ad.beta2, ad.eps);
+                        ngp_step::adam_update(pp.y, mm.y, vv.y, (float)n[1], ac, ad.beta1, ad.beta2, ad.eps);
+                        a_dp[ebase + e] = pp;
+                        a_dm[ebase + e] = mm;
+                        a_dv[ebase + e] = vv;
+                    } else if (x0 != 0 || x1 != 0) {
+                        cur.tbl[e] = n;
+                    }
+                }
+                if (adam_bin && t == 0) ad.done[cur.gb] = tag;
+            }
+        } else if (!ZEROED && (cur.flags & kOwner)) {
             need_zero = true;
             // one entry per lane per step: a lane reads its entry's two 8-byte
             // sums as one 16-byte LDS read (consecutive lanes, consecutive 16 B:
@@ -1287,7 +1447,9 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                 }
             }
         }
-        if (unit_bad && t == 0) cur.tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
+        // a NaN grad marks a bad unit for a caller without the flag (a flagged
+        // one, and every fused-Adam unit, which writes no grads, reports below)
+        if (unit_bad && !nonfinite && t == 0) cur.tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
         if (nonfinite && (__ballot(inf_out) != 0 || unit_bad) && (t & 63) == 0) atomicOr(nonfinite, 1);
         lds_barrier();  // the image is rezeroed by the next unit
         STAMP(sb + 2, __builtin_amdgcn_s_memtime());
@@ -1332,6 +1494,8 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
         bp.cap[l] = (uint32_t)std::max<uint64_t>(cap, 1);
         bp.item0[l] = (uint32_t)slots;
         if (lv.res[l] <= kMergeMaxRes) bp.merge_mask |= 1u << l;  // cells span several ray steps
+        bp.mslot0[l] = bp.cap[l] > kSegItems ? bp.nmslots : kNoSlot;
+        if (bp.cap[l] > kSegItems) bp.nmslots += nb;
         bins += nb;
         slots += (uint64_t)nb * bp.cap[l];
         bp.nlev = l + 1;
@@ -1343,11 +1507,19 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
 
 static size_t bin_counters_bytes(const BinPlan& bp) { return ((size_t)bp.total_bins * 4 + 255) / 256 * 256; }
 
-// workspace: [bin cursors][retire counter][items]
-static size_t bin_workspace_bytes(const BinPlan& bp) {
+// workspace: [bin cursors][retire counter][items][int64 sums of the multi-unit
+// slots][their arrival counters]
+static size_t bin_items_bytes(const BinPlan& bp) {
     size_t slots = 0;
     for (uint32_t l = 0; l < bp.nlev; ++l) slots += (size_t)bp.nbins[l] * bp.cap[l];
-    return bin_counters_bytes(bp) + 256 + slots * sizeof(BinItem);
+    return (slots * sizeof(BinItem) + 255) / 256 * 256;
+}
+static size_t bin_sums_offset(const BinPlan& bp) { return bin_counters_bytes(bp) + 256 + bin_items_bytes(bp); }
+static size_t bin_arrive_offset(const BinPlan& bp) {
+    return bin_sums_offset(bp) + (size_t)bp.nmslots * kBinEntries * 2 * sizeof(unsigned long long);
+}
+static size_t bin_workspace_bytes(const BinPlan& bp) {
+    return bin_arrive_offset(bp) + ((size_t)bp.nmslots * 4 + 255) / 256 * 256;
 }
 
 template <typename T, uint32_t D, uint32_t C>
@@ -1665,6 +1837,30 @@ extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, cons
                                   align_corners != 0, interp, out_layout, ngp_stream(stream), im);
 }
 
+extern "C" int ngp_grid_encode_forward_fused_sel(const float* xyz, float bound, const void* table0,
+                                                 const void* table1, const int32_t* sel, int32_t emb_dtype,
+                                                 const int32_t* offsets, void* outputs, uint32_t B,
+                                                 const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
+                                                 uint32_t H, uint32_t gridtype, int32_t align_corners,
+                                                 uint32_t interp, int32_t out_layout, void* stream) {
+    if (int e = check_common(L, table0, offsets, outputs)) return e;
+    NGP_REQUIRE(xyz && bound > 0.0f && table1 && sel, NGP_ERR_ARG,
+                "grid_encode_forward_fused_sel: null xyz / second table / selector or bound <= 0");
+    if (B == 0) return NGP_OK;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    InMap im{bound, 1.0f / (2.0f * bound), count};
+    im.alt = table1;
+    im.sel = sel;
+    NGP_REQUIRE(emb_dtype == NGP_DTYPE_F32 || emb_dtype == NGP_DTYPE_F16, NGP_ERR_ARG,
+                "grid_encode_forward_fused_sel: emb_dtype %d (F32 or F16)", emb_dtype);
+    if (emb_dtype == NGP_DTYPE_F16)
+        return fwd_t<ngp_half, ngp_half>(xyz, table0, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
+                                         align_corners != 0, interp, out_layout, ngp_stream(stream), im);
+    return fwd_t<ngp_half, float>(xyz, table0, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
+                                  align_corners != 0, interp, out_layout, ngp_stream(stream), im);
+}
+
 extern "C" size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, uint32_t C,
                                                                 uint32_t L, float S, uint32_t H,
                                                                 int32_t align_corners,
@@ -1686,14 +1882,12 @@ extern "C" size_t ngp_grid_encode_backward_fused_counter_bytes(uint32_t B, uint3
     return bp.nlev ? bin_counters_bytes(bp) : 0;
 }
 
-extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
-                                              const int32_t* offsets, void* grad_embeddings,
-                                              uint32_t B, const int32_t* count, uint32_t D,
-                                              uint32_t C, uint32_t L, float S, uint32_t H,
-                                              uint32_t gridtype, int32_t align_corners,
-                                              uint32_t interp, const int32_t* offsets_host,
-                                              void* workspace, size_t workspace_bytes, int32_t grad_layout,
-                                              int32_t* nonfinite, void* stream) {
+namespace {
+int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_t* offsets, void* grad_embeddings,
+                   uint32_t B, const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+                   uint32_t gridtype, int32_t align_corners, uint32_t interp, const int32_t* offsets_host,
+                   void* workspace, size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
+                   const AccAdam& ad, void* stream) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
     const bool zeroed = (grad_layout & NGP_GRID_GRAD_ZEROED) != 0;
     const bool external = (grad_layout & NGP_GRID_CURSORS_EXTERNAL) != 0;
@@ -1721,6 +1915,9 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
         uint32_t* cursor = static_cast<uint32_t*>(workspace);
         uint32_t* retire = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_counters_bytes(bp));
         BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) + bin_counters_bytes(bp) + 256);
+        unsigned long long* msums =
+            reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + bin_sums_offset(bp));
+        uint32_t* marrive = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_arrive_offset(bp));
         const dim3 grid(bp.nlev, ngp_div_up(B, kBinPts));
         uint32_t nbmax = 0;
         for (uint32_t l = 0; l < bp.nlev; ++l) nbmax = std::max(nbmax, bp.nbins[l]);
@@ -1736,8 +1933,14 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
         // 64 KiB image + two words per bin), else one
         const size_t dyn = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
         const uint32_t per_cu = 2 * (dyn + kAccStaticLds) <= 160 * 1024 ? 2u : 1u;
-        k_grid_bin_accum<<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
-            offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, zeroed, external);
+        if (zeroed)
+            k_grid_bin_accum<true><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
+                offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
+                marrive);
+        else
+            k_grid_bin_accum<false><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
+                offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
+                marrive);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
@@ -1756,6 +1959,83 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
         }
     }
     return ngp_check_launch("grid_encode_backward_fused");
+}
+}  // namespace
+
+extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
+                                              const int32_t* offsets, void* grad_embeddings,
+                                              uint32_t B, const int32_t* count, uint32_t D,
+                                              uint32_t C, uint32_t L, float S, uint32_t H,
+                                              uint32_t gridtype, int32_t align_corners,
+                                              uint32_t interp, const int32_t* offsets_host,
+                                              void* workspace, size_t workspace_bytes, int32_t grad_layout,
+                                              int32_t* nonfinite, void* stream) {
+    return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
+                          align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
+                          AccAdam{}, stream);
+}
+
+extern "C" int ngp_grid_encode_backward_fused_adam(const void* grad, const float* xyz, float bound,
+                                                   const int32_t* offsets, void* grad_embeddings, uint32_t B,
+                                                   const int32_t* count, uint32_t D, uint32_t C, uint32_t L,
+                                                   float S, uint32_t H, uint32_t gridtype, int32_t align_corners,
+                                                   uint32_t interp, const int32_t* offsets_host, void* workspace,
+                                                   size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
+                                                   const ngp_adam_table* at, void* state, void* stream) {
+    NGP_REQUIRE(at && state && nonfinite, NGP_ERR_ARG,
+                "grid_encode_backward_fused_adam: table, state and the nonfinite flag are required");
+    NGP_REQUIRE(grad_layout & NGP_GRID_GRAD_ZEROED, NGP_ERR_ARG,
+                "grid_encode_backward_fused_adam: the grad must be zeroed on entry (NGP_GRID_GRAD_ZEROED)");
+    NGP_REQUIRE(at->grad == grad_embeddings && C == 2 && at->channels == 2 && at->done, NGP_ERR_ARG,
+                "grid_encode_backward_fused_adam: table / grad / channels mismatch");
+    for (int k = 0; k < 2; ++k)
+        NGP_REQUIRE(at->params[k] && at->exp_avg[k] && at->exp_avg_sq[k] &&
+                        ((reinterpret_cast<uintptr_t>(at->params[k]) | reinterpret_cast<uintptr_t>(at->exp_avg[k]) |
+                          reinterpret_cast<uintptr_t>(at->exp_avg_sq[k])) & 7) == 0,
+                    NGP_ERR_ARG, "grid_encode_backward_fused_adam: buffer %d null or misaligned", k);
+    AccAdam ad{};
+    for (int k = 0; k < 2; ++k) {
+        ad.p[k] = at->params[k];
+        ad.m[k] = at->exp_avg[k];
+        ad.v[k] = at->exp_avg_sq[k];
+    }
+    ad.done = at->done;
+    ad.st = static_cast<const ngp_step::StepState*>(state);
+    ad.lr = at->lr;
+    ad.beta1 = at->beta1;
+    ad.beta2 = at->beta2;
+    ad.eps = at->eps;
+    ad.iters = at->iters;
+    return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
+                          align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
+                          ad, stream);
+}
+
+extern "C" int ngp_grid_table_slices(const int32_t* offsets_host, uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                     float S, uint32_t H, int32_t align_corners, uint32_t* slices_host,
+                                     uint32_t max_slices) {
+    NGP_REQUIRE(offsets_host && slices_host && L >= 1 && L <= kMaxLevels, NGP_ERR_ARG,
+                "grid_table_slices: null offsets / output or L out of range");
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    BinPlan bp{};
+    if (C == 2 && D == 3) bp = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B);
+    uint32_t n = 0;
+    auto add = [&](uint32_t e0, uint32_t ne, uint32_t bin) {
+        if (n < max_slices) {
+            slices_host[3 * n] = e0;
+            slices_host[3 * n + 1] = ne;
+            slices_host[3 * n + 2] = bin;
+        }
+        ++n;
+    };
+    for (uint32_t l = 0; l < L; ++l) {
+        const uint32_t off0 = (uint32_t)offsets_host[l], hs = (uint32_t)offsets_host[l + 1] - off0;
+        for (uint32_t e = 0, k = 0; e < hs; e += kBinEntries, ++k)
+            add(off0 + e, std::min(kBinEntries, hs - e), l < bp.nlev ? bp.bin0[l] + k : 0xffffffffu);
+    }
+    NGP_REQUIRE(n <= max_slices, NGP_ERR_ARG, "grid_table_slices: %u slices, room for %u", n, max_slices);
+    return (int)n;
 }
 
 #ifdef NGP_STAMPS

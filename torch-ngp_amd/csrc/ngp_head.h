@@ -261,5 +261,53 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
     }
 }
 
+// ---- the double-buffered hash table (fused Adam, ngp_adam_table) --------------
+struct DbTable {
+    float* p[2];
+    float* m[2];
+    float* v[2];
+    ngp_half* g;
+    const uint32_t* done;
+    const uint32_t* slices;  // (first entry, entries, bin) triplets
+    uint32_t nslices, C;
+    bool on;
+};
+
+// The table slices the grid backward's accumulate did not update (their bin's
+// done tag is not this update's): Adam from the fp16 grads into the other
+// buffer, grads cleared; one block per slice (<= 4096 entries x C). On a skip
+// only the grads are cleared. The first block marks the flip for step_end.
+NGP_DEV void adam_slices(const DbTable& db, StepState* __restrict__ st, const AdamArgs& aa, uint32_t blk,
+                         uint32_t nblk, uint32_t tid) {
+    const ngp_step::AdamConsts ac = ngp_step::adam_consts(st, aa.base_lr, aa.beta1, aa.beta2, aa.iters,
+                                                          aa.grad_mult);
+    const bool skip = st->found_inf != 0 || ac.inv_bad;
+    const int src = st->cur & 1;
+    const uint32_t tag = (uint32_t)st->iter + 1u;
+    if (blk == 0 && tid == 0) st->flip_pending = 1;  // read by step_end only (a later launch or block)
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    for (uint32_t s = blk; s < db.nslices; s += nblk) {
+        const uint32_t e0 = db.slices[3 * s], ne = db.slices[3 * s + 1], bin = db.slices[3 * s + 2];
+        if (bin != 0xffffffffu && db.done[bin] == tag) continue;  // updated by the accumulate
+        const size_t q0 = (size_t)e0 * db.C, nq = (size_t)ne * db.C;  // multiples of 8 (offsets are)
+        for (size_t i = (size_t)tid * 4; i < nq; i += (size_t)blockDim.x * 4) {
+            half4* gp = reinterpret_cast<half4*>(db.g + q0 + i);
+            if (!skip) {
+                float4 p = *reinterpret_cast<const float4*>(db.p[src] + q0 + i);
+                float4 m = *reinterpret_cast<const float4*>(db.m[src] + q0 + i);
+                float4 v = *reinterpret_cast<const float4*>(db.v[src] + q0 + i);
+                const half4 g = *gp;
+                ngp_step::adam_update(p.x, m.x, v.x, (float)g[0], ac, aa.beta1, aa.beta2, aa.eps);
+                ngp_step::adam_update(p.y, m.y, v.y, (float)g[1], ac, aa.beta1, aa.beta2, aa.eps);
+                ngp_step::adam_update(p.z, m.z, v.z, (float)g[2], ac, aa.beta1, aa.beta2, aa.eps);
+                ngp_step::adam_update(p.w, m.w, v.w, (float)g[3], ac, aa.beta1, aa.beta2, aa.eps);
+                *reinterpret_cast<float4*>(db.p[src ^ 1] + q0 + i) = p;
+                *reinterpret_cast<float4*>(db.m[src ^ 1] + q0 + i) = m;
+                *reinterpret_cast<float4*>(db.v[src ^ 1] + q0 + i) = v;
+            }
+            *gp = half4{0, 0, 0, 0};
+        }
+    }
+}
 
 }  // namespace ngp_head

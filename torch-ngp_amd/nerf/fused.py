@@ -55,12 +55,19 @@ def _vp_array(ptrs):
 class FusedTrainer:
     def __init__(self, model, dataset, M, lr=1e-2, iters=30000, max_steps=1024, T_thresh=1e-4,
                  dt_gamma=0.0, seed=0, betas=(0.9, 0.99), eps=1e-15, init_scale=65536.0,
-                 growth_interval=2000, distributed=False):
+                 growth_interval=2000, distributed=False, fused_adam=None):
         """distributed: ray-sharded data parallelism over the initialised
         torch.distributed group: each rank draws its own rays; the flat fp16
         gradient is averaged with one RCCL reduce-scatter, each rank's Adam
         updates its 1/world shard and the fp16 forward copy is all-gathered
-        (ZeRO-1; see `_reduce`)."""
+        (ZeRO-1; see `_reduce`).
+        fused_adam (world 1; default on, NGP_FUSED_ADAM=0 turns it off): the
+        grid backward's accumulate applies Adam to the table slices it owns,
+        into a second buffer of the table's p / m / v (ngp_adam_table), and
+        the table grads of those slices are never written; the step's
+        optimizer launch updates the rest. Bit-identical parameters either way
+        (tests/test_gpu_fused.py); off, every table grad is materialised in
+        `grads[0]`, which the parity tests inspect."""
         assert model.cuda_ray, "the fused step marches the density bitfield (cuda_ray=True)"
         enc = model.encoder
         assert enc.level_dim == 2 and enc.num_levels * enc.level_dim == 32 and enc.input_dim == 3
@@ -201,6 +208,11 @@ class FusedTrainer:
             sizes=(ctypes.c_uint64 * len(sec))(*[n for _, n, _ in sec]),
             n=len(sec))
         self._nccl = self.dp and dist.get_backend() == "nccl"
+        if fused_adam is None:
+            fused_adam = os.environ.get("NGP_FUSED_ADAM", "1") != "0"
+        self.fused_adam = bool(fused_adam) and not self.dp and self.table32
+        if self.fused_adam:
+            self._setup_fused_adam(sec)
         # GradScaler's inf check is made by the kernels that write the grads
         # (grid backward, MLP dW reduce) into this flag: the optimizer's found-inf
         # flag (world 1) or the data-parallel guard's per-rank flag
@@ -210,6 +222,58 @@ class FusedTrainer:
         self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
         self._pending = False  # gradients of the last forward/backward not yet applied
+
+    def _setup_fused_adam(self, sec):
+        """The double-buffered table (ngp_adam_table): buffer 0 is the table
+        part of flat_param / exp_avg / exp_avg_sq (what the model's Parameter
+        and the checkpoints see after flush()), buffer 1 a second copy; the
+        optimizer's own tensor list keeps only the MLPs."""
+        nt = self._starts[1]  # table values, 8-aligned
+        n_tab = self.params[0].numel()
+        dev = self.dev
+        self._nt = nt
+        self.table_b = torch.zeros(nt, device=dev)
+        self.exp_avg_b, self.exp_avg_sq_b = torch.zeros(nt, device=dev), torch.zeros(nt, device=dev)
+        e = self.enc
+        cap = int(self.params[0].shape[0]) // 4096 + 2 * e.num_levels + 8
+        host = (ctypes.c_uint32 * (3 * cap))()
+        n = nat.lib().ngp_grid_table_slices(self._offsets_host, self.M, e.input_dim, e.level_dim, e.num_levels,
+                                            self.S, e.base_resolution, int(e.align_corners), host, cap)
+        if n < 0:
+            nat.check(n, "grid_table_slices")
+        sl = np.frombuffer(host, dtype=np.uint32)[:3 * n].reshape(n, 3).copy()
+        assert int(sl[-1, 0] + sl[-1, 1]) * e.level_dim == n_tab and int(sl[0, 0]) == 0
+        self.slices = torch.from_numpy(sl.view(np.int32)).to(dev)
+        bins = sl[:, 2][sl[:, 2] != 0xFFFFFFFF]
+        self.bin_done = torch.zeros(int(bins.max()) + 1 if bins.size else 1, dtype=torch.int32, device=dev)
+        at = nat.AdamTable()
+        at.params[0], at.params[1] = nat.ptr(self.flat_param), nat.ptr(self.table_b)
+        at.exp_avg[0], at.exp_avg[1] = nat.ptr(self.exp_avg), nat.ptr(self.exp_avg_b)
+        at.exp_avg_sq[0], at.exp_avg_sq[1] = nat.ptr(self.exp_avg_sq), nat.ptr(self.exp_avg_sq_b)
+        at.grad, at.size = nat.ptr(self.flat_grad), n_tab
+        at.done, at.slices, at.nslices, at.channels = nat.ptr(self.bin_done), nat.ptr(self.slices), n, e.level_dim
+        at.lr, at.beta1, at.beta2, at.eps, at.iters = self.lr, self.betas[0], self.betas[1], self.eps, self.iters
+        self._at = at
+        # the optimizer launches update the MLP section; the table goes through `at`
+        mlp = [t for t in sec if t[0] != 0]
+        self._opt = dict(
+            params=_vp_array([nat.ptr(self.flat_param) + 4 * a for a, _, _ in mlp]),
+            grads=_vp_array([nat.ptr(self.grad_shard) + 2 * a for a, _, _ in mlp]),
+            m=_vp_array([nat.ptr(self.exp_avg) + 4 * a for a, _, _ in mlp]),
+            v=_vp_array([nat.ptr(self.exp_avg_sq) + 4 * a for a, _, _ in mlp]),
+            half=_vp_array([nat.ptr(self.flat_half) + 2 * a for a, _, _ in mlp]),
+            sizes=(ctypes.c_uint64 * len(mlp))(*[k for _, k, _ in mlp]),
+            n=len(mlp))
+        self._table_sel = nat.lib().ngp_fused_table_select(nat.ptr(self.state))
+
+    def _normalize_table(self):
+        """Make buffer 0 of the double-buffered table current (device side: a
+        copy when buffer 1 is, then cur = 0), so the Parameter views, the
+        moments and every host read-out see the current table."""
+        if self.fused_adam:
+            nat.check(nat.lib().ngp_fused_table_normalize(ctypes.byref(self._at), nat.ptr(self.state),
+                                                          self.params[0].numel(), nat.stream_of(self.state)),
+                      "fused_table_normalize")
 
     def sync_half(self):
         """Refresh the fp16 forward copies after the fp32 parameters were
@@ -412,14 +476,17 @@ class FusedTrainer:
     def _optimizer_head(self):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         o, m, d = self._opt, self.model, self.data
-        nat.check(lib.ngp_fused_optimizer_update_head(
-            o["n"], o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
-            self.betas[1], self.eps, self.iters, 1, 1.0, _PRECHECKED, P(self.state),
-            P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N, self._boxes, self._nboxes, self._aabb,
-            float(m.min_near), self.seed, P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
-            P(self.nears), P(self.fars), P(self.noises), P(self.counter), P(m.step_counter),
-            P(self.grid_ws) if self._grid_counter_bytes else None, self._grid_counter_bytes, s),
-            "fused_optimizer_update_head")
+        args = (o["n"], o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
+                self.betas[1], self.eps, self.iters, 1, 1.0, _PRECHECKED, P(self.state),
+                P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N, self._boxes, self._nboxes, self._aabb,
+                float(m.min_near), self.seed, P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
+                P(self.nears), P(self.fars), P(self.noises), P(self.counter), P(m.step_counter),
+                P(self.grid_ws) if self._grid_counter_bytes else None, self._grid_counter_bytes)
+        if self.fused_adam:
+            nat.check(lib.ngp_fused_optimizer_update_head_db(*args, ctypes.byref(self._at), s),
+                      "fused_optimizer_update_head_db")
+        else:
+            nat.check(lib.ngp_fused_optimizer_update_head(*args, s), "fused_optimizer_update_head")
         self._tick("optimizer")
 
     # ---- data parallel (world > 1): ZeRO-1 --------------------------------
@@ -524,8 +591,14 @@ class FusedTrainer:
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
         table, tdt = (self.params[0], _F32) if self.table32 else (self.w_half[0], _F16)
-        chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets),
-                                              P(self.enc_out), M, cnt, *grid_args[:-1], 0, s), "grid_encode_fused")
+        if self.fused_adam:  # the current one of the double-buffered table
+            chk(lib.ngp_grid_encode_forward_fused_sel(P(self.xyzs), float(m.bound), P(table), P(self.table_b),
+                                                      self._table_sel, tdt, P(e.offsets), P(self.enc_out), M, cnt,
+                                                      *grid_args[:-1], 0, s), "grid_encode_fused_sel")
+        else:
+            chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets),
+                                                  P(self.enc_out), M, cnt, *grid_args[:-1], 0, s),
+                "grid_encode_fused")
         self._tick("grid_encode_forward")
         sn, cn, img, pk = self.sig_net, self.col_net, self.mlp_img, self._pk
         if self.dp:  # after the all-gather of the fp16 forward copy (see _sample)
@@ -565,11 +638,14 @@ class FusedTrainer:
                                  self._inf_flag, s),
             "ffmlp_reduce")
         self._tick("ffmlp_reduce")
-        chk(lib.ngp_grid_encode_backward_fused(P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets),
-                                               P(self.grads[0]), M, cnt, *grid_args[:-1], self._offsets_host,
-                                               P(self.grid_ws), self.grid_ws.numel(), self._grid_flags,
-                                               self._inf_flag, s),
-            "grid_backward_fused")
+        bargs = (P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets), P(self.grads[0]), M, cnt,
+                 *grid_args[:-1], self._offsets_host, P(self.grid_ws), self.grid_ws.numel(), self._grid_flags,
+                 self._inf_flag)
+        if self.fused_adam:
+            chk(lib.ngp_grid_encode_backward_fused_adam(*bargs, ctypes.byref(self._at), P(self.state), s),
+                "grid_backward_fused_adam")
+        else:
+            chk(lib.ngp_grid_encode_backward_fused(*bargs, s), "grid_backward_fused")
         self._tick("grid_encode_backward")
 
     def _optimizer(self, defer=False):
@@ -585,7 +661,15 @@ class FusedTrainer:
         # inside a step (world 1) the found-inf flag was set by the backward's kernels;
         # otherwise (flush, direct calls, the averaged shard) the grads are swept
         mode = _PRECHECKED if defer and not self.dp else _SCAN
-        if defer:
+        if self.fused_adam:
+            at = ctypes.byref(self._at)
+            if defer:
+                chk(lib.ngp_fused_optimizer_update_db(*args, mode, P(self.state), at, s), "fused_optimizer_update_db")
+            else:
+                chk(lib.ngp_fused_optimizer_step_db(*args, 2.0, 0.5, self.growth_interval, mode, N, cnt, None,
+                                                    P(self.loss_ray), P(self.state), at, s),
+                    "fused_optimizer_step_db")
+        elif defer:
             chk(lib.ngp_fused_optimizer_update(*args, mode, P(self.state), s), "fused_optimizer_update")
         else:
             chk(lib.ngp_fused_optimizer_step(*args, 2.0, 0.5, self.growth_interval, mode, N, cnt, None,
@@ -636,6 +720,7 @@ class FusedTrainer:
             self._gather_half(wait=True)
             self._gather_masters()
             self._pending = False
+        self._normalize_table()
 
     def capture(self, warmup=2, ring=0):
         """hipGraph(s) of the step body. World 1: one graph (optimizer of the
@@ -789,6 +874,8 @@ class FusedTrainer:
             return
         si = self.state.view(torch.int32)
         si[self._S_ITER] = int(state.get("global_step", 0))
+        if self.fused_adam:  # the accumulate's tags are iteration numbers: none may match the restored ones
+            self.bin_done.zero_()
         if "fused" in state:
             si[self._S_DRAW] = int(state["fused"]["draw"])
         if "optimizer" in state:
