@@ -9,9 +9,9 @@ colour FFMLP -> composite -> MSE -> full backward -> Adam.
 --engine fused (default): nerf/fused.py, the step as 11 fused launches in
 one hipGraph; --engine autograd: nerf/train.py, the same step through the
 reference-API autograd Functions (torch glue ops between them).
-Per-launch device times (the roofline) come from HIP event-record nodes
-inside the graphs replayed in the timed region (a ring of --ring copies of
-the step graph), with the sample counts of those same steps.
+Per-launch device times (the roofline) come from HIP events between the
+launches of eager steps run right after the timed region (ROCm refuses event
+nodes inside captured graphs), with the sample counts of those same steps.
 The density bitfield is the analytic Lego-like fixture (density-grid update
 excluded from the timed step as SURVEY §8(d) defines it; its cost is reported
 separately as `density_update_ms`). Rank 0 prints ONE JSON line.
@@ -61,10 +61,12 @@ def parse():
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--kernel-steps", type=int, default=10,
                     help="eager instrumented steps for kernel timing (only without --ring / hipGraphs)")
-    ap.add_argument("--ring", type=int, default=16,
+    ap.add_argument("--ring", type=int, default=0,
                     help="copies of the step graph with event-record nodes, replayed in turn in the timed "
-                         "region; per-launch times are read from the last min(steps, ring) of them (0: plain "
-                         "graph, per-launch times from eager steps after the timed region)")
+                         "region; per-launch times are read from the last min(steps, ring) of them. ROCm 7 "
+                         "refuses event nodes in captured graphs ('External events are disallowed in rocm'), "
+                         "so the default 0 times the launches with events between eager steps run right after "
+                         "the timed region, with those steps' own sample counts")
     ap.add_argument("--settle-steps", type=int, default=1000,
                     help="untimed steps after the warmup that bring the GPU to its sustained clock")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")

@@ -61,13 +61,16 @@ class FusedTrainer:
         gradient is averaged with one RCCL reduce-scatter, each rank's Adam
         updates its 1/world shard and the fp16 forward copy is all-gathered
         (ZeRO-1; see `_reduce`).
-        fused_adam (world 1; default on, NGP_FUSED_ADAM=0 turns it off): the
+        fused_adam (world 1; default off, NGP_FUSED_ADAM=1 turns it on): the
         grid backward's accumulate applies Adam to the table slices it owns,
         into a second buffer of the table's p / m / v (ngp_adam_table), and
         the table grads of those slices are never written; the step's
         optimizer launch updates the rest. Bit-identical parameters either way
         (tests/test_gpu_fused.py); off, every table grad is materialised in
-        `grads[0]`, which the parity tests inspect."""
+        `grads[0]`, which the parity tests inspect. Measured slower on the
+        Lego step (DESIGN.md "Measured and dropped": the accumulate becomes
+        bandwidth-bound on the moved Adam stream, 14.5 -> 62 us, while the
+        head's Adam fell 50.6 -> 17 us)."""
         assert model.cuda_ray, "the fused step marches the density bitfield (cuda_ray=True)"
         enc = model.encoder
         assert enc.level_dim == 2 and enc.num_levels * enc.level_dim == 32 and enc.input_dim == 3
@@ -209,7 +212,7 @@ class FusedTrainer:
             n=len(sec))
         self._nccl = self.dp and dist.get_backend() == "nccl"
         if fused_adam is None:
-            fused_adam = os.environ.get("NGP_FUSED_ADAM", "1") != "0"
+            fused_adam = os.environ.get("NGP_FUSED_ADAM", "0") == "1"
         self.fused_adam = bool(fused_adam) and not self.dp and self.table32
         if self.fused_adam:
             self._setup_fused_adam(sec)
