@@ -905,7 +905,11 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t o = 16 * m + 4 * g + r;
+#if NGP_NT_SLAB  // streamed once by the reduce: keep the slab out of the caches
+            if (o < out_w && i < in_w) __builtin_nontemporal_store(a[r] + b[r], slab_row + off + o * in_w + i);
+#else
             if (o < out_w && i < in_w) slab_row[off + o * in_w + i] = a[r] + b[r];
+#endif
         }
     }
     MSTAMP(14);
@@ -915,6 +919,14 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
 // (deterministic). Block = 64 parameters (one 256 B row segment per wave) x
 // kReducePhases row phases; each thread keeps 4 independent partial sums so
 // its loads stay in flight. Several networks' slabs in one launch (jobs).
+#ifndef NGP_NT_SLAB  // same-box A/B builds only: nontemporal slab stores / loads
+#define NGP_NT_SLAB 0
+#endif
+#if NGP_NT_SLAB
+#define NGP_SLAB_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define NGP_SLAB_LOAD(p) (*(p))
+#endif
 constexpr int kReducePhases = 16;
 constexpr int kMaxReduceJobs = 4;
 struct ReduceJobs {
@@ -940,12 +952,12 @@ k_slab_reduce(ReduceJobs jobs) {
     if (p < n) {
         uint32_t r = ph;
         for (; r + 3 * kReducePhases < rows; r += 4 * kReducePhases) {
-            s0 += slab[(size_t)r * n + p];
-            s1 += slab[(size_t)(r + kReducePhases) * n + p];
-            s2 += slab[(size_t)(r + 2 * kReducePhases) * n + p];
-            s3 += slab[(size_t)(r + 3 * kReducePhases) * n + p];
+            s0 += NGP_SLAB_LOAD(slab + (size_t)r * n + p);
+            s1 += NGP_SLAB_LOAD(slab + (size_t)(r + kReducePhases) * n + p);
+            s2 += NGP_SLAB_LOAD(slab + (size_t)(r + 2 * kReducePhases) * n + p);
+            s3 += NGP_SLAB_LOAD(slab + (size_t)(r + 3 * kReducePhases) * n + p);
         }
-        for (; r < rows; r += kReducePhases) s0 += slab[(size_t)r * n + p];
+        for (; r < rows; r += kReducePhases) s0 += NGP_SLAB_LOAD(slab + (size_t)r * n + p);
     }
     part[ph][lane] = (s0 + s1) + (s2 + s3);
     __syncthreads();

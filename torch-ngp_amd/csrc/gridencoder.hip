@@ -574,6 +574,9 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #ifndef NGP_SPARSE_Q
 #define NGP_SPARSE_Q 4
 #endif
+#ifndef NGP_NT_ITEMS  // same-box A/B builds only: nontemporal item stores
+#define NGP_NT_ITEMS 0
+#endif
 #ifndef NGP_MULTI_UNITS  // 0: bins of several units flush with fp16 atomics (order-dependent rounding)
 #define NGP_MULTI_UNITS 1
 #endif
@@ -929,7 +932,15 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     for (uint32_t k = threadIdx.x; k < total; k += kBinPts) {
         const BinItem it = stage[k];
         const uint2 bi = binfo[it.e >> 16];
-        if (k < bi.y) lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
+        if (k < bi.y) {
+#if NGP_NT_ITEMS  // streamed once (the accumulate reads them nontemporally): keep them out of the caches
+            const BinItem v{it.e & 0xffffu, it.v};
+            __builtin_nontemporal_store(*reinterpret_cast<const uint64_t*>(&v),
+                                        reinterpret_cast<uint64_t*>(lvl_items + k + bi.x));
+#else
+            lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
+#endif
+        }
     }
     for (uint32_t k = threadIdx.x; s_over && k < total; k += kBinPts) {
         const BinItem it = stage[k];
