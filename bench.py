@@ -9,9 +9,12 @@ colour FFMLP -> composite -> MSE -> full backward -> Adam.
 --engine fused (default): nerf/fused.py, the step as 11 fused launches in
 one hipGraph; --engine autograd: nerf/train.py, the same step through the
 reference-API autograd Functions (torch glue ops between them).
-Per-launch device times (the roofline) come from HIP events between the
-launches of eager steps run right after the timed region (ROCm refuses event
-nodes inside captured graphs), with the sample counts of those same steps.
+The roofline's grid backward is timed by the kernels themselves on the chip's
+100 MHz constant clock over the timed region's own graph replays (bin launch
+start -> accumulate end, NGP_GRID_TIMING; ROCm refuses event nodes inside
+captured graphs); the other per-launch device times come from HIP events
+between the launches of eager steps run right after the timed region, with
+the sample counts of those same steps.
 The density bitfield is the analytic Lego-like fixture (density-grid update
 excluded from the timed step as SURVEY §8(d) defines it; its cost is reported
 separately as `density_update_ms`). Rank 0 prints ONE JSON line.
@@ -391,6 +394,7 @@ def run_fused(args, model, data, bits, world, dev):
     # ---------------- timed region ----------------
     if world > 1:
         dist.barrier()
+    ft.grid_timing_reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -399,6 +403,7 @@ def run_fused(args, model, data, bits, world, dev):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    grid_clock = ft.grid_timing()  # (calls, ms per call, samples) of the timed region's grid backwards
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -425,6 +430,22 @@ def run_fused(args, model, data, bits, world, dev):
     dominant = max(per_sample, key=lambda k: kernel_ms[k])
     dom_bytes = per_sample[dominant] * rows
     achieved = per_sample[dominant] * sum(counts) / (sum(per_replay[dominant]) * 1e-3) / 1e9
+    roof_timing = {"timing": timing, "launches_timed": len(counts), "samples_per_timed_launch": counts,
+                   "launch_ms_per_timed_step": [round(v, 5) for v in per_replay[dominant]],
+                   "avg_launch_ms": round(kernel_ms[dominant], 5)}
+    if dominant == "grid_encode_backward" and grid_clock and grid_clock[0] == args.steps:
+        # the grid backward's own clock over the timed region's graph replays:
+        # bin launch start -> accumulate end on the 100 MHz constant clock,
+        # the samples of exactly those launches (NGP_GRID_TIMING)
+        calls, ms, samp = grid_clock
+        dom_bytes = per_sample[dominant] * samp / calls
+        achieved = per_sample[dominant] * samp / (ms * calls * 1e-3) / 1e9
+        roof_timing = {"timing": "device_clock_timed_region", "launches_timed": calls,
+                       "samples_timed": samp, "avg_launch_ms": round(ms, 5),
+                       "eager_events": {"avg_launch_ms": round(kernel_ms[dominant], 5),
+                                        "frac": round(per_sample[dominant] * sum(counts)
+                                                      / (sum(per_replay[dominant]) * 1e-3) / 1e9
+                                                      / HBM_PEAK_GBS, 4)}}
     mlp_ms = sum(v for k, v in kernel_ms.items() if k.startswith("ffmlp"))
     ffmlp_flops = 110592 * rows
     step_bytes = whole_step_bytes(rows, args.num_rays, sum(p.numel() for p in model.parameters()),
@@ -469,11 +490,7 @@ def run_fused(args, model, data, bits, world, dev):
             "traffic": pmc_traffic(dominant, args.workload)[0],
             "traffic_source": pmc_traffic(dominant, args.workload)[1],
             "algorithmic_bytes_per_launch": int(dom_bytes),
-            "avg_launch_ms": round(kernel_ms[dominant], 5),
-            "timing": timing,
-            "launches_timed": len(counts),
-            "samples_per_timed_launch": counts,
-            "launch_ms_per_timed_step": [round(v, 5) for v in per_replay[dominant]],
+            **roof_timing,
         },
         "kernels_ms": {k: round(v, 5) for k, v in kernel_ms.items()},
         "ffmlp_mfma": {"flops_per_step": int(ffmlp_flops), "ms": round(mlp_ms, 5),

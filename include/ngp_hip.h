@@ -266,6 +266,15 @@ size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, ui
  * between calls (the fused step's head kernel does), so the call does not
  * leave them zeroed itself. */
 #define NGP_GRID_CURSORS_EXTERNAL 0x20
+/* grad_layout | NGP_GRID_TIMING: the binned launches time themselves on the
+ * chip's 100 MHz constant clock (s_memrealtime): the first blocks of the bin
+ * launch open the span, the last workgroup of the accumulate closes it, and
+ * the workspace's timing words (ngp_grid_encode_backward_fused_timing_offset:
+ * u64 start (all ones when idle), ticks, samples, calls) keep running sums
+ * over the calls, e.g. the launches of a benchmark's timed steps. */
+#define NGP_GRID_TIMING 0x40
+size_t ngp_grid_encode_backward_fused_timing_offset(uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S,
+                                                    uint32_t H, int32_t align_corners, const int32_t* offsets_host);
 size_t ngp_grid_encode_backward_fused_counter_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S,
                                                     uint32_t H, int32_t align_corners,
                                                     const int32_t* offsets_host);
@@ -276,6 +285,20 @@ int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bou
                                    uint32_t interp, const int32_t* offsets_host, void* workspace,
                                    size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
                                    void* stream);
+/* ngp_grid_encode_backward_fused plus ngp_ffmlp_reduce of n_nets deferred MLP
+ * backward calls (its arguments, fp16 grad_weights, mlp_nonfinite as its
+ * nonfinite) carried by the bin launch as an extra column of blocks: the same
+ * sums in the same order, one launch less. Without binned levels the reduce
+ * runs on its own first. */
+int ngp_grid_encode_backward_fused_reduce(const void* grad, const float* xyz, float bound, const int32_t* offsets,
+                                          void* grad_embeddings, uint32_t B, const int32_t* count, uint32_t D,
+                                          uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                          int32_t align_corners, uint32_t interp, const int32_t* offsets_host,
+                                          void* workspace, size_t workspace_bytes, int32_t grad_layout,
+                                          int32_t* nonfinite, int32_t n_nets, void* const* mlp_workspaces,
+                                          const uint32_t* mlp_Bs, const uint32_t* in_dims,
+                                          const uint32_t* hidden_dims, const uint32_t* num_layers,
+                                          void* const* grad_weights, int32_t* mlp_nonfinite, void* stream);
 /* Fused Adam over the hash table (world 1; torch.optim.Adam + GradScaler of
  * nerf/utils.py:975-978 / main_nerf.py:194 on the table, inside the grid
  * backward). The table's fp32 parameters and Adam moments are double

@@ -485,6 +485,27 @@ def test_grid_backward_is_deterministic(cuda):
     assert torch.equal(g1.view(torch.int16), ft.grads[0].view(torch.int16))
 
 
+def test_grid_backward_self_timing_counts_graph_replays(cuda):
+    """NGP_GRID_TIMING (the bench's roofline clock): every grid backward of
+    the captured step adds one call, its samples and a positive span; the
+    arrival counters reset themselves, so consecutive replays keep counting."""
+    _, _, _, ft = _setup(cuda, num_rays=4096, mean_count=120000, fused_adam=False)
+    assert ft._grid_timing_at > ft._grid_counter_bytes
+    ft.step()
+    ft.capture(warmup=1)
+    ft.grid_timing_reset()
+    counts = []
+    for _ in range(5):
+        ft.step()
+        torch.cuda.synchronize()
+        counts.append(min(ft.sample_count(), ft.M))
+    calls, ms, samples = ft.grid_timing()
+    assert calls == 5 and samples == sum(counts)
+    assert 1e-3 < ms < 5.0
+    start = int(ft._grid_timing_words()[0])
+    assert start == -1  # the span closed by the last accumulate (idle marker)
+
+
 def test_composite_loss_large_densities_match_serial(cuda):
     """The fused composite's prefix-sum transmittance against the reference's
     serial loop (raymarching.cu composite_rays_train_forward) at the densities a

@@ -95,8 +95,11 @@ def main(tag, out=None):
         # the roofline recomputed from this trace: SURVEY 8(d) 1100 B per sample
         # x the mean samples of the bench's timed steps / the trace's time
         r = bench.get("roofline", {})
-        counts = r.get("samples_per_timed_launch") or [bench["config"]["samples_per_step"]]
-        samples = sum(counts) / len(counts)
+        if r.get("samples_timed"):  # device-clock timing: the samples of the timed launches themselves
+            samples = r["samples_timed"] / r["launches_timed"]
+        else:
+            counts = r.get("samples_per_timed_launch") or [bench["config"]["samples_per_step"]]
+            samples = sum(counts) / len(counts)
         res["roofline_recomputed"] = {
             "samples_per_step": round(samples, 1),
             "frac_from_kernels_sum": round(1100 * samples / (bwd_kernels * 1e-6) / 8e12, 4),
@@ -104,6 +107,9 @@ def main(tag, out=None):
                                     / 8e12, 4),
             "bench_frac": r.get("frac"), "bench_avg_launch_ms": r.get("avg_launch_ms"),
             "bench_timing": r.get("timing")}
+        if r.get("frac"):
+            rr = res["roofline_recomputed"]
+            rr["bench_vs_kernels_sum"] = round(r["frac"] / rr["frac_from_kernels_sum"] - 1, 4)
     txt = json.dumps(res, indent=1)
     print(txt)
     if out:

@@ -113,6 +113,10 @@ SIGNATURES = {
     "ngp_density_grid_ema_pack": [c_vp, c_vp, c_u32, c_u32, c_f32, ctypes.c_double, c_vp, c_vp, c_vp],
     "ngp_density_grid_draw_workspace_bytes": [c_u32, c_u32],
     "ngp_density_grid_draw": [c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_sz, c_vp],
+    "ngp_grid_encode_backward_fused_timing_offset": [c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32, c_vp],
+    "ngp_grid_encode_backward_fused_reduce": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
+                                              c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_i32, c_vp,
+                                              c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     # fused table Adam (ngp_adam_table, double-buffered hash table)
     "ngp_grid_table_slices": [c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32, c_vp, c_u32],
     "ngp_grid_encode_forward_fused_sel": [c_vp, c_f32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32,
@@ -138,6 +142,7 @@ _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,
     "ngp_fused_inf_flag": c_vp,
     "ngp_fused_table_select": c_vp,
+    "ngp_grid_encode_backward_fused_timing_offset": c_sz,
     "ngp_grid_encode_backward_fused_counter_bytes": c_sz,
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
     "ngp_march_rays_train_workspace_bytes": c_sz,

@@ -24,6 +24,7 @@
 //     order: no atomics, bit-reproducible weight gradients.
 #include "ffmlp_pack.h"
 #include "ngp_common.h"
+#include "ngp_reduce.h"
 #include "sh_basis.h"
 
 #include <type_traits>
@@ -916,59 +917,17 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
 }
 
 // grad_weights[p] = sum over workgroup rows of the slab, in a fixed order
-// (deterministic). Block = 64 parameters (one 256 B row segment per wave) x
-// kReducePhases row phases; each thread keeps 4 independent partial sums so
-// its loads stay in flight. Several networks' slabs in one launch (jobs).
-#ifndef NGP_NT_SLAB  // same-box A/B builds only: nontemporal slab stores / loads
-#define NGP_NT_SLAB 0
-#endif
-#if NGP_NT_SLAB
-#define NGP_SLAB_LOAD(p) __builtin_nontemporal_load(p)
-#else
-#define NGP_SLAB_LOAD(p) (*(p))
-#endif
-constexpr int kReducePhases = 16;
-constexpr int kMaxReduceJobs = 4;
-struct ReduceJobs {
-    int n;
-    const float* slab[kMaxReduceJobs];
-    void* out[kMaxReduceJobs];
-    uint32_t rows[kMaxReduceJobs], np[kMaxReduceJobs];
-    uint32_t block0[kMaxReduceJobs + 1];
-    int32_t* nonfinite;  // nullable: set when a written grad is inf/nan (GradScaler's check)
-};
+// (deterministic; ngp_reduce.h). Block = 64 parameters x 16 row phases.
+// Several networks' slabs in one launch (jobs).
+using ngp_reduce::kMaxReduceJobs;
+using ngp_reduce::kReducePhases;
+using ngp_reduce::ReduceJobs;
 
 template <typename OUT>
 __global__ void __launch_bounds__(64 * kReducePhases)
 k_slab_reduce(ReduceJobs jobs) {
     __shared__ float part[kReducePhases][64];
-    int j = 0;
-    while (j + 1 < jobs.n && blockIdx.x >= jobs.block0[j + 1]) ++j;
-    const float* __restrict__ slab = jobs.slab[j];
-    const uint32_t rows = jobs.rows[j], n = jobs.np[j];
-    const uint32_t lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
-    const uint32_t p = (blockIdx.x - jobs.block0[j]) * 64 + lane;
-    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-    if (p < n) {
-        uint32_t r = ph;
-        for (; r + 3 * kReducePhases < rows; r += 4 * kReducePhases) {
-            s0 += NGP_SLAB_LOAD(slab + (size_t)r * n + p);
-            s1 += NGP_SLAB_LOAD(slab + (size_t)(r + kReducePhases) * n + p);
-            s2 += NGP_SLAB_LOAD(slab + (size_t)(r + 2 * kReducePhases) * n + p);
-            s3 += NGP_SLAB_LOAD(slab + (size_t)(r + 3 * kReducePhases) * n + p);
-        }
-        for (; r < rows; r += kReducePhases) s0 += NGP_SLAB_LOAD(slab + (size_t)r * n + p);
-    }
-    part[ph][lane] = (s0 + s1) + (s2 + s3);
-    __syncthreads();
-    if (ph == 0 && p < n) {
-        float t = 0.0f;
-#pragma unroll
-        for (int k = 0; k < kReducePhases; ++k) t += part[k][lane];
-        const OUT o = (OUT)t;
-        static_cast<OUT*>(jobs.out[j])[p] = o;
-        if (jobs.nonfinite && !__builtin_isfinite((float)o)) atomicOr(jobs.nonfinite, 1);
-    }
+    ngp_reduce::slab_reduce_block<OUT, 64 * kReducePhases>(jobs, blockIdx.x, part);
 }
 
 __global__ void __launch_bounds__(256)
@@ -1341,17 +1300,14 @@ extern "C" int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, con
 
 /* Sums the deferred dW partials of n backward calls (same B / shapes as
  * those calls) into grad_weights[k], one launch. */
-extern "C" int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32_t* Bs, const uint32_t* in_dims,
-                                const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* grad_weights,
-                                int32_t gw_dtype, int32_t* nonfinite, void* stream) {
-    NGP_REQUIRE(n >= 1 && n <= kMaxReduceJobs, NGP_ERR_ARG, "ffmlp_reduce: 1..%d networks", kMaxReduceJobs);
-    NGP_REQUIRE(gw_dtype == NGP_DTYPE_F16 || gw_dtype == NGP_DTYPE_F32, NGP_ERR_ARG,
-                "grad_weights must be float16 or float32");
-    ReduceJobs rj{};
-    rj.n = 0;
+uint32_t ngp_reduce::build_reduce_jobs(int32_t n, void* const* workspaces, const uint32_t* Bs,
+                                       const uint32_t* in_dims, const uint32_t* hidden_dims,
+                                       const uint32_t* num_layers, void* const* grad_weights, int32_t* nonfinite,
+                                       ReduceJobs& rj) {
+    rj = ReduceJobs{};
     rj.nonfinite = nonfinite;
     uint32_t blocks = 0;
-    for (int k = 0; k < n; ++k) {
+    for (int k = 0; k < n && k < kMaxReduceJobs; ++k) {
         const uint32_t rows = bwd_blocks(Bs[k]);
         if (rows == 0) continue;
         const int j = rj.n++;
@@ -1363,6 +1319,18 @@ extern "C" int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32
         blocks += ngp_div_up(rj.np[j], 64);
     }
     rj.block0[rj.n] = blocks;
+    return blocks;
+}
+
+extern "C" int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32_t* Bs, const uint32_t* in_dims,
+                                const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* grad_weights,
+                                int32_t gw_dtype, int32_t* nonfinite, void* stream) {
+    NGP_REQUIRE(n >= 1 && n <= kMaxReduceJobs, NGP_ERR_ARG, "ffmlp_reduce: 1..%d networks", kMaxReduceJobs);
+    NGP_REQUIRE(gw_dtype == NGP_DTYPE_F16 || gw_dtype == NGP_DTYPE_F32, NGP_ERR_ARG,
+                "grad_weights must be float16 or float32");
+    ReduceJobs rj{};
+    const uint32_t blocks = ngp_reduce::build_reduce_jobs(n, workspaces, Bs, in_dims, hidden_dims, num_layers,
+                                                          grad_weights, nonfinite, rj);
     if (blocks == 0) return NGP_OK;
     if (gw_dtype == NGP_DTYPE_F16)
         hipLaunchKernelGGL(k_slab_reduce<ngp_half>, dim3(blocks), dim3(64 * kReducePhases), 0, ngp_stream(stream), rj);

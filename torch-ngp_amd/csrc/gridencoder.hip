@@ -22,6 +22,7 @@
 //   * a hashed level's size is a power of two: the modulo becomes a mask.
 #include "ngp_common.h"
 #include "ngp_dpp.h"
+#include "ngp_reduce.h"
 #include "ngp_step.h"
 #include <stdlib.h>
 
@@ -663,13 +664,29 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
                const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
                InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
-               int32_t grad_layout, int32_t* __restrict__ nonfinite) {
+               int32_t grad_layout, int32_t* __restrict__ nonfinite, ngp_reduce::ReduceJobs rj, uint32_t nred,
+               unsigned long long* __restrict__ timing) {
     constexpr uint32_t C = 2, NC = 1u << D, NW = kBinPts / 64;
     constexpr uint32_t BPT = (NBMAX + kBinPts - 1) / kBinPts;  // bins per thread in the reservation step
     __shared__ uint32_t cnt[NBMAX], soff[NBMAX + 1], wsum[NW];
     __shared__ uint2 binfo[NBMAX];  // (slot - stage index, end of the bin's in-capacity stage run)
     __shared__ uint32_t s_over;                // some bin of this workgroup ran past its capacity
     extern __shared__ BinItem stage[];  // kBinPts * NC
+    // launch timing (NGP_GRID_TIMING): the first row of blocks, dispatched
+    // first, marks the start on the chip's constant 100 MHz clock; block (0, 0)
+    // counts the samples of this call
+    if (timing && blockIdx.y == 0 && threadIdx.x == 0) {
+        atomicMin(timing, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (blockIdx.x == 0) atomicAdd(timing + 2, (unsigned long long)rows_of(B, im));
+    }
+    // the extra column of blocks (x == nlev): the MLP dW slab reduce, which
+    // neither needs nor feeds this kernel (one launch less per step; the same
+    // fixed summation order as k_slab_reduce, ngp_reduce.h)
+    if (blockIdx.x >= bp.nlev) {
+        if (blockIdx.y < nred)
+            ngp_reduce::slab_reduce_block<ngp_half, kBinPts>(rj, blockIdx.y, reinterpret_cast<float(*)[64]>(stage));
+        return;
+    }
     // the grid covers the row capacity; workgroups past the marched sample
     // count (about a fifth of them on the Lego step) leave before any work
     // grid (level, point block): consecutive workgroups take different levels
@@ -1016,7 +1033,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
                  const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
                  bool external, AccAdam ad, unsigned long long* __restrict__ msums,
-                 uint32_t* __restrict__ marrive) {
+                 uint32_t* __restrict__ marrive, unsigned long long* __restrict__ timing) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     // [entry][channel]; a channel-planar image (8-byte lane stride for the
     // 64-bit atomics instead of 16) measured the same
@@ -1470,6 +1487,24 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         u = un;
     }
     RSTAMP(61);
+    // launch timing (NGP_GRID_TIMING): the last workgroup to finish (arrivals
+    // counted per XCD, then across XCDs) closes the span the bin launch opened
+    // and adds it to the running sums [start, ticks, samples, calls]
+    if (timing && t == 0) {
+        uint32_t* ctr = reinterpret_cast<uint32_t*>(timing + 4);  // [0] XCDs done, [1 + x] workgroups of XCD x
+        const uint32_t x = blockIdx.x & 7u;
+        const uint32_t members = gridDim.x / 8 + (x < gridDim.x % 8 ? 1u : 0u);
+        if (atomicAdd(ctr + 1 + x, 1u) == members - 1) {
+            ctr[1 + x] = 0;  // every member of the XCD has arrived
+            if (atomicAdd(ctr, 1u) == min(gridDim.x, 8u) - 1) {
+                ctr[0] = 0;
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                const unsigned long long t0 = atomicExch(timing, ~0ull);
+                atomicAdd(timing + 1, now - t0);
+                atomicAdd(timing + 3, 1ull);
+            }
+        }
+    }
 }
 
 // GradScaler's inf/nan check over a grad range (levels the binned path does
@@ -1517,6 +1552,9 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
 }
 
 static size_t bin_counters_bytes(const BinPlan& bp) { return ((size_t)bp.total_bins * 4 + 255) / 256 * 256; }
+// the launch-timing words (NGP_GRID_TIMING) in the upper half of the 256-byte
+// retire block: u64 [start, ticks, samples, calls], u32 arrival counters
+static size_t bin_timing_offset(const BinPlan& bp) { return bin_counters_bytes(bp) + 128; }
 
 // workspace: [bin cursors][retire counter][items][int64 sums of the multi-unit
 // slots][their arrival counters]
@@ -1898,11 +1936,13 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
                    uint32_t B, const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
                    uint32_t gridtype, int32_t align_corners, uint32_t interp, const int32_t* offsets_host,
                    void* workspace, size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
-                   const AccAdam& ad, void* stream) {
+                   const AccAdam& ad, void* stream, const ngp_reduce::ReduceJobs* rj = nullptr,
+                   uint32_t nred = 0) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
     const bool zeroed = (grad_layout & NGP_GRID_GRAD_ZEROED) != 0;
     const bool external = (grad_layout & NGP_GRID_CURSORS_EXTERNAL) != 0;
-    grad_layout &= ~(NGP_GRID_GRAD_ZEROED | NGP_GRID_CURSORS_EXTERNAL);
+    const bool timed = (grad_layout & NGP_GRID_TIMING) != 0;
+    grad_layout &= ~(NGP_GRID_GRAD_ZEROED | NGP_GRID_CURSORS_EXTERNAL | NGP_GRID_TIMING);
     NGP_REQUIRE(grad_layout == 0 || grad_layout == 1, NGP_ERR_ARG,
                 "grid_encode_backward_fused: grad_layout 0 ([L,B,C]) or 1 ([B,L*C])");
     NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_backward_fused: null xyz or bound <= 0");
@@ -1928,18 +1968,24 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) + bin_counters_bytes(bp) + 256);
         unsigned long long* msums =
             reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + bin_sums_offset(bp));
+        unsigned long long* timing =
+            timed ? reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + bin_timing_offset(bp))
+                  : nullptr;
         uint32_t* marrive = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_arrive_offset(bp));
-        const dim3 grid(bp.nlev, ngp_div_up(B, kBinPts));
+        // (level, point block) + one column of slab-reduce blocks when merged
+        const ngp_reduce::ReduceJobs rjv = rj ? *rj : ngp_reduce::ReduceJobs{};
+        if (!rj) nred = 0;
+        const dim3 grid(bp.nlev + (nred ? 1u : 0u), std::max(ngp_div_up(B, kBinPts), nred));
         uint32_t nbmax = 0;
         for (uint32_t l = 0; l < bp.nlev; ++l) nbmax = std::max(nbmax, bp.nbins[l]);
         if (nbmax <= kMaxBinsPerLevel)
             k_grid_bwd_bin<3, kMaxBinsPerLevel><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite);
+                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing);
         else
             k_grid_bwd_bin<3, kMaxBinsPerLevelBig><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite);
+                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing);
         // two persistent workgroups per CU while both fit the CU's LDS (the
         // 64 KiB image + two words per bin), else one
         const size_t dyn = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
@@ -1947,11 +1993,11 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         if (zeroed)
             k_grid_bin_accum<true><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
-                marrive);
+                marrive, timing);
         else
             k_grid_bin_accum<false><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
-                marrive);
+                marrive, timing);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
@@ -1973,6 +2019,16 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
 }
 }  // namespace
 
+extern "C" size_t ngp_grid_encode_backward_fused_timing_offset(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
+                                                               float S, uint32_t H, int32_t align_corners,
+                                                               const int32_t* offsets_host) {
+    if (!offsets_host || C != 2 || D < 2 || D > 5 || L == 0 || L > kMaxLevels) return 0;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const BinPlan bp = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B);
+    return bp.nlev ? bin_timing_offset(bp) : 0;
+}
+
 extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz, float bound,
                                               const int32_t* offsets, void* grad_embeddings,
                                               uint32_t B, const int32_t* count, uint32_t D,
@@ -1984,6 +2040,45 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
     return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                           align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
                           AccAdam{}, stream);
+}
+
+extern "C" int ngp_grid_encode_backward_fused_reduce(const void* grad, const float* xyz, float bound,
+                                                     const int32_t* offsets, void* grad_embeddings, uint32_t B,
+                                                     const int32_t* count, uint32_t D, uint32_t C, uint32_t L,
+                                                     float S, uint32_t H, uint32_t gridtype,
+                                                     int32_t align_corners, uint32_t interp,
+                                                     const int32_t* offsets_host, void* workspace,
+                                                     size_t workspace_bytes, int32_t grad_layout,
+                                                     int32_t* nonfinite, int32_t n_nets,
+                                                     void* const* mlp_workspaces, const uint32_t* mlp_Bs,
+                                                     const uint32_t* in_dims, const uint32_t* hidden_dims,
+                                                     const uint32_t* num_layers, void* const* grad_weights,
+                                                     int32_t* mlp_nonfinite, void* stream) {
+    NGP_REQUIRE(n_nets >= 1 && n_nets <= ngp_reduce::kMaxReduceJobs && mlp_workspaces && mlp_Bs && in_dims &&
+                    hidden_dims && num_layers && grad_weights,
+                NGP_ERR_ARG, "grid_encode_backward_fused_reduce: 1..%d networks with their arguments",
+                ngp_reduce::kMaxReduceJobs);
+    // the plan decides whether there is a bin launch to carry the reduce
+    bool binned = false;
+    if (workspace && offsets_host && C == 2 && D == 3 && L >= 1 && L <= kMaxLevels) {
+        GridLevels lv;
+        make_levels(lv, L, S, H);
+        binned = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B).nlev > 0;
+    }
+    if (!binned) {  // no bin launch: the reduce on its own, then the backward
+        if (int e = ngp_ffmlp_reduce(n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims, num_layers, grad_weights,
+                                     NGP_DTYPE_F16, mlp_nonfinite, stream))
+            return e;
+        return ngp_grid_encode_backward_fused(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H,
+                                              gridtype, align_corners, interp, offsets_host, workspace,
+                                              workspace_bytes, grad_layout, nonfinite, stream);
+    }
+    ngp_reduce::ReduceJobs rj{};
+    const uint32_t nred = ngp_reduce::build_reduce_jobs(n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims,
+                                                        num_layers, grad_weights, mlp_nonfinite, rj);
+    return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
+                          align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
+                          AccAdam{}, stream, &rj, nred);
 }
 
 extern "C" int ngp_grid_encode_backward_fused_adam(const void* grad, const float* xyz, float bound,

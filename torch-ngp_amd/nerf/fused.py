@@ -46,6 +46,7 @@ _RELU, _NONE = 0, 6
 _DEFER, _GEO, _PAIR = 1, 2, 4  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO, NGP_FFMLP_PAIR_MAJOR
 _SCAN, _PRECHECKED = 1, 2  # NGP_SCALER_SCAN, NGP_SCALER_PRECHECKED
 _ZEROED, _EXTERNAL = 0x10, 0x20  # NGP_GRID_GRAD_ZEROED, NGP_GRID_CURSORS_EXTERNAL (grad layout 0: [L,M,2])
+_TIMING = 0x40  # NGP_GRID_TIMING
 
 
 def _vp_array(ptrs):
@@ -158,6 +159,14 @@ class FusedTrainer:
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
             int(enc.align_corners), self._offsets_host))
         self._grid_flags = _ZEROED | (_EXTERNAL if self._grid_counter_bytes else 0)
+        # the binned grid backward times itself (a few atomics per launch): the
+        # workspace's timing words keep [start, ticks, samples, calls]
+        self._grid_timing_at = int(nat.lib().ngp_grid_encode_backward_fused_timing_offset(
+            M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
+            int(enc.align_corners), self._offsets_host))
+        if self._grid_timing_at:
+            self._grid_flags |= _TIMING
+            self.grid_timing_reset()
         self.mlp_ws = []
         for net in (self.sig_net, self.col_net):
             b = nat.lib().ngp_ffmlp_backward_workspace_bytes(M, net.input_dim, net.padded_output_dim,
@@ -191,6 +200,8 @@ class FusedTrainer:
         # Data parallel: the fp16 copy is what the all-gather moves.
         self.table32 = not self.dp and os.environ.get("NGP_FUSED_TABLE16") != "1"
         self._merge_head = not self.dp and os.environ.get("NGP_FUSED_SPLIT_HEAD") != "1"
+        # the MLP dW reduce in the grid backward's bin launch (NGP_FUSED_SPLIT_REDUCE=1: its own launch)
+        self._split_reduce = os.environ.get("NGP_FUSED_SPLIT_REDUCE") == "1"
         # one launch for the sigma + colour forwards where ngp_nerf_forward covers
         # the shapes (NGP_FUSED_SPLIT_FWD=1 keeps two launches, for A/B and tests)
         sn_, cn_ = self.sig_net, self.col_net
@@ -398,6 +409,29 @@ class FusedTrainer:
             ev = torch.cuda.Event(enable_timing=True, external=self._capturing)
             ev.record()
             self._events.append((name, ev))
+
+    def _grid_timing_words(self):
+        a = self._grid_timing_at
+        return self.grid_ws[a:a + 32].view(torch.int64)
+
+    def grid_timing_reset(self):
+        """Zero the grid backward's self-timing sums (start := idle)."""
+        if self._grid_timing_at:
+            w = self._grid_timing_words()
+            w.zero_()
+            w[0] = -1
+
+    def grid_timing(self):
+        """(calls, mean device ms per call, samples) of the grid backward
+        (bin launch start -> accumulate end, on the chip's 100 MHz constant
+        clock) since grid_timing_reset(); None when the backward is unbinned.
+        The spans are measured inside the kernels, so graph replays are timed
+        as they run, with no events in the graphs."""
+        if not self._grid_timing_at:
+            return None
+        torch.cuda.synchronize()
+        _, ticks, samples, calls = self._grid_timing_words().cpu().tolist()
+        return calls, (ticks / calls * 1e-5 if calls else 0.0), samples
 
     def _recent_counts(self, n):
         """Sample counts of the last n batches (oldest first) as a device
@@ -637,18 +671,23 @@ class FusedTrainer:
                                         _DEFER | _PAIR, P(self.mlp_ws[0]), self.mlp_ws[0].numel(), s),
             "sigma_mlp_backward")
         self._tick("ffmlp_backward_sigma")
-        chk(lib.ngp_ffmlp_reduce(2, pk["ws"], pk["B"], pk["ins"], pk["hid"], pk["nl"], pk["gw"], _F16,
-                                 self._inf_flag, s),
-            "ffmlp_reduce")
-        self._tick("ffmlp_reduce")
         bargs = (P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets), P(self.grads[0]), M, cnt,
                  *grid_args[:-1], self._offsets_host, P(self.grid_ws), self.grid_ws.numel(), self._grid_flags,
                  self._inf_flag)
-        if self.fused_adam:
-            chk(lib.ngp_grid_encode_backward_fused_adam(*bargs, ctypes.byref(self._at), P(self.state), s),
-                "grid_backward_fused_adam")
+        if self.fused_adam or self._split_reduce:
+            chk(lib.ngp_ffmlp_reduce(2, pk["ws"], pk["B"], pk["ins"], pk["hid"], pk["nl"], pk["gw"], _F16,
+                                     self._inf_flag, s), "ffmlp_reduce")
+            self._tick("ffmlp_reduce")
+            if self.fused_adam:
+                chk(lib.ngp_grid_encode_backward_fused_adam(*bargs, ctypes.byref(self._at), P(self.state), s),
+                    "grid_backward_fused_adam")
+            else:
+                chk(lib.ngp_grid_encode_backward_fused(*bargs, s), "grid_backward_fused")
         else:
-            chk(lib.ngp_grid_encode_backward_fused(*bargs, s), "grid_backward_fused")
+            # the MLP dW reduce rides in the grid backward's bin launch (same sums)
+            chk(lib.ngp_grid_encode_backward_fused_reduce(*bargs, 2, pk["ws"], pk["B"], pk["ins"], pk["hid"],
+                                                          pk["nl"], pk["gw"], self._inf_flag, s),
+                "grid_backward_fused_reduce")
         self._tick("grid_encode_backward")
 
     def _optimizer(self, defer=False):
