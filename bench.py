@@ -403,7 +403,7 @@ def run_fused(args, model, data, bits, world, dev):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    grid_clock = ft.grid_timing()  # (calls, ms per call, samples) of the timed region's grid backwards
+    grid_clock = ft.grid_timing(last=args.steps)  # the timed region's grid backwards (<= 256 of them)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -437,11 +437,14 @@ def run_fused(args, model, data, bits, world, dev):
         # the grid backward's own clock over the timed region's graph replays:
         # bin launch start -> accumulate end on the 100 MHz constant clock,
         # the samples of exactly those launches (NGP_GRID_TIMING)
-        calls, ms, samp = grid_clock
-        dom_bytes = per_sample[dominant] * samp / calls
-        achieved = per_sample[dominant] * samp / (ms * calls * 1e-3) / 1e9
+        _, ms, samp = grid_clock
+        calls = len(ms)
+        dom_bytes = per_sample[dominant] * sum(samp) / calls
+        achieved = per_sample[dominant] * sum(samp) / (sum(ms) * 1e-3) / 1e9
         roof_timing = {"timing": "device_clock_timed_region", "launches_timed": calls,
-                       "samples_timed": samp, "avg_launch_ms": round(ms, 5),
+                       "samples_timed": sum(samp), "avg_launch_ms": round(sum(ms) / calls, 5),
+                       "launch_ms_min_median_max": [round(float(v), 5) for v in
+                                                    (min(ms), np.median(ms), max(ms))],
                        "eager_events": {"avg_launch_ms": round(kernel_ms[dominant], 5),
                                         "frac": round(per_sample[dominant] * sum(counts)
                                                       / (sum(per_replay[dominant]) * 1e-3) / 1e9

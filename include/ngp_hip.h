@@ -267,12 +267,17 @@ size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, ui
  * leave them zeroed itself. */
 #define NGP_GRID_CURSORS_EXTERNAL 0x20
 /* grad_layout | NGP_GRID_TIMING: the binned launches time themselves on the
- * chip's 100 MHz constant clock (s_memrealtime): the first blocks of the bin
- * launch open the span, the last workgroup of the accumulate closes it, and
- * the workspace's timing words (ngp_grid_encode_backward_fused_timing_offset:
- * u64 start (all ones when idle), ticks, samples, calls) keep running sums
- * over the calls, e.g. the launches of a benchmark's timed steps. */
+ * chip's 100 MHz constant clock (s_memrealtime) into a ring in the workspace
+ * (ngp_grid_encode_backward_fused_timing_offset; u32 words): [0] calls so
+ * far; the head of call c at word 64 + 4 (c % NGP_GRID_TIMING_RING) holds
+ * {start (bin launch, block (0, 0)), samples, accumulate workgroups n, 0};
+ * its ends at word 64 + 4 NGP_GRID_TIMING_RING + (c % RING) MAX_WG + w, one
+ * per accumulate workgroup w < n. A call's span is max_w(end_w - start)
+ * (mod 2^32 ticks of 10 ns). Plain stores only: the timed kernels keep their
+ * critical path. Zero word 0 to restart. */
 #define NGP_GRID_TIMING 0x40
+#define NGP_GRID_TIMING_RING 256
+#define NGP_GRID_TIMING_MAX_WG 1024
 size_t ngp_grid_encode_backward_fused_timing_offset(uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S,
                                                     uint32_t H, int32_t align_corners, const int32_t* offsets_host);
 size_t ngp_grid_encode_backward_fused_counter_bytes(uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S,

@@ -635,6 +635,9 @@ NGP_DEV uint32_t lanes_below(uint64_t m) {
 }
 
 constexpr uint32_t kBinPts = 512;  // samples (threads) per bin-kernel workgroup
+// NGP_GRID_TIMING ring (u32 words): [0] calls, heads {start, samples,
+// accumulate workgroups, -} from word 64, per-workgroup ends from kTimingEnds
+constexpr uint32_t kTimingHeads = 64, kTimingEnds = kTimingHeads + 4 * NGP_GRID_TIMING_RING;
 
 // Workgroup barrier that orders LDS only: unlike __syncthreads() it does not
 // wait for the wave's outstanding global loads, stores and atomics.
@@ -665,19 +668,23 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
                InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
                int32_t grad_layout, int32_t* __restrict__ nonfinite, ngp_reduce::ReduceJobs rj, uint32_t nred,
-               unsigned long long* __restrict__ timing) {
+               uint32_t* __restrict__ timing) {
     constexpr uint32_t C = 2, NC = 1u << D, NW = kBinPts / 64;
     constexpr uint32_t BPT = (NBMAX + kBinPts - 1) / kBinPts;  // bins per thread in the reservation step
     __shared__ uint32_t cnt[NBMAX], soff[NBMAX + 1], wsum[NW];
     __shared__ uint2 binfo[NBMAX];  // (slot - stage index, end of the bin's in-capacity stage run)
     __shared__ uint32_t s_over;                // some bin of this workgroup ran past its capacity
     extern __shared__ BinItem stage[];  // kBinPts * NC
-    // launch timing (NGP_GRID_TIMING): the first row of blocks, dispatched
-    // first, marks the start on the chip's constant 100 MHz clock; block (0, 0)
-    // counts the samples of this call
-    if (timing && blockIdx.y == 0 && threadIdx.x == 0) {
-        atomicMin(timing, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        if (blockIdx.x == 0) atomicAdd(timing + 2, (unsigned long long)rows_of(B, im));
+    // launch timing (NGP_GRID_TIMING): block (0, 0), dispatched first, opens
+    // this call's ring entry: start on the chip's constant 100 MHz clock, the
+    // samples, the call count (plain stores: one thread, and the previous
+    // call's kernels have finished)
+    if (timing && (blockIdx.x | blockIdx.y) == 0 && threadIdx.x == 0) {
+        const uint32_t c = timing[0];
+        uint32_t* h = timing + kTimingHeads + (c % NGP_GRID_TIMING_RING) * 4;
+        h[0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        h[1] = rows_of(B, im);
+        timing[0] = c + 1;
     }
     // the extra column of blocks (x == nlev): the MLP dW slab reduce, which
     // neither needs nor feeds this kernel (one launch less per step; the same
@@ -1033,7 +1040,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
                  const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
                  bool external, AccAdam ad, unsigned long long* __restrict__ msums,
-                 uint32_t* __restrict__ marrive, unsigned long long* __restrict__ timing) {
+                 uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     // [entry][channel]; a channel-planar image (8-byte lane stride for the
     // 64-bit atomics instead of 16) measured the same
@@ -1487,25 +1494,15 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         u = un;
     }
     RSTAMP(61);
-    // launch timing (NGP_GRID_TIMING): the last workgroup to finish (arrivals
-    // counted per XCD, then across XCDs) closes the span the bin launch opened
-    // and adds it to the running sums [start, ticks, samples, calls]
+    // launch timing (NGP_GRID_TIMING): every workgroup stores its end in the
+    // call's ring entry (one vector store each, no atomics, so the timed
+    // kernel keeps its critical path); the host takes the latest
     if (timing && t == 0) {
-        uint32_t* ctr = reinterpret_cast<uint32_t*>(timing + 4);  // [0] XCDs done, [1 + x] workgroups of XCD x
-        const uint32_t x = blockIdx.x & 7u;
-        const uint32_t members = gridDim.x / 8 + (x < gridDim.x % 8 ? 1u : 0u);
-        if (atomicAdd(ctr + 1 + x, 1u) == members - 1) {
-            ctr[1 + x] = 0;  // every member of the XCD has arrived
-            if (atomicAdd(ctr, 1u) == min(gridDim.x, 8u) - 1) {
-                ctr[0] = 0;
-                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-                const unsigned long long t0 = atomicExch(timing, ~0ull);
-                atomicAdd(timing + 1, now - t0);
-                atomicAdd(timing + 3, 1ull);
-            }
-        }
-    }
-}
+        const uint32_t c = (timing[0] - 1) % NGP_GRID_TIMING_RING;
+        if (blockIdx.x == 0) timing[kTimingHeads + c * 4 + 2] = gridDim.x;
+        if (blockIdx.x < NGP_GRID_TIMING_MAX_WG)
+            timing[kTimingEnds + c * NGP_GRID_TIMING_MAX_WG + blockIdx.x] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    }}
 
 // GradScaler's inf/nan check over a grad range (levels the binned path does
 // not cover): sets *flag.
@@ -1552,9 +1549,6 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
 }
 
 static size_t bin_counters_bytes(const BinPlan& bp) { return ((size_t)bp.total_bins * 4 + 255) / 256 * 256; }
-// the launch-timing words (NGP_GRID_TIMING) in the upper half of the 256-byte
-// retire block: u64 [start, ticks, samples, calls], u32 arrival counters
-static size_t bin_timing_offset(const BinPlan& bp) { return bin_counters_bytes(bp) + 128; }
 
 // workspace: [bin cursors][retire counter][items][int64 sums of the multi-unit
 // slots][their arrival counters]
@@ -1567,8 +1561,12 @@ static size_t bin_sums_offset(const BinPlan& bp) { return bin_counters_bytes(bp)
 static size_t bin_arrive_offset(const BinPlan& bp) {
     return bin_sums_offset(bp) + (size_t)bp.nmslots * kBinEntries * 2 * sizeof(unsigned long long);
 }
-static size_t bin_workspace_bytes(const BinPlan& bp) {
+// the launch-timing ring (NGP_GRID_TIMING, include/ngp_hip.h): u32 words
+static size_t bin_timing_offset(const BinPlan& bp) {
     return bin_arrive_offset(bp) + ((size_t)bp.nmslots * 4 + 255) / 256 * 256;
+}
+static size_t bin_workspace_bytes(const BinPlan& bp) {
+    return bin_timing_offset(bp) + (size_t)(kTimingEnds + NGP_GRID_TIMING_RING * NGP_GRID_TIMING_MAX_WG) * 4;
 }
 
 template <typename T, uint32_t D, uint32_t C>
@@ -1968,9 +1966,8 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) + bin_counters_bytes(bp) + 256);
         unsigned long long* msums =
             reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + bin_sums_offset(bp));
-        unsigned long long* timing =
-            timed ? reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + bin_timing_offset(bp))
-                  : nullptr;
+        uint32_t* timing =
+            timed ? reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_timing_offset(bp)) : nullptr;
         uint32_t* marrive = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_arrive_offset(bp));
         // (level, point block) + one column of slab-reduce blocks when merged
         const ngp_reduce::ReduceJobs rjv = rj ? *rj : ngp_reduce::ReduceJobs{};
@@ -2022,7 +2019,7 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
 extern "C" size_t ngp_grid_encode_backward_fused_timing_offset(uint32_t B, uint32_t D, uint32_t C, uint32_t L,
                                                                float S, uint32_t H, int32_t align_corners,
                                                                const int32_t* offsets_host) {
-    if (!offsets_host || C != 2 || D < 2 || D > 5 || L == 0 || L > kMaxLevels) return 0;
+    if (!offsets_host || C != 2 || D != 3 || L == 0 || L > kMaxLevels) return 0;
     GridLevels lv;
     make_levels(lv, L, S, H);
     const BinPlan bp = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B);

@@ -410,28 +410,39 @@ class FusedTrainer:
             ev.record()
             self._events.append((name, ev))
 
+    _TIMING_RING, _TIMING_MAX_WG, _TIMING_HEADS = 256, 1024, 64  # include/ngp_hip.h NGP_GRID_TIMING_*
+
     def _grid_timing_words(self):
         a = self._grid_timing_at
-        return self.grid_ws[a:a + 32].view(torch.int64)
+        n = self._TIMING_HEADS + 4 * self._TIMING_RING + self._TIMING_RING * self._TIMING_MAX_WG
+        return self.grid_ws[a:a + 4 * n].view(torch.int32)
 
     def grid_timing_reset(self):
-        """Zero the grid backward's self-timing sums (start := idle)."""
+        """Restart the grid backward's self-timing ring (calls := 0)."""
         if self._grid_timing_at:
-            w = self._grid_timing_words()
-            w.zero_()
-            w[0] = -1
+            self._grid_timing_words()[0] = 0
 
-    def grid_timing(self):
-        """(calls, mean device ms per call, samples) of the grid backward
-        (bin launch start -> accumulate end, on the chip's 100 MHz constant
-        clock) since grid_timing_reset(); None when the backward is unbinned.
-        The spans are measured inside the kernels, so graph replays are timed
-        as they run, with no events in the graphs."""
+    def grid_timing(self, last=None):
+        """Device time of the grid backward's last calls since
+        grid_timing_reset() (at most 256, `last` if given): bin launch start ->
+        the accumulate's last workgroup end, measured by the kernels on the
+        chip's 100 MHz constant clock, so graph replays are timed as they run
+        (no events in the graphs). Returns (calls, ms per call, samples per
+        call), oldest first, or None when the backward is unbinned."""
         if not self._grid_timing_at:
             return None
         torch.cuda.synchronize()
-        _, ticks, samples, calls = self._grid_timing_words().cpu().tolist()
-        return calls, (ticks / calls * 1e-5 if calls else 0.0), samples
+        w = self._grid_timing_words().cpu().numpy().view(np.uint32)
+        R, W, H = self._TIMING_RING, self._TIMING_MAX_WG, self._TIMING_HEADS
+        calls = int(w[0])
+        n = min(calls, R, last or R)
+        ms, samples = [], []
+        for c in range(calls - n, calls):
+            start, samp, nwg = (int(v) for v in w[H + 4 * (c % R):H + 4 * (c % R) + 3])
+            ends = w[H + 4 * R + (c % R) * W:][:min(nwg, W)].astype(np.int64)
+            ms.append(float(((ends - start) & 0xffffffff).max()) * 1e-5)
+            samples.append(samp)
+        return calls, ms, samples
 
     def _recent_counts(self, n):
         """Sample counts of the last n batches (oldest first) as a device
