@@ -164,6 +164,8 @@ class FusedTrainer:
         self._grid_timing_at = int(nat.lib().ngp_grid_encode_backward_fused_timing_offset(
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
             int(enc.align_corners), self._offsets_host))
+        if os.environ.get("NGP_GRID_TIMING", "1") == "0":  # A/B: the kernels without their clock
+            self._grid_timing_at = 0
         if self._grid_timing_at:
             self._grid_flags |= _TIMING
             self.grid_timing_reset()
