@@ -179,6 +179,20 @@ int ngp_sh_encode_backward(const void* grad, const void* inputs, uint32_t B, uin
                            void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* freqencoder                                                              */
+/* ------------------------------------------------------------------------ */
+
+/* freqencoder/src/freqencoder.h:7, freqencoder.cu:97-111
+ * (kernel_freq :30-59). inputs f32 [B, D], outputs f32 [B, C] with
+ * C = D (1 + 2 deg): [x, sin(2^0 x), cos(2^0 x), ..., cos(2^(deg-1) x)]. */
+int ngp_freq_encode_forward(const float* inputs, uint32_t B, uint32_t D, uint32_t deg, uint32_t C,
+                            float* outputs, void* stream);
+/* freqencoder.h:10, freqencoder.cu:114-131 (kernel_freq_backward :63-94). grad f32 [B, C],
+ * outputs the forward's; grad_inputs f32 [B, D] is written (not added to). */
+int ngp_freq_encode_backward(const float* grad, const float* outputs, uint32_t B, uint32_t D,
+                             uint32_t deg, uint32_t C, float* grad_inputs, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* ffmlp (fp16 storage, fp16 MFMA with fp32 accumulation)                   */
 /* ------------------------------------------------------------------------ */
 

@@ -9,8 +9,9 @@ Contents:
   * ctypes bindings to ngp_oracle.c (sequential C restatements of the
     reference CUDA kernels, bit-exact contract with the HIP kernels);
   * numpy restatements of shencoder (values, float32 op order of
-    shencoder.cu:49-121), of the fused MLP (ffmlp.cu layer semantics) and of
-    trunc_exp (activation.py:5-18);
+    shencoder.cu:49-121), of the fused MLP (ffmlp.cu layer semantics), of
+    trunc_exp (activation.py:5-18) and of the frequency encoder
+    (freqencoder.cu:30-94);
   * `pipeline` (oracle/pipeline.py): an end-to-end CPU train step built from
     the above, used for bench.py's cpu_baseline.
 """
@@ -490,3 +491,38 @@ def trunc_exp(x):
 
 def trunc_exp_grad(x, g):
     return np.asarray(g, np.float32) * np.exp(np.clip(np.asarray(x, np.float32), -15, 15))
+
+
+# ---- freqencoder (freqencoder/src/freqencoder.cu) ---------------------------
+
+def freq_encode_forward(inputs, degree):
+    """[B, D] -> [B, D (1 + 2 degree)] (kernel_freq, freqencoder.cu:30-59):
+    [x, sin(2^0 x), sin(2^0 x + pi/2), ..., sin(2^(deg-1) x + pi/2)]. The
+    argument is formed in float32 as the kernel does (scalbnf(x, f) exact, then
+    + float(pi / 2) rounded); the sine itself is evaluated in float64 (the
+    kernel's __sinf approximation is what the tests bound). Also returns the
+    float32 arguments, which the tolerance scales with."""
+    x = np.asarray(inputs, np.float32)
+    B, D = x.shape
+    out, args = [x.astype(np.float64)], [np.zeros_like(x)]
+    half_pi = np.float32(np.pi / 2)
+    for f in range(degree):
+        a = (x * np.float32(2.0 ** f)).astype(np.float32)
+        for ph in (np.float32(0.0), half_pi):
+            arg = (a + ph).astype(np.float32)
+            out.append(np.sin(arg.astype(np.float64)))
+            args.append(arg)
+    return np.concatenate(out, axis=1), np.concatenate(args, axis=1)
+
+
+def freq_encode_backward(grad, outputs, D, degree):
+    """grad_inputs [B, D] = grad[:, :D] + sum_f 2^f (g_sin * out_cos - g_cos *
+    out_sin), from the saved outputs (kernel_freq_backward,
+    freqencoder.cu:63-94), in float64."""
+    g = np.asarray(grad, np.float64)
+    o = np.asarray(outputs, np.float64)
+    r = g[:, :D].copy()
+    for f in range(degree):
+        s = D + 2 * D * f
+        r += 2.0 ** f * (g[:, s:s + D] * o[:, s + D:s + 2 * D] - g[:, s + D:s + 2 * D] * o[:, s:s + D])
+    return r

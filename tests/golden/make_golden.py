@@ -17,6 +17,10 @@ not):
   * get_rays         — nerf/utils.py:52-136 (+ custom_meshgrid :45-49): whole
                        images (N=-1) and random pixel batches (N>0, seeded)
   * nerf_matrix_to_ngp — nerf/provider.py:19-27
+  * FreqEncoder      — encoding.py:5-43 (the reference's pure-torch positional
+                       encoding, the same layout as freqencoder's CUDA op with
+                       max_freq_log2 = degree - 1, N_freqs = degree): outputs
+                       and input grads for a seeded output grad
 
 Only the class / function definitions are extracted (ast) and executed; the
 scripts' module-level CUDA code never runs. Usage:
@@ -191,6 +195,21 @@ def nerf_matrix_fixture():
                         offsets=np.array([a[1] for a in args], np.float32), out=out)
 
 
+def freq_fixture():
+    ns = extract(os.path.join(REF, "encoding.py"), {"FreqEncoder"})
+    g = torch.Generator().manual_seed(13)
+    res = {}
+    for deg in (4, 10):
+        enc = ns["FreqEncoder"](input_dim=3, max_freq_log2=deg - 1, N_freqs=deg, log_sampling=True)
+        x = (torch.rand(257, 3, generator=g) * 2 - 1).requires_grad_(True)
+        y = enc(x)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy)
+        res.update({f"x{deg}": x.detach().numpy(), f"y{deg}": y.detach().numpy(),
+                    f"gy{deg}": gy.numpy(), f"gx{deg}": x.grad.numpy()})
+    np.savez_compressed(os.path.join(HERE, "freq_reference.npz"), **res)
+
+
 if __name__ == "__main__":
     sh_fixture()
     mlp_fixture()
@@ -198,4 +217,5 @@ if __name__ == "__main__":
     renderer_run_fixture()
     get_rays_fixture()
     nerf_matrix_fixture()
+    freq_fixture()
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

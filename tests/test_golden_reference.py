@@ -157,3 +157,42 @@ def test_device_sampler_matches_reference_get_rays(cuda):
         pix = (_rng_u32(seed, draw, np.arange(N, dtype=np.uint32), 1) % np.uint32(H * W)).astype(np.int64)
         np.testing.assert_array_equal(rays_o.cpu().numpy(), f["rays_o"][pose][pix])
         np.testing.assert_allclose(rays_d.cpu().numpy(), f["rays_d"][pose][pix], rtol=0, atol=2e-6)
+
+
+# ---------------------------------------------------------------- freqencoder
+
+def freq_forward_tol(args):
+    """|sin approximation - sin| bound for a float32 argument: a 2^-22
+    absolute floor plus 2^-22 of |arg| (the float32 argument reduction of
+    sin(arg) and of the + pi/2 phase lose |arg| * 2^-24 each)."""
+    return 2.0 ** -22 + np.abs(args.astype(np.float64)) * 2.0 ** -22
+
+
+def freq_backward_tol(gy, args, D, degree, fwd_tol):
+    """Per input: sum over the 2 deg terms of 2^f |grad| times the forward
+    bound of the output it multiplies, plus float32 summation rounding."""
+    tol = np.zeros((gy.shape[0], D))
+    mag = np.abs(gy[:, :D]).astype(np.float64)
+    for f in range(degree):
+        s = D + 2 * D * f
+        gs, gc = np.abs(gy[:, s:s + D]), np.abs(gy[:, s + D:s + 2 * D])
+        tol += 2.0 ** f * (gs * fwd_tol[:, s + D:s + 2 * D] + gc * fwd_tol[:, s:s + D])
+        mag += 2.0 ** f * (gs + gc)
+    return tol + mag * 2.0 ** -21
+
+
+@pytest.mark.parametrize("deg", [4, 10])
+def test_freq_oracle_matches_reference_torch_encoder(deg):
+    """oracle.freq_encode_* (freqencoder.cu:30-94) against the reference's
+    pure-torch FreqEncoder (encoding.py:5-43, cos as torch.cos) and its
+    autograd input gradient."""
+    f = _load("freq_reference.npz")
+    x, y, gy, gx = f[f"x{deg}"], f[f"y{deg}"], f[f"gy{deg}"], f[f"gx{deg}"]
+    out, args = oracle.freq_encode_forward(x, deg)
+    assert out.shape == y.shape == (x.shape[0], 3 * (1 + 2 * deg))
+    tol = freq_forward_tol(args)
+    assert np.array_equal(out[:, :3], x)
+    assert (np.abs(out - y) <= tol).all(), float((np.abs(out - y) / tol).max())
+    gi = oracle.freq_encode_backward(gy, out, 3, deg)
+    btol = freq_backward_tol(gy, args, 3, deg, tol)
+    assert (np.abs(gi - gx) <= btol).all(), float((np.abs(gi - gx) / btol).max())

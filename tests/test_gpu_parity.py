@@ -248,11 +248,28 @@ def _assert_march_equal(ref, got):
 
 
 @pytest.mark.parametrize("N,C,bound,dt_gamma", [(4096, 1, 1.0, 0.0), (1000, 2, 2.0, 1 / 128), (77, 1, 1.0, 0.0),
-                                                (1000, 2, 2.0, 0.0), (600, 3, 4.0, 0.0)])
+                                                (1000, 2, 2.0, 0.0), (600, 3, 4.0, 0.0), (4096, 1, 1.0, 1 / 128),
+                                                (600, 3, 4.0, 1 / 256), (900, 2, 2.0, 0.01), (300, 2, 2.0, 0.5)])
 def test_march_rays_train_bit_exact(cuda, N, C, bound, dt_gamma):
-    # dt_gamma == 0: one wave per ray, 64 speculative segments stitched
-    # (multi-level cascades skip across whole segments); dt_gamma > 0: serial
+    # one wave per ray, 64 speculative segments stitched (multi-level
+    # cascades skip across whole segments); dt_gamma == 0: segment starts in
+    # closed form, dt_gamma > 0: from the wave's records of the bare chain
+    # (0.01: a rounded t * dt_gamma; 0.5: every step at dt_max)
     _assert_march_equal(*_march_case(cuda, N, C, bound, dt_gamma))
+
+
+@pytest.mark.parametrize("dt_gamma,max_steps,density", [(1 / 128, 1024, 0.02), (1 / 128, 1024, 0.3),
+                                                        (1 / 128, 1024, 1.0), (1 / 128, 7, 0.3),
+                                                        (1 / 4096, 16384, 0.3), (1 / 64, 64, 1.0)])
+def test_march_rays_train_gamma_random_bitfields(cuda, dt_gamma, max_steps, density):
+    """dt_gamma > 0 over irregular two-cascade occupancy: re-walks that seek
+    into other lanes' chain records, truncation at max_steps, and (1/4096 with
+    max_steps 16384: dt_min 2.1e-4, ~10K indices to far) chains longer than
+    the 4096 indices the records cover, which the serial walk marches."""
+    rng = np.random.default_rng(int(density * 100) + max_steps)
+    bits = np.packbits(rng.random(2 * 128 ** 3) < density, bitorder="little")
+    _assert_march_equal(*_march_case(cuda, 300, C=2, bound=2.0, dt_gamma=dt_gamma, bits=bits,
+                                     perturb_seed=7, max_steps=max_steps))
 
 
 @pytest.mark.parametrize("density", [0.02, 0.3, 1.0])

@@ -56,6 +56,8 @@ SIGNATURES = {
                            c_vp],
     "ngp_sh_encode_forward": [c_vp, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp],
     "ngp_sh_encode_backward": [c_vp, c_vp, c_u32, c_u32, c_u32, c_vp, c_vp, c_i32, c_vp],
+    "ngp_freq_encode_forward": [c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp],
+    "ngp_freq_encode_backward": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp],
     "ngp_ffmlp_forward": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp,
                           c_vp],
     "ngp_ffmlp_inference": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp,

@@ -309,9 +309,11 @@ NGP_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds_waves, uint32_t&
 // form per binade (advance0), the chain splits into 64 index segments: lane s
 // walks segment s speculatively from its first index, then the true walk is
 // stitched across segments (a walk that reaches an index the speculative walk
-// visited continues identically from there). Exact for every ray; rays the
-// closed form does not cover (dt_gamma > 0, > 64 x 64 chain steps) are
-// marched serially by lane 0 (the reference loop).
+// visited continues identically from there). With dt_gamma > 0 there is no
+// closed form: the wave steps the bare chain first (three VALU operations per
+// index against a probe's ~130 and its LDS/L2 lookups) and keeps every 16th t
+// (ChainGamma). Exact for every ray; chains over 64 x 64 indices are marched
+// serially by lane 0 (the reference loop).
 constexpr uint32_t kMarchThreads = 256;   // rays per k_march_emit group
 constexpr uint32_t kSegWaves = 16;        // rays (waves) per march workgroup
 constexpr uint32_t kSegThreads = kSegWaves * 64;
@@ -471,13 +473,90 @@ NGP_DEV float advance0(float t, uint32_t m, float delta) {
     return t;
 }
 
-// One ray, one wave (dt_gamma == 0 path). Returns the sample count (all lanes).
-template <bool ONE_LEVEL, typename OCC>
-NGP_DEV uint32_t march_ray_segmented(const Ray& r, const MarchConst& k, const OCC& occ, float t0,
-                                     float far, float delta, uint32_t L, float* __restrict__ ts) {
+// The chain t_{k+1} = f(t_k) the walk moves along, two forms:
+//   ChainConst (dt_gamma == 0): f(t) = t + delta, t_i in closed form (advance0);
+//   ChainGamma (dt_gamma > 0):  f(t) = t + clamp(t * dt_gamma, dt_min, dt_max),
+//     no closed form, so the wave steps the chain once up front (wave-uniform,
+//     three dependent VALU operations per index, no memory) and keeps every
+//     16th value in registers: record r = t_{16 r} sits in lane r % 64 of
+//     rec[r / 64], 256 records cover 4096 indices. t_i is then record i / 16
+//     plus i % 16 steps.
+// seek_u(i): t_i for a wave-uniform i (every lane gets it); start(a): t_a for
+// a lane's own a (a multiple of 16 for ChainGamma, all lanes active).
+NGP_DEV float chain_step_g(float t, const MarchConst& k) { return t + clampf(t * k.dt_gamma, k.dt_min, k.dt_max); }
+
+struct ChainConst {
+    float t0, delta;
+    NGP_DEV float step(float t) const { return t + delta; }
+    NGP_DEV float start(uint32_t a) const { return advance0(t0, a, delta); }
+    NGP_DEV float seek_u(uint32_t i) const { return advance0(t0, i, delta); }
+};
+
+constexpr uint32_t kRecStride = 16, kRecRegs = 4;
+constexpr uint32_t kGammaMaxChain = kRecStride * 64 * kRecRegs;  // 4096 = 64 segments x 64
+
+struct ChainGamma {
+    float rec[kRecRegs];
+    MarchConst k;
+    uint32_t nrec;  // records written: ceil(K / 16)
+    NGP_DEV float step(float t) const { return chain_step_g(t, k); }
+    NGP_DEV float start(uint32_t a) const {
+        const uint32_t r = a / kRecStride;
+        // a segment past the chain's end (a >= K) starts at +inf: its walk ends at once
+        float v = __builtin_inff();
+#pragma unroll
+        for (uint32_t j = 0; j < kRecRegs; ++j) {
+            const float x = __shfl(rec[j], (int)(r & 63u), 64);
+            if ((r >> 6) == j && r < nrec) v = x;
+        }
+        return v;  // a % kRecStride == 0 by construction (segment lengths)
+    }
+    NGP_DEV float seek_u(uint32_t i) const {
+        const uint32_t r = i / kRecStride, j = r >> 6;
+        const float base = j == 0 ? rec[0] : j == 1 ? rec[1] : j == 2 ? rec[2] : rec[3];
+        float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(base), (int)(r & 63u)));
+        for (uint32_t m = i % kRecStride; m > 0; --m) t = step(t);
+        return t;
+    }
+};
+
+// Steps the chain from t0 (wave-uniform) and fills the records. Returns the
+// chain length K = the first index with t_K >= far (the walk only visits
+// indices below it), or kInf if K > kGammaMaxChain.
+NGP_DEV uint32_t chain_records(float t0, float far, const MarchConst& k, float (&rec)[kRecRegs]) {
+    const uint32_t lane = threadIdx.x & 63;
+    float t = t0;
+#pragma unroll
+    for (uint32_t j = 0; j < kRecRegs; ++j) {
+        rec[j] = 0.0f;
+        for (uint32_t rr = 0; rr < 64; ++rr) {
+            if (!(t < far)) return (j * 64 + rr) * kRecStride;  // t_{16 r} >= far: K <= 16 r
+            if (lane == rr) rec[j] = t;
+            float u = t;
+#pragma unroll
+            for (uint32_t m = 0; m < kRecStride; ++m) u = chain_step_g(u, k);
+            if (!(u < far)) {  // K in (16 r, 16 r + 16]: find it
+                uint32_t kk = (j * 64 + rr) * kRecStride;
+                while (t < far) {
+                    t = chain_step_g(t, k);
+                    ++kk;
+                }
+                return kk;
+            }
+            t = u;
+        }
+    }
+    return kInf;
+}
+
+// One ray, one wave: the chain splits into 64 index segments of L indices
+// (L <= 64; a multiple of 16 for ChainGamma). Returns the sample count (all lanes).
+template <bool ONE_LEVEL, typename OCC, typename CHAIN>
+NGP_DEV uint32_t march_ray_segmented(const Ray& r, const MarchConst& k, const OCC& occ, const CHAIN& ch,
+                                     float far, uint32_t L, float* __restrict__ ts) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t a = lane * L, b = a + L;
-    const float ta = advance0(t0, a, delta);
+    const float ta = ch.start(a);
     // speculative walk of segment [a, b) from a
     uint64_t vis = 0, occm = 0;
     uint32_t kk = a;
@@ -494,11 +573,11 @@ NGP_DEV uint32_t march_ray_segmented(const Ray& r, const MarchConst& k, const OC
             float tt;
             if (probe<ONE_LEVEL>(r, k, occ, t, s, tt)) {
                 occm |= bit;
-                t += delta;
+                t = ch.step(t);  // == t + s.dt, the reference's occupied step
                 ++kk;
             } else {
                 do {
-                    t += delta;
+                    t = ch.step(t);
                     ++kk;
                 } while (t < tt);
             }
@@ -525,8 +604,12 @@ NGP_DEV uint32_t march_ray_segmented(const Ray& r, const MarchConst& k, const OC
         const bool merged = !inside || ((vis >> (in - a)) & 1ull);
         const uint64_t bad = __ballot(!merged);
         if (!bad) break;
-        if (lane == (uint32_t)__ffsll((unsigned long long)bad) - 1) {  // re-walk from the true entry
-            walk(in, advance0(t0, in, delta));
+        // re-walk the first unmerged segment from its true entry (t of the
+        // entry found wave-uniformly: ChainGamma reads another lane's record)
+        const uint32_t fb = (uint32_t)__ffsll((unsigned long long)bad) - 1;
+        const float tin = ch.seek_u((uint32_t)__builtin_amdgcn_readlane((int)in, (int)fb));
+        if (lane == fb) {
+            walk(in, tin);
             X = t < far ? kk : kInf;
             kend = kk;
             ended = !(t < far);
@@ -541,7 +624,7 @@ NGP_DEV uint32_t march_ray_segmented(const Ray& r, const MarchConst& k, const OC
     if (mine && off < k.max_steps) {
         float tj = ta;
         uint64_t m = mine;
-        for (uint32_t j = 0; m && off < k.max_steps; ++j, tj += delta) {
+        for (uint32_t j = 0; m && off < k.max_steps; ++j, tj = ch.step(tj)) {
             if ((m >> j) & 1ull) {
                 ts[off++] = tj;
                 m &= m - 1;
@@ -555,15 +638,24 @@ template <bool ONE_LEVEL, typename OCC>
 NGP_DEV uint32_t march_ray_wave(const Ray& r, const MarchConst& k, const OCC& occ, float t0, float far,
                                 float* __restrict__ ts) {
     if (!(t0 < far)) return 0;
-    const float delta = clampf(0.0f, k.dt_min, k.dt_max);  // the update when dt_gamma == 0
     if (k.dt_gamma == 0.0f) {
+        const float delta = clampf(0.0f, k.dt_min, k.dt_max);  // the update when dt_gamma == 0
         // every chain step is >= delta - ulp(far); chain length to far bounds
         const float ulp_far = __uint_as_float(((__float_as_uint(far) >> 23) & 0xffu) << 23) * 1.1920929e-7f;
         const double smin = (double)delta - (double)ulp_far;
         if (smin > 0.0) {
             const double kest = ceil(((double)far - (double)t0) / smin) + 2.0;
             const uint32_t L = (uint32_t)ceil(kest / 64.0);
-            if (L <= 64) return march_ray_segmented<ONE_LEVEL>(r, k, occ, t0, far, delta, L, ts);
+            if (L <= 64) return march_ray_segmented<ONE_LEVEL>(r, k, occ, ChainConst{t0, delta}, far, L, ts);
+        }
+    } else if (k.dt_gamma > 0.0f) {
+        ChainGamma ch;
+        ch.k = k;
+        const uint32_t K = chain_records(t0, far, k, ch.rec);
+        if (K != kInf) {
+            ch.nrec = ngp_div_up(K, kRecStride);
+            const uint32_t L = kRecStride * ngp_div_up(ngp_div_up(K, 64u), kRecStride);
+            return march_ray_segmented<ONE_LEVEL>(r, k, occ, ch, far, L > 0 ? L : kRecStride, ts);
         }
     }
     uint32_t n = 0;

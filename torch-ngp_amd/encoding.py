@@ -2,8 +2,9 @@
 
 `get_encoder(name, ...) -> (module, output_dim)` with the reference's keyword
 names. 'hashgrid' / 'tiledgrid' -> gridencoder.GridEncoder, 'sphere_harmonics'
--> shencoder.SHEncoder, 'frequency' -> the pure-torch FreqEncoder below (the
-reference's freqencoder CUDA extension is out of scope, SURVEY §2), 'None' ->
+-> shencoder.SHEncoder, 'frequency' -> freqencoder.FreqEncoder (the gfx950
+kernels, as the reference's :66-69 picks its CUDA extension; the pure-torch
+FreqEncoder below is the reference's own restatement, :5-43), 'None' ->
 identity. The fork's Minkowski encoders are out of scope.
 """
 import torch
@@ -39,8 +40,8 @@ def get_encoder(encoding, input_dim=3, multires=6, degree=4, num_levels=16, leve
     if encoding == "None":
         return lambda x, **kw: x, input_dim
     if encoding == "frequency":
-        encoder = FreqEncoder(input_dim=input_dim, max_freq_log2=multires - 1, N_freqs=multires,
-                              log_sampling=True)
+        from freqencoder import FreqEncoder as _FreqEncoderHIP
+        encoder = _FreqEncoderHIP(input_dim=input_dim, degree=multires)
     elif encoding == "sphere_harmonics":
         from shencoder import SHEncoder
         encoder = SHEncoder(input_dim=input_dim, degree=degree)
