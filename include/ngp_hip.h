@@ -142,6 +142,39 @@ int ngp_march_rays_train_prebuilt_tail(const float* rays_o, const float* rays_d,
                                        const uint32_t* hidden_dims, const uint32_t* num_layers,
                                        void* const* images, void* stream);
 
+/* ngp_march_rays_train_prebuilt_tail whose march launch also carries a
+ * deferred optimizer update (world 1, fused step): the march's workgroups
+ * split into march waves and Adam waves that sweep the parameters while the
+ * march waves probe the occupancy image (a latency-bound LDS chain beside an
+ * HBM stream). job: ngp_fused_optimizer_update's arguments; its scaler check
+ * must already be done (NGP_SCALER_PRECHECKED: the backward's kernels set the
+ * found-inf flag). The batch must come from ngp_fused_step_head (n_nets 0);
+ * the deferred bookkeeping and the MLP packs stay in the emit launch. */
+#define NGP_ADAM_JOB_MAX_TENSORS 8
+typedef struct ngp_adam_job {
+    int32_t n_tensors;
+    float* params[NGP_ADAM_JOB_MAX_TENSORS];
+    void* grads[NGP_ADAM_JOB_MAX_TENSORS];       /* fp16 */
+    float* exp_avg[NGP_ADAM_JOB_MAX_TENSORS];
+    float* exp_avg_sq[NGP_ADAM_JOB_MAX_TENSORS];
+    void* half_params[NGP_ADAM_JOB_MAX_TENSORS]; /* fp16 shadows or NULL */
+    uint64_t sizes[NGP_ADAM_JOB_MAX_TENSORS];
+    float lr, beta1, beta2, eps;
+    int32_t iters, zero_grads;
+    float grad_mult;
+} ngp_adam_job;
+int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const float* rays_d, const uint8_t* grid,
+                                       float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
+                                       uint32_t C, uint32_t H, uint32_t M, const float* nears,
+                                       const float* fars, float* xyzs, float* dirs, float* deltas,
+                                       int32_t* rays, int32_t* counter, const float* noises,
+                                       void* workspace, size_t workspace_bytes, void* state,
+                                       float growth_factor, float backoff_factor, int32_t growth_interval,
+                                       int32_t scaler_enabled, const float* loss_ray, int32_t n_nets,
+                                       const void* const* mlp_weights, const uint32_t* in_dims,
+                                       const uint32_t* hidden_dims, const uint32_t* num_layers,
+                                       void* const* images, const ngp_adam_job* job, void* stream);
+
 /* raymarching.h:14, raymarching.cu:580-588 */
 int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs, const float* deltas,
                                      const int32_t* rays, uint32_t M, uint32_t N, float T_thresh,

@@ -44,6 +44,10 @@ SIGNATURES = {
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
                                            c_vp, c_f32, c_f32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp,
                                            c_vp, c_vp, c_vp],
+    "ngp_march_rays_train_prebuilt_adam": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
+                                           c_vp, c_f32, c_f32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp, c_vp],
     "ngp_march_rays_train": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_composite_rays_train_forward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_vp, c_vp,
@@ -164,6 +168,14 @@ class AdamTable(ctypes.Structure):
                 ("size", ctypes.c_uint64), ("done", c_vp), ("slices", c_vp), ("nslices", c_u32),
                 ("channels", c_u32), ("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32),
                 ("iters", c_i32)]
+
+class AdamJob(ctypes.Structure):
+    """ngp_adam_job (include/ngp_hip.h): the optimizer update a march launch
+    carries (ngp_march_rays_train_prebuilt_adam)."""
+    _fields_ = [("n_tensors", c_i32), ("params", c_vp * 8), ("grads", c_vp * 8), ("exp_avg", c_vp * 8),
+                ("exp_avg_sq", c_vp * 8), ("half_params", c_vp * 8), ("sizes", ctypes.c_uint64 * 8),
+                ("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32), ("iters", c_i32),
+                ("zero_grads", c_i32), ("grad_mult", c_f32)]
 
 _lib = None
 

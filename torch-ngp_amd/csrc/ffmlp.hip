@@ -54,6 +54,9 @@ constexpr int kThreads = kWaves * 64;
 #ifndef NGP_MLP_BWD_WAVES
 #define NGP_MLP_BWD_WAVES 4
 #endif
+#ifndef NGP_MLP_BWD_OVERLAP  // see k_mlp_bwd's chunk loop (0: same-box A/B builds)
+#define NGP_MLP_BWD_OVERLAP 1
+#endif
 constexpr int kBwdWaves = NGP_MLP_BWD_WAVES;
 constexpr int kBwdThreads = kBwdWaves * 64;
 static_assert(kBwdWaves % 2 == 0 && kBwdWaves <= 16, "the dW fold pairs waves (two LDS images)");
@@ -826,30 +829,48 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
             dense<N::MTW, N::KSW>(fr, fwd_desc<W, IN_KS, NH>(q, in_dim).frag0, h[q - 1], a);
             pack_act<N::MTW, N::KSW>(a, act, h[q]);
         }
+        // Per matmul: the transposing tiles are stored, then the next delta's
+        // product (register operands + fragment reads) is issued BEFORE the
+        // dW product that reads the tiles back, so its MFMAs cover the tile
+        // round trip (LDS executes one wave's operations in order, the reads
+        // see the stores). NGP_MLP_BWD_OVERLAP=0: the dW product first.
         // last matmul: dW += dout^T . h[NH]
         write_rows<1, false>(dT, dout, kOut);
         write_rows<N::KSW, true>(hT, h[NH], W);
-        dw_accum<1, N::MTW>(dT, hT, dw_last);
-        half8 d[kNB][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
+#if NGP_MLP_BWD_OVERLAP
         dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
+        dw_accum<1, N::MTW>(dT, hT, dw_last);
+#else
+        dw_accum<1, N::MTW>(dT, hT, dw_last);
+        dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
+#endif
+        half8 d[kNB][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
         pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
 #pragma unroll
         for (int q = NH; q >= 1; --q) {
             write_rows<N::KSW, true>(dT, d, W);
             write_rows<N::KSW, true>(hT, h[q - 1], W);
+#if NGP_MLP_BWD_OVERLAP
+            dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
+            dw_accum<N::MTW, N::MTW>(dT, hT, dw_hid[q - 1]);
+#else
             dw_accum<N::MTW, N::MTW>(dT, hT, dw_hid[q - 1]);
             dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
+#endif
             pack_delta<N::MTW, N::KSW>(a, h[q - 1], act, d);
         }
         // first matmul: dW += d^T . x, and grad_inputs = W_0^T d
         write_rows<N::KSW, true>(dT, d, W);
         write_rows<IN_KS, false>(hT, x, in_dim);
+        f32x4 gi[kNB][N::IN_MT];
+#if NGP_MLP_BWD_OVERLAP
+        if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
         dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
-        if (want_gi) {
-            f32x4 gi[kNB][N::IN_MT];
-            dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
-            gi_out(row0, B, in_dim, gi);
-        }
+#else
+        dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
+        if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
+#endif
+        if (want_gi) gi_out(row0, B, in_dim, gi);
         MSTAMP(2 + min(nst, 9u));
         ++nst;
     }

@@ -432,23 +432,6 @@ struct HeadLaunch {  // the batch + clear parts of k_adam_head
     uint32_t clear16;
 };
 
-TensorList make_list(int n, float* const* p, void* const* g, float* const* m, float* const* v,
-                     void* const* ph, const uint64_t* sizes) {
-    TensorList tl{};
-    tl.n = n;
-    tl.start[0] = 0;
-    for (int k = 0; k < n; ++k) {
-        tl.p[k] = p ? p[k] : nullptr;
-        tl.g[k] = static_cast<ngp_half*>(g[k]);
-        tl.m[k] = m ? m[k] : nullptr;
-        tl.v[k] = v ? v[k] : nullptr;
-        tl.ph[k] = ph ? static_cast<ngp_half*>(ph[k]) : nullptr;
-        tl.size[k] = sizes[k];
-        tl.start[k + 1] = tl.start[k] + (sizes[k] + 7) / 8 * 8;
-    }
-    return tl;
-}
-
 uint32_t sweep_blocks(uint64_t total, uint32_t per_thread) {
     uint64_t b = (total / per_thread + 255) / 256;
     if (b > 8192) b = 8192;

@@ -1,7 +1,7 @@
 // Device code of the fused step's head shared by nerf_fused.hip (its own
 // head launches) and raymarching.hip (the march launch that carries the
-// optimizer update, ngp_fused_march_head): the synthetic Lego sampler and
-// the Adam sweep. Header-only, internal linkage per translation unit.
+// optimizer update, ngp_march_rays_train_prebuilt_adam): the synthetic Lego
+// sampler and the Adam sweep. Header-only, internal linkage per translation unit.
 #pragma once
 #include "ngp_common.h"
 #include "ngp_step.h"
@@ -163,6 +163,23 @@ struct TensorList {
     uint64_t size[kMaxTensors];
     uint64_t start[kMaxTensors + 1];  // flat index space; each tensor starts 8-aligned
 };
+
+static inline TensorList make_list(int n, float* const* p, void* const* g, float* const* m, float* const* v,
+                                   void* const* ph, const uint64_t* sizes) {
+    TensorList tl{};
+    tl.n = n;
+    tl.start[0] = 0;
+    for (int k = 0; k < n; ++k) {
+        tl.p[k] = p ? p[k] : nullptr;
+        tl.g[k] = static_cast<ngp_half*>(g[k]);
+        tl.m[k] = m ? m[k] : nullptr;
+        tl.v[k] = v ? v[k] : nullptr;
+        tl.ph[k] = ph ? static_cast<ngp_half*>(ph[k]) : nullptr;
+        tl.size[k] = sizes[k];
+        tl.start[k + 1] = tl.start[k] + (sizes[k] + 7) / 8 * 8;
+    }
+    return tl;
+}
 
 NGP_DEV int find_tensor(const TensorList& tl, uint64_t i) {
     int k = 0;

@@ -24,6 +24,7 @@
 #include "ffmlp_pack.h"
 #include "ngp_common.h"
 #include "ngp_dpp.h"
+#include "ngp_head.h"
 #include "ngp_step.h"
 
 #include <algorithm>
@@ -494,6 +495,7 @@ struct ChainConst {
 
 constexpr uint32_t kRecStride = 16, kRecRegs = 4;
 constexpr uint32_t kGammaMaxChain = kRecStride * 64 * kRecRegs;  // 4096 = 64 segments x 64
+static_assert(kGammaMaxChain == 64 * 64, "the records cover exactly the indices 64 segments of <= 64 hold");
 
 struct ChainGamma {
     float rec[kRecRegs];
@@ -663,23 +665,42 @@ NGP_DEV uint32_t march_ray_wave(const Ray& r, const MarchConst& k, const OCC& oc
     return (uint32_t)__builtin_amdgcn_readlane((int)n, 0);
 }
 
+// The optimizer update a march launch may carry (ngp_march_rays_train_prebuilt_adam):
+// the march's workgroups keep their 16 waves and their LDS image, waves
+// [0, kMarchAdamWaves) march rays and the rest sweep Adam as virtual
+// 256-thread blocks (adam_sweep has no barriers). The occupancy lookups are an
+// LDS latency chain and Adam an HBM stream: one CU runs both at once.
+struct MarchAdam {
+    ngp_head::TensorList tl;
+    ngp_head::AdamArgs aa;
+    ngp_step::StepState* st;  // null: no Adam in this launch
+};
+constexpr uint32_t kMarchAdamWaves = 8;
+
+template <uint32_t MW>  // march waves per workgroup (kSegWaves: the whole workgroup)
 __global__ void __launch_bounds__(kSegThreads)
 k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
               const uint8_t* __restrict__ grid, const uint8_t* __restrict__ img, OccLayout L,
               MarchConst k, uint32_t N, const float* __restrict__ nears, const float* __restrict__ fars,
               const float* __restrict__ noises, int32_t* __restrict__ rays, float* __restrict__ ts,
-              const int32_t* __restrict__ counter, uint32_t* __restrict__ scan) {
+              const int32_t* __restrict__ counter, uint32_t* __restrict__ scan, MarchAdam ma) {
     extern __shared__ uint4 dyn[];
     // scan[0] = the offset of the first sample (the reference's counter[0] on entry,
     // raymarching.cu:405); scan[4 + n] = ray n's count (read by k_march_emit)
     if (blockIdx.x == 0 && threadIdx.x == 0) scan[0] = (uint32_t)counter[0];
     uint32_t* sum = reinterpret_cast<uint32_t*>(dyn);
     uint32_t* pre = sum + 4 * L.ngroups;
-    const bool lds = L.ngroups > 0 && load_occ_index(img, L, dyn);
+    const bool lds = L.ngroups > 0 && load_occ_index(img, L, dyn);  // every wave copies (one barrier)
+    const uint32_t wave = threadIdx.x >> 6;
+    if (MW < kSegWaves && wave >= MW) {  // the Adam waves (workgroup-uniform split, no barrier follows)
+        constexpr uint32_t kVirt = (kSegWaves - MW) / 4;  // 256-thread virtual blocks per workgroup
+        ngp_head::adam_sweep(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4, gridDim.x * kVirt,
+                             threadIdx.x & 255u);
+        return;
+    }
     const OccLds occ_lds{sum, pre, reinterpret_cast<const uint8_t*>(pre + L.ngroups)};
     const OccGlobal occ_glb{grid};
-    const uint32_t wave = threadIdx.x >> 6;
-    for (uint32_t n = blockIdx.x * kSegWaves + wave; n < N; n += gridDim.x * kSegWaves) {
+    for (uint32_t n = blockIdx.x * MW + wave; n < N; n += gridDim.x * MW) {
         const Ray r = load_ray(rays_o, rays_d, n);
         const float t0 = ray_t0(nears[n], noises[n], k);
         const float far = fars[n];
@@ -699,6 +720,7 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
         }
     }
 }
+static_assert((kSegWaves - kMarchAdamWaves) % 4 == 0, "Adam waves form 256-thread virtual blocks");
 
 // Grid (ray groups of 256, kEmitSplit): each workgroup sums the counts of all
 // rays before its group (a few thousand coalesced L2 reads), scans the
@@ -1103,7 +1125,8 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
                              uint32_t H, uint32_t M, const float* nears, const float* fars,
                              float* xyzs, float* dirs, float* deltas, int32_t* rays, int32_t* counter,
                              const float* noises, void* workspace, size_t workspace_bytes,
-                             bool build_image, void* stream, const EmitTail* tail = nullptr) {
+                             bool build_image, void* stream, const EmitTail* tail = nullptr,
+                             const MarchAdam* ma = nullptr) {
     if (int e = check_cascade(C, H, max_steps)) return e;
     NGP_REQUIRE(rays && counter, NGP_ERR_ARG, "march_rays_train: null rays/counter");
     if (N == 0) return NGP_OK;
@@ -1127,8 +1150,13 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
         k_occ_count<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
         k_occ_compact<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
     }
-    k_march_train<<<blocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
-        rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan);
+    if (ma && ma->st) {  // every CU gets a workgroup: the Adam waves sweep 1/gridDim of the parameters each
+        k_march_train<kMarchAdamWaves><<<kMaxMarchBlocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
+            rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan, *ma);
+    } else {
+        k_march_train<kSegWaves><<<blocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
+            rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan, MarchAdam{});
+    }
     EmitTail et{};
     if (tail) et = *tail;
     et.groups = groups;
@@ -1204,6 +1232,49 @@ extern "C" int ngp_march_rays_train_prebuilt_tail(const float* rays_o, const flo
     return march_train_impl(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, M, nears, fars,
                             xyzs, dirs, deltas, rays, counter, noises, workspace, workspace_bytes, false,
                             stream, &tail);
+}
+
+extern "C" int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const float* rays_d,
+                                                  const uint8_t* grid, float bound, float dt_gamma,
+                                                  uint32_t max_steps, uint32_t N, uint32_t C, uint32_t H,
+                                                  uint32_t M, const float* nears, const float* fars,
+                                                  float* xyzs, float* dirs, float* deltas, int32_t* rays,
+                                                  int32_t* counter, const float* noises, void* workspace,
+                                                  size_t workspace_bytes, void* state, float growth_factor,
+                                                  float backoff_factor, int32_t growth_interval,
+                                                  int32_t scaler_enabled, const float* loss_ray, int32_t n_nets,
+                                                  const void* const* mlp_weights, const uint32_t* in_dims,
+                                                  const uint32_t* hidden_dims, const uint32_t* num_layers,
+                                                  void* const* images, const ngp_adam_job* job, void* stream) {
+    NGP_REQUIRE(state && loss_ray && job, NGP_ERR_ARG, "march_rays_train_prebuilt_adam: null state, loss_ray or job");
+    NGP_REQUIRE(job->n_tensors >= 1 && job->n_tensors <= ngp_head::kMaxTensors, NGP_ERR_ARG,
+                "march_rays_train_prebuilt_adam: 1..%d tensors", ngp_head::kMaxTensors);
+    for (int q = 0; q < job->n_tensors; ++q) {
+        NGP_REQUIRE(((reinterpret_cast<uintptr_t>(job->params[q]) | reinterpret_cast<uintptr_t>(job->exp_avg[q]) |
+                      reinterpret_cast<uintptr_t>(job->exp_avg_sq[q])) & 15) == 0 &&
+                        (reinterpret_cast<uintptr_t>(job->grads[q]) & 7) == 0 &&
+                        (reinterpret_cast<uintptr_t>(job->half_params[q]) & 7) == 0,
+                    NGP_ERR_ARG, "march_rays_train_prebuilt_adam: tensor %d misaligned", q);
+    }
+    EmitTail tail{};
+    tail.st = static_cast<ngp_step::StepState*>(state);
+    tail.sa = ngp_step::ScalerArgs{growth_factor, backoff_factor, growth_interval, scaler_enabled,
+                                   N ? 1.0f / (float)N : 0.0f};
+    tail.loss_ray = loss_ray;
+    tail.n_rays = N;
+    if (n_nets > 0)
+        if (int e = ngp_pack::build_jobs(n_nets, mlp_weights, in_dims, hidden_dims, num_layers, images, tail.jobs))
+            return e;
+    MarchAdam ma{};
+    ma.tl = ngp_head::make_list(job->n_tensors, job->params, job->grads, job->exp_avg, job->exp_avg_sq,
+                                job->half_params, job->sizes);
+    // the bookkeeping is deferred to the emit tail (defer_end)
+    ma.aa = ngp_head::AdamArgs{job->lr, job->beta1, job->beta2, job->eps, job->iters, job->zero_grads,
+                               job->grad_mult, 1};
+    ma.st = tail.st;
+    return march_train_impl(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, M, nears, fars,
+                            xyzs, dirs, deltas, rays, counter, noises, workspace, workspace_bytes, false,
+                            stream, &tail, &ma);
 }
 
 extern "C" int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs,

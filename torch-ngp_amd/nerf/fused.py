@@ -233,6 +233,21 @@ class FusedTrainer:
         # (grid backward, MLP dW reduce) into this flag: the optimizer's found-inf
         # flag (world 1) or the data-parallel guard's per-rank flag
         self._inf_flag = nat.lib().ngp_fused_inf_flag(nat.ptr(self.state), int(self.dp))
+        # World 1: the pending Adam rides in the march launch (its workgroups'
+        # Adam waves stream the parameters while the march waves probe the
+        # occupancy image); the step head then only draws the batch.
+        # NGP_MARCH_ADAM=0: Adam in the head launch, before the march.
+        self._march_adam = (self._merge_head and not self.fused_adam
+                            and os.environ.get("NGP_MARCH_ADAM", "0") != "0")
+        if self._march_adam:
+            o, job = self._opt, nat.AdamJob()
+            job.n_tensors = o["n"]
+            for q in range(o["n"]):
+                job.params[q], job.grads[q], job.exp_avg[q] = o["params"][q], o["grads"][q], o["m"][q]
+                job.exp_avg_sq[q], job.half_params[q], job.sizes[q] = o["v"][q], o["half"][q], o["sizes"][q]
+            job.lr, job.beta1, job.beta2, job.eps = self.lr, self.betas[0], self.betas[1], self.eps
+            job.iters, job.zero_grads, job.grad_mult = self.iters, 1, 1.0
+            self._job = job
         self.graph = None
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
@@ -512,8 +527,13 @@ class FusedTrainer:
         sample -> march -> network forward/backward. With an update pending,
         Adam and the batch draw share one launch and the deferred scaler
         bookkeeping + MLP packs ride in the march's emit launch (12 launches
-        instead of 13; NGP_FUSED_SPLIT_HEAD=1 keeps them apart)."""
-        if pending and self._merge_head:
+        instead of 13; NGP_FUSED_SPLIT_HEAD=1 keeps them apart). By default
+        (NGP_MARCH_ADAM) Adam runs inside the march launch instead, beside the
+        march waves, and the head launch only draws the batch."""
+        if pending and self._march_adam:
+            self._sample(nets=0)  # the MLP packs need Adam's fp16 weights: emit tail
+            self._march(tail=True, adam=True)
+        elif pending and self._merge_head:
             self._optimizer_head()
             self._march(tail=True)
         else:
@@ -591,7 +611,7 @@ class FusedTrainer:
             dist.all_gather_into_tensor(full, shard.cpu())
             self.flat_param.copy_(full)
 
-    def _sample(self):
+    def _sample(self, nets=None):
         """The step head: batch of N rays (rays, RGBA target, background, march
         noise, near/far), the pending bookkeeping of a deferred optimizer
         update, and both networks' MLP fragment images, in one launch."""
@@ -599,7 +619,8 @@ class FusedTrainer:
         m, d, pk = self.model, self.data, self._pk
         # data parallel: the fp16 weights are still being all-gathered while
         # the batch is drawn, so the networks are packed in _network instead
-        nets = 0 if self.dp else 2
+        if nets is None:
+            nets = 0 if self.dp else 2
         nat.check(lib.ngp_fused_step_head(P(d.poses), d.poses.shape[0], self._intr, d.H, d.W, self.N,
                                           self._boxes, self._nboxes, self._aabb, float(m.min_near), self.seed,
                                           P(self.state), P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
@@ -616,14 +637,19 @@ class FusedTrainer:
         self._march()
         self._network()
 
-    def _march(self, tail=False):
+    def _march(self, tail=False, adam=False):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         m, M, N, cnt = self.model, self.M, self.N, P(self.counter)
         args = (P(self.rays_o), P(self.rays_d), P(m.density_bitfield), float(m.bound), self.dt_gamma,
                 self.max_steps, N, m.cascade, m.grid_size, M, P(self.nears), P(self.fars), P(self.xyzs),
                 P(self.dirs), P(self.deltas), P(self.rays), cnt, P(self.noises), P(self.march_ws),
                 self.march_ws.numel())
-        if tail:  # + the deferred scaler bookkeeping and the MLP packs (see _body)
+        if adam:  # + the pending Adam (march launch) and the bookkeeping + MLP packs (emit launch)
+            pk = self._pk
+            nat.check(lib.ngp_march_rays_train_prebuilt_adam(
+                *args, P(self.state), 2.0, 0.5, self.growth_interval, 1, P(self.loss_ray), 2, pk["w"], pk["ins"],
+                pk["hid"], pk["nl"], pk["img"], ctypes.byref(self._job), s), "march_rays_train_adam")
+        elif tail:  # + the deferred scaler bookkeeping and the MLP packs (see _body)
             pk = self._pk
             nat.check(lib.ngp_march_rays_train_prebuilt_tail(
                 *args, P(self.state), 2.0, 0.5, self.growth_interval, 1, P(self.loss_ray), 2, pk["w"], pk["ins"],
