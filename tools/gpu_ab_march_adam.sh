@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_e2e_oracle.py tests/test_gpu_rccl.py \
+NGP_MARCH_ADAM=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_e2e_oracle.py tests/test_gpu_rccl.py \
     -x -v --timeout 200 --timeout-method thread > $O/t.log 2>&1
 bash tools/ab_env.sh $TAG/env "NGP_MARCH_ADAM=0" "NGP_MARCH_ADAM=1" 2 > $O/env_ab.txt 2>&1
 for i in 1 2; do

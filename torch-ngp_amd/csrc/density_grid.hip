@@ -78,8 +78,8 @@ NGP_DEV float rng_unit(uint32_t seed, uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // Point p of cascade p / ppc. coords: [P, 3] cell coordinates, or null for
-// every cell of each cascade in the reference's meshgrid(x, y, z, 'ij') order
-// (ppc = H^3). noise: [P, 3] uniform [0, 1).
+// every cell of each cascade (ppc = H^3), whose noise rows are in the
+// reference's meshgrid(x, y, z, 'ij') order. noise: [P, 3] uniform [0, 1).
 __global__ void __launch_bounds__(256)
 k_density_points(const int32_t* __restrict__ coords, const float* __restrict__ noise, uint32_t P, uint32_t ppc,
                  uint32_t H, CascadeScales cs, float* __restrict__ xyzs, int32_t* __restrict__ indices) {
@@ -87,15 +87,30 @@ k_density_points(const int32_t* __restrict__ coords, const float* __restrict__ n
     if (p >= P) return;
     const uint32_t cas = p / ppc;
     uint32_t c[3];
+    size_t q = p;  // the draw's row of this point (noise)
     if (coords) {
         c[0] = (uint32_t)coords[(size_t)p * 3];
         c[1] = (uint32_t)coords[(size_t)p * 3 + 1];
         c[2] = (uint32_t)coords[(size_t)p * 3 + 2];
     } else {
+        // every cell of the cascade: point i is the cell of Morton code i, so
+        // a wave's 64 points form a 4x4x4 brick and their coarse levels'
+        // corners share cache lines in the query's grid forward (row order
+        // of the points: meshgrid, as the reference's draws, :521-533, read
+        // from the cell's meshgrid row)
+        // (H a power of two, where the Morton codes below H^3 are exactly the
+        // cube's cells; otherwise meshgrid order)
         const uint32_t i = p - cas * ppc;
-        c[0] = i / (H * H);
-        c[1] = (i / H) % H;
-        c[2] = i % H;
+        if ((H & (H - 1)) == 0) {
+            c[0] = compact_bits(i);
+            c[1] = compact_bits(i >> 1);
+            c[2] = compact_bits(i >> 2);
+            q = (size_t)cas * ppc + ((size_t)c[0] * H + c[1]) * H + c[2];
+        } else {
+            c[0] = i / (H * H);
+            c[1] = (i / H) % H;
+            c[2] = i % H;
+        }
     }
     // xyzs = 2 * coords.float() / (H - 1) - 1 (tensor / scalar: times the fp32 reciprocal)
     const float inv = 1.0f / (float)(H - 1);
@@ -106,7 +121,7 @@ k_density_points(const int32_t* __restrict__ coords, const float* __restrict__ n
         x = x * inv;
         x = x - 1.0f;
         x = x * s;                                  // cas_xyzs = xyzs * (bound - hgs)
-        const float n = noise[(size_t)p * 3 + k];
+        const float n = noise[q * 3 + k];
         float j = n * 2.0f;                         // (rand * 2 - 1) * hgs
         j = j - 1.0f;
         j = j * h;

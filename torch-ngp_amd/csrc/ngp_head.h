@@ -201,13 +201,18 @@ struct AdamArgs {
 // in Adam's last block instead of k_step_end was measured: 4096 blocks
 // retiring through one counter cost ~180 us of contended atomics.)
 //
-// Layout: chunks of kAdamChunk elements of the flat (8-aligned per tensor)
-// index space, chunk c to block c mod gridDim; every thread keeps two 16-byte
+// Layout: chunks of 1024 U elements of the flat (8-aligned per tensor)
+// index space, chunk c to block c mod gridDim; every thread keeps U 16-byte
 // groups of each stream in flight. A chunk inside one tensor (all but the few
 // at the seams) takes its pointers from scalar loads.
 constexpr uint32_t kAdamThreads = 256, kAdamChunk = kAdamThreads * 8;
+// U: 16-byte groups of each stream per thread and chunk (chunk = 1024 U
+// elements). The standalone sweep keeps 2 in flight; the sweep inside the
+// march launch (a quarter of a CU's waves) keeps 4 to stream at HBM rate.
+template <int U = 2>
 NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const AdamArgs& aa, uint32_t blk,
                         uint32_t nblk, uint32_t tid) {
+    constexpr uint32_t kChunk = kAdamThreads * 4 * U;
     const ngp_step::AdamConsts ac = ngp_step::adam_consts(st, aa.base_lr, aa.beta1, aa.beta2, aa.iters,
                                                           aa.grad_mult);
     const bool skip = st->found_inf != 0 || ac.inv_bad;
@@ -220,30 +225,33 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
         ngp_step::adam_update(p, m, v, gh, ac, aa.beta1, aa.beta2, aa.eps);
     };
     const uint64_t total = tl.start[tl.n];
-    const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
+    const uint64_t nchunks = (total + kChunk - 1) / kChunk;
     for (uint64_t c = blk; c < nchunks; c += nblk) {
-        const uint64_t c0 = c * kAdamChunk, c1 = min(c0 + kAdamChunk, total);
+        const uint64_t c0 = c * kChunk, c1 = min(c0 + kChunk, total);
         const int k = find_tensor(tl, c0);
         if (find_tensor(tl, c1 - 1) == k && c1 - tl.start[k] <= tl.size[k]) {
-            // whole chunk inside tensor k: two float4 groups per thread, loads first
+            // whole chunk inside tensor k: U float4 groups per thread, loads first
             const uint64_t base = c0 - tl.start[k] + tid * 4;
-            float4 pv[2], mv[2], vv[2];
-            half4 gh[2];
-            bool in[2];
+            float4 pv[U], mv[U], vv[U];
+            half4 gh[U];
+            bool in[U];
+            // loads without branches: a group past the chunk's end reads the
+            // chunk's first group and is dropped (a load under a divergent
+            // branch made the compiler wait for each one before the next)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const uint64_t off = base + u * (kAdamChunk / 2);
+            for (int u = 0; u < U; ++u) {
+                const uint64_t off = base + u * (kChunk / U);
                 in[u] = c0 + (off - (c0 - tl.start[k])) < c1;
-                if (!in[u]) continue;
-                pv[u] = *reinterpret_cast<const float4*>(tl.p[k] + off);
-                mv[u] = *reinterpret_cast<const float4*>(tl.m[k] + off);
-                vv[u] = *reinterpret_cast<const float4*>(tl.v[k] + off);
-                gh[u] = *reinterpret_cast<const half4*>(tl.g[k] + off);
+                const uint64_t lo = in[u] ? off : c0 - tl.start[k];
+                pv[u] = *reinterpret_cast<const float4*>(tl.p[k] + lo);
+                mv[u] = *reinterpret_cast<const float4*>(tl.m[k] + lo);
+                vv[u] = *reinterpret_cast<const float4*>(tl.v[k] + lo);
+                gh[u] = *reinterpret_cast<const half4*>(tl.g[k] + lo);
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < U; ++u) {
                 if (!in[u]) continue;
-                const uint64_t off = base + u * (kAdamChunk / 2);
+                const uint64_t off = base + u * (kChunk / U);
                 if (!skip) {
                     adam1(pv[u].x, mv[u].x, vv[u].x, (float)gh[u][0]);
                     adam1(pv[u].y, mv[u].y, vv[u].y, (float)gh[u][1]);

@@ -675,7 +675,10 @@ struct MarchAdam {
     ngp_head::AdamArgs aa;
     ngp_step::StepState* st;  // null: no Adam in this launch
 };
-constexpr uint32_t kMarchAdamWaves = 8;
+#ifndef NGP_MARCH_ADAM_WAVES  // march waves of a march + Adam workgroup (same-box A/B builds)
+#define NGP_MARCH_ADAM_WAVES 4
+#endif
+constexpr uint32_t kMarchAdamWaves = NGP_MARCH_ADAM_WAVES;
 
 template <uint32_t MW>  // march waves per workgroup (kSegWaves: the whole workgroup)
 __global__ void __launch_bounds__(kSegThreads)
@@ -694,8 +697,8 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
     const uint32_t wave = threadIdx.x >> 6;
     if (MW < kSegWaves && wave >= MW) {  // the Adam waves (workgroup-uniform split, no barrier follows)
         constexpr uint32_t kVirt = (kSegWaves - MW) / 4;  // 256-thread virtual blocks per workgroup
-        ngp_head::adam_sweep(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4, gridDim.x * kVirt,
-                             threadIdx.x & 255u);
+        ngp_head::adam_sweep<4>(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4, gridDim.x * kVirt,
+                                threadIdx.x & 255u);
         return;
     }
     const OccLds occ_lds{sum, pre, reinterpret_cast<const uint8_t*>(pre + L.ngroups)};

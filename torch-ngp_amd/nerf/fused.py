@@ -238,7 +238,7 @@ class FusedTrainer:
         # occupancy image); the step head then only draws the batch.
         # NGP_MARCH_ADAM=0: Adam in the head launch, before the march.
         self._march_adam = (self._merge_head and not self.fused_adam
-                            and os.environ.get("NGP_MARCH_ADAM", "0") != "0")
+                            and os.environ.get("NGP_MARCH_ADAM", "1") != "0")
         if self._march_adam:
             o, job = self._opt, nat.AdamJob()
             job.n_tensors = o["n"]
