@@ -162,6 +162,8 @@ typedef struct ngp_adam_job {
     float lr, beta1, beta2, eps;
     int32_t iters, zero_grads;
     float grad_mult;
+    void* clear;            /* zeroed by the launch too (the grid backward's bin cursors), or NULL */
+    uint32_t clear_bytes;   /* multiple of 16, clear 16-byte aligned */
 } ngp_adam_job;
 int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const float* rays_d, const uint8_t* grid,
                                        float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
@@ -351,6 +353,38 @@ int ngp_grid_encode_backward_fused_reduce(const void* grad, const float* xyz, fl
                                           const uint32_t* mlp_Bs, const uint32_t* in_dims,
                                           const uint32_t* hidden_dims, const uint32_t* num_layers,
                                           void* const* grad_weights, int32_t* mlp_nonfinite, void* stream);
+/* The fused step's next batch (ngp_fused_step_head's sampler arguments),
+ * drawn by ngp_grid_encode_backward_fused_reduce_batch while this batch's
+ * backward runs: the batch buffers are dead once the composite has read its
+ * targets. The draw records this batch's counts (step_counter) without
+ * resetting the counter, which the backward still reads; the accumulate
+ * resets it. */
+typedef struct ngp_batch_job {
+    const float* poses;
+    uint32_t n_poses;
+    const float* intrinsics4;
+    uint32_t H, W, N;
+    const float* boxes;
+    int32_t nboxes;
+    const float* aabb6;
+    float min_near;
+    uint32_t seed;
+    void* state;
+    float *rays_o, *rays_d, *rgba, *bg, *nears, *fars, *noises;
+    int32_t *counter, *step_counter;
+} ngp_batch_job;
+/* ngp_grid_encode_backward_fused_reduce + the next batch (job) as another
+ * column of blocks of the bin launch. Requires a binned plan. */
+int ngp_grid_encode_backward_fused_reduce_batch(const void* grad, const float* xyz, float bound,
+                                                const int32_t* offsets, void* grad_embeddings, uint32_t B,
+                                                const int32_t* count, uint32_t D, uint32_t C, uint32_t L,
+                                                float S, uint32_t H, uint32_t gridtype, int32_t align_corners,
+                                                uint32_t interp, const int32_t* offsets_host, void* workspace,
+                                                size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
+                                                int32_t n_nets, void* const* mlp_workspaces, const uint32_t* mlp_Bs,
+                                                const uint32_t* in_dims, const uint32_t* hidden_dims,
+                                                const uint32_t* num_layers, void* const* grad_weights,
+                                                int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream);
 /* Fused Adam over the hash table (world 1; torch.optim.Adam + GradScaler of
  * nerf/utils.py:975-978 / main_nerf.py:194 on the table, inside the grid
  * backward). The table's fp32 parameters and Adam moments are double

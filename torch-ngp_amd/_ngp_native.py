@@ -48,6 +48,10 @@ SIGNATURES = {
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
                                            c_vp, c_f32, c_f32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp,
                                            c_vp, c_vp, c_vp, c_vp],
+    "ngp_grid_encode_backward_fused_reduce_batch": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32,
+                                                    c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz,
+                                                    c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                    c_vp, c_vp],
     "ngp_march_rays_train": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_composite_rays_train_forward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_vp, c_vp,
@@ -175,7 +179,16 @@ class AdamJob(ctypes.Structure):
     _fields_ = [("n_tensors", c_i32), ("params", c_vp * 8), ("grads", c_vp * 8), ("exp_avg", c_vp * 8),
                 ("exp_avg_sq", c_vp * 8), ("half_params", c_vp * 8), ("sizes", ctypes.c_uint64 * 8),
                 ("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32), ("iters", c_i32),
-                ("zero_grads", c_i32), ("grad_mult", c_f32)]
+                ("zero_grads", c_i32), ("grad_mult", c_f32), ("clear", c_vp), ("clear_bytes", c_u32)]
+
+
+class BatchJob(ctypes.Structure):
+    """ngp_batch_job (include/ngp_hip.h): the fused step's next batch, drawn by
+    ngp_grid_encode_backward_fused_reduce_batch."""
+    _fields_ = [("poses", c_vp), ("n_poses", c_u32), ("intrinsics4", c_vp), ("H", c_u32), ("W", c_u32),
+                ("N", c_u32), ("boxes", c_vp), ("nboxes", c_i32), ("aabb6", c_vp), ("min_near", c_f32),
+                ("seed", c_u32), ("state", c_vp), ("rays_o", c_vp), ("rays_d", c_vp), ("rgba", c_vp), ("bg", c_vp),
+                ("nears", c_vp), ("fars", c_vp), ("noises", c_vp), ("counter", c_vp), ("step_counter", c_vp)]
 
 _lib = None
 

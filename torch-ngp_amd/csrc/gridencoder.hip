@@ -22,6 +22,7 @@
 //   * a hashed level's size is a power of two: the modulo becomes a mask.
 #include "ngp_common.h"
 #include "ngp_dpp.h"
+#include "ngp_head.h"
 #include "ngp_reduce.h"
 #include "ngp_step.h"
 #include <stdlib.h>
@@ -661,6 +662,17 @@ __device__ unsigned long long* g_stamps;
 #define BSTAMP(slot) do { } while (0)
 #endif
 
+// The next batch of the fused step drawn as one more column of the bin
+// launch (ngp_grid_encode_backward_fused_reduce_batch): nlego blocks of the
+// sampler (ngp_head::lego_rays_block), counter kept (the accumulate resets it)
+struct BinLego {
+    ngp_head::LegoScene sc;
+    ngp_head::LegoOut out;
+    const float* poses;
+    ngp_step::StepState* st;
+    uint32_t N, nlego;
+};
+
 template <uint32_t D, uint32_t NBMAX>
 __global__ void __launch_bounds__(kBinPts, 8)  // 4 workgroups per CU: <= 64 VGPRs
 k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
@@ -668,7 +680,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
                InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
                int32_t grad_layout, int32_t* __restrict__ nonfinite, ngp_reduce::ReduceJobs rj, uint32_t nred,
-               uint32_t* __restrict__ timing) {
+               uint32_t* __restrict__ timing, BinLego next_batch) {
     constexpr uint32_t C = 2, NC = 1u << D, NW = kBinPts / 64;
     constexpr uint32_t BPT = (NBMAX + kBinPts - 1) / kBinPts;  // bins per thread in the reservation step
     __shared__ uint32_t cnt[NBMAX], soff[NBMAX + 1], wsum[NW];
@@ -689,9 +701,16 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // the extra column of blocks (x == nlev): the MLP dW slab reduce, which
     // neither needs nor feeds this kernel (one launch less per step; the same
     // fixed summation order as k_slab_reduce, ngp_reduce.h)
+    // and the column after it (x == nlev + (nred != 0)): the next batch's
+    // sampler blocks, when the launch carries it
     if (blockIdx.x >= bp.nlev) {
-        if (blockIdx.y < nred)
-            ngp_reduce::slab_reduce_block<ngp_half, kBinPts>(rj, blockIdx.y, reinterpret_cast<float(*)[64]>(stage));
+        if (nred && blockIdx.x == bp.nlev) {
+            if (blockIdx.y < nred)
+                ngp_reduce::slab_reduce_block<ngp_half, kBinPts>(rj, blockIdx.y, reinterpret_cast<float(*)[64]>(stage));
+        } else if (blockIdx.y < next_batch.nlego) {
+            const BinLego& q = next_batch;
+            ngp_head::lego_rays_block(blockIdx.y, q.nlego, q.poses, q.sc, q.N, q.st, q.out);
+        }
         return;
     }
     // the grid covers the row capacity; workgroups past the marched sample
@@ -1040,7 +1059,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
                  const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
                  bool external, AccAdam ad, unsigned long long* __restrict__ msums,
-                 uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing) {
+                 uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing,
+                 int32_t* __restrict__ reset_counter) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     // [entry][channel]; a channel-planar image (8-byte lane stride for the
     // 64-bit atomics instead of 16) measured the same
@@ -1061,6 +1081,9 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     __shared__ uint32_t s_lastunit;
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t nlev = bp.nlev;
+    // the sample counter of the batch whose backward this is, once every
+    // kernel that reads it has finished (the bin launch drew the next batch)
+    if (reset_counter && blockIdx.x == 0 && t < 2) reset_counter[t] = 0;
     // the first group of this thread's bin counts (step 1 below) is loaded
     // before anything else: its round trip overlaps the plan's LDS copy
     constexpr uint32_t kStep1Loads = 4;
@@ -1930,12 +1953,17 @@ extern "C" size_t ngp_grid_encode_backward_fused_counter_bytes(uint32_t B, uint3
 }
 
 namespace {
+__global__ void __launch_bounds__(256)
+k_lego_draw(BinLego bl) {
+    ngp_head::lego_rays_block(blockIdx.x, bl.nlego, bl.poses, bl.sc, bl.N, bl.st, bl.out);
+}
+
 int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_t* offsets, void* grad_embeddings,
                    uint32_t B, const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
                    uint32_t gridtype, int32_t align_corners, uint32_t interp, const int32_t* offsets_host,
                    void* workspace, size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
                    const AccAdam& ad, void* stream, const ngp_reduce::ReduceJobs* rj = nullptr,
-                   uint32_t nred = 0) {
+                   uint32_t nred = 0, const BinLego* blp = nullptr) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
     const bool zeroed = (grad_layout & NGP_GRID_GRAD_ZEROED) != 0;
     const bool external = (grad_layout & NGP_GRID_CURSORS_EXTERNAL) != 0;
@@ -1972,29 +2000,33 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         // (level, point block) + one column of slab-reduce blocks when merged
         const ngp_reduce::ReduceJobs rjv = rj ? *rj : ngp_reduce::ReduceJobs{};
         if (!rj) nred = 0;
-        const dim3 grid(bp.nlev + (nred ? 1u : 0u), std::max(ngp_div_up(B, kBinPts), nred));
+        // + one column of the next batch's sampler blocks (blp, fully binned plans only)
+        const BinLego bl = blp && bp.nlev == L ? *blp : BinLego{};
+        const dim3 grid(bp.nlev + (nred ? 1u : 0u) + (bl.nlego ? 1u : 0u),
+                        std::max(std::max(ngp_div_up(B, kBinPts), nred), bl.nlego));
         uint32_t nbmax = 0;
         for (uint32_t l = 0; l < bp.nlev; ++l) nbmax = std::max(nbmax, bp.nbins[l]);
         if (nbmax <= kMaxBinsPerLevel)
             k_grid_bwd_bin<3, kMaxBinsPerLevel><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing);
+                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl);
         else
             k_grid_bwd_bin<3, kMaxBinsPerLevelBig><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing);
+                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl);
         // two persistent workgroups per CU while both fit the CU's LDS (the
         // 64 KiB image + two words per bin), else one
         const size_t dyn = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
         const uint32_t per_cu = 2 * (dyn + kAccStaticLds) <= 160 * 1024 ? 2u : 1u;
+        int32_t* reset = bl.nlego ? bl.out.counter : nullptr;
         if (zeroed)
             k_grid_bin_accum<true><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
-                marrive, timing);
+                marrive, timing, reset);
         else
             k_grid_bin_accum<false><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
-                marrive, timing);
+                marrive, timing, reset);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
@@ -2011,6 +2043,12 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
             const uint32_t blocks = (uint32_t)std::min<size_t>(ngp_div_up(e1 - e0, 256), 4096);
             k_flag_nonfinite<<<blocks, 256, 0, st>>>((const ngp_half*)grad_embeddings + e0, e1 - e0, nonfinite);
         }
+    }
+    if (blp && !(bp.nlev && bp.nlev == L)) {  // not carried by a bin launch: the draw after the backward
+        BinLego b2 = *blp;
+        b2.out.keep_counter = 0;
+        b2.nlego = ngp_div_up(b2.N, 256);
+        k_lego_draw<<<b2.nlego, 256, 0, st>>>(b2);
     }
     return ngp_check_launch("grid_encode_backward_fused");
 }
@@ -2076,6 +2114,52 @@ extern "C" int ngp_grid_encode_backward_fused_reduce(const void* grad, const flo
     return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                           align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
                           AccAdam{}, stream, &rj, nred);
+}
+
+extern "C" int ngp_grid_encode_backward_fused_reduce_batch(
+    const void* grad, const float* xyz, float bound, const int32_t* offsets, void* grad_embeddings, uint32_t B,
+    const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
+    int32_t align_corners, uint32_t interp, const int32_t* offsets_host, void* workspace, size_t workspace_bytes,
+    int32_t grad_layout, int32_t* nonfinite, int32_t n_nets, void* const* mlp_workspaces, const uint32_t* mlp_Bs,
+    const uint32_t* in_dims, const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* grad_weights,
+    int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream) {
+    NGP_REQUIRE(job && job->state && job->counter && job->poses && job->N > 0 && job->n_poses > 0, NGP_ERR_ARG,
+                "grid_encode_backward_fused_reduce_batch: incomplete batch job");
+    NGP_REQUIRE(job->nboxes >= 0 && job->nboxes <= ngp_head::kMaxBoxes, NGP_ERR_ARG,
+                "grid_encode_backward_fused_reduce_batch: at most %d boxes", ngp_head::kMaxBoxes);
+    NGP_REQUIRE(n_nets >= 1 && n_nets <= ngp_reduce::kMaxReduceJobs && mlp_workspaces && mlp_Bs && in_dims &&
+                    hidden_dims && num_layers && grad_weights,
+                NGP_ERR_ARG, "grid_encode_backward_fused_reduce_batch: 1..%d networks with their arguments",
+                ngp_reduce::kMaxReduceJobs);
+    BinLego bl{};
+    bl.sc = ngp_head::make_scene(job->n_poses, job->intrinsics4, job->H, job->W, job->boxes, job->nboxes,
+                                 job->aabb6, job->min_near, job->seed);
+    bl.out = ngp_head::LegoOut{job->rays_o, job->rays_d, job->rgba, job->bg, job->nears, job->fars, job->noises,
+                               job->counter, job->step_counter, 1};
+    bl.poses = job->poses;
+    bl.st = static_cast<ngp_step::StepState*>(job->state);
+    bl.N = job->N;
+    bl.nlego = ngp_div_up(job->N, kBinPts);
+    ngp_reduce::ReduceJobs rj{};
+    const uint32_t nred = ngp_reduce::build_reduce_jobs(n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims,
+                                                        num_layers, grad_weights, mlp_nonfinite, rj);
+    bool binned = false;
+    if (workspace && offsets_host && C == 2 && D == 3 && L >= 1 && L <= kMaxLevels) {
+        GridLevels lv;
+        make_levels(lv, L, S, H);
+        binned = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B).nlev > 0;
+    }
+    if (!binned) {  // no bin launch to carry the reduce: it goes first, on its own
+        if (int e = ngp_ffmlp_reduce(n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims, num_layers, grad_weights,
+                                     NGP_DTYPE_F16, mlp_nonfinite, stream))
+            return e;
+        return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
+                              align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout,
+                              nonfinite, AccAdam{}, stream, nullptr, 0, &bl);
+    }
+    return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
+                          align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
+                          AccAdam{}, stream, &rj, nred, &bl);
 }
 
 extern "C" int ngp_grid_encode_backward_fused_adam(const void* grad, const float* xyz, float bound,

@@ -438,24 +438,6 @@ uint32_t sweep_blocks(uint64_t total, uint32_t per_thread) {
     return b ? (uint32_t)b : 1u;
 }
 
-LegoScene make_scene(uint32_t n_poses, const float* intrinsics4, uint32_t H, uint32_t W, const float* boxes,
-                     int32_t nboxes, const float* aabb6, float min_near, uint32_t seed) {
-    LegoScene sc{};
-    for (int b = 0; b < nboxes; ++b)
-        for (int k = 0; k < 3; ++k) {
-            sc.lo[b][k] = boxes[b * 9 + k];
-            sc.hi[b][k] = boxes[b * 9 + 3 + k];
-            sc.rgb[b][k] = boxes[b * 9 + 6 + k];
-        }
-    sc.nboxes = nboxes;
-    sc.fx = intrinsics4[0]; sc.fy = intrinsics4[1]; sc.cx = intrinsics4[2]; sc.cy = intrinsics4[3];
-    sc.H = H; sc.W = W; sc.n_poses = n_poses;
-    for (int k = 0; k < 6; ++k) sc.aabb[k] = aabb6[k];
-    sc.min_near = min_near;
-    sc.seed = seed;
-    return sc;
-}
-
 DbTable make_db(const ngp_adam_table* at) {
     DbTable db{};
     if (!at) return db;

@@ -63,7 +63,30 @@ NGP_DEV void near_far(const float o[3], const float d[3], const float aabb[6], f
 struct LegoOut {
     float *rays_o, *rays_d, *rgba, *bg, *nears, *fars, *noises;
     int32_t *counter, *step_counter;
+    // the draw runs while the previous batch's kernels may still read the
+    // counter (the next batch drawn in the grid backward's bin launch): its
+    // counts are recorded but the counter is left to the accumulate to reset
+    int32_t keep_counter;
 };
+
+static inline LegoScene make_scene(uint32_t n_poses, const float* intrinsics4, uint32_t H, uint32_t W,
+                                   const float* boxes, int32_t nboxes, const float* aabb6, float min_near,
+                                   uint32_t seed) {
+    LegoScene sc{};
+    for (int b = 0; b < nboxes; ++b)
+        for (int k = 0; k < 3; ++k) {
+            sc.lo[b][k] = boxes[b * 9 + k];
+            sc.hi[b][k] = boxes[b * 9 + 3 + k];
+            sc.rgb[b][k] = boxes[b * 9 + 6 + k];
+        }
+    sc.nboxes = nboxes;
+    sc.fx = intrinsics4[0]; sc.fy = intrinsics4[1]; sc.cx = intrinsics4[2]; sc.cy = intrinsics4[3];
+    sc.H = H; sc.W = W; sc.n_poses = n_poses;
+    for (int k = 0; k < 6; ++k) sc.aabb[k] = aabb6[k];
+    sc.min_near = min_near;
+    sc.seed = seed;
+    return sc;
+}
 
 // Ray n of draw `it` (the fused sampler, reference get_rays utils.py:52-136 +
 // the analytic target + background + march noise + near/far): writes the
@@ -121,8 +144,10 @@ NGP_DEV void lego_begin(uint32_t it, const LegoOut& out) {
         out.step_counter[slot * 2] = out.counter[0];
         out.step_counter[slot * 2 + 1] = out.counter[1];
     }
-    out.counter[0] = 0;
-    out.counter[1] = 0;
+    if (!out.keep_counter) {
+        out.counter[0] = 0;
+        out.counter[1] = 0;
+    }
 }
 
 // End of a draw: after the whole workgroup has read `draw`, its first thread

@@ -674,6 +674,8 @@ struct MarchAdam {
     ngp_head::TensorList tl;
     ngp_head::AdamArgs aa;
     ngp_step::StepState* st;  // null: no Adam in this launch
+    uint4* clear;             // also zeroed (the grid backward's bin cursors), or null
+    uint32_t clear16;
 };
 #ifndef NGP_MARCH_ADAM_WAVES  // march waves of a march + Adam workgroup (same-box A/B builds)
 #define NGP_MARCH_ADAM_WAVES 4
@@ -697,6 +699,8 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
     const uint32_t wave = threadIdx.x >> 6;
     if (MW < kSegWaves && wave >= MW) {  // the Adam waves (workgroup-uniform split, no barrier follows)
         constexpr uint32_t kVirt = (kSegWaves - MW) / 4;  // 256-thread virtual blocks per workgroup
+        if (blockIdx.x == 0 && wave == MW)
+            for (uint32_t i = threadIdx.x & 63u; i < ma.clear16; i += 64) ma.clear[i] = uint4{0u, 0u, 0u, 0u};
         ngp_head::adam_sweep<4>(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4, gridDim.x * kVirt,
                                 threadIdx.x & 255u);
         return;
@@ -1275,6 +1279,10 @@ extern "C" int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const flo
     ma.aa = ngp_head::AdamArgs{job->lr, job->beta1, job->beta2, job->eps, job->iters, job->zero_grads,
                                job->grad_mult, 1};
     ma.st = tail.st;
+    NGP_REQUIRE(job->clear_bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(job->clear) & 15) == 0, NGP_ERR_ARG,
+                "march_rays_train_prebuilt_adam: clear must be 16-byte aligned, a multiple of 16 bytes");
+    ma.clear = static_cast<uint4*>(job->clear);
+    ma.clear16 = job->clear ? job->clear_bytes / 16 : 0u;
     return march_train_impl(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, M, nears, fars,
                             xyzs, dirs, deltas, rays, counter, noises, workspace, workspace_bytes, false,
                             stream, &tail, &ma);

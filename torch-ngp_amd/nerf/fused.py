@@ -248,6 +248,26 @@ class FusedTrainer:
             job.lr, job.beta1, job.beta2, job.eps = self.lr, self.betas[0], self.betas[1], self.eps
             job.iters, job.zero_grads, job.grad_mult = self.iters, 1, 1.0
             self._job = job
+        # ... and the next batch is drawn while this step's grid backward runs
+        # (a column of the bin launch; the batch buffers are dead once the
+        # composite has read its targets), so the step starts with the march:
+        # no head launch. The march + Adam launch clears the bin cursors.
+        # NGP_DRAW_AHEAD=0: the head launch draws the batch.
+        self._draw_ahead = (self._march_adam and not self._split_reduce
+                            and os.environ.get("NGP_DRAW_AHEAD", "1") != "0")
+        self._ahead = False  # the batch buffers hold the next step's batch
+        if self._draw_ahead:
+            self._job.clear, self._job.clear_bytes = nat.ptr(self.grid_ws), self._grid_counter_bytes
+            m_, d_, bj = self.model, self.data, nat.BatchJob()
+            bj.poses, bj.n_poses, bj.intrinsics4 = nat.ptr(d_.poses), d_.poses.shape[0], ctypes.addressof(self._intr)
+            bj.H, bj.W, bj.N = d_.H, d_.W, self.N
+            bj.boxes, bj.nboxes, bj.aabb6 = ctypes.addressof(self._boxes), self._nboxes, ctypes.addressof(self._aabb)
+            bj.min_near, bj.seed, bj.state = float(m_.min_near), self.seed, nat.ptr(self.state)
+            bj.rays_o, bj.rays_d, bj.rgba, bj.bg = (nat.ptr(self.rays_o), nat.ptr(self.rays_d), nat.ptr(self.rgba),
+                                                    nat.ptr(self.bg))
+            bj.nears, bj.fars, bj.noises = nat.ptr(self.nears), nat.ptr(self.fars), nat.ptr(self.noises)
+            bj.counter, bj.step_counter = nat.ptr(self.counter), nat.ptr(m_.step_counter)
+            self._batch_job = bj
         self.graph = None
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
@@ -467,6 +487,9 @@ class FusedTrainer:
         step_counter slot it % 16 when batch it + 1 was drawn (n <= 16)."""
         assert 1 <= n <= 16
         draw = self.state.view(torch.int32)[self._S_DRAW].long()
+        if self._ahead:  # the next batch is drawn: the newest count went to step_counter too
+            k = torch.arange(n - 1, -1, -1, device=self.dev)
+            return self.model.step_counter[(draw - 2 - k) & 15, 0].long()
         k = torch.arange(n - 1, 0, -1, device=self.dev)
         old = self.model.step_counter[(draw - 1 - k) & 15, 0].long()
         return torch.cat([old, self.counter[:1].long()])
@@ -531,7 +554,8 @@ class FusedTrainer:
         (NGP_MARCH_ADAM) Adam runs inside the march launch instead, beside the
         march waves, and the head launch only draws the batch."""
         if pending and self._march_adam:
-            self._sample(nets=0)  # the MLP packs need Adam's fp16 weights: emit tail
+            if not self._ahead:
+                self._sample(nets=0)  # the MLP packs need Adam's fp16 weights: emit tail
             self._march(tail=True, adam=True)
         elif pending and self._merge_head:
             self._optimizer_head()
@@ -539,9 +563,16 @@ class FusedTrainer:
         else:
             if pending:
                 self._optimizer(defer=True)
-            self._sample()
+            if self._ahead:  # the batch is drawn: the head's other parts (packs, cursor clear)
+                lib, pk = nat.lib(), self._pk
+                nat.check(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"],
+                                             nat.stream_of(self.rays_o)), "ffmlp_pack")
+                if self._grid_counter_bytes:
+                    self.grid_ws[:self._grid_counter_bytes].zero_()
+            else:
+                self._sample()
             self._march()
-        self._network()
+        self._network(draw=self._draw_ahead)
 
     def _optimizer_head(self):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
@@ -617,6 +648,7 @@ class FusedTrainer:
         update, and both networks' MLP fragment images, in one launch."""
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         m, d, pk = self.model, self.data, self._pk
+        self._ahead = False  # this draw replaces a batch drawn ahead (and resets the counter)
         # data parallel: the fp16 weights are still being all-gathered while
         # the batch is drawn, so the networks are packed in _network instead
         if nets is None:
@@ -658,7 +690,7 @@ class FusedTrainer:
             nat.check(lib.ngp_march_rays_train_prebuilt(*args, s), "march_rays_train")
         self._tick("march_rays_train")
 
-    def _network(self):
+    def _network(self, draw=False):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         m, e = self.model, self.enc
         M, N, cnt = self.M, self.N, P(self.counter)
@@ -722,6 +754,13 @@ class FusedTrainer:
                     "grid_backward_fused_adam")
             else:
                 chk(lib.ngp_grid_encode_backward_fused(*bargs, s), "grid_backward_fused")
+        elif draw:
+            # + the next step's batch, as another column of the bin launch
+            chk(lib.ngp_grid_encode_backward_fused_reduce_batch(*bargs, 2, pk["ws"], pk["B"], pk["ins"], pk["hid"],
+                                                                pk["nl"], pk["gw"], self._inf_flag,
+                                                                ctypes.byref(self._batch_job), s),
+                "grid_backward_fused_reduce_batch")
+            self._ahead = True
         else:
             # the MLP dW reduce rides in the grid backward's bin launch (same sums)
             chk(lib.ngp_grid_encode_backward_fused_reduce(*bargs, 2, pk["ws"], pk["B"], pk["ins"], pk["hid"],
@@ -870,7 +909,8 @@ class FusedTrainer:
         return int(self._state_i()[6].item())
 
     def sample_count(self):
-        return int(self.counter[0].item())
+        """Samples of the last step's batch."""
+        return int(self._recent_counts(1)[0].item())
 
     # ------------------------------------------------------ checkpoints
     # StepState as int32 words: 0 scale (f32), 4 growth tracker, 6 Adam steps,
@@ -911,7 +951,9 @@ class FusedTrainer:
                                                            "checkpoints": [], "best_result": None},
                  "mean_count": self.mean_count, "mean_density": self.mean_density,
                  "model": m.state_dict(),
-                 "fused": {"draw": int(si[self._S_DRAW])}}
+                 # draw: batches drawn; ahead: the last of them is the next step's (drawn during
+                 # the last backward, NGP_DRAW_AHEAD), which a restored trainer draws again
+                 "fused": {"draw": int(si[self._S_DRAW]), "ahead": int(self._ahead)}}
         if full:
             m1, m2 = self._moments()
             # param indices follow model.get_params: encoder [0], sigma_net [1], encoder_dir [], color_net [2]
@@ -957,8 +999,15 @@ class FusedTrainer:
         si[self._S_ITER] = int(state.get("global_step", 0))
         if self.fused_adam:  # the accumulate's tags are iteration numbers: none may match the restored ones
             self.bin_done.zero_()
+        self._ahead = False
         if "fused" in state:
-            si[self._S_DRAW] = int(state["fused"]["draw"])
+            draw = int(state["fused"]["draw"])
+            if state["fused"].get("ahead"):
+                # redraw the saved trainer's next batch (same draw index, so the same
+                # rays); its draw re-records the last step's counts from the counter
+                draw -= 1
+                self.counter.copy_(self.model.step_counter[(draw - 1) & 15])
+            si[self._S_DRAW] = draw
         if "optimizer" in state:
             st = state["optimizer"]["state"]
             for i, (a, p) in enumerate(zip(self._starts, self.params)):
