@@ -36,10 +36,14 @@ def main(tag, out=None):
     name = lambda i: rows[i]["Kernel_Name"] if i < len(rows) else ""  # noqa: E731
     # a step starts with k_adam_head (merged optimizer + batch launch) or, with
     # NGP_FUSED_SPLIT_HEAD=1 / older builds, k_adam_multi followed by k_step_head
-    # or (NGP_MARCH_ADAM, Adam inside the march launch) k_step_head alone
+    # or (NGP_MARCH_ADAM, Adam inside the march launch) k_step_head alone, or
+    # (NGP_DRAW_AHEAD: the batch drawn in the previous bin launch) the march +
+    # Adam launch k_march_train<4> itself
     starts = [i for i in range(spin) if "k_adam_head" in name(i) or
               ("k_adam_multi" in name(i) and "k_step_head" in name(i + 1)) or
-              ("k_step_head" in name(i) and "k_adam_multi" not in name(i - 1) and "k_march_train" in name(i + 1))]
+              ("k_step_head" in name(i) and "k_adam_multi" not in name(i - 1) and "k_march_train" in name(i + 1)) or
+              ("k_march_train<" in name(i) and "k_march_train<16" not in name(i) and
+               "k_step_head" not in name(i - 1))]
     sel = starts[-steps:]
     per = collections.defaultdict(list)
     spans = []

@@ -311,6 +311,102 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
     }
 }
 
+// adam_sweep software-pipelined for few waves (the sweep inside the march
+// launch: 12 of a CU's waves): the loads of this block's next chunk are
+// issued before the current chunk is computed and stored, so every wave keeps
+// a chunk's worth of loads in flight all the time (the plain sweep waits out a
+// full memory round trip per chunk; ~4 chunks per block left it at 80 % of
+// the standalone sweep's bandwidth). Same arithmetic, same stores.
+template <int U>
+NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, const AdamArgs& aa, uint32_t blk,
+                             uint32_t nblk, uint32_t tid) {
+    constexpr uint32_t kChunk = kAdamThreads * 4 * U;
+    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    const ngp_step::AdamConsts ac = ngp_step::adam_consts(st, aa.base_lr, aa.beta1, aa.beta2, aa.iters,
+                                                          aa.grad_mult);
+    const bool skip = st->found_inf != 0 || ac.inv_bad;
+    if (blk == 0 && tid == 0) {
+        if (ac.inv_bad) st->found_inf = 1;
+        if (aa.defer_end) st->end_pending = 1;
+    }
+    const uint64_t total = tl.start[tl.n];
+    const uint64_t nchunks = (total + kChunk - 1) / kChunk;
+    struct Buf {
+        float4 p[U], m[U], v[U];
+        half4 g[U];
+    };
+    // the chunk's tensor if the chunk lies inside one, else -1 (a seam)
+    auto whole = [&](uint64_t c) {
+        const uint64_t c0 = c * kChunk, c1 = min(c0 + kChunk, total);
+        const int k = find_tensor(tl, c0);
+        return find_tensor(tl, c1 - 1) == k && c1 - tl.start[k] <= tl.size[k] ? k : -1;
+    };
+    auto load = [&](uint64_t c, int k, Buf& b) {  // unconditional: past the end reads the chunk's first group
+        const uint64_t c0 = c * kChunk, c1 = min(c0 + kChunk, total), first = c0 - tl.start[k];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t off = first + tid * 4 + u * (kChunk / U);
+            const uint64_t lo = off + tl.start[k] < c1 ? off : first;
+            b.p[u] = *reinterpret_cast<const float4*>(tl.p[k] + lo);
+            b.m[u] = *reinterpret_cast<const float4*>(tl.m[k] + lo);
+            b.v[u] = *reinterpret_cast<const float4*>(tl.v[k] + lo);
+            b.g[u] = *reinterpret_cast<const half4*>(tl.g[k] + lo);
+        }
+    };
+    auto apply = [&](uint64_t c, int k, Buf& b) {
+        const uint64_t c0 = c * kChunk, c1 = min(c0 + kChunk, total), first = c0 - tl.start[k];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t off = first + tid * 4 + u * (kChunk / U);
+            if (off + tl.start[k] >= c1) continue;
+            if (!skip) {
+                ngp_step::adam_update(b.p[u].x, b.m[u].x, b.v[u].x, (float)b.g[u][0], ac, aa.beta1, aa.beta2, aa.eps);
+                ngp_step::adam_update(b.p[u].y, b.m[u].y, b.v[u].y, (float)b.g[u][1], ac, aa.beta1, aa.beta2, aa.eps);
+                ngp_step::adam_update(b.p[u].z, b.m[u].z, b.v[u].z, (float)b.g[u][2], ac, aa.beta1, aa.beta2, aa.eps);
+                ngp_step::adam_update(b.p[u].w, b.m[u].w, b.v[u].w, (float)b.g[u][3], ac, aa.beta1, aa.beta2, aa.eps);
+                *reinterpret_cast<float4*>(tl.p[k] + off) = b.p[u];
+                *reinterpret_cast<float4*>(tl.m[k] + off) = b.m[u];
+                *reinterpret_cast<float4*>(tl.v[k] + off) = b.v[u];
+                if (tl.ph[k])
+                    *reinterpret_cast<half4*>(tl.ph[k] + off) =
+                        half4{(ngp_half)b.p[u].x, (ngp_half)b.p[u].y, (ngp_half)b.p[u].z, (ngp_half)b.p[u].w};
+            }
+            if (aa.zero_grads) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
+        }
+    };
+    auto seam = [&](uint64_t c) {  // per element (the few chunks across a tensor boundary)
+        const uint64_t c0 = c * kChunk, c1 = min(c0 + kChunk, total);
+        for (uint64_t i = c0 + tid; i < c1; i += kAdamThreads) {
+            const int kk = find_tensor(tl, i);
+            const uint64_t off = i - tl.start[kk];
+            if (off >= tl.size[kk]) continue;
+            if (!skip) {
+                float p = tl.p[kk][off], m = tl.m[kk][off], v = tl.v[kk][off];
+                ngp_step::adam_update(p, m, v, (float)tl.g[kk][off], ac, aa.beta1, aa.beta2, aa.eps);
+                tl.p[kk][off] = p;
+                tl.m[kk][off] = m;
+                tl.v[kk][off] = v;
+                if (tl.ph[kk]) tl.ph[kk][off] = (ngp_half)p;
+            }
+            if (aa.zero_grads) tl.g[kk][off] = (ngp_half)0.0f;
+        }
+    };
+    Buf a{}, b{};
+    uint64_t c = blk;
+    int ka = c < nchunks ? whole(c) : -1;
+    if (ka >= 0) load(c, ka, a);
+    while (c < nchunks) {
+        const uint64_t cn = c + nblk;
+        const int kb = cn < nchunks ? whole(cn) : -1;
+        if (kb >= 0) load(cn, kb, b);  // in flight while this chunk computes
+        if (ka >= 0) apply(c, ka, a);
+        else seam(c);
+        a = b;
+        ka = kb;
+        c = cn;
+    }
+}
+
 // ---- the double-buffered hash table (fused Adam, ngp_adam_table) --------------
 struct DbTable {
     float* p[2];

@@ -681,6 +681,12 @@ struct MarchAdam {
 #define NGP_MARCH_ADAM_WAVES 4
 #endif
 constexpr uint32_t kMarchAdamWaves = NGP_MARCH_ADAM_WAVES;
+#ifndef NGP_MARCH_ADAM_PIPE  // the Adam waves' sweep: software-pipelined (1) or plain (0)
+#define NGP_MARCH_ADAM_PIPE 1
+#endif
+#ifndef NGP_MARCH_ADAM_U     // 16-byte groups per stream, thread and chunk
+#define NGP_MARCH_ADAM_U 2
+#endif
 
 template <uint32_t MW>  // march waves per workgroup (kSegWaves: the whole workgroup)
 __global__ void __launch_bounds__(kSegThreads)
@@ -701,8 +707,13 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
         constexpr uint32_t kVirt = (kSegWaves - MW) / 4;  // 256-thread virtual blocks per workgroup
         if (blockIdx.x == 0 && wave == MW)
             for (uint32_t i = threadIdx.x & 63u; i < ma.clear16; i += 64) ma.clear[i] = uint4{0u, 0u, 0u, 0u};
-        ngp_head::adam_sweep<4>(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4, gridDim.x * kVirt,
-                                threadIdx.x & 255u);
+#if NGP_MARCH_ADAM_PIPE
+        ngp_head::adam_sweep_pipe<NGP_MARCH_ADAM_U>(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4,
+                                                    gridDim.x * kVirt, threadIdx.x & 255u);
+#else
+        ngp_head::adam_sweep<NGP_MARCH_ADAM_U>(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4,
+                                               gridDim.x * kVirt, threadIdx.x & 255u);
+#endif
         return;
     }
     const OccLds occ_lds{sum, pre, reinterpret_cast<const uint8_t*>(pre + L.ngroups)};
