@@ -191,13 +191,13 @@ __host__ __device__ inline MatDesc bwd_desc(int q, uint32_t in_dim) {
     return m;
 }
 
-// acc[nb][mt] = A(frags) · B[nb] (NB column blocks of 16 samples)
-template <int MT, int KS, int NB>
-NGP_DEV void dense(const half8* __restrict__ lds, uint32_t frag0, const half8 (&b)[NB][KS],
-                   f32x4 (&acc)[NB][MT]) {
+// acc[nb][mt] = A(frags) · B[nb]
+template <int MT, int KS>
+NGP_DEV void dense(const half8* __restrict__ lds, uint32_t frag0, const half8 (&b)[kNB][KS],
+                   f32x4 (&acc)[kNB][MT]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int nb = 0; nb < kNB; ++nb)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[nb][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -206,16 +206,16 @@ NGP_DEV void dense(const half8* __restrict__ lds, uint32_t frag0, const half8 (&
         for (int s = 0; s < KS; ++s) {
             const half8 a = lds[(frag0 + mt * KS + s) * 64 + lane];
 #pragma unroll
-            for (int nb = 0; nb < NB; ++nb) acc[nb][mt] = mfma(a, b[nb][s], acc[nb][mt]);
+            for (int nb = 0; nb < kNB; ++nb) acc[nb][mt] = mfma(a, b[nb][s], acc[nb][mt]);
         }
     }
 }
 
 // accumulator tiles -> activation -> permuted B operand of the next product
-template <int MT, int KS, typename ACT, int NB>
-NGP_DEV void pack_act(const f32x4 (&acc)[NB][MT], ACT act, half8 (&out)[NB][KS]) {
+template <int MT, int KS, typename ACT>
+NGP_DEV void pack_act(const f32x4 (&acc)[kNB][MT], ACT act, half8 (&out)[kNB][KS]) {
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int nb = 0; nb < kNB; ++nb)
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             half8 v;
@@ -229,12 +229,12 @@ NGP_DEV void pack_act(const f32x4 (&acc)[NB][MT], ACT act, half8 (&out)[NB][KS])
 }
 
 // load a [rows, width] fp16 row-major block as natural-K B operands
-template <int KS, int NB>
+template <int KS>
 NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
-                       half8 (&out)[NB][KS]) {
+                       half8 (&out)[kNB][KS]) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
+    for (int nb = 0; nb < kNB; ++nb) {
         const uint32_t row = row0 + nb * 16 + c;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -250,9 +250,9 @@ NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_
 
 // First-layer input loaders (natural-K B operands).
 struct InRowMajor {  // [B, width] row-major
-    template <int KS, int NB>
+    template <int KS>
     NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
-                            half8 (&out)[NB][KS]) const {
+                            half8 (&out)[kNB][KS]) const {
         load_rows<KS>(src, width, row0, B, out);
     }
 };
@@ -262,12 +262,12 @@ struct InRowMajor {  // [B, width] row-major
 // group read 64 contiguous bytes per pair.
 struct InPairMajor {
     uint32_t ld;  // allocated rows
-    template <int KS, int NB>
+    template <int KS>
     NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
-                            half8 (&out)[NB][KS]) const {
+                            half8 (&out)[kNB][KS]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
+        for (int nb = 0; nb < kNB; ++nb) {
             const uint32_t row = row0 + nb * 16 + c;
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
@@ -288,12 +288,12 @@ struct InPairMajor {
 };
 
 // store accumulator tiles (optionally activated) as fp16 rows [row][16 mt + 4g .. +3]
-template <int MT, typename ACT, int NB>
+template <int MT, typename ACT>
 NGP_DEV void store_tiles(ngp_half* __restrict__ dst, uint32_t width, uint32_t row0, uint32_t B,
-                         const f32x4 (&acc)[NB][MT], ACT act) {
+                         const f32x4 (&acc)[kNB][MT], ACT act) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
+    for (int nb = 0; nb < kNB; ++nb) {
         const uint32_t row = row0 + nb * 16 + c;
         if (row >= B) continue;
 #pragma unroll
@@ -569,11 +569,11 @@ k_nerf_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img_s, co
 // K slot j of lane group g holds sample perm_unit(g, j) in BOTH operands.
 typedef short short4v __attribute__((ext_vector_type(4)));
 
-template <int KS, bool PERM, int NB>
-NGP_DEV void write_rows(ngp_half* __restrict__ tile, const half8 (&v)[NB][KS], uint32_t units) {
+template <int KS, bool PERM>
+NGP_DEV void write_rows(ngp_half* __restrict__ tile, const half8 (&v)[kNB][KS], uint32_t units) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
+    for (int nb = 0; nb < kNB; ++nb) {
         ngp_half* row = tile + (nb * 16 + c) * kTileLd;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -604,35 +604,10 @@ NGP_DEV half8 read_tr(const ngp_half* __restrict__ tile, int m) {
                                    0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// the same operand over the chunk's first 16 samples only (a K = 16 MFMA)
-NGP_DEV half4 read_tr_lo(const ngp_half* __restrict__ tile, int m) {
-    const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const ngp_half* a = tile + (4 * g + q) * kTileLd + 16 * m + 4 * p;
-    return __builtin_bit_cast(half4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                         (__attribute__((address_space(3))) short4v*)(a)));
-}
-
-// dW[o][i] (MO x MI tiles of 16x16) += dT^T . hT over the chunk (NB = 1: its
-// 16 samples, v_mfma_f32_16x16x16_f16; the K slots of lane group g are samples
-// 4g..4g+3 in both operands, and the accumulator layout is the same)
-template <int MO, int MI, int NB = kNB>
+// dW[o][i] (MO x MI tiles of 16x16) += dT^T . hT over the chunk
+template <int MO, int MI>
 NGP_DEV void dw_accum(const ngp_half* __restrict__ dT, const ngp_half* __restrict__ hT,
                       f32x4 (&acc)[MO][MI]) {
-    if constexpr (NB == 1) {
-        half4 a[MO], b[MI];
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int m = 0; m < MO; ++m) a[m] = read_tr_lo(dT, m);
-#pragma unroll
-        for (int n = 0; n < MI; ++n) b[n] = read_tr_lo(hT, n);
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int m = 0; m < MO; ++m)
-#pragma unroll
-            for (int n = 0; n < MI; ++n)
-                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x16f16(a[m], b[n], acc[m][n], 0, 0, 0);
-        return;
-    }
     half8 a[MO], b[MI];
     // the transposed reads are opaque intrinsics on an LDS address-space cast:
     // keep the compiler from moving them across the wave's own tile stores
@@ -650,11 +625,11 @@ NGP_DEV void dw_accum(const ngp_half* __restrict__ dT, const ngp_half* __restric
 }
 
 // delta (C layout, MT tiles) * act'(post-activation h, permuted B form) -> permuted B form
-template <int MT, int KS, typename ACT, int NB>
-NGP_DEV void pack_delta(const f32x4 (&acc)[NB][MT], const half8 (&h)[NB][KS], ACT act,
-                        half8 (&out)[NB][KS]) {
+template <int MT, int KS, typename ACT>
+NGP_DEV void pack_delta(const f32x4 (&acc)[kNB][MT], const half8 (&h)[kNB][KS], ACT act,
+                        half8 (&out)[kNB][KS]) {
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int nb = 0; nb < kNB; ++nb)
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             half8 v;
@@ -730,20 +705,20 @@ struct BwdLds {
 // gradient, written by the composite kernel).
 struct GiStore {
     ngp_half* gi;
-    template <int IN_MT, int NB>
-    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[NB][IN_MT]) const {
+    template <int IN_MT>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[kNB][IN_MT]) const {
         store_tiles<IN_MT>(gi, in_dim, row0, B, t, ActNone{});
     }
 };
 
 struct GiNerfGeo {
     ngp_half* gh;
-    template <int IN_MT, int NB>
-    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t, const f32x4 (&t)[NB][IN_MT]) const {
+    template <int IN_MT>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t, const f32x4 (&t)[kNB][IN_MT]) const {
         static_assert(IN_MT == 2, "the color network input is 32 wide");  // see launch_bwd
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
+        for (int nb = 0; nb < kNB; ++nb) {
             // lane group g holds input columns 16 + 4g .. +3 (tile 1); output
             // columns 4g .. 4g+3 take input columns 15 + 4g .. 18 + 4g
             const ngp_half r0 = (ngp_half)t[nb][1][0], r1 = (ngp_half)t[nb][1][1], r2 = (ngp_half)t[nb][1][2];
@@ -766,11 +741,11 @@ struct GiNerfGeo {
 struct GiPairMajor {
     ngp_half* gi;
     uint32_t ld;
-    template <int IN_MT, int NB>
-    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[NB][IN_MT]) const {
+    template <int IN_MT>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[kNB][IN_MT]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
+        for (int nb = 0; nb < kNB; ++nb) {
             const uint32_t row = row0 + nb * 16 + c;
             if (row >= B) continue;
 #pragma unroll
@@ -808,22 +783,14 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
 
     MSTAMP(0);
-    // Work split: the rows form U = ceil(B / 16) units of 16 samples and wave q
-    // takes the contiguous units [q U / Wt, (q + 1) U / Wt): every wave gets
-    // floor or ceil of U / Wt, which it runs as 32-sample chunks plus, for an
-    // odd count, one 16-sample chunk (NB = 1). Dealing 32-sample chunks round
-    // robin gave some waves 3 chunks and others 2 (Lego: 2528 chunks over 1024
-    // waves), a third of the loop in imbalance.
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t U = ngp_div_up(B, 16u);
-    const uint64_t Wt = (uint64_t)gridDim.x * kBwdWaves, qw = (uint64_t)blockIdx.x * kBwdWaves + wave;
-    uint32_t u = (uint32_t)(qw * U / Wt);
-    const uint32_t u1 = (uint32_t)((qw + 1) * U / Wt);
     // the first chunk's inputs and output grads are requested before the
     // fragment image copy, so the two latencies overlap
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t stride = gridDim.x * kBwdWaves;
+    uint32_t chunk = blockIdx.x * kBwdWaves + wave;
     half8 xn[kNB][IN_KS], dn[kNB][1];
-    xl.template operator()<IN_KS>(inputs, in_dim, 16 * u, B, xn);
-    load_rows<1>(grad, kOut, 16 * u, B, dn);  // output activation ignored (ffmlp.cu:783)
+    xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
+    load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn);  // output activation ignored (ffmlp.cu:783)
     copy_frags<L::FRAGS, kBwdThreads>(lds, image);
     __syncthreads();
     MSTAMP(1);
@@ -831,6 +798,7 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
 
     ngp_half* dT = tiles + (size_t)wave * 2 * kTileRows * kTileLd;
     ngp_half* hT = dT + (size_t)kTileRows * kTileLd;
+    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
 
     f32x4 dw_last[1][N::MTW], dw_hid[NH][N::MTW][N::MTW], dw_first[N::MTW][N::IN_MT];
     zero_tiles(dw_last);
@@ -838,12 +806,22 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     for (int q = 0; q < NH; ++q) zero_tiles(dw_hid[q]);
     zero_tiles(dw_first);
 
-    // one chunk of NB x 16 samples at row0 (x, dout: its inputs and output grads)
-    auto chunk_bwd = [&](auto nbc, uint32_t row0, const auto& x, const auto& dout) {
-        constexpr int NB = decltype(nbc)::value;
+    // inputs and output gradients of the next chunk are prefetched while the
+    // current one computes (one wave per SIMD: nothing else hides the latency)
+    for (; chunk < nchunks; chunk += stride) {
+        const uint32_t row0 = chunk * 16 * kNB;
+        half8 x[kNB][IN_KS], dout[kNB][1];
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+#pragma unroll
+            for (int s = 0; s < IN_KS; ++s) x[nb][s] = xn[nb][s];
+            dout[nb][0] = dn[nb][0];
+        }
+        xl.template operator()<IN_KS>(inputs, in_dim, row0 + stride * 16 * kNB, B, xn);
+        load_rows<1>(grad, kOut, row0 + stride * 16 * kNB, B, dn);
         // recompute the post-activations of every hidden layer
-        half8 h[NH + 1][NB][N::KSW];
-        f32x4 a[NB][N::MTW];
+        half8 h[NH + 1][kNB][N::KSW];
+        f32x4 a[kNB][N::MTW];
         dense<N::MTW, IN_KS>(fr, fwd_desc<W, IN_KS, NH>(0, in_dim).frag0, x, a);
         pack_act<N::MTW, N::KSW>(a, act, h[0]);
 #pragma unroll
@@ -861,12 +839,12 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
         write_rows<N::KSW, true>(hT, h[NH], W);
 #if NGP_MLP_BWD_OVERLAP
         dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
-        dw_accum<1, N::MTW, NB>(dT, hT, dw_last);
+        dw_accum<1, N::MTW>(dT, hT, dw_last);
 #else
-        dw_accum<1, N::MTW, NB>(dT, hT, dw_last);
+        dw_accum<1, N::MTW>(dT, hT, dw_last);
         dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
 #endif
-        half8 d[NB][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
+        half8 d[kNB][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
         pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
 #pragma unroll
         for (int q = NH; q >= 1; --q) {
@@ -874,9 +852,9 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
             write_rows<N::KSW, true>(hT, h[q - 1], W);
 #if NGP_MLP_BWD_OVERLAP
             dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
-            dw_accum<N::MTW, N::MTW, NB>(dT, hT, dw_hid[q - 1]);
+            dw_accum<N::MTW, N::MTW>(dT, hT, dw_hid[q - 1]);
 #else
-            dw_accum<N::MTW, N::MTW, NB>(dT, hT, dw_hid[q - 1]);
+            dw_accum<N::MTW, N::MTW>(dT, hT, dw_hid[q - 1]);
             dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
 #endif
             pack_delta<N::MTW, N::KSW>(a, h[q - 1], act, d);
@@ -884,39 +862,17 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
         // first matmul: dW += d^T . x, and grad_inputs = W_0^T d
         write_rows<N::KSW, true>(dT, d, W);
         write_rows<IN_KS, false>(hT, x, in_dim);
-        f32x4 gi[NB][N::IN_MT];
+        f32x4 gi[kNB][N::IN_MT];
 #if NGP_MLP_BWD_OVERLAP
         if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
-        dw_accum<N::MTW, N::IN_MT, NB>(dT, hT, dw_first);
+        dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
 #else
-        dw_accum<N::MTW, N::IN_MT, NB>(dT, hT, dw_first);
+        dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
         if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
 #endif
         if (want_gi) gi_out(row0, B, in_dim, gi);
         MSTAMP(2 + min(nst, 9u));
         ++nst;
-    };
-
-    // inputs and output gradients of the next chunk are prefetched while the
-    // current one computes (one wave per SIMD: nothing else hides the latency)
-    for (; u + 2 <= u1; u += 2) {
-        half8 x[kNB][IN_KS], dout[kNB][1];
-#pragma unroll
-        for (int nb = 0; nb < kNB; ++nb) {
-#pragma unroll
-            for (int s = 0; s < IN_KS; ++s) x[nb][s] = xn[nb][s];
-            dout[nb][0] = dn[nb][0];
-        }
-        xl.template operator()<IN_KS>(inputs, in_dim, 16 * (u + 2), B, xn);
-        load_rows<1>(grad, kOut, 16 * (u + 2), B, dn);
-        chunk_bwd(std::integral_constant<int, 2>{}, 16 * u, x, dout);
-    }
-    if (u < u1) {  // the odd unit: a 16-sample chunk (its rows are the prefetch's first block)
-        half8 x[1][IN_KS], dout[1][1];
-#pragma unroll
-        for (int s = 0; s < IN_KS; ++s) x[0][s] = xn[0][s];
-        dout[0][0] = dn[0][0];
-        chunk_bwd(std::integral_constant<int, 1>{}, 16 * u, x, dout);
     }
     MSTAMP(12);
 
