@@ -470,6 +470,20 @@ int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* we
                             uint32_t activation, void* grad_inputs, void* grad_weights,
                             int32_t gw_dtype, uint32_t flags, void* workspace,
                             size_t workspace_bytes, void* stream);
+/* Fused-step: both FFMLP backwards of NeRFNetwork (nerf/network_ff.py:
+ * color_net then sigma_net, each ffmlp.cu kernel_mlp_fused_backward :410-518)
+ * in one launch. Equals ngp_ffmlp_backward_rows of the colour network
+ * (flags NGP_FFMLP_NERF_GEO | NGP_FFMLP_DEFER_REDUCE, input width 32, writing
+ * g_h[:, 1:16]) followed by that of the sigma network (grad g_h, inputs enc
+ * [16][B][2], flags NGP_FFMLP_PAIR_MAJOR | NGP_FFMLP_DEFER_REDUCE, input
+ * gradient g_enc): the input gradients bit for bit, the dW partials summed in
+ * another order. Workspaces as ngp_ffmlp_backward_workspace_bytes of each
+ * network; reduce with ngp_ffmlp_reduce. 64-wide networks, num_layers 2..3. */
+int ngp_nerf_backward(const void* g_color_out, const void* color_in, const void* color_image, void* g_h,
+                      const void* enc, const void* sigma_image, void* g_enc, uint32_t B, const int32_t* count,
+                      uint32_t hidden_dim, uint32_t num_layers, uint32_t hidden_dim_color,
+                      uint32_t num_layers_color, void* sigma_workspace, size_t sigma_workspace_bytes,
+                      void* color_workspace, size_t color_workspace_bytes, void* stream);
 /* Sums the deferred dW partials of n backward calls (same B and shapes as
  * those calls) into grad_weights[k], in one launch (n <= 4). nonfinite
  * (nullable): set to 1 when a written grad is inf/nan (GradScaler's check). */

@@ -305,6 +305,31 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
     gx_rows = gxp.view(16, B, 2).permute(1, 0, 2).reshape(B, 32)
     assert torch.equal(gx_rows[:n].view(torch.int16), gx_ref[:n].view(torch.int16))
     assert torch.equal(gw2.view(torch.int16), gw_ref[0].view(torch.int16))
+    # both backwards in one launch (ngp_nerf_backward) against the two calls on
+    # the pair-major input: input gradients bit for bit; dW summed in another
+    # order (chunks dealt to other waves), so within fp16 rounding of the
+    # same fp32 sums
+    gh1, gxp1 = gh0.clone(), torch.zeros_like(gx_ref)
+    nat.check(lib.ngp_ffmlp_backward_rows(P(go), P(ci), P(ws[1]), P(imgs[1]), B, P(cnt), 32, 16, 64, 3, 0, P(gh1),
+                                          None, 1, 3, P(wsb[1]), wsb[1].numel(), s), "b_geo")
+    nat.check(lib.ngp_ffmlp_backward_rows(P(gh1), P(xp), P(ws[0]), P(imgs[0]), B, P(cnt), 32, 16, 64, 2, 0,
+                                          P(gxp1), None, 1, 5, P(wsb[0]), wsb[0].numel(), s), "b_pair_defer")
+    gw_two = [torch.zeros_like(t) for t in gw_ref]
+    nat.check(lib.ngp_ffmlp_reduce(2, arr([wsb[1], wsb[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
+                                   u32([3, 2]), arr([gw_two[1], gw_two[0]]), 1, None, s), "reduce")
+    gh2, gxp2 = gh0.clone(), torch.zeros_like(gx_ref)
+    wsm = [torch.full_like(w, 7) for w in wsb]  # stale slab contents must not leak through
+    nat.check(lib.ngp_nerf_backward(P(go), P(ci), P(imgs[1]), P(gh2), P(xp), P(imgs[0]), P(gxp2), B, P(cnt),
+                                    64, 2, 64, 3, P(wsm[0]), wsm[0].numel(), P(wsm[1]), wsm[1].numel(), s), "nerf_bwd")
+    gw_one = [torch.zeros_like(t) for t in gw_ref]
+    nat.check(lib.ngp_ffmlp_reduce(2, arr([wsm[1], wsm[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
+                                   u32([3, 2]), arr([gw_one[1], gw_one[0]]), 1, None, s), "reduce")
+    torch.cuda.synchronize()
+    assert torch.equal(gh2.view(torch.int16), gh1.view(torch.int16))  # column 0 kept, rows past n untouched
+    assert torch.equal(gxp2.view(torch.int16), gxp1.view(torch.int16))
+    for a, b in zip(gw_one, gw_two):
+        a, b = a.float(), b.float()
+        assert torch.all((a - b).abs() <= 2.0 ** -10 * b.abs() + 1e-6), float((a - b).abs().max())
 
 
 def test_grad_guard_poisons_every_shard(cuda):

@@ -768,31 +768,27 @@ struct GiPairMajor {
 #define MSTAMP(slot) do { } while (0)
 #endif
 
-template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI>
-__global__ void __launch_bounds__(kBwdThreads)
-k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
-          const half8* __restrict__ image, XL xl, GI gi_out, bool want_gi,
-          float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, FA act,
-          const int32_t* __restrict__ count) {
+// One backward pass over the 32-sample chunks a wave takes (map(k): the
+// wave's k-th chunk; a chunk >= the chunk count ends the loop), then the fold
+// of the waves' dW tiles and the workgroup's slab row. fr: the network's
+// fragment image in LDS; tiles: the per-wave staging tiles; img: where the
+// two fold images go (they may overlay fr and tiles, dead by then). pre()
+// runs once the first chunk's loads are issued (a standalone launch copies
+// its fragment image there, so the two latencies overlap).
+template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI, typename MAP, typename PRE>
+NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tiles, float* __restrict__ img_base,
+                       const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs, XL xl, GI gi_out,
+                       bool want_gi, float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim,
+                       FA act, MAP map, PRE pre) {
     using N = Net<W, IN_KS, NH>;
-    using L = BwdLds<W, IN_KS, NH>;
-    if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);  // rows past the sample count
     constexpr int LAST = N::NMAT - 1;
-    extern __shared__ half8 lds[];
-    const half8* fr = lds;
-    ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
-
     MSTAMP(0);
-    // the first chunk's inputs and output grads are requested before the
-    // fragment image copy, so the two latencies overlap
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t stride = gridDim.x * kBwdWaves;
-    uint32_t chunk = blockIdx.x * kBwdWaves + wave;
+    uint32_t chunk = map(0u);
     half8 xn[kNB][IN_KS], dn[kNB][1];
     xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
     load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn);  // output activation ignored (ffmlp.cu:783)
-    copy_frags<L::FRAGS, kBwdThreads>(lds, image);
-    __syncthreads();
+    pre();
     MSTAMP(1);
     [[maybe_unused]] uint32_t nst = 0;
 
@@ -808,7 +804,7 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
 
     // inputs and output gradients of the next chunk are prefetched while the
     // current one computes (one wave per SIMD: nothing else hides the latency)
-    for (; chunk < nchunks; chunk += stride) {
+    for (uint32_t kc = 1; chunk < nchunks; ++kc) {
         const uint32_t row0 = chunk * 16 * kNB;
         half8 x[kNB][IN_KS], dout[kNB][1];
 #pragma unroll
@@ -817,8 +813,9 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
             for (int s = 0; s < IN_KS; ++s) x[nb][s] = xn[nb][s];
             dout[nb][0] = dn[nb][0];
         }
-        xl.template operator()<IN_KS>(inputs, in_dim, row0 + stride * 16 * kNB, B, xn);
-        load_rows<1>(grad, kOut, row0 + stride * 16 * kNB, B, dn);
+        const uint32_t next = map(kc);
+        xl.template operator()<IN_KS>(inputs, in_dim, next * 16 * kNB, B, xn);
+        load_rows<1>(grad, kOut, next * 16 * kNB, B, dn);
         // recompute the post-activations of every hidden layer
         half8 h[NH + 1][kNB][N::KSW];
         f32x4 a[kNB][N::MTW];
@@ -873,9 +870,9 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
         if (want_gi) gi_out(row0, B, in_dim, gi);
         MSTAMP(2 + min(nst, 9u));
         ++nst;
+        chunk = next;
     }
     MSTAMP(12);
-
     // fold the waves' register tiles into two LDS dW images (round r: waves
     // 2r and 2r + 1 store (r = 0) or add into images 0 and 1), then publish
     // image0 + image1 as the slab row: a fixed summation order, so dW is
@@ -883,8 +880,7 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     // MTW x IN_MT tiles, each hidden layer's MTW x MTW, the last layer's 1 x MTW.
     constexpr int T_FIRST = N::MTW * N::IN_MT, T_HID = N::MTW * N::MTW, T_LAST = N::MTW;
     constexpr int NT = T_FIRST + NH * T_HID + T_LAST;
-    static_assert((size_t)2 * NT * 1024 <= L::total, "fold images exceed the workgroup's LDS");
-    float* img = reinterpret_cast<float*>(lds) + (size_t)(wave & 1) * NT * 256;
+        float* img = img_base + (size_t)(wave & 1) * NT * 256;
     auto fold = [&](auto first) {
         constexpr bool F = decltype(first)::value;
         fold_tiles<F>(dw_first, img);
@@ -905,7 +901,7 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     // lane adds its two 16-byte slots and stores its 4 outputs (rows 16m + 4g +
     // r, column 16k + c: 64-byte segments per row)
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    const f32x4* i0 = reinterpret_cast<const f32x4*>(lds);
+    const f32x4* i0 = reinterpret_cast<const f32x4*>(img_base);
     const f32x4* i1 = i0 + NT * 64;
     float* slab_row = slab + (size_t)blockIdx.x * nparams;
     for (int tt = (int)wave; tt < NT; tt += kBwdWaves) {
@@ -935,6 +931,94 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
         }
     }
     MSTAMP(14);
+}
+
+
+template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI>
+__global__ void __launch_bounds__(kBwdThreads)
+k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs,
+          const half8* __restrict__ image, XL xl, GI gi_out, bool want_gi,
+          float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim, FA act,
+          const int32_t* __restrict__ count) {
+    using N = Net<W, IN_KS, NH>;
+    using L = BwdLds<W, IN_KS, NH>;
+    static_assert((size_t)2 * (N::MTW * N::IN_MT + NH * N::MTW * N::MTW + N::MTW) * 1024 <= L::total,
+                  "fold images exceed the workgroup's LDS");
+    if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);  // rows past the sample count
+    extern __shared__ half8 lds[];
+    ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
+    const uint32_t stride = gridDim.x * kBwdWaves, c0 = blockIdx.x * kBwdWaves + (threadIdx.x >> 6);
+    bwd_phase<W, IN_KS, NH>(lds, tiles, reinterpret_cast<float*>(lds), grad, inputs, xl, gi_out, want_gi, slab,
+                            nparams, B, in_dim, act, [=](uint32_t k) { return c0 + k * stride; },
+                            [&]() {
+                                copy_frags<L::FRAGS, kBwdThreads>(lds, image);
+                                __syncthreads();
+                            });
+}
+
+// The NeRF step's two backward networks in one launch (ngp_nerf_backward):
+// the colour network (its geo-feature grads into g_h's columns 1..15), then,
+// after a workgroup barrier, the sigma network over the same workgroup's
+// chunks (its output grad g_h is complete for them). Workgroup b takes chunks
+// b, b + G, b + 2G, ... (G workgroups) for both networks; its j-th chunk goes
+// to wave j % 4 in the colour pass and to wave 3 - j % 4 in the sigma pass, so
+// a wave with an extra colour chunk has one sigma chunk less. (Two launches:
+// 2,528 Lego chunks over 1,024 waves gave the same waves the third chunk of
+// both networks.) Both fragment images are copied at the start; the sigma
+// one lies past everything the colour pass uses (its fragments, tiles and
+// fold images), and the sigma pass's tiles and fold images overlay the
+// colour pass's.
+struct NerfBwdArgs {
+    const ngp_half* g_color_out;   // [B, 16]
+    const ngp_half* color_in;      // [B, 32]
+    const half8* color_image;
+    ngp_half* g_h;                 // [B, 16]: column 0 (density grad) given, columns 1..15 written
+    const ngp_half* enc;           // [16][B][2] pair-major grid encoding
+    const half8* sigma_image;
+    ngp_half* g_enc;               // [16][B][2]
+    float* slab_color;
+    float* slab_sigma;
+    uint32_t np_color, np_sigma, B;
+    const int32_t* count;
+};
+
+template <int NHS, int NHC>
+struct NerfBwdLds {
+    using LC = BwdLds<64, 1, NHC>;
+    using LS = BwdLds<64, 1, NHS>;
+    static constexpr size_t sigma_frags = LC::total;  // the sigma image's offset
+    static constexpr size_t total = sigma_frags + LS::frag_bytes;
+    static constexpr bool fits = total <= 160 * 1024 && LS::total <= sigma_frags;
+};
+
+template <int NHS, int NHC>
+__global__ void __launch_bounds__(kBwdThreads)
+k_nerf_bwd(NerfBwdArgs a) {
+    using LC = BwdLds<64, 1, NHC>;
+    using LS = BwdLds<64, 1, NHS>;
+    using NL = NerfBwdLds<NHS, NHC>;
+    static_assert(NL::fits, "nerf backward LDS budget exceeded");
+    uint32_t B = a.B;
+    if (a.count) B = *a.count <= 0 ? 0u : min(B, (uint32_t)*a.count);
+    extern __shared__ half8 lds[];
+    half8* sfr = reinterpret_cast<half8*>(reinterpret_cast<char*>(lds) + NL::sigma_frags);
+    const uint32_t G = gridDim.x, b = blockIdx.x, w = threadIdx.x >> 6;
+    bwd_phase<64, 1, NHC>(lds, reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes),
+                          reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{}, GiNerfGeo{a.g_h},
+                          true, a.slab_color, a.np_color, B, 32u, ActReLU{},
+                          [=](uint32_t k) { return b + (w + k * kBwdWaves) * G; },
+                          [&]() {
+                              copy_frags<LC::FRAGS, kBwdThreads>(lds, a.color_image);
+                              copy_frags<LS::FRAGS, kBwdThreads>(sfr, a.sigma_image);
+                              __syncthreads();
+                          });
+    // the colour pass's geo grads (global stores of every wave) are complete
+    // and its fold images read before the sigma pass loads g_h and reuses LDS
+    __syncthreads();
+    bwd_phase<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
+                          InPairMajor{a.B}, GiPairMajor{a.g_enc, a.B}, true, a.slab_sigma, a.np_sigma, B, 32u,
+                          ActReLU{}, [=](uint32_t k) { return b + (kBwdWaves - 1 - w + k * kBwdWaves) * G; },
+                          []() {});
 }
 
 // grad_weights[p] = sum over workgroup rows of the slab, in a fixed order
@@ -1121,6 +1205,19 @@ int launch_bwd(const void* grad, const void* in, const void* w, const void* imag
                                       gw_dtype, defer, ws, count, st);
 }
 
+template <int NHS, int NHC>
+int launch_nerf_bwd(const NerfBwdArgs& a, hipStream_t st) {
+    if constexpr (!NerfBwdLds<NHS, NHC>::fits) {
+        return ngp_set_error(NGP_ERR_UNSUPPORTED, "nerf_backward: networks too large for one launch's LDS");
+    } else {
+        const uint32_t blocks = bwd_blocks(a.B);
+        if (blocks == 0) return NGP_OK;
+        constexpr size_t lds_bytes = NerfBwdLds<NHS, NHC>::total;
+        hipLaunchKernelGGL((k_nerf_bwd<NHS, NHC>), dim3(blocks), dim3(kBwdThreads), lds_bytes, st, a);
+        return ngp_check_launch("nerf_backward");
+    }
+}
+
 #define NGP_MLP_DISPATCH(FN, ...)                                                              \
     do {                                                                                        \
         const int ks = (int)((in_dim + 31) / 32);                                                \
@@ -1211,6 +1308,59 @@ extern "C" int ngp_nerf_forward(const void* enc, const void* sigma_image, const 
         case 2 * 8 + 1: return launch_nerf_fwd<64, 2, 1>(enc, sigma_image, color_image, B, count, es, color_out, st);
         case 2 * 8 + 2: return launch_nerf_fwd<64, 2, 2>(enc, sigma_image, color_image, B, count, es, color_out, st);
         default: return launch_nerf_fwd<64, 2, 3>(enc, sigma_image, color_image, B, count, es, color_out, st);
+    }
+}
+
+/* Both networks' backward of the fused step in one launch: the colour
+ * network's (grad g_color_out [B,16], inputs color_in [B,32]; its input
+ * gradient's geo columns into g_h[:, 1:16], as ngp_ffmlp_backward_rows with
+ * NGP_FFMLP_NERF_GEO), then the sigma network's (grad g_h [B,16], inputs enc
+ * pair-major [16][B][2], input gradient g_enc pair-major, as
+ * NGP_FFMLP_PAIR_MAJOR). Both networks' dW partials are left in their
+ * workspaces (ngp_ffmlp_backward_workspace_bytes of each network) for
+ * ngp_ffmlp_reduce, as NGP_FFMLP_DEFER_REDUCE. Input gradients equal the two
+ * calls bit for bit; dW is summed in another order. */
+extern "C" int ngp_nerf_backward(const void* g_color_out, const void* color_in, const void* color_image,
+                                 void* g_h, const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
+                                 const int32_t* count, uint32_t hidden_dim, uint32_t num_layers,
+                                 uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
+                                 size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
+                                 void* stream) {
+    NGP_REQUIRE(hidden_dim == 64 && hidden_dim_color == 64, NGP_ERR_UNSUPPORTED,
+                "nerf_backward: 64-wide networks only on this build, got %u / %u", hidden_dim, hidden_dim_color);
+    NGP_REQUIRE(num_layers >= 2 && num_layers <= 3 && num_layers_color >= 2 && num_layers_color <= 3,
+                NGP_ERR_UNSUPPORTED, "nerf_backward: num_layers in [2, 3] (sigma) / [2, 3] (color), got %u / %u",
+                num_layers, num_layers_color);
+    NGP_REQUIRE(g_color_out && color_in && color_image && g_h && enc && sigma_image && g_enc, NGP_ERR_ARG,
+                "nerf_backward: null pointer");
+    if (B == 0) return NGP_OK;
+    const size_t need_s = ngp_ffmlp_backward_workspace_bytes(B, 32, kOut, hidden_dim, num_layers);
+    const size_t need_c = ngp_ffmlp_backward_workspace_bytes(B, 32, kOut, hidden_dim_color, num_layers_color);
+    NGP_REQUIRE(sigma_workspace && sigma_workspace_bytes >= need_s && color_workspace &&
+                    color_workspace_bytes >= need_c,
+                NGP_ERR_ARG, "nerf_backward: workspaces of %zu / %zu bytes required, got %zu / %zu", need_s, need_c,
+                sigma_workspace_bytes, color_workspace_bytes);
+    NerfBwdArgs a{};
+    a.g_color_out = static_cast<const ngp_half*>(g_color_out);
+    a.color_in = static_cast<const ngp_half*>(color_in);
+    a.color_image = static_cast<const half8*>(color_image);
+    a.g_h = static_cast<ngp_half*>(g_h);
+    a.enc = static_cast<const ngp_half*>(enc);
+    a.sigma_image = static_cast<const half8*>(sigma_image);
+    a.g_enc = static_cast<ngp_half*>(g_enc);
+    a.slab_color = reinterpret_cast<float*>(static_cast<char*>(color_workspace) + kImageBytes);
+    a.slab_sigma = reinterpret_cast<float*>(static_cast<char*>(sigma_workspace) + kImageBytes);
+    a.np_color = num_params(32, 64, num_layers_color);
+    a.np_sigma = num_params(32, 64, num_layers);
+    a.B = B;
+    a.count = count;
+    hipStream_t st = ngp_stream(stream);
+    const uint32_t key = (num_layers - 1) * 8 + (num_layers_color - 1);
+    switch (key) {
+        case 1 * 8 + 1: return launch_nerf_bwd<1, 1>(a, st);
+        case 1 * 8 + 2: return launch_nerf_bwd<1, 2>(a, st);
+        case 2 * 8 + 1: return launch_nerf_bwd<2, 1>(a, st);
+        default: return launch_nerf_bwd<2, 2>(a, st);
     }
 }
 

@@ -210,6 +210,10 @@ class FusedTrainer:
         self._one_fwd = (os.environ.get("NGP_FUSED_SPLIT_FWD") != "1" and sn_.hidden_dim == 64
                          and cn_.hidden_dim == 64 and sn_.input_dim == 32 and cn_.input_dim == 32
                          and 2 <= sn_.num_layers <= 3 and 2 <= cn_.num_layers <= 4)
+        # ... and for both backwards (ngp_nerf_backward; NGP_FUSED_SPLIT_BWD=1: two launches)
+        self._one_bwd = (os.environ.get("NGP_FUSED_SPLIT_BWD") != "1" and sn_.hidden_dim == 64
+                         and cn_.hidden_dim == 64 and sn_.input_dim == 32 and cn_.input_dim == 32
+                         and 2 <= sn_.num_layers <= 3 and 2 <= cn_.num_layers <= 3)
         if self.table32:
             nt = self._starts[1]  # the table, then the two MLPs
             sec = [(0, nt, False), (nt, chunk - nt, True)]
@@ -731,6 +735,19 @@ class FusedTrainer:
                                         P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
                                         P(self.g_h), None, None, P(self.loss_ray), s), "composite_loss")
         self._tick("composite_loss")
+        if self._one_bwd:  # both networks' backward in one launch (ngp_nerf_backward)
+            chk(lib.ngp_nerf_backward(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
+                                      P(self.enc_out), P(img[0]), P(self.g_enc), M, cnt, sn.hidden_dim,
+                                      sn.num_layers, cn.hidden_dim, cn.num_layers, P(self.mlp_ws[0]),
+                                      self.mlp_ws[0].numel(), P(self.mlp_ws[1]), self.mlp_ws[1].numel(), s),
+                "nerf_backward")
+            self._tick("ffmlp_backward")
+        else:
+            self._mlp_backward_split(lib, P, s, M, cnt, img)
+        self._grid_backward(lib, P, s, M, cnt, draw, grid_args)
+
+    def _mlp_backward_split(self, lib, P, s, M, cnt, img):
+        chk, sn, cn = nat.check, self.sig_net, self.col_net
         # color backward: its input gradient's geo columns land in g_h[:, 1:16]
         chk(lib.ngp_ffmlp_backward_rows(P(self.g_color_out), P(self.color_in), P(self.w_half[2]), P(img[1]), M,
                                         cnt, 32, 16, cn.hidden_dim, cn.num_layers, _RELU, P(self.g_h),
@@ -742,6 +759,9 @@ class FusedTrainer:
                                         _DEFER | _PAIR, P(self.mlp_ws[0]), self.mlp_ws[0].numel(), s),
             "sigma_mlp_backward")
         self._tick("ffmlp_backward_sigma")
+
+    def _grid_backward(self, lib, P, s, M, cnt, draw, grid_args):
+        chk, m, e, pk = nat.check, self.model, self.enc, self._pk
         bargs = (P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets), P(self.grads[0]), M, cnt,
                  *grid_args[:-1], self._offsets_host, P(self.grid_ws), self.grid_ws.numel(), self._grid_flags,
                  self._inf_flag)
