@@ -126,20 +126,35 @@ struct Chunk {
     float d0, c0, c1, c2, w, Tafter, t;
 };
 
-NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __restrict__ color_out,
-                         const float* __restrict__ deltas, uint32_t offset, uint32_t base,
-                         uint32_t num_steps, uint32_t lane, float& S, float& tacc, float T_thresh,
-                         bool& stop) {
-    Chunk c;
-    const uint32_t i = offset + base + lane;
-    c.ok = base + lane < num_steps;
+// The loaded rows of one chunk (what the scans and the backward read).
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+struct Raw {
+    float sg, h0;
+    float2 dd;
+    half4 co;
+};
+
+NGP_DEV Raw load_raw(const float* __restrict__ sigma, const ngp_half* __restrict__ color_out,
+                     const float* __restrict__ deltas, const ngp_half* __restrict__ h_sigma, uint32_t offset,
+                     uint32_t base, uint32_t num_steps, uint32_t lane) {
     // unconditional loads (lanes past the ray read row 0 and drop the value):
     // a load under a divergent branch makes the compiler wait for it on the spot
-    const uint32_t ic = c.ok ? i : 0u;
-    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-    const float sgl = sigma[ic];
-    const float2 ddl = *reinterpret_cast<const float2*>(deltas + (size_t)ic * 2);
-    const half4 co = *reinterpret_cast<const half4*>(color_out + (size_t)ic * 16);
+    const uint32_t ic = base + lane < num_steps ? offset + base + lane : 0u;
+    Raw r;
+    r.sg = sigma[ic];
+    r.dd = *reinterpret_cast<const float2*>(deltas + (size_t)ic * 2);
+    r.co = *reinterpret_cast<const half4*>(color_out + (size_t)ic * 16);
+    r.h0 = (float)h_sigma[(size_t)ic * 16];
+    return r;
+}
+
+NGP_DEV Chunk scan_chunk(const Raw& rw, uint32_t base, uint32_t num_steps, uint32_t lane, float& S, float& tacc,
+                         float T_thresh, bool& stop) {
+    Chunk c;
+    c.ok = base + lane < num_steps;
+    const float sgl = rw.sg;
+    const float2 ddl = rw.dd;
+    const half4 co = rw.co;
     const float sg = c.ok ? sgl : 0.0f;
     c.d0 = c.ok ? ddl.x : 0.0f;
     const float d1 = c.ok ? ddl.y : 0.0f;
@@ -167,6 +182,15 @@ NGP_DEV Chunk load_chunk(const float* __restrict__ sigma, const ngp_half* __rest
     tacc = lane63(c.t);
     return c;
 }
+
+// Chunks of a ray whose rows are requested together, before the first scan
+// (and kept for the backward): the serial per-chunk round trips of a long ray
+// set the kernel's time (a ray of 256 samples took 4 dependent loads in the
+// forward and 3 more in the backward).
+#ifndef NGP_LOSS_PRE
+#define NGP_LOSS_PRE 4
+#endif
+constexpr uint32_t kLossPre = NGP_LOSS_PRE;
 
 __global__ void __launch_bounds__(kLossWaves * 64)
 k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ color_out,
@@ -196,35 +220,48 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
         const float v = gt[(size_t)index * gch + min((uint32_t)k, gch - 1u)];
         gt4[k] = (uint32_t)k < gch ? v : 1.0f;
     }
-    const bool h_ok = valid && lane < num_steps;
-    const float h0l = (float)h_sigma[(size_t)(h_ok ? offset + lane : 0u) * 16];
-    const float h0_first = h_ok ? h0l : 0.0f;
+    // the ray's first kLossPre chunks of rows (clamped: a short ray's spare
+    // chunks read its row 0 again)
+    const uint32_t nrows = valid ? num_steps : 0u;
+    Raw raw[kLossPre];
+#pragma unroll
+    for (uint32_t k = 0; k < kLossPre; ++k)
+        raw[k] = load_raw(sigma, color_out, deltas, h_sigma, offset, 64 * k, nrows, lane);
 
     // ---- forward (composite_rays_train_forward)
-    // The first 64-sample chunk (all of most rays) is kept for the backward
-    // pass instead of being loaded and scanned again.
+    // The first kLossPre 64-sample chunks (all of most rays) are kept for the
+    // backward pass instead of being loaded and scanned again.
     float r = 0, g = 0, b = 0, ws = 0, d = 0;
-    Chunk first{};
-    float S1 = 0.0f, tacc1 = 0.0f;
-    bool stop1 = false;
+    Chunk kept[kLossPre];
+    float Sk[kLossPre], tk[kLossPre];
+    bool stopk[kLossPre];
+    uint32_t nkept = 0;  // kept chunks scanned (the forward stopped in the last of them, or ran on)
     if (valid) {
         float S = 0.0f, tacc = 0.0f;
-        for (uint32_t base = 0; base < num_steps; base += 64) {
-            bool stop;
-            const Chunk c = load_chunk(sigma, color_out, deltas, offset, base, num_steps, lane, S, tacc,
-                                       la.T_thresh, stop);
-            if (base == 0) {
-                first = c;
-                S1 = S;
-                tacc1 = tacc;
-                stop1 = stop;
-            }
+        bool stop = false;
+#pragma unroll
+        for (uint32_t k = 0; k < kLossPre; ++k) {
+            if (64 * k >= num_steps || stop) break;
+            const Chunk c = scan_chunk(raw[k], 64 * k, num_steps, lane, S, tacc, la.T_thresh, stop);
+            kept[k] = c;
+            Sk[k] = S;
+            tk[k] = tacc;
+            stopk[k] = stop;
+            nkept = k + 1;
             r += wave_sum(c.w * c.c0);
             g += wave_sum(c.w * c.c1);
             b += wave_sum(c.w * c.c2);
             ws += wave_sum(c.w);
             d += wave_sum(c.w * c.t);
-            if (stop) break;
+        }
+        for (uint32_t base = 64 * kLossPre; !stop && base < num_steps; base += 64) {
+            const Chunk c = scan_chunk(load_raw(sigma, color_out, deltas, h_sigma, offset, base, num_steps, lane),
+                                       base, num_steps, lane, S, tacc, la.T_thresh, stop);
+            r += wave_sum(c.w * c.c0);
+            g += wave_sum(c.w * c.c1);
+            b += wave_sum(c.w * c.c2);
+            ws += wave_sum(c.w);
+            d += wave_sum(c.w * c.t);
         }
     }
     // ---- background blend + MSE (utils.py train_step) and its gradient
@@ -269,16 +306,31 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     bool stopped = false;
     for (uint32_t base = 0; base < num_steps; base += 64) {
         bool stop = false;
-        Chunk c;
-        if (base == 0) {
-            c = first;
-            S = S1;
-            tacc = tacc1;
-            stop = stop1;
+        Chunk c{};
+        float h0 = 0.0f;
+        const uint32_t kc = base / 64;
+        if (kc < kLossPre) {
+            // a kept chunk (every one up to the forward's stop), or a chunk past
+            // the stop: inactive, only its rows' zero grads are written
+#pragma unroll
+            for (uint32_t k = 0; k < kLossPre; ++k)
+                if (k == kc) {
+                    if (k < nkept) {
+                        c = kept[k];
+                        S = Sk[k];
+                        tacc = tk[k];
+                        stop = stopk[k];
+                    } else {
+                        c.ok = base + lane < num_steps;
+                    }
+                    h0 = raw[k].h0;
+                }
         } else {
-            c = load_chunk(sigma, color_out, deltas, offset, base, num_steps, lane, S, tacc, la.T_thresh, stop);
+            const Raw rw = load_raw(sigma, color_out, deltas, h_sigma, offset, base, num_steps, lane);
+            c = scan_chunk(rw, base, num_steps, lane, S, tacc, la.T_thresh, stop);
+            h0 = rw.h0;
         }
-        if (stopped) { c.active = false; c.w = 0.0f; }
+        if (stopped || (kc >= nkept && kc < kLossPre)) { c.active = false; c.w = 0.0f; }
         // running sums after this lane's sample (inclusive prefix)
         const float pr = rr + scan_incl(c.w * c.c0, lane);
         const float pg = rg + scan_incl(c.w * c.c1, lane);
@@ -303,7 +355,6 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
             go[0] = o0;
             go[1] = o1;
             // sigmas = ds * trunc_exp(h0): grad_h0 = (gs * ds) * exp(clamp(h0, -15, 15)), -> half
-            const float h0 = base == 0 ? h0_first : (float)h_sigma[(size_t)i * 16];
             grad_h[(size_t)i * 16] = ngp_f2h((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
         }
         stopped = stopped || stop;
