@@ -70,6 +70,9 @@ def parse():
                          "refuses event nodes in captured graphs ('External events are disallowed in rocm'), "
                          "so the default 0 times the launches with events between eager steps run right after "
                          "the timed region, with those steps' own sample counts")
+    ap.add_argument("--graph-steps", type=int, default=8,
+                    help="fused engine, world 1: training steps captured back to back in one hipGraph (the "
+                         "timed region replays it K / S times, every step complete); 1: one step per graph")
     ap.add_argument("--settle-steps", type=int, default=1000,
                     help="untimed steps after the warmup that bring the GPU to its sustained clock")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
@@ -365,9 +368,8 @@ def run_fused(args, model, data, bits, world, dev):
     timing = "eager"
     if args.graph:
         try:
-            ft.capture()
-            for _ in range(3):
-                ft.step()
+            ft.capture(multi=args.graph_steps if world == 1 else 1)
+            ft.run(3 * max(1, args.graph_steps))
             used_graph = True
         except Exception as e:  # eager launches are the same kernels; record why
             print(f"[bench] graph capture failed, running eager: {e!r}", file=sys.stderr)
@@ -385,10 +387,9 @@ def run_fused(args, model, data, bits, world, dev):
     # 17.3M for 200 steps on the same box (profiles/r02zl_settle.txt), so a
     # fixed number of untimed steps (same on every rank: they hold
     # collectives) runs before the timed region.
-    for i in range(args.settle_steps):
-        ft.step()
-        if i % 64 == 63:
-            torch.cuda.synchronize()
+    for i in range(0, args.settle_steps, 64):
+        ft.run(min(64, args.settle_steps - i))
+        torch.cuda.synchronize()
     torch.cuda.synchronize()
 
     # ---------------- timed region ----------------
@@ -397,8 +398,7 @@ def run_fused(args, model, data, bits, world, dev):
     ft.grid_timing_reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ft.step()
+    ft.run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -476,6 +476,7 @@ def run_fused(args, model, data, bits, world, dev):
             "mean_count_M": mean_count,
             "parallelism": f"dp{world}",
             "hipgraph": used_graph,
+            "graph_steps": ft._multi if used_graph and ft.graph_multi is not None else 1,
             "settle_steps": args.settle_steps,
             "engine": "fused",
             "dt_gamma": args.dt_gamma,

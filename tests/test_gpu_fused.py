@@ -198,6 +198,31 @@ def test_pipelined_steps_match_serial_steps(cuda):
     assert int(a._state_i()[7]) == int(b._state_i()[7])  # LambdaLR epoch
 
 
+def test_multi_step_graph_equals_single_steps(cuda):
+    """run(k) with a graph of S step bodies (capture(multi=S), what the bench
+    replays) equals k single-step replays bit for bit, remainder included:
+    parameters, optimizer steps, sample counts, scaler and loss."""
+    _, _, _, a = _setup(cuda)
+    _, _, _, b = _setup(cuda)
+    for t in (a, b):
+        for _ in range(2):
+            t.step()
+    a.capture(warmup=2, multi=4)
+    b.capture(warmup=2)
+    a.run(11)  # two multi-step replays + 3 single steps
+    for _ in range(11):
+        b.step()
+    assert a.model.local_step == b.model.local_step
+    a.flush()
+    b.flush()
+    torch.cuda.synchronize()
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+    assert a.optimizer_steps == b.optimizer_steps
+    assert torch.equal(a._recent_counts(15), b._recent_counts(15))
+    assert a.scale == b.scale and a.last_loss == b.last_loss
+
+
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
 def test_fused_training_reduces_loss_and_captures(cuda, bound, dt_gamma):
     model, ref, data, ft = _setup(cuda, num_rays=4096, mean_count=100000, bound=bound, dt_gamma=dt_gamma)

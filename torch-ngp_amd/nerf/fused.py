@@ -273,6 +273,7 @@ class FusedTrainer:
             bj.counter, bj.step_counter = nat.ptr(self.counter), nat.ptr(m_.step_counter)
             self._batch_job = bj
         self.graph = None
+        self.graph_multi, self._multi = None, 1  # capture(multi=S): S step bodies in one graph
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
@@ -851,6 +852,20 @@ class FusedTrainer:
         self._pending = True
         self.model.local_step += 1
 
+    def run(self, k):
+        """k training iterations. With a multi-step graph (capture(multi=S),
+        world 1) it replays floor(k / S) times -- S steps back to back in one
+        graph launch, so the per-launch gap between graph replays is paid once
+        per S steps -- and step() runs the rest."""
+        g, S = self.graph_multi, self._multi
+        if g is not None and self._pending and not self.dp and not self._ring:
+            for _ in range(k // S):
+                g.replay()
+                self.model.local_step += S
+            k -= (k // S) * S
+        for _ in range(k):
+            self.step()
+
     def flush(self):
         """Apply the pending optimizer step (before reading or saving the
         parameters, or evaluating); data parallel: every rank then holds the
@@ -862,14 +877,15 @@ class FusedTrainer:
             self._pending = False
         self._normalize_table()
 
-    def capture(self, warmup=2, ring=0):
+    def capture(self, warmup=2, ring=0, multi=1):
         """hipGraph(s) of the step body. World 1: one graph (optimizer of the
         previous gradients, sample, march, network). Data parallel: three
         (optimizer | sample + march | network); the collectives between them
         stay outside. ring=R (world 1): R further copies of the body graph
         with an event-record node after each launch; step() then replays
         them in turn (instead of the plain graph) and `ring_times` reads the
-        per-launch device times of the last R replays."""
+        per-launch device times of the last R replays. multi=S (world 1): also
+        a graph of S consecutive step bodies, replayed by run()."""
         for _ in range(max(1, warmup)):
             self.step()
         torch.cuda.synchronize()
@@ -893,6 +909,13 @@ class FusedTrainer:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._body(True)
+            self.graph_multi, self._multi = None, 1
+            if multi > 1:
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm):
+                    for _ in range(multi):
+                        self._body(True)
+                self.graph_multi, self._multi = gm, multi
         else:
             graphs = {k: torch.cuda.CUDAGraph() for k in ("opt", "pre", "net")}
             with torch.cuda.graph(graphs["opt"]):
