@@ -320,7 +320,13 @@ constexpr uint32_t kSegWaves = 16;        // rays (waves) per march workgroup
 constexpr uint32_t kSegThreads = kSegWaves * 64;
 constexpr uint32_t kMaxMarchBlocks = 256;
 constexpr size_t kMarchLdsBytes = 156 * 1024;
-constexpr uint32_t kEmitSplit = 8;        // workgroups per ray group in k_march_emit
+// workgroups per ray group in k_march_emit: 8 left half the SIMDs idle on a
+// 4096-ray batch (16 groups); 32 (same box, profiles/r04w_emit_split_ab.txt):
+// the march + emit tick 33.6 -> 30.8 us
+#ifndef NGP_EMIT_SPLIT  // same-box A/B builds
+#define NGP_EMIT_SPLIT 32
+#endif
+constexpr uint32_t kEmitSplit = NGP_EMIT_SPLIT;
 constexpr uint32_t kInf = 0xffffffffu;
 
 struct OccLayout {
