@@ -70,7 +70,7 @@ def parse():
                          "refuses event nodes in captured graphs ('External events are disallowed in rocm'), "
                          "so the default 0 times the launches with events between eager steps run right after "
                          "the timed region, with those steps' own sample counts")
-    ap.add_argument("--graph-steps", type=int, default=8,
+    ap.add_argument("--graph-steps", type=int, default=10,
                     help="fused engine, world 1: training steps captured back to back in one hipGraph (the "
                          "timed region replays it K / S times, every step complete); 1: one step per graph")
     ap.add_argument("--settle-steps", type=int, default=1000,
