@@ -478,12 +478,16 @@ int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, const void* we
  * [16][B][2], flags NGP_FFMLP_PAIR_MAJOR | NGP_FFMLP_DEFER_REDUCE, input
  * gradient g_enc): the input gradients bit for bit, the dW partials summed in
  * another order. Workspaces as ngp_ffmlp_backward_workspace_bytes of each
- * network; reduce with ngp_ffmlp_reduce. 64-wide networks, num_layers 2..3. */
+ * network; reduce with ngp_ffmlp_reduce. 64-wide networks, num_layers 2..3.
+ * timing (nullable): the grid backward's NGP_GRID_TIMING ring (the fused grid
+ * workspace at ngp_grid_encode_backward_fused_timing_offset): workgroup b's
+ * end goes into end slot NGP_GRID_TIMING_MAX_WG - 1 - b of the next call, and
+ * the grid backward's span then starts at the latest of them. */
 int ngp_nerf_backward(const void* g_color_out, const void* color_in, const void* color_image, void* g_h,
                       const void* enc, const void* sigma_image, void* g_enc, uint32_t B, const int32_t* count,
                       uint32_t hidden_dim, uint32_t num_layers, uint32_t hidden_dim_color,
                       uint32_t num_layers_color, void* sigma_workspace, size_t sigma_workspace_bytes,
-                      void* color_workspace, size_t color_workspace_bytes, void* stream);
+                      void* color_workspace, size_t color_workspace_bytes, uint32_t* timing, void* stream);
 /* Sums the deferred dW partials of n backward calls (same B and shapes as
  * those calls) into grad_weights[k], in one launch (n <= 4). nonfinite
  * (nullable): set to 1 when a written grad is inf/nan (GradScaler's check). */

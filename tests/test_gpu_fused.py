@@ -345,7 +345,8 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
     gh2, gxp2 = gh0.clone(), torch.zeros_like(gx_ref)
     wsm = [torch.full_like(w, 7) for w in wsb]  # stale slab contents must not leak through
     nat.check(lib.ngp_nerf_backward(P(go), P(ci), P(imgs[1]), P(gh2), P(xp), P(imgs[0]), P(gxp2), B, P(cnt),
-                                    64, 2, 64, 3, P(wsm[0]), wsm[0].numel(), P(wsm[1]), wsm[1].numel(), s), "nerf_bwd")
+                                    64, 2, 64, 3, P(wsm[0]), wsm[0].numel(), P(wsm[1]), wsm[1].numel(), None, s),
+              "nerf_bwd")
     gw_one = [torch.zeros_like(t) for t in gw_ref]
     nat.check(lib.ngp_ffmlp_reduce(2, arr([wsm[1], wsm[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
                                    u32([3, 2]), arr([gw_one[1], gw_one[0]]), 1, None, s), "reduce")

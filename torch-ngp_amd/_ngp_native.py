@@ -107,7 +107,7 @@ SIGNATURES = {
     "ngp_ffmlp_backward_rows": [c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32,
                                 c_vp, c_vp, c_i32, c_u32, c_vp, c_sz, c_vp],
     "ngp_nerf_backward": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32,
-                          c_vp, c_sz, c_vp, c_sz, c_vp],
+                          c_vp, c_sz, c_vp, c_sz, c_vp, c_vp],
     "ngp_ffmlp_reduce": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
     "ngp_fused_state_bytes": [],
     "ngp_fused_state_init": [c_vp, c_f32, c_vp],

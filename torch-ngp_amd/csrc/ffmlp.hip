@@ -980,6 +980,13 @@ struct NerfBwdArgs {
     float* slab_sigma;
     uint32_t np_color, np_sigma, B;
     const int32_t* count;
+    // the grid backward's timing ring (NGP_GRID_TIMING, include/ngp_hip.h), or
+    // null: workgroup b stores its end (after its last store) in end slot
+    // MAX_WG - 1 - b of the call the next bin launch opens (the accumulate's
+    // workgroups fill the slots from 0), so the grid backward's span can start
+    // where this launch ended. Plain stores: one contended atomic per
+    // workgroup cost ~2 us at the launch's end.
+    uint32_t* timing;
 };
 
 template <int NHS, int NHC>
@@ -1003,6 +1010,7 @@ k_nerf_bwd(NerfBwdArgs a) {
     extern __shared__ half8 lds[];
     half8* sfr = reinterpret_cast<half8*>(reinterpret_cast<char*>(lds) + NL::sigma_frags);
     const uint32_t G = gridDim.x, b = blockIdx.x, w = threadIdx.x >> 6;
+    const uint32_t tcall = a.timing && threadIdx.x == 0 ? a.timing[0] : 0u;  // requested early
     bwd_phase<64, 1, NHC>(lds, reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes),
                           reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{}, GiNerfGeo{a.g_h},
                           true, a.slab_color, a.np_color, B, 32u, ActReLU{},
@@ -1019,6 +1027,12 @@ k_nerf_bwd(NerfBwdArgs a) {
                           InPairMajor{a.B}, GiPairMajor{a.g_enc, a.B}, true, a.slab_sigma, a.np_sigma, B, 32u,
                           ActReLU{}, [=](uint32_t k) { return b + (kBwdWaves - 1 - w + k * kBwdWaves) * G; },
                           []() {});
+    if (a.timing && b < NGP_GRID_TIMING_MAX_WG / 4) {
+        __syncthreads();
+        if (threadIdx.x == 0)
+            a.timing[64 + 4 * NGP_GRID_TIMING_RING + (tcall % NGP_GRID_TIMING_RING) * NGP_GRID_TIMING_MAX_WG +
+                     NGP_GRID_TIMING_MAX_WG - 1 - b] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // grad_weights[p] = sum over workgroup rows of the slab, in a fixed order
@@ -1325,7 +1339,7 @@ extern "C" int ngp_nerf_backward(const void* g_color_out, const void* color_in, 
                                  const int32_t* count, uint32_t hidden_dim, uint32_t num_layers,
                                  uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
                                  size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
-                                 void* stream) {
+                                 uint32_t* timing, void* stream) {
     NGP_REQUIRE(hidden_dim == 64 && hidden_dim_color == 64, NGP_ERR_UNSUPPORTED,
                 "nerf_backward: 64-wide networks only on this build, got %u / %u", hidden_dim, hidden_dim_color);
     NGP_REQUIRE(num_layers >= 2 && num_layers <= 3 && num_layers_color >= 2 && num_layers_color <= 3,
@@ -1354,6 +1368,7 @@ extern "C" int ngp_nerf_backward(const void* g_color_out, const void* color_in, 
     a.np_sigma = num_params(32, 64, num_layers);
     a.B = B;
     a.count = count;
+    a.timing = timing;
     hipStream_t st = ngp_stream(stream);
     const uint32_t key = (num_layers - 1) * 8 + (num_layers_color - 1);
     switch (key) {

@@ -466,8 +466,9 @@ class FusedTrainer:
 
     def grid_timing(self, last=None):
         """Device time of the grid backward's last calls since
-        grid_timing_reset() (at most 256, `last` if given): bin launch start ->
-        the accumulate's last workgroup end, measured by the kernels on the
+        grid_timing_reset() (at most 256, `last` if given): the MLP backward
+        launch's end (or the bin launch's start) -> the accumulate's last
+        workgroup end, measured by the kernels on the
         chip's 100 MHz constant clock, so graph replays are timed as they run
         (no events in the graphs). Returns (calls, ms per call, samples per
         call), oldest first, or None when the backward is unbinned."""
@@ -481,7 +482,18 @@ class FusedTrainer:
         ms, samples = [], []
         for c in range(calls - n, calls):
             start, samp, nwg = (int(v) for v in w[H + 4 * (c % R):H + 4 * (c % R) + 3])
-            ends = w[H + 4 * R + (c % R) * W:][:min(nwg, W)].astype(np.int64)
+            row = w[H + 4 * R + (c % R) * W:][:W].astype(np.int64)
+            ends = row[:min(nwg, W)]
+            # the span starts where the previous launch (the MLP backward,
+            # ngp_nerf_backward: its workgroups' ends fill the row from the
+            # top) ended, when those ends are this call's (within 100 us before
+            # the bin launch's first block): the bin launch's dispatch ramp
+            # then counts, as in the trace's kernel times
+            prev = row[max(min(nwg, W), W - W // 4):]
+            d = (start - prev) & 0xffffffff
+            fresh = prev[(d > 0) & (d < 10_000)]
+            if fresh.size:
+                start = int(fresh[((start - fresh) & 0xffffffff).argmin()])
             ms.append(float(((ends - start) & 0xffffffff).max()) * 1e-5)
             samples.append(samp)
         return calls, ms, samples
@@ -740,7 +752,8 @@ class FusedTrainer:
             chk(lib.ngp_nerf_backward(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
                                       P(self.enc_out), P(img[0]), P(self.g_enc), M, cnt, sn.hidden_dim,
                                       sn.num_layers, cn.hidden_dim, cn.num_layers, P(self.mlp_ws[0]),
-                                      self.mlp_ws[0].numel(), P(self.mlp_ws[1]), self.mlp_ws[1].numel(), s),
+                                      self.mlp_ws[0].numel(), P(self.mlp_ws[1]), self.mlp_ws[1].numel(),
+                                      P(self.grid_ws) + self._grid_timing_at if self._grid_timing_at else None, s),
                 "nerf_backward")
             self._tick("ffmlp_backward")
         else:
