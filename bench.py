@@ -505,8 +505,23 @@ def run_fused(args, model, data, bits, world, dev):
         "step_roofline": {"algorithmic_bytes": int(step_bytes),
                           "frac": round(step_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)},
         "density_update_ms": density,
+        # beside the headline (which SURVEY §8(d) defines without it): the step
+        # with upstream's density-grid cadence amortized in, one partial
+        # device-draw update (FusedTrainer.update_density) per 16 steps
+        "with_density_update": amortized_density(ms_per_step, density, args.num_rays * world),
         "loss": loss,
     }
+
+
+def amortized_density(ms_per_step, density, rays_per_step):
+    """ms/step and rays/s with one partial density update per 16 steps
+    (nerf/utils.py update_extra_interval = 16), or None if not measured."""
+    upd = (density or {}).get("fused_partial")
+    if not upd or not ms_per_step:
+        return None
+    ms = ms_per_step + upd / 16.0
+    return {"ms_per_step": round(ms, 4), "rays_per_s": round(rays_per_step / (ms * 1e-3), 1),
+            "update": "fused_partial / 16"}
 
 
 def density_update_times(model, bits, ft=None, reps=3):
