@@ -27,6 +27,17 @@ def test_gpus_must_match_the_launchers_world_size():
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
 
 
+def test_amortized_density_update():
+    """One partial device update per 16 steps (nerf/utils.py:
+    update_extra_interval) added to the step; None when it was not measured."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    r = bench.amortized_density(0.2, {"fused_partial": 0.48}, 4096)
+    assert r["ms_per_step"] == 0.23 and abs(r["rays_per_s"] - 4096 / 0.23e-3) < 1
+    assert bench.amortized_density(0.2, {}, 4096) is None
+    assert bench.amortized_density(0.2, None, 4096) is None
+
+
 @pytest.mark.gpu
 def test_bench_gpus2_gloo_runs_two_ranks():
     """`bench.py --gpus 2 --backend gloo` on the one-GPU box: both ranks run the
