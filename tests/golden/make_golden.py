@@ -163,6 +163,71 @@ def renderer_run_fixture():
                         weights_sum=out["weights_sum"].reshape(-1).numpy(), depth=out["depth"].reshape(-1).numpy())
 
 
+def renderer_run_backward_fixture():
+    """Autograd of NeRFRenderer.run's compositing (renderer.py:206-240): the
+    gradients composite_rays_train_backward (raymarching.cu:601-691) and the
+    fused composite + loss kernel must reproduce. The field is built from
+    fp16-representable logits, as the fused step's MLP outputs are:
+    sigma = exp(h0) (trunc_exp in range, activation.py:5-18) and
+    rgb = half(sigmoid(logit)) (autocast's half sigmoid). h0 and the colour
+    logits are the autograd leaves; two losses are differentiated on the same
+    graph:
+      * lin = sum(gI * image) + sum(gD * depth) + sum(gW * weights_sum), seeded
+        gI / gD / gW (every term of the composite backward), recorded as
+        d lin / d sigma and d lin / d rgb;
+      * mse = mean((image - gt)^2) over rays and channels (the train step's
+        MSELoss(reduction='none').mean(-1).mean(), nerf/utils.py), recorded as
+        d mse / d h0 and d mse / d logit."""
+    import types
+    run = extract_method(os.path.join(REF, "nerf/renderer.py"), "NeRFRenderer", "run",
+                         {"raymarching": types.SimpleNamespace(near_far_from_aabb=_slab_near_far)})
+    rec = {}
+
+    def density(x):
+        h0 = (np.log(40.0) - ((x - torch.tensor([0.05, 0.1, -0.1])) ** 2).sum(-1) / 0.15).half().float()
+        rec["h0"] = h0.detach().clone().requires_grad_(True)
+        sigma = torch.exp(rec["h0"])
+        rec["sigma"] = sigma
+        return {"sigma": sigma, "geo_feat": torch.zeros(x.shape[0], 15)}
+
+    def color(x, d, mask=None, geo_feat=None, **kw):
+        logit = torch.stack([2 * x[:, 0] - d[:, 2], 3 * x[:, 1] + d[:, 0], -x[:, 2] + 0.7 * d[:, 1]], -1)
+        rec["logit"] = logit.half().float().detach().clone().requires_grad_(True)
+        rgb = torch.sigmoid(rec["logit"]).half().float()
+        rec["rgb"] = rgb
+        return rgb
+
+    bound = 1.0
+    stub = types.SimpleNamespace(
+        aabb_train=torch.tensor([-bound] * 3 + [bound] * 3), aabb_infer=torch.tensor([-bound] * 3 + [bound] * 3),
+        training=True, min_near=0.2, density_scale=1.0, bg_radius=-1, density=density, color=color)
+    g = torch.Generator().manual_seed(6)
+    N, T = 80, 112
+    cam = torch.tensor([-0.4, -2.8, 0.9])
+    tgt = (torch.rand(N, 3, generator=g) - 0.5) * 1.3
+    rays_d = tgt - cam
+    rays_d = rays_d / rays_d.norm(dim=-1, keepdim=True)
+    rays_o = cam.expand(N, 3).contiguous()
+    out = run(stub, rays_o[None], rays_d[None], num_steps=T, upsample_steps=0, bg_color=None, perturb=False)
+    image, depth, ws = out["image"][0], out["depth"].reshape(-1), out["weights_sum"].reshape(-1)
+    gI, gD, gW = torch.randn(N, 3, generator=g), torch.randn(N, generator=g), torch.randn(N, generator=g)
+    gt = torch.rand(N, 3, generator=g)
+    sigma, rgb = rec["sigma"], rec["rgb"]
+    lin = (gI * image).sum() + (gD * depth).sum() + (gW * ws).sum()
+    d_sigma, d_rgb = torch.autograd.grad(lin, [sigma, rgb], retain_graph=True)
+    mse = ((image - gt) ** 2).mean(-1).mean()
+    d_h0, d_logit = torch.autograd.grad(mse, [rec["h0"], rec["logit"]])
+    nears, fars = _slab_near_far(rays_o, rays_d, stub.aabb_train, stub.min_near)
+    np.savez_compressed(os.path.join(HERE, "renderer_run_backward_reference.npz"), rays_o=rays_o.numpy(),
+                        rays_d=rays_d.numpy(), nears=nears.numpy(), fars=fars.numpy(), num_steps=np.int32(T),
+                        density_scale=np.float32(stub.density_scale), h0=rec["h0"].detach().numpy(),
+                        logit=rec["logit"].detach().numpy(), sigma=sigma.detach().numpy(),
+                        rgb=rgb.detach().numpy(), image=image.detach().numpy(), depth=depth.detach().numpy(),
+                        weights_sum=ws.detach().numpy(), gI=gI.numpy(), gD=gD.numpy(), gW=gW.numpy(),
+                        d_sigma=d_sigma.numpy(), d_rgb=d_rgb.numpy(), gt=gt.numpy(),
+                        mse=np.float32(mse.item()), d_h0=d_h0.numpy(), d_logit=d_logit.numpy())
+
+
 def get_rays_fixture():
     ns = extract(os.path.join(REF, "nerf/utils.py"), {"get_rays", "custom_meshgrid"})
     rng = np.random.default_rng(11)
@@ -215,6 +280,7 @@ if __name__ == "__main__":
     mlp_fixture()
     trunc_exp_fixture()
     renderer_run_fixture()
+    renderer_run_backward_fixture()
     get_rays_fixture()
     nerf_matrix_fixture()
     freq_fixture()

@@ -86,6 +86,106 @@ def test_hip_composite_matches_reference_run(cuda):
     _check_composite(f, ws.cpu().numpy(), depth.cpu().numpy(), image.cpu().numpy())
 
 
+# ------------------------------------------------- composite backward (autograd)
+
+def _grad_close(got, ref, what, rel=1e-3):
+    """Elementwise 1e-3 rel + 1e-3 of the largest magnitude, and 1e-3 rel-norm."""
+    g, r = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    assert g.shape == r.shape and np.isfinite(g).all(), what
+    err = float(np.linalg.norm(g - r) / max(np.linalg.norm(r), 1e-30))
+    assert err <= rel, (what, err)
+    tol = rel * np.abs(r) + rel * np.abs(r).max()
+    assert (np.abs(g - r) <= tol).all(), (what, float(np.abs(g - r).max()), float(np.abs(r).max()))
+    return err
+
+
+def _backward_case():
+    """renderer_run_backward_reference.npz: run()'s samples as the composite
+    kernels' inputs, and the kernel-side gradients of the fixture's linear
+    functional: run()'s image includes the white background, so
+    d/d weights_sum = gW - sum_c gI (renderer.py:240)."""
+    f = _load("renderer_run_backward_reference.npz")
+    _, deltas, rays = _run_samples(f)
+    g_ws = (f["gW"] - f["gI"].sum(-1)).astype(np.float32)
+    return f, deltas, rays, g_ws
+
+
+def test_oracle_composite_backward_matches_reference_autograd():
+    """oracle.composite_rays_train_backward (raymarching.cu:601-691) against
+    torch autograd of the reference's run() compositing (renderer.py:206-240):
+    d/d sigma and d/d rgb of sum(gI image) + sum(gD depth) + sum(gW ws)."""
+    f, deltas, rays, g_ws = _backward_case()
+    sigma = (f["sigma"] * f["density_scale"]).astype(np.float32)
+    ws, depth, image = oracle.composite_rays_train_forward(sigma, f["rgb"], deltas, rays, 0.0)
+    np.testing.assert_allclose(image + (1 - ws)[:, None], f["image"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(depth, f["depth"], rtol=1e-5, atol=1e-5)
+    g_sig, g_rgb = oracle.composite_rays_train_backward(g_ws, f["gD"], f["gI"], sigma, f["rgb"], deltas, rays,
+                                                        ws, depth, image, 0.0)
+    _grad_close(g_sig, f["d_sigma"], "d sigma")
+    _grad_close(g_rgb, f["d_rgb"], "d rgb")
+
+
+@pytest.mark.gpu
+def test_hip_composite_backward_matches_reference_autograd(cuda, parity_report):
+    """The HIP composite_rays_train backward through the reference-API autograd
+    Function (raymarching.py:238-289) against the reference's autograd."""
+    import raymarching
+    f, deltas, rays, g_ws = _backward_case()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    sigma = t((f["sigma"] * f["density_scale"]).astype(np.float32)).requires_grad_(True)
+    rgbs = t(f["rgb"]).requires_grad_(True)
+    ws, depth, image = raymarching.composite_rays_train(sigma, rgbs, t(deltas), t(rays), 0.0)
+    g_sig, g_rgb = torch.autograd.grad([ws, depth, image], [sigma, rgbs], [t(g_ws), t(f["gD"]), t(f["gI"])])
+    e1 = _grad_close(g_sig.cpu().numpy(), f["d_sigma"], "d sigma")
+    e2 = _grad_close(g_rgb.cpu().numpy(), f["d_rgb"], "d rgb")
+    parity_report(f"vs reference run() autograd: d_sigma rel {e1:.2e}, d_rgb rel {e2:.2e}")
+
+
+@pytest.mark.gpu
+def test_fused_composite_loss_matches_reference_autograd(cuda, parity_report):
+    """The fused step's k_composite_loss (composite + white background + MSE +
+    composite backward + trunc_exp / sigmoid backward, csrc/nerf_fused.hip)
+    against autograd of the reference's run() + MSE (renderer.py:206-240,
+    nerf/utils.py train_step): d mse / d h0 and d mse / d (colour logits),
+    loss-scaled fp16 outputs divided by the scale; loss within 1e-4."""
+    import _ngp_native as nat
+    f, deltas, rays, _ = _backward_case()
+    N, M = rays.shape[0], deltas.shape[0]
+    scale = 65536.0  # GradScaler's init_scale
+    h = np.zeros((M, 16), np.float16)
+    h[:, 0] = f["h0"]
+    col = np.zeros((M, 16), np.float16)
+    col[:, :3] = f["logit"]
+    assert np.array_equal(h[:, 0].astype(np.float32), f["h0"]) and np.array_equal(col[:, :3].astype(np.float32),
+                                                                                 f["logit"])
+    sigma = (np.float32(f["density_scale"]) * np.exp(f["h0"])).astype(np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    d_sigma, d_col, d_h, d_del, d_rays, d_gt = map(t, (sigma, col, h, deltas, rays, f["gt"]))
+    d_bg = torch.ones(N, 3, device=cuda)
+    state = torch.zeros(nat.lib().ngp_fused_state_bytes(), dtype=torch.uint8, device=cuda)
+    nat.check(nat.lib().ngp_fused_state_init(nat.ptr(state), scale, nat.stream_of(state)), "state_init")
+    g_col = torch.zeros(M, 16, dtype=torch.float16, device=cuda)
+    g_h = torch.zeros(M, 16, dtype=torch.float16, device=cuda)
+    img = torch.zeros(N, 3, device=cuda)
+    ws = torch.zeros(N, device=cuda)
+    loss = torch.zeros(N, device=cuda)
+    P = nat.ptr
+    nat.check(nat.lib().ngp_nerf_composite_loss(
+        P(d_sigma), P(d_col), P(d_h), P(d_del), P(d_rays), M, N, 0.0, float(f["density_scale"]), P(d_gt), 3,
+        P(d_bg), P(state), P(g_col), P(g_h), P(img), P(ws), P(loss), nat.stream_of(img)), "composite_loss")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(img.cpu().numpy(), f["image"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ws.cpu().numpy(), f["weights_sum"], rtol=1e-5, atol=1e-5)
+    got_loss = float(loss.double().sum().item()) / N
+    assert abs(got_loss - float(f["mse"])) <= 1e-4 * float(f["mse"]), (got_loss, float(f["mse"]))
+    gh0 = g_h[:, 0].float().cpu().numpy() / scale
+    gl = g_col[:, :3].float().cpu().numpy() / scale
+    assert (g_col[:, 3:] == 0).all() and (g_h[:, 1:] == 0).all()
+    e1 = _grad_close(gh0, f["d_h0"], "d mse / d h0")
+    e2 = _grad_close(gl, f["d_logit"], "d mse / d logit")
+    parity_report(f"vs reference run()+MSE autograd: d_h0 rel {e1:.2e}, d_logit rel {e2:.2e}, loss {got_loss:.6f}")
+
+
 def test_torch_get_rays_matches_reference():
     from nerf.utils import get_rays
     f = _load("get_rays_reference.npz")

@@ -126,7 +126,7 @@ IDS = ["lego", "fox", "truck"]
 
 
 @pytest.mark.parametrize("bound,dt_gamma,log2T,hw", CONFIGS, ids=IDS)
-def test_fused_step_stages_match_oracle(cuda, bound, dt_gamma, log2T, hw):
+def test_fused_step_stages_match_oracle(cuda, parity_report, bound, dt_gamma, log2T, hw):
     ft = _setup(cuda, bound, dt_gamma, log2T, hw)
     if bound == 1:  # SURVEY §8 table sizes (bound 2 has a finer desired resolution)
         assert ft.enc.embeddings.shape[0] == (39625280 if log2T == 22 else 6119864)
@@ -221,10 +221,14 @@ def test_fused_step_stages_match_oracle(cuda, bound, dt_gamma, log2T, hw):
     tol = 4e-3 * np.abs(gemb_ref) + 1e-3 * np.abs(gemb_ref).max()
     assert (np.abs(gemb - gemb_ref) <= tol).all(), np.abs(gemb - gemb_ref).max()
     assert np.all(gemb[gemb_ref == 0] == 0)  # nothing lands where no sample contributed
+    parity_report(f"bound {bound} dt_gamma {dt_gamma:g} log2T {log2T} {hw[1]}x{hw[0]}: {n} samples, march/grid fwd "
+                  f"bit-exact, d_rgb_logit rel {_rel(gc[:n], gc_ref):.1e}, d_sigma_logit rel "
+                  f"{_rel(gh[:n, 0], gh0_ref):.1e}, dW color {_rel(gw_color, gwc_ref):.1e} sigma "
+                  f"{_rel(gw_sigma, gws_ref):.1e}, table grad {_rel(gemb, gemb_ref):.1e}")
 
 
 @pytest.mark.parametrize("bound,dt_gamma,log2T,hw", CONFIGS, ids=IDS)
-def test_fused_step_end_to_end_matches_oracle(cuda, bound, dt_gamma, log2T, hw):
+def test_fused_step_end_to_end_matches_oracle(cuda, parity_report, bound, dt_gamma, log2T, hw):
     """north_star: rendered RGB / sigma within 1e-3 rel of the reference,
     sample counts / indices bit-exact; the oracle runs from the batch alone."""
     ft = _setup(cuda, bound, dt_gamma, log2T, hw)
@@ -258,4 +262,5 @@ def test_fused_step_end_to_end_matches_oracle(cuda, bound, dt_gamma, log2T, hw):
         assert np.isfinite(g).all() and np.abs(want).max() > 0, what
         report[f"grad_{what}_rel"] = _rel(g, want)
         assert _rel(g, want) <= 5e-3, (what, _rel(g, want))
-    print(f"e2e vs oracle (bound {bound}, log2T {log2T}, {hw[1]}x{hw[0]}):", report)
+    parity_report(f"bound {bound} dt_gamma {dt_gamma:g} log2T {log2T} {hw[1]}x{hw[0]}: "
+                  + ", ".join(f"{k} {v:.2e}" if isinstance(v, float) else f"{k} {v}" for k, v in report.items()))

@@ -15,7 +15,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0, fused_adam=None, occ="boxes"):
+def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0, fused_adam=None, occ="boxes",
+           grid_timing=None):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield, sphere_bitfield
@@ -29,7 +30,7 @@ def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0, fused_a
     data = SyntheticLego(cuda, num_rays=num_rays)
     M = mean_count + 128 - mean_count % 128  # what run_cuda's align=128 makes of mean_count
     ref.mean_count = mean_count
-    ft = FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma, fused_adam=fused_adam)
+    ft = FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma, fused_adam=fused_adam, grid_timing=grid_timing)
     return model, ref, data, ft
 
 
@@ -221,6 +222,41 @@ def test_multi_step_graph_equals_single_steps(cuda):
     assert a.optimizer_steps == b.optimizer_steps
     assert torch.equal(a._recent_counts(15), b._recent_counts(15))
     assert a.scale == b.scale and a.last_loss == b.last_loss
+
+
+class _CountingGraph:
+    def __init__(self, g):
+        self.g, self.replays = g, 0
+
+    def replay(self):
+        self.replays += 1
+        self.g.replay()
+
+
+def test_run_after_flush_replays_multi_step_graph(cuda):
+    """After a flush() (update_density, checkpoints, read-outs) nothing is
+    pending; run(k) then runs one step() and replays the multi-step graph for
+    the rest, bit for bit equal to k single steps."""
+    _, _, _, a = _setup(cuda)
+    _, _, _, b = _setup(cuda)
+    for t in (a, b):
+        t.step()
+    a.capture(warmup=2, multi=4)
+    b.capture(warmup=2)
+    a.graph_multi = _CountingGraph(a.graph_multi)
+    for t in (a, b):
+        t.flush()
+        assert not t._pending
+    a.run(10)  # one step(), two 4-step replays, one step()
+    assert a.graph_multi.replays == 2
+    for _ in range(10):
+        b.step()
+    a.flush()
+    b.flush()
+    torch.cuda.synchronize()
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+    assert a.optimizer_steps == b.optimizer_steps and a.model.local_step == b.model.local_step
 
 
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
@@ -543,7 +579,7 @@ def test_grid_backward_self_timing_counts_graph_replays(cuda):
     """NGP_GRID_TIMING (the bench's roofline clock): every grid backward of
     the captured step opens a ring entry with its samples and the accumulate
     closes it; the spans are positive and a step's worth."""
-    _, _, _, ft = _setup(cuda, num_rays=4096, mean_count=120000, fused_adam=False)
+    _, _, _, ft = _setup(cuda, num_rays=4096, mean_count=120000, fused_adam=False, grid_timing=True)
     assert ft._grid_timing_at > ft._grid_counter_bytes
     ft.step()
     ft.capture(warmup=1)
@@ -557,6 +593,28 @@ def test_grid_backward_self_timing_counts_graph_replays(cuda):
     assert calls == 5 and samples == counts
     assert all(1e-3 < v < 5.0 for v in ms), ms
     assert ft.grid_timing(last=2)[1] == ms[-2:]
+
+
+def test_grid_timing_off_by_default(cuda):
+    """The self-timing ring is bench instrumentation: off unless asked for."""
+    _, _, _, ft = _setup(cuda)
+    assert ft._grid_timing_at == 0 and ft.grid_timing() is None
+
+
+def test_plain_capture_after_ring_capture_replays_plain_graph(cuda):
+    """capture() after capture(ring=R) drops the timing ring, so
+    step() replays the newly captured graph."""
+    _, _, _, ft = _setup(cuda)
+    ft.step()
+    ft.capture(warmup=1)
+    # a timing ring left by an earlier capture(ring=R) (ROCm 7 refuses its event
+    # nodes, so it is stood in for here: step() would replay it first)
+    ft._ring, ft._ring_i = [(ft.graph, [])], 0
+    ft.capture(warmup=1)
+    assert ft._ring == [] and ft.graph is not None
+    ft.graph = _CountingGraph(ft.graph)
+    ft.step()
+    assert ft.graph.replays == 1
 
 
 def test_composite_loss_large_densities_match_serial(cuda):

@@ -76,7 +76,7 @@ def test_oracle_gradcheck(B, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,seed", [(1, 42), (1, 7), (16, 3)])
-def test_hip_grid_encode_gradcheck(cuda, B, seed):
+def test_hip_grid_encode_gradcheck(cuda, parity_report, B, seed):
     """testing/test_hashgrid_grad.py:51-61 on the HIP path, argument tuple as there."""
     from gridencoder.grid import _grid_encode
     torch.manual_seed(seed)
@@ -91,3 +91,4 @@ def test_hip_grid_encode_gradcheck(cuda, B, seed):
                                         embeddings.detach().cpu().numpy(), offsets.cpu().numpy(),
                                         PER_LEVEL_SCALE, H)
     assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
+    parity_report(f"reference gradcheck (test_hashgrid_grad.py) B {B} seed {seed}: passed, fp64 forward bit-exact")

@@ -56,7 +56,7 @@ def _vp_array(ptrs):
 class FusedTrainer:
     def __init__(self, model, dataset, M, lr=1e-2, iters=30000, max_steps=1024, T_thresh=1e-4,
                  dt_gamma=0.0, seed=0, betas=(0.9, 0.99), eps=1e-15, init_scale=65536.0,
-                 growth_interval=2000, distributed=False, fused_adam=None):
+                 growth_interval=2000, distributed=False, fused_adam=None, grid_timing=None):
         """distributed: ray-sharded data parallelism over the initialised
         torch.distributed group: each rank draws its own rays; the flat fp16
         gradient is averaged with one RCCL reduce-scatter, each rank's Adam
@@ -71,7 +71,11 @@ class FusedTrainer:
         `grads[0]`, which the parity tests inspect. Measured slower on the
         Lego step (DESIGN.md "Measured and dropped": the accumulate becomes
         bandwidth-bound on the moved Adam stream, 14.5 -> 62 us, while the
-        head's Adam fell 50.6 -> 17 us)."""
+        head's Adam fell 50.6 -> 17 us).
+        grid_timing: the binned grid backward times itself on the chip's
+        constant clock (`grid_timing()`, the bench's roofline clock); off by
+        default (NGP_GRID_TIMING=1 turns it on), since it adds ring stores to
+        the backward's launches."""
         assert model.cuda_ray, "the fused step marches the density bitfield (cuda_ray=True)"
         enc = model.encoder
         assert enc.level_dim == 2 and enc.num_levels * enc.level_dim == 32 and enc.input_dim == 3
@@ -159,12 +163,15 @@ class FusedTrainer:
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
             int(enc.align_corners), self._offsets_host))
         self._grid_flags = _ZEROED | (_EXTERNAL if self._grid_counter_bytes else 0)
-        # the binned grid backward times itself (a few atomics per launch): the
-        # workspace's timing words keep [start, ticks, samples, calls]
+        # the binned grid backward can time itself (grid_timing; plain stores
+        # into a ring in the workspace: per call its start, samples and the
+        # accumulate workgroups' ends)
         self._grid_timing_at = int(nat.lib().ngp_grid_encode_backward_fused_timing_offset(
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
             int(enc.align_corners), self._offsets_host))
-        if os.environ.get("NGP_GRID_TIMING", "1") == "0":  # A/B: the kernels without their clock
+        if grid_timing is None:
+            grid_timing = os.environ.get("NGP_GRID_TIMING", "0") == "1"
+        if not grid_timing:
             self._grid_timing_at = 0
         if self._grid_timing_at:
             self._grid_flags |= _TIMING
@@ -682,7 +689,8 @@ class FusedTrainer:
         self._tick("step_head")
 
     def _forward_backward(self):
-        """march -> network -> composite + MSE -> full backward into the fp16 grads."""
+        """march -> network -> composite + MSE -> full backward into the fp16 grads
+        (on the batch in the buffers; `_sample()` draws one)."""
         self._march()
         self._network()
 
@@ -800,6 +808,10 @@ class FusedTrainer:
             chk(lib.ngp_grid_encode_backward_fused_reduce(*bargs, 2, pk["ws"], pk["B"], pk["ins"], pk["hid"],
                                                           pk["nl"], pk["gw"], self._inf_flag, s),
                 "grid_backward_fused_reduce")
+        if not draw:
+            # this backward consumed the batch in the buffers and drew none: a
+            # batch drawn ahead earlier is spent, the next step draws its own
+            self._ahead = False
         self._tick("grid_encode_backward")
 
     def _optimizer(self, defer=False):
@@ -869,9 +881,14 @@ class FusedTrainer:
         """k training iterations. With a multi-step graph (capture(multi=S),
         world 1) it replays floor(k / S) times -- S steps back to back in one
         graph launch, so the per-launch gap between graph replays is paid once
-        per S steps -- and step() runs the rest."""
+        per S steps -- and step() runs the rest. The graphs hold a pending
+        update at their head, so after a flush() (update_density, checkpoint,
+        read-outs) the first iteration runs as step()."""
         g, S = self.graph_multi, self._multi
-        if g is not None and self._pending and not self.dp and not self._ring:
+        if g is not None and not self.dp and not self._ring:
+            if not self._pending and k > 0:
+                self.step()
+                k -= 1
             for _ in range(k // S):
                 g.replay()
                 self.model.local_step += S
@@ -919,6 +936,7 @@ class FusedTrainer:
                 self._events, self._capturing = None, False
             return
         if not self.dp:
+            self._ring, self._ring_i = [], 0  # step() would replay an older timing ring first
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._body(True)
