@@ -49,10 +49,11 @@ WORKLOADS = {
                    "hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19, "ball", 1, 0.0),
     "truck": ("truck_1920x1080_train_step (Config 5 single-GPU leg: synthetic scene at 1920x1080, bound 1, "
               "hashgrid L16 C2 T2^22 = 39.6M entries, FFMLP 64-wide)", 1080, 1920, 22, "boxes", 1, 0.0),
-    "fox": ("fox_shaped_800x800_train_step (Config 3 shapes on the synthetic scene: bound 2, 2 cascades, "
-            "dt_gamma 1/128, desired_resolution 4096, hashgrid L16 C2 T2^19, FFMLP 64-wide)", 800, 800, 19,
-            "boxes", 2, 1.0 / 128),
+    "fox": ("fox_shaped_800x800_train_step (Config 3 shapes: bound 2, 2 cascades, dt_gamma 1/128, "
+            "desired_resolution 4096, a Fox-shaped ellipsoid occupancy, hashgrid L16 C2 T2^19, FFMLP 64-wide)",
+            800, 800, 19, "fox", 2, 1.0 / 128),
 }
+LEGS = ("lego_dense", "truck", "fox")
 
 
 def parse():
@@ -77,6 +78,14 @@ def parse():
                     help="untimed steps after the warmup that bring the GPU to its sustained clock")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
+    ap.add_argument("--no-legs", dest="legs", action="store_false",
+                    help="skip the other workloads (lego_dense, truck, fox) run after the headline at N=1")
+    ap.add_argument("--leg-steps", type=int, default=50)
+    ap.add_argument("--leg-settle", type=int, default=300)
+    ap.add_argument("--no-render", dest="render", action="store_false",
+                    help="skip the test-render speed (one full image per iteration) at N=1")
+    ap.add_argument("--no-dp-path", dest="dp_path", action="store_false",
+                    help="skip the data-parallel engine path measured on a one-rank RCCL group at N=1")
     ap.add_argument("--engine", choices=["fused", "autograd"], default="fused")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="lego",
                     help="lego: the headline (Config 2, Lego 800x800, box occupancy, ~19 samples/ray); "
@@ -167,22 +176,11 @@ def main():
     torch.manual_seed(1234 + rank)
     np.random.seed(rank)
 
-    from nerf.network_ff import NeRFNetwork
-    from nerf.provider import SyntheticLego, lego_bitfield, sphere_bitfield
-
-    desc, img_h, img_w, log2T, occ, bound, dt_gamma = WORKLOADS[args.workload]
-    model = NeRFNetwork(bound=bound, cuda_ray=True, density_thresh=10, log2_hashmap_size=log2T).to(dev)
-    if world > 1:  # identical initial parameters on every rank
-        for p in model.parameters():
-            dist.broadcast(p.data, 0)
-    bits = (lego_bitfield(cascade=model.cascade, bound=float(bound)) if occ == "boxes"
-            else sphere_bitfield(cascade=model.cascade, bound=float(bound)))
-    bits = torch.from_numpy(bits).to(dev)
-    model.density_bitfield.copy_(bits)
-    data = SyntheticLego(dev, H=img_h, W=img_w, num_rays=args.num_rays)
+    model, data, bits, desc, img_h, img_w, dt_gamma = make_workload(args.workload, dev, world, args.num_rays)
     args.dt_gamma = dt_gamma
+    ft = None
     if args.engine == "fused":
-        result = run_fused(args, model, data, bits, world, dev)
+        result, ft = run_fused(args, model, data, bits, world, dev)
     else:
         result = run_autograd(args, model, data, bits, world, dev)
     result["config"]["collective"] = comm
@@ -191,6 +189,16 @@ def main():
     spr = result["config"]["samples_per_step"] / args.num_rays
     result["samples_per_ray"] = round(spr, 2)
     result["samples_per_s"] = round(result["value"] * spr, 1)
+    if world == 1 and args.engine == "fused":
+        ft.flush()
+        if args.render:
+            result["render"] = render_probe(args, model, data, dev)
+        if args.dp_path:
+            result["dp_path"] = dp_path_probe(args, model, data, dev, result)
+        if args.legs:
+            del ft
+            torch.cuda.empty_cache()
+            result["legs"] = {w: run_leg(args, w, dev) for w in LEGS if w != args.workload}
 
     if rank == 0 and world == 1 and args.cpu:
         result["cpu_baseline"] = cpu_baseline(model, data, args)
@@ -199,6 +207,158 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def make_workload(name, dev, world, num_rays):
+    """Model (random init, identical on every rank), its benched occupancy
+    bitfield and the synthetic dataset of a WORKLOADS entry."""
+    from nerf.network_ff import NeRFNetwork
+    from nerf.provider import SyntheticLego, fox_bitfield, lego_bitfield, sphere_bitfield
+    desc, img_h, img_w, log2T, occ, bound, dt_gamma = WORKLOADS[name]
+    model = NeRFNetwork(bound=bound, cuda_ray=True, density_thresh=10, log2_hashmap_size=log2T).to(dev)
+    if world > 1:  # identical initial parameters on every rank
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    occupancy = {"boxes": lego_bitfield, "ball": sphere_bitfield, "fox": fox_bitfield}[occ]
+    bits = torch.from_numpy(occupancy(cascade=model.cascade, bound=float(bound))).to(dev)
+    model.density_bitfield.copy_(bits)
+    data = SyntheticLego(dev, H=img_h, W=img_w, num_rays=num_rays)
+    return model, data, bits, desc, img_h, img_w, dt_gamma
+
+
+def run_leg(args, name, dev):
+    """One more workload in the same invocation (N=1): the same timed region
+    (warmup, capture, clock settle, exactly leg_steps complete steps), with its
+    samples / ray, rays/s and the grid backward on its own clock beside the
+    same workload's committed PMC traffic."""
+    model, data, bits, desc, img_h, img_w, dt_gamma = make_workload(name, dev, 1, args.num_rays)
+    ft, mean_count = make_trainer(args, model, data, 1, dev, dt_gamma)
+    elapsed, used_graph, grid_clock = timed_run(args, ft, 1, dev, args.leg_steps, 5, args.leg_settle,
+                                                args.graph_steps)
+    counts = ft._recent_counts(min(16, args.leg_steps)).float().mean().item()
+    rays_s = args.num_rays * args.leg_steps / elapsed
+    out = {"workload": desc, "rays_per_s": round(rays_s, 1), "ms_per_step": round(elapsed / args.leg_steps * 1e3, 4),
+           "steps": args.leg_steps, "samples_per_ray": round(counts / args.num_rays, 2),
+           "samples_per_s": round(rays_s * counts / args.num_rays, 1), "mean_count_M": mean_count,
+           "hipgraph": used_graph, "grid_encode_backward": grid_roofline(grid_clock, args.leg_steps, name)}
+    del ft, model
+    torch.cuda.empty_cache()
+    return out
+
+
+def render_probe(args, model, data, dev, images=5, pose=7):
+    """Test-render speed (the reference publishes 7.8 it/s
+    test speed on a V100, readme.md:211): one full HxW image per iteration of
+    the model as the bench run trained it, eval mode, through the
+    device-driven loop (nerf/fused_render.py: march / network / composite with
+    the alive-ray list kept on the device, K iterations per hipGraph replay,
+    one host read of the loop state per replay), wall time per image
+    synchronised; beside it the reference-API loop (NeRFRenderer.run_cuda,
+    one host sync per iteration) on the same rays."""
+    from nerf.fused_render import FusedRenderer
+    from nerf.utils import get_rays
+    model.eval()
+    try:
+        rays = get_rays(data.poses[pose:pose + 1], data.intrinsics, data.H, data.W, -1)
+        ro, rd = rays["rays_o"], rays["rays_d"]
+        N = data.H * data.W
+        r = FusedRenderer(model, N, dt_gamma=args.dt_gamma)
+        r.load_weights()
+        r.capture()
+
+        def timed(fn, reps):
+            ts = []
+            for _ in range(reps + 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                out = fn()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            return float(np.mean(ts[1:])), out
+
+        secs, out = timed(lambda: r.render(ro, rd, bg_color=1), images)
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+            ref_secs, ref = timed(lambda: model.render(ro, rd, staged=True, bg_color=1, perturb=False,
+                                                       dt_gamma=args.dt_gamma, max_steps=1024), 2)
+        diff = (out["image"].reshape(-1, 3) - ref["image"].reshape(-1, 3).float()).abs().max(-1).values
+        res = {"metric": "test render (one full image per iteration, inference march / network / composite loop)",
+               "image_hw": [data.H, data.W], "images_timed": images, "ms_per_image": round(secs * 1e3, 3),
+               "it_per_s": round(1.0 / secs, 2), "rays_per_s": round(N / secs, 1),
+               "device_iterations": r.iterations, "iterations_per_graph": r.K,
+               "reference_api_loop": {"ms_per_image": round(ref_secs * 1e3, 3), "it_per_s": round(1.0 / ref_secs, 2)},
+               "image_vs_reference_api": {"pixels_within_1e-3": round(float((diff <= 1e-3).float().mean()), 6),
+                                          "max_abs": float(diff.max())},
+               "weights_sum_mean": round(float(out["weights_sum"].mean()), 4),
+               "baseline_ref": "V100 7.8 it/s test speed (readme.md:211)",
+               "vs_published": round(1.0 / secs / 7.8, 2)}
+        del r
+        torch.cuda.empty_cache()
+        return res
+    finally:
+        model.train()
+
+
+def dp_path_probe(args, model, data, dev, headline):
+    """The data-parallel engine path (FusedTrainer(distributed=True), ZeRO-1:
+    three graphs, grad guard, reduce-scatter, sharded Adam, async all-gather)
+    on a one-rank RCCL (`nccl`) group on this GPU: its per-rank step time and
+    per-phase times (eager, serial phases with events between them; at world
+    1 the collectives are RCCL's local copies), the bytes each rank's
+    collectives move per step at 8 ranks, and what the 1 -> 8 scaling target
+    leaves for exposed collective time. Reference: the DDP all-reduce it
+    replaces, nerf/utils.py:325-327."""
+    import socket
+    if dist.is_initialized():
+        return None
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        m2, d2, bits2, _, _, _, dtg = make_workload(args.workload, dev, 1, args.num_rays)
+        ft, _ = make_trainer(args, m2, d2, 1, dev, dtg, distributed=True)
+        assert ft.dp and ft._nccl
+        steps = max(20, args.steps)
+        elapsed, used_graph, _ = timed_run(args, ft, 1, dev, steps, 5, 300, 1)
+        ms = elapsed / steps * 1e3
+        phases = ft.timed_steps(args.kernel_steps)
+        grad_bytes = 2 * ft.total  # the flat fp16 gradient = the fp16 forward copy
+        truck_bytes = 2 * _flat_total(22)
+        W = 8
+        headline_ms = headline["ms_per_step"]
+        budget = W * headline_ms / 6.0  # per-rank step time that still gives 6x at 8 ranks
+        out = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "graphs": used_graph,
+               "ms_per_step": round(ms, 4), "rays_per_s": round(args.num_rays / (ms * 1e-3), 1),
+               "phases_ms": {k: round(v, 5) for k, v in phases.items()},
+               "flat_grad_bytes": int(grad_bytes),
+               "per_rank_bytes_8_ranks": {
+                   "config4_lego": {"reduce_scatter": int(grad_bytes * (W - 1) / W),
+                                    "all_gather": int(grad_bytes * (W - 1) / W)},
+                   "config5_truck": {"flat_grad_bytes": int(truck_bytes),
+                                     "reduce_scatter": int(truck_bytes * (W - 1) / W),
+                                     "all_gather": int(truck_bytes * (W - 1) / W)}},
+               "scaling_budget_8_ranks": {"per_rank_ms_for_6x": round(budget, 4),
+                                          "compute_ms_world1_dp_path": round(ms, 4),
+                                          "exposed_collective_ms_allowed": round(budget - ms, 4)}}
+        del ft, m2
+        torch.cuda.empty_cache()
+        return out
+    finally:
+        dist.destroy_process_group()
+
+
+def _flat_total(log2T):
+    """Length of the flat parameter buffer (table + both MLPs, 8-aligned
+    each) for a bound-1 model with a 2^log2T-entry hash table."""
+    from gridencoder import GridEncoder
+    enc = GridEncoder(input_dim=3, num_levels=16, level_dim=2, base_resolution=16, log2_hashmap_size=log2T,
+                      desired_resolution=2048)
+    n_tab = int(enc.offsets[-1]) * 2
+    r8 = lambda n: (n + 7) // 8 * 8  # noqa: E731
+    return r8(n_tab) + r8(64 * (32 + 64 + 16)) + r8(64 * (32 + 64 + 64 + 16))
 
 
 def run_autograd(args, model, data, bits, world, dev):
@@ -344,11 +504,33 @@ def run_autograd(args, model, data, bits, world, dev):
     return result
 
 
-def run_fused(args, model, data, bits, world, dev):
-    from nerf.fused import FusedTrainer
+def adam_bytes(ft):
+    """Algorithmic HBM bytes of one Adam sweep of this rank (SURVEY §8(d) and
+    DESIGN.md §4): per parameter p, m, v read + write (24 B) and the fp16 grad
+    read + clear (4 B); + 2 B for an fp16 forward copy where one is written (the
+    MLPs; the table too when it is kept, data parallel)."""
+    n_tab = int(ft.params[0].numel())
+    n_mlp = int(sum(p.numel() for p in ft.params[1:]))
+    if ft.dp:
+        return int(30 * ft.chunk)
+    return int((28 if ft.table32 else 30) * n_tab + 30 * n_mlp)
 
-    # sample-buffer size: measured counts x 1.25 (mean_count, update_extra_state)
-    probe = FusedTrainer(model, data, M=args.num_rays * 64, distributed=world > 1, dt_gamma=args.dt_gamma)
+
+def launch_bytes(ft, samples, rays):
+    """SURVEY §8(d) per-unit bytes of each launch of the world-1 step body
+    (timed_body_steps names): None for the MFMA-bound MLP launches."""
+    march = 48 * rays + 32 * samples
+    return {"march_rays_train+adam": adam_bytes(ft) + march, "march_rays_train": march,
+            "step_head": None, "grid_encode_forward": 588 * samples, "grid_encode_backward": 1100 * samples,
+            "composite_loss": (32 + 52) * rays + (24 + 40) * samples, "ffmlp_forward": None, "ffmlp_backward": None}
+
+
+def make_trainer(args, model, data, world, dev, dt_gamma, grid_timing=True, distributed=None):
+    """A FusedTrainer with its sample buffer sized as upstream sizes it
+    (mean_count = measured counts x 1.25, update_extra_state)."""
+    from nerf.fused import FusedTrainer
+    dp = world > 1 if distributed is None else distributed
+    probe = FusedTrainer(model, data, M=args.num_rays * 64, distributed=dp, dt_gamma=dt_gamma)
     counts = []
     for _ in range(4):
         probe.step()
@@ -361,100 +543,134 @@ def run_fused(args, model, data, bits, world, dev):
     probe.flush()  # data parallel: every rank's shard of the masters gathered back
     del probe
     torch.cuda.empty_cache()
-    ft = FusedTrainer(model, data, M=mean_count, distributed=world > 1, dt_gamma=args.dt_gamma)
-    for _ in range(max(1, args.warmup)):
+    ft = FusedTrainer(model, data, M=mean_count, distributed=dp, dt_gamma=dt_gamma, grid_timing=grid_timing)
+    return ft, mean_count
+
+
+def timed_run(args, ft, world, dev, steps, warmup, settle, graph_steps):
+    """Warm up, capture, settle the clocks, then time exactly `steps` complete
+    steps between barriers + synchronize (max over ranks). Returns (elapsed s,
+    used_graph, the grid backward's own clock over the timed steps)."""
+    for _ in range(max(1, warmup)):
         ft.step()
     used_graph = False
-    timing = "eager"
     if args.graph:
         try:
-            ft.capture(multi=args.graph_steps if world == 1 else 1)
-            ft.run(3 * max(1, args.graph_steps))
+            ft.capture(multi=graph_steps if not ft.dp else 1)
+            ft.run(3 * max(1, graph_steps))
             used_graph = True
         except Exception as e:  # eager launches are the same kernels; record why
             print(f"[bench] graph capture failed, running eager: {e!r}", file=sys.stderr)
             ft.graph = None
-    if used_graph and args.ring > 0 and not ft.dp:
-        try:  # the timed region replays graphs that carry event-record nodes
-            ft.capture(warmup=1, ring=min(args.ring, 16))
-            timing = "graph_events"
-        except Exception as e:
-            print(f"[bench] timing-ring capture failed, per-launch times from eager steps: {e!r}",
-                  file=sys.stderr)
     torch.cuda.synchronize()
     # clock settle: the GPU raises its clocks only under sustained load. A
     # 20-step run right after 5 warmup steps measured 15.0M rays/s against
     # 17.3M for 200 steps on the same box (profiles/r02zl_settle.txt), so a
     # fixed number of untimed steps (same on every rank: they hold
     # collectives) runs before the timed region.
-    for i in range(0, args.settle_steps, 64):
-        ft.run(min(64, args.settle_steps - i))
+    for i in range(0, settle, 64):
+        ft.run(min(64, settle - i))
         torch.cuda.synchronize()
     torch.cuda.synchronize()
-
     # ---------------- timed region ----------------
     if world > 1:
         dist.barrier()
     ft.grid_timing_reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ft.run(args.steps)
+    ft.run(steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    grid_clock = ft.grid_timing(last=args.steps)  # the timed region's grid backwards (<= 256 of them)
+    grid_clock = ft.grid_timing(last=steps)  # the timed region's grid backwards (<= 256 of them)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    return elapsed, used_graph, grid_clock
+
+
+def grid_roofline(grid_clock, steps, workload):
+    """The grid backward (bin + accumulate) on its own clock over the timed
+    region's graph replays: 1,100 B per sample x the samples of
+    exactly those launches / their summed spans (NGP_GRID_TIMING). north_star's
+    grid_encode target is read against this figure."""
+    if not grid_clock or grid_clock[0] != steps:
+        return None
+    _, ms, samp = grid_clock
+    calls = len(ms)
+    achieved = 1100 * sum(samp) / (sum(ms) * 1e-3) / 1e9
+    traffic, src = pmc_traffic("grid_encode_backward", workload)
+    return {"kernel": "grid_encode_backward", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+            "algorithmic_bytes_per_launch": int(1100 * sum(samp) / calls), "timing": "device_clock_timed_region",
+            "launches_timed": calls, "samples_timed": int(sum(samp)), "avg_launch_ms": round(sum(ms) / calls, 5),
+            "launch_ms_min_median_max": [round(float(v), 5) for v in (min(ms), np.median(ms), max(ms))]}
+
+
+def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload):
+    """The step's longest launch (over all launches of the body, timed with
+    HIP events between the launches of eager body steps on the launch stream,
+    the sample counts of those same steps): its algorithmic bytes (SURVEY
+    §8(d)) over its mean duration. World 1 that is the march launch carrying
+    the previous step's Adam; `adam_bytes_frac` is Adam's share of its bytes."""
+    S = float(np.mean(counts))
+    nbytes = launch_bytes(ft, S, rays)
+    dom = max(kernel_ms, key=lambda k: kernel_ms[k])
+    out = {"kernel": dom, "timing": "eager_body_events", "launches_timed": len(per_step[dom]),
+           "avg_launch_ms": round(kernel_ms[dom], 5),
+           "share_of_launch_time": round(kernel_ms[dom] / sum(kernel_ms.values()), 4)}
+    if nbytes.get(dom) is None:  # an MLP launch: MFMA-bound
+        flops = 110592 * S / 2
+        ach = flops / (kernel_ms[dom] * 1e-3) / 1e12
+        out.update(bound="mfma", achieved=round(ach, 2), peak=FP16_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                   frac=round(ach / FP16_MFMA_PEAK_TFLOPS, 4), traffic=None)
+        return out
+    b = nbytes[dom]
+    ach = b / (kernel_ms[dom] * 1e-3) / 1e9
+    traffic, src = pmc_traffic(dom, workload)
+    out.update(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
+               traffic=traffic, traffic_source=src, algorithmic_bytes_per_launch=int(b))
+    if dom == "march_rays_train+adam":
+        out["adam_bytes"] = adam_bytes(ft)
+        out["adam_bytes_frac"] = round(adam_bytes(ft) / b, 4)
+    out["per_launch_ms"] = {k: round(v, 5) for k, v in kernel_ms.items()}
+    out["per_launch_frac"] = {k: round(nbytes[k] / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                              for k, v in kernel_ms.items() if nbytes.get(k)}
+    return out
+
+
+def run_fused(args, model, data, bits, world, dev):
+    ft, mean_count = make_trainer(args, model, data, world, dev, args.dt_gamma)
+    elapsed, used_graph, grid_clock = timed_run(args, ft, world, dev, args.steps, args.warmup, args.settle_steps,
+                                                args.graph_steps)
     ms_per_step = elapsed / args.steps * 1e3
     value = args.num_rays * world * args.steps / elapsed
     samples = model.step_counter[:, 0].float()
     samples_per_step = int(samples[samples > 0].mean().item()) if (samples > 0).any() else 0
     loss = ft.last_loss
 
-    # ---------------- per-kernel device time (roofline) ----------------
-    # timing "graph_events": the event nodes of the last min(steps, ring) graph
-    # replays of the timed region, with those steps' own sample counts;
-    # "eager": eager steps after the timed region, events between launches
-    if timing == "graph_events":
-        kernel_ms, per_replay, counts = ft.ring_times(last=args.steps)
+    # ---------------- per-launch device time (roofline) ----------------
+    if world == 1:
+        kernel_ms, per_step, counts = ft.timed_body_steps(args.kernel_steps)
     else:
         ft.flush()
-        kernel_ms, per_replay, counts = ft.timed_steps(args.kernel_steps, with_counts=True)
+        kernel_ms, per_step, counts = ft.timed_steps(args.kernel_steps, with_counts=True)
     counts = [min(int(c), ft.M) for c in counts]
-    rows = float(np.mean(counts))  # mean samples per step of the timed launches
-    # SURVEY §8(d) per-sample bytes; achieved = sum of bytes / sum of times
-    per_sample = {"grid_encode_backward": 1100, "grid_encode_forward": 588}
-    dominant = max(per_sample, key=lambda k: kernel_ms[k])
-    dom_bytes = per_sample[dominant] * rows
-    achieved = per_sample[dominant] * sum(counts) / (sum(per_replay[dominant]) * 1e-3) / 1e9
-    roof_timing = {"timing": timing, "launches_timed": len(counts), "samples_per_timed_launch": counts,
-                   "launch_ms_per_timed_step": [round(v, 5) for v in per_replay[dominant]],
-                   "avg_launch_ms": round(kernel_ms[dominant], 5)}
-    if dominant == "grid_encode_backward" and grid_clock and grid_clock[0] == args.steps:
-        # the grid backward's own clock over the timed region's graph replays:
-        # bin launch start -> accumulate end on the 100 MHz constant clock,
-        # the samples of exactly those launches (NGP_GRID_TIMING)
-        _, ms, samp = grid_clock
-        calls = len(ms)
-        dom_bytes = per_sample[dominant] * sum(samp) / calls
-        achieved = per_sample[dominant] * sum(samp) / (sum(ms) * 1e-3) / 1e9
-        roof_timing = {"timing": "device_clock_timed_region", "launches_timed": calls,
-                       "samples_timed": sum(samp), "avg_launch_ms": round(sum(ms) / calls, 5),
-                       "launch_ms_min_median_max": [round(float(v), 5) for v in
-                                                    (min(ms), np.median(ms), max(ms))],
-                       "eager_events": {"avg_launch_ms": round(kernel_ms[dominant], 5),
-                                        "frac": round(per_sample[dominant] * sum(counts)
-                                                      / (sum(per_replay[dominant]) * 1e-3) / 1e9
-                                                      / HBM_PEAK_GBS, 4)}}
+    rows = float(np.mean(counts))
+    grid = grid_roofline(grid_clock, args.steps, args.workload)
+    if world == 1:
+        roofline = launch_roofline(ft, kernel_ms, per_step, counts, args.num_rays, args.workload)
+    else:  # the data-parallel step's phases include collectives: the grid backward names the roofline
+        roofline = grid
     mlp_ms = sum(v for k, v in kernel_ms.items() if k.startswith("ffmlp"))
     ffmlp_flops = 110592 * rows
     step_bytes = whole_step_bytes(rows, args.num_rays, sum(p.numel() for p in model.parameters()),
                                   int(model.encoder.embeddings.numel()))
 
     density = density_update_times(model, bits, ft)
+    cadence = density_cadence(ft, bits, args) if world == 1 else None
 
     return {
         "metric": METRIC,
@@ -484,19 +700,11 @@ def run_fused(args, model, data, bits, world, dev):
             "bound": float(model.bound),
             "baseline_ref": "V100 97 it/s x 4096 rays (readme.md:211)",
         },
-        "roofline": {
-            "kernel": dominant,
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(dominant, args.workload)[0],
-            "traffic_source": pmc_traffic(dominant, args.workload)[1],
-            "algorithmic_bytes_per_launch": int(dom_bytes),
-            **roof_timing,
-        },
+        "roofline": roofline,
+        # north_star's grid_encode target, on the grid backward's own clock
+        "roofline_grid_encode": grid,
         "kernels_ms": {k: round(v, 5) for k, v in kernel_ms.items()},
+        "kernel_samples": counts,
         "ffmlp_mfma": {"flops_per_step": int(ffmlp_flops), "ms": round(mlp_ms, 5),
                         "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
                         "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
@@ -505,23 +713,41 @@ def run_fused(args, model, data, bits, world, dev):
         "step_roofline": {"algorithmic_bytes": int(step_bytes),
                           "frac": round(step_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)},
         "density_update_ms": density,
-        # beside the headline (which SURVEY §8(d) defines without it): the step
-        # with upstream's density-grid cadence amortized in, one partial
-        # device-draw update (FusedTrainer.update_density) per 16 steps
-        "with_density_update": amortized_density(ms_per_step, density, args.num_rays * world),
+        # beside the headline (which SURVEY §8(d) defines without it): upstream's
+        # density-grid cadence timed end to end, one partial update per 16 steps
+        "with_density_update": cadence,
         "loss": loss,
-    }
+    }, ft
 
 
-def amortized_density(ms_per_step, density, rays_per_step):
-    """ms/step and rays/s with one partial density update per 16 steps
-    (nerf/utils.py update_extra_interval = 16), or None if not measured."""
-    upd = (density or {}).get("fused_partial")
-    if not upd or not ms_per_step:
-        return None
-    ms = ms_per_step + upd / 16.0
-    return {"ms_per_step": round(ms, 4), "rays_per_s": round(rays_per_step / (ms * 1e-3), 1),
-            "update": "fused_partial / 16"}
+def density_cadence(ft, bits, args, cycles=6, every=16):
+    """The training loop at upstream's density cadence (update_extra_interval
+    = 16, nerf/utils.py), timed end to end: `cycles` x [update_density()
+    (partial, device draws; it flushes the pending Adam first), restore the
+    benched bitfield fixture (a device copy + the occupancy image rebuild, so
+    the steps march the same workload as the headline), run(16) (the first
+    step after the flush eager, then the multi-step graph)]."""
+    model = ft.model
+    grid0 = model.density_grid.clone()
+    it0 = model.iter_density
+    model.iter_density = 16  # partial updates, as upstream after the first 16
+    ft.run(every)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(cycles):
+        ft.update_density()
+        model.density_bitfield.copy_(bits)
+        ft.refresh_occupancy()
+        ft.run(every)
+    torch.cuda.synchronize()
+    secs = time.perf_counter() - t0
+    model.density_grid.copy_(grid0)
+    model.iter_density = it0
+    model.density_bitfield.copy_(bits)
+    ft.refresh_occupancy()
+    ms = secs * 1e3 / (cycles * every)
+    return {"ms_per_step": round(ms, 4), "rays_per_s": round(args.num_rays / (ms * 1e-3), 1),
+            "timing": f"{cycles} x [partial update_density + bitfield fixture restore + run({every})], wall"}
 
 
 def density_update_times(model, bits, ft=None, reps=3):
@@ -563,7 +789,8 @@ def density_update_times(model, bits, ft=None, reps=3):
 
 
 _PMC_KERNELS = {"grid_encode_backward": ("k_grid_bwd_bin", "k_grid_bin_accum"),
-                "grid_encode_forward": ("k_grid_fwd_pair",)}
+                "grid_encode_forward": ("k_grid_fwd_pair",),
+                "march_rays_train+adam": ("void k_march_train<4u>", "k_march_emit")}
 
 
 def whole_step_bytes(samples, rays, n_params, n_table):

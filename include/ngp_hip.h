@@ -200,6 +200,34 @@ int ngp_composite_rays(uint32_t n_alive, uint32_t n_step, float T_thresh, int32_
                        float* rays_t, const float* sigmas, const float* rgbs, const float* deltas,
                        float* weights_sum, float* depth, float* image, void* stream);
 
+/* Device-driven inference render loop (the alive-ray loop of run_cuda with
+ * training off, renderer.py:376-426, without its host round trip per
+ * iteration). The loop state is a two-slot device record (state_bytes);
+ * iteration i reads slot i & 1 and prepares slot (i + 1) & 1:
+ *   render_init: alive list 0 = arange(N), rays_t = nears, outputs zeroed;
+ *   render_march: kernel_march_rays (raymarching.cu:709-814) for the
+ *     iteration's n_alive and n_step = max(min(N / n_alive, 8), 1), unused
+ *     sample slots zeroed, noise in the first iteration only; writes the
+ *     iteration's sample count (render_count) for the grid / MLP kernels;
+ *   render_composite: kernel_composite_rays (raymarching.cu:827-914) on
+ *     sigmas [n_alive * n_step] and the colour network's fp16 logits
+ *     color_out [*, 16] (rgb = half(sigmoid)), appending surviving rays to
+ *     rays_alive_next (order within the list is unspecified; per-ray results
+ *     do not depend on it).
+ * Once step >= max_steps or no ray is alive, every launch is a no-op. */
+size_t ngp_render_state_bytes(void);
+int32_t* ngp_render_count(void* state, uint32_t iter);
+int ngp_render_init(uint32_t N, const float* nears, int32_t* rays_alive, float* rays_t, float* weights_sum,
+                    float* depth, float* image, void* state, void* stream);
+int ngp_render_march(uint32_t N, uint32_t iter, void* state, const int32_t* rays_alive, const float* rays_t,
+                     const float* rays_o, const float* rays_d, float bound, float dt_gamma, uint32_t max_steps,
+                     uint32_t C, uint32_t H, const uint8_t* grid, const float* fars, float* xyzs, float* dirs,
+                     float* deltas, const float* noises, void* stream);
+int ngp_render_composite(uint32_t N, uint32_t iter, uint32_t max_steps, void* state, float T_thresh,
+                         const int32_t* rays_alive, int32_t* rays_alive_next, float* rays_t, const float* sigmas,
+                         const void* color_out, const float* deltas, float* weights_sum, float* depth,
+                         float* image, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* shencoder                                                                */
 /* ------------------------------------------------------------------------ */

@@ -27,15 +27,57 @@ def test_gpus_must_match_the_launchers_world_size():
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
 
 
-def test_amortized_density_update():
-    """One partial device update per 16 steps (nerf/utils.py:
-    update_extra_interval) added to the step; None when it was not measured."""
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+def test_algorithmic_bytes_of_the_step_launches():
+    """SURVEY §8(d) per-unit bytes: Adam 28 B per table value (world 1, no fp16
+    table copy) and 30 B per MLP weight; march 48 B/ray + 32 B/sample; grid
+    forward 588 and backward 1,100 B/sample; composite 84 B/ray + 64 B/sample."""
+    import types
+    import torch
+    sys.path.insert(0, ROOT)
     import bench
-    r = bench.amortized_density(0.2, {"fused_partial": 0.48}, 4096)
-    assert r["ms_per_step"] == 0.23 and abs(r["rays_per_s"] - 4096 / 0.23e-3) < 1
-    assert bench.amortized_density(0.2, {}, 4096) is None
-    assert bench.amortized_density(0.2, None, 4096) is None
+    ft = types.SimpleNamespace(params=[torch.zeros(6119864, 2), torch.zeros(7168), torch.zeros(11264)],
+                               table32=True, dp=False)
+    assert bench.adam_bytes(ft) == 28 * 12239728 + 30 * 18432
+    b = bench.launch_bytes(ft, 80000, 4096)
+    assert b["march_rays_train+adam"] == bench.adam_bytes(ft) + 48 * 4096 + 32 * 80000
+    assert b["grid_encode_backward"] == 1100 * 80000 and b["grid_encode_forward"] == 588 * 80000
+    assert b["composite_loss"] == 84 * 4096 + 64 * 80000 and b["ffmlp_backward"] is None
+    dp = types.SimpleNamespace(params=ft.params, table32=False, dp=True, chunk=1532288)
+    assert bench.adam_bytes(dp) == 30 * 1532288
+
+
+def test_flat_buffer_sizes_of_configs_4_and_5():
+    """The data-parallel collectives move the flat fp16 gradient / forward copy:
+    table + both MLPs, 8-aligned (12,239,728 table values at log2T
+    19, 39,625,280 entries x 2 at log2T 22)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench._flat_total(19) == 12239728 + 7168 + 11264
+    assert bench._flat_total(22) == 2 * 39625280 + 7168 + 11264
+
+
+def test_fox_leg_occupancy_is_not_degenerate():
+    """The Config-3 leg's Fox-shaped occupancy gives >= 20 samples per ray at
+    dt_gamma 1/128 from the bench's cameras (the Lego boxes at bound 2 gave
+    2.7), counted by the oracle's march_rays_train on two poses."""
+    import numpy as np
+    import torch
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "torch-ngp_amd")]
+    import oracle
+    from nerf.provider import SyntheticLego, fox_bitfield
+    from nerf.utils import get_rays
+    bits = fox_bitfield()
+    data = SyntheticLego("cpu", num_rays=2048)
+    total = 0
+    for k in (10, 60):
+        torch.manual_seed(k)
+        r = get_rays(data.poses[k:k + 1], data.intrinsics, 800, 800, 2048)
+        ro, rd = (r[n][0].numpy().astype(np.float32) for n in ("rays_o", "rays_d"))
+        nears, fars = oracle.near_far_from_aabb(ro, rd, np.array([-2.0] * 3 + [2.0] * 3, np.float32), 0.2)
+        out = oracle.march_rays_train(ro, rd, 2.0, bits, 2, 128, nears, fars, np.zeros(2048, np.float32),
+                                      M=2048 * 1024, dt_gamma=1 / 128)
+        total += int(out[4][0])
+    assert total / (2 * 2048) >= 20, total / 4096
 
 
 @pytest.mark.gpu

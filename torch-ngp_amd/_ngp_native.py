@@ -60,6 +60,13 @@ SIGNATURES = {
                                           c_vp, c_u32, c_u32, c_f32, c_vp, c_vp, c_vp],
     "ngp_march_rays": [c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32,
                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_render_state_bytes": [],
+    "ngp_render_count": [c_vp, c_u32],
+    "ngp_render_init": [c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_render_march": [c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_vp,
+                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_render_composite": [c_u32, c_u32, c_u32, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_vp, c_vp],
     "ngp_composite_rays": [c_u32, c_u32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                            c_vp],
     "ngp_sh_encode_forward": [c_vp, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp],
@@ -159,6 +166,8 @@ _RESTYPES = {
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
     "ngp_march_rays_train_workspace_bytes": c_sz,
     "ngp_fused_state_bytes": c_sz,
+    "ngp_render_state_bytes": c_sz,
+    "ngp_render_count": c_vp,
     "ngp_grid_encode_backward_fused_workspace_bytes": c_sz,
     "ngp_ffmlp_image_bytes": c_sz,
     "ngp_density_grid_draw_workspace_bytes": c_sz,

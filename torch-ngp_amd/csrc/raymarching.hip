@@ -1087,6 +1087,165 @@ k_composite_rays(uint32_t n_alive, uint32_t n_step, float T_thresh, int32_t* ray
     image[index * 3 + 2] = b;
 }
 
+// ---- device-driven inference loop (renderer.py:376-426) ------------------------
+// The reference's test render loops on the host: count the alive rays, pick
+// n_step = max(min(N // n_alive, 8), 1), march / network / composite, compact
+// rays_alive[rays_alive >= 0], step += n_step, until step >= max_steps or no
+// ray is alive -- a host round trip per iteration. Here the loop state lives
+// in a two-slot device record (iteration i reads slot i & 1 and prepares slot
+// (i + 1) & 1), every kernel derives n_step from it, and the composite kernel
+// appends its surviving rays to the other alive list (one atomic per wave),
+// so a hipGraph holds any number of iterations and the host checks the state
+// once per replay. Per ray everything is the reference's arithmetic: the
+// list's order only moves a ray's samples to other rows, and the grid / MLP
+// kernels compute every row from that row alone.
+struct RenderSlot {
+    int32_t count;    // samples this iteration: n_alive * n_step (0 once done); the grid / MLP count
+    int32_t n_alive;  // rays in this iteration's alive list
+    int32_t step;     // the reference's `step` before this iteration
+    int32_t pad;
+};
+
+NGP_DEV bool render_live(const RenderSlot& s, uint32_t max_steps) {
+    return s.n_alive > 0 && (uint32_t)s.step < max_steps;
+}
+NGP_DEV uint32_t render_n_step(uint32_t N, uint32_t n_alive) {
+    return max(min(N / n_alive, 8u), 1u);
+}
+
+__global__ void __launch_bounds__(256)
+k_render_init(uint32_t N, const float* __restrict__ nears, int32_t* rays_alive, float* rays_t, float* weights_sum,
+              float* depth, float* image, RenderSlot* state) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n == 0) {
+        state[0] = RenderSlot{0, (int32_t)N, 0, 0};
+        state[1] = RenderSlot{0, 0, 0, 0};
+    }
+    if (n >= N) return;
+    rays_alive[n] = (int32_t)n;
+    rays_t[n] = nears[n];
+    weights_sum[n] = 0.0f;
+    depth[n] = 0.0f;
+    image[n * 3] = 0.0f; image[n * 3 + 1] = 0.0f; image[n * 3 + 2] = 0.0f;
+}
+
+// kernel_march_rays (raymarching.cu:709-814) with n_alive / n_step from the
+// state; slots past a ray's last sample are zeroed (the reference allocates
+// xyzs / dirs / deltas with torch.zeros every iteration); noise only in the
+// first iteration (`perturb if step == 0 else False`, renderer.py:407).
+__global__ void __launch_bounds__(128)
+k_render_march(uint32_t N, RenderSlot* __restrict__ state, uint32_t cur, const int32_t* __restrict__ rays_alive,
+               const float* __restrict__ rays_t, const float* __restrict__ rays_o,
+               const float* __restrict__ rays_d, MarchConst k, const uint8_t* __restrict__ grid,
+               const float* __restrict__ fars, float* xyzs, float* dirs, float* deltas,
+               const float* __restrict__ noises) {
+    const RenderSlot S = state[cur];
+    const bool live = render_live(S, k.max_steps);
+    const uint32_t n_alive = live ? (uint32_t)S.n_alive : 0u;
+    const uint32_t n_step = live ? render_n_step(N, n_alive) : 0u;
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n == 0) {
+        state[cur].count = (int32_t)(n_alive * n_step);
+        state[cur ^ 1u] = RenderSlot{0, 0, S.step + (int32_t)n_step, 0};
+    }
+    if (n >= n_alive) return;
+    const int index = rays_alive[n];
+    const float noise = (S.step == 0 && noises) ? noises[n] : 0.0f;
+    const Ray r = load_ray(rays_o, rays_d, (size_t)index);
+    float* xyz = xyzs + (size_t)n * n_step * 3;
+    float* dir = dirs + (size_t)n * n_step * 3;
+    float* dlt = deltas + (size_t)n * n_step * 2;
+    float t = rays_t[index];
+    const float far = fars[index];
+    t = fmaf(clampf(t * k.dt_gamma, k.dt_min, k.dt_max), noise, t);
+    float last_t = t;
+    uint32_t step = 0;
+    Sample s;
+    const OccGlobal occ{grid};
+    while (t < far && step < n_step) {
+        if (march_step<false>(r, k, occ, t, s)) {
+            xyz[step * 3] = s.x; xyz[step * 3 + 1] = s.y; xyz[step * 3 + 2] = s.z;
+            dir[step * 3] = r.dx; dir[step * 3 + 1] = r.dy; dir[step * 3 + 2] = r.dz;
+            t += s.dt;
+            dlt[step * 2] = s.dt;
+            dlt[step * 2 + 1] = t - last_t;
+            last_t = t;
+            step++;
+        }
+    }
+    for (; step < n_step; ++step) {
+        xyz[step * 3] = 0.0f; xyz[step * 3 + 1] = 0.0f; xyz[step * 3 + 2] = 0.0f;
+        dir[step * 3] = 0.0f; dir[step * 3 + 1] = 0.0f; dir[step * 3 + 2] = 0.0f;
+        dlt[step * 2] = 0.0f; dlt[step * 2 + 1] = 0.0f;
+    }
+}
+
+// torch.sigmoid on the colour network's half output: fp32 math, half result
+// (autocast), then composite_rays' float32 cast.
+NGP_DEV float render_sigmoid_h(ngp_half x) { return (float)(ngp_half)(1.0f / (1.0f + expf(-(float)x))); }
+
+// kernel_composite_rays (raymarching.cu:827-914) on sigma = density_scale *
+// trunc_exp(h0) (the MLP epilogue) and rgb = sigmoid of the colour logits;
+// a ray that stays alive joins the next iteration's list.
+__global__ void __launch_bounds__(256)
+k_render_composite(uint32_t N, uint32_t max_steps, RenderSlot* __restrict__ state, uint32_t cur, float T_thresh,
+                   const int32_t* __restrict__ rays_alive, int32_t* __restrict__ rays_alive_next, float* rays_t,
+                   const float* __restrict__ sigmas, const ngp_half* __restrict__ color_out,
+                   const float* __restrict__ deltas, float* weights_sum, float* depth, float* image) {
+    const RenderSlot S = state[cur];
+    const bool live = render_live(S, max_steps);
+    if (!live) return;  // the whole grid: no wave reaches the ballot
+    const uint32_t n_alive = (uint32_t)S.n_alive;
+    const uint32_t n_step = render_n_step(N, n_alive);
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x * blockDim.x >= n_alive) return;  // whole workgroup past the list
+    bool survives = false;
+    int index = 0;
+    if (n < n_alive) {
+        index = rays_alive[n];
+        const float* sg = sigmas + (size_t)n * n_step;
+        const ngp_half* cl = color_out + (size_t)n * n_step * 16;
+        const float* dl = deltas + (size_t)n * n_step * 2;
+        float t = rays_t[index];
+        float weight_sum = weights_sum[index];
+        float d = depth[index];
+        float r = image[index * 3], g = image[index * 3 + 1], b = image[index * 3 + 2];
+        uint32_t step = 0;
+        while (step < n_step) {
+            const float d0 = dl[step * 2];
+            if (d0 == 0) break;
+            const float alpha = 1.0f - expf(-sg[step] * d0);
+            const float T = 1 - weight_sum;
+            const float weight = alpha * T;
+            weight_sum += weight;
+            t += dl[step * 2 + 1];
+            d = fmaf(weight, t, d);
+            r = fmaf(weight, render_sigmoid_h(cl[step * 16 + 0]), r);
+            g = fmaf(weight, render_sigmoid_h(cl[step * 16 + 1]), g);
+            b = fmaf(weight, render_sigmoid_h(cl[step * 16 + 2]), b);
+            if (T < T_thresh) break;
+            step++;
+        }
+        survives = step >= n_step;
+        if (survives) rays_t[index] = t;
+        weights_sum[index] = weight_sum;
+        depth[index] = d;
+        image[index * 3] = r;
+        image[index * 3 + 1] = g;
+        image[index * 3 + 2] = b;
+    }
+    // rays_alive[rays_alive >= 0]: the survivors of this wave take consecutive
+    // places after one atomic on the next slot's count
+    const uint64_t mask = __ballot(survives);
+    if (mask == 0) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    int32_t base = 0;
+    if (lane == (uint32_t)__ffsll((long long)mask) - 1u)
+        base = atomicAdd(&state[cur ^ 1u].n_alive, (int32_t)__popcll(mask));
+    base = __shfl(base, __ffsll((long long)mask) - 1, 64);
+    if (survives) rays_alive_next[base + __popcll(mask & ((1ull << lane) - 1ull))] = index;
+}
+
 int check_cascade(uint32_t C, uint32_t H, uint32_t max_steps) {
     NGP_REQUIRE(C >= 1 && C <= 8, NGP_ERR_ARG, "raymarching: cascade C must be in [1, 8], got %u", C);
     NGP_REQUIRE(H >= 1 && H <= 1024, NGP_ERR_ARG, "raymarching: grid size H must be in [1, 1024], got %u", H);
@@ -1355,4 +1514,48 @@ extern "C" int ngp_composite_rays(uint32_t n_alive, uint32_t n_step, float T_thr
         n_alive, n_step, T_thresh, rays_alive, rays_t, sigmas, rgbs, deltas, weights_sum, depth,
         image);
     return ngp_check_launch("composite_rays");
+}
+
+/* ---- device-driven inference render loop --------------------------------- */
+
+extern "C" size_t ngp_render_state_bytes(void) { return 2 * sizeof(RenderSlot); }
+
+extern "C" int32_t* ngp_render_count(void* state, uint32_t iter) {
+    return state ? &static_cast<RenderSlot*>(state)[iter & 1u].count : nullptr;
+}
+
+extern "C" int ngp_render_init(uint32_t N, const float* nears, int32_t* rays_alive, float* rays_t,
+                               float* weights_sum, float* depth, float* image, void* state, void* stream) {
+    NGP_REQUIRE(N >= 1 && N <= 0x7fffffffu / 8u, NGP_ERR_ARG, "render: N must be in [1, 2^28), got %u", N);
+    NGP_REQUIRE(state && nears && rays_alive && rays_t && weights_sum && depth && image, NGP_ERR_ARG,
+                "render_init: null buffer");
+    k_render_init<<<ngp_div_up(N, 256), 256, 0, ngp_stream(stream)>>>(N, nears, rays_alive, rays_t, weights_sum,
+                                                                      depth, image, static_cast<RenderSlot*>(state));
+    return ngp_check_launch("render_init");
+}
+
+extern "C" int ngp_render_march(uint32_t N, uint32_t iter, void* state, const int32_t* rays_alive,
+                                const float* rays_t, const float* rays_o, const float* rays_d, float bound,
+                                float dt_gamma, uint32_t max_steps, uint32_t C, uint32_t H, const uint8_t* grid,
+                                const float* fars, float* xyzs, float* dirs, float* deltas, const float* noises,
+                                void* stream) {
+    if (int e = check_cascade(C, H, max_steps)) return e;
+    NGP_REQUIRE(N >= 1 && N <= 0x7fffffffu / 8u, NGP_ERR_ARG, "render: N must be in [1, 2^28), got %u", N);
+    const MarchConst k = make_march_const(bound, dt_gamma, max_steps, C, H);
+    k_render_march<<<ngp_div_up(N, 128), 128, 0, ngp_stream(stream)>>>(
+        N, static_cast<RenderSlot*>(state), iter & 1u, rays_alive, rays_t, rays_o, rays_d, k, grid, fars, xyzs, dirs,
+        deltas, noises);
+    return ngp_check_launch("render_march");
+}
+
+extern "C" int ngp_render_composite(uint32_t N, uint32_t iter, uint32_t max_steps, void* state, float T_thresh,
+                                    const int32_t* rays_alive, int32_t* rays_alive_next, float* rays_t,
+                                    const float* sigmas, const void* color_out, const float* deltas,
+                                    float* weights_sum, float* depth, float* image, void* stream) {
+    NGP_REQUIRE(N >= 1 && N <= 0x7fffffffu / 8u, NGP_ERR_ARG, "render: N must be in [1, 2^28), got %u", N);
+    NGP_REQUIRE(rays_alive != rays_alive_next, NGP_ERR_ARG, "render_composite: the alive lists must differ");
+    k_render_composite<<<ngp_div_up(N, 256), 256, 0, ngp_stream(stream)>>>(
+        N, max_steps, static_cast<RenderSlot*>(state), iter & 1u, T_thresh, rays_alive, rays_alive_next, rays_t,
+        sigmas, static_cast<const ngp_half*>(color_out), deltas, weights_sum, depth, image);
+    return ngp_check_launch("render_composite");
 }

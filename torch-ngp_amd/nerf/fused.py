@@ -569,6 +569,31 @@ class FusedTrainer:
         mean = {n: v / k for n, v in acc.items()}
         return (mean, per, counts) if with_counts else mean
 
+    def timed_body_steps(self, k):
+        """Per-launch device time of the world-1 step body exactly as the
+        graphs run it (Adam inside the march launch, the next batch drawn in
+        the bin launch, ...): k eager steps, events between consecutive
+        launches on the launch stream, a spin kernel ahead of each step so the
+        host has queued every launch before the first runs. Returns (per-launch
+        mean ms, per-step ms of each launch, per-step sample counts)."""
+        assert not self.dp
+        if not self._pending:
+            self.step()
+        per, counts = {}, []
+        for _ in range(k):
+            torch.cuda.synchronize()
+            torch.cuda._sleep(4_000_000)
+            self._events = []
+            self._tick("start")
+            self._body(True)
+            self.model.local_step += 1
+            torch.cuda.synchronize()
+            ev, self._events = self._events, None
+            counts.append(self.sample_count())
+            for (_, a), (name, b) in zip(ev[:-1], ev[1:]):
+                per.setdefault(name, []).append(a.elapsed_time(b))
+        return {n: float(np.mean(v)) for n, v in per.items()}, per, counts
+
     def _body(self, pending):
         """One step's launches (world 1): [optimizer(previous grads)] ->
         sample -> march -> network forward/backward. With an update pending,
@@ -713,7 +738,7 @@ class FusedTrainer:
                 pk["hid"], pk["nl"], pk["img"], s), "march_rays_train_tail")
         else:
             nat.check(lib.ngp_march_rays_train_prebuilt(*args, s), "march_rays_train")
-        self._tick("march_rays_train")
+        self._tick("march_rays_train+adam" if adam else "march_rays_train")
 
     def _network(self, draw=False):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
