@@ -392,6 +392,32 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
     for a, b in zip(gw_one, gw_two):
         a, b = a.float(), b.float()
         assert torch.all((a - b).abs() <= 2.0 ** -10 * b.abs() + 1e-6), float((a - b).abs().max())
+    # the pair kernel (NGP_MLP_BWD_PAIR=1: two waves per SIMD, a wave pair per
+    # chunk) against the one-wave-per-SIMD kernel (=0): the same input
+    # gradients bit for bit, dW within fp16 rounding of the same sums
+    import os
+    knob = os.environ.get("NGP_MLP_BWD_PAIR")
+    os.environ["NGP_MLP_BWD_PAIR"] = "0" if knob == "1" else "1"
+    try:
+        gh3, gxp3 = gh0.clone(), torch.zeros_like(gx_ref)
+        ws1 = [torch.full_like(w, 7) for w in wsb]
+        nat.check(lib.ngp_nerf_backward(P(go), P(ci), P(imgs[1]), P(gh3), P(xp), P(imgs[0]), P(gxp3), B, P(cnt),
+                                        64, 2, 64, 3, P(ws1[0]), ws1[0].numel(), P(ws1[1]), ws1[1].numel(), None,
+                                        s), "nerf_bwd_one_wave")
+        gw_w1 = [torch.zeros_like(t) for t in gw_ref]
+        nat.check(lib.ngp_ffmlp_reduce(2, arr([ws1[1], ws1[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
+                                       u32([3, 2]), arr([gw_w1[1], gw_w1[0]]), 1, None, s), "reduce")
+        torch.cuda.synchronize()
+    finally:
+        if knob is None:
+            del os.environ["NGP_MLP_BWD_PAIR"]
+        else:
+            os.environ["NGP_MLP_BWD_PAIR"] = knob
+    assert torch.equal(gh3.view(torch.int16), gh2.view(torch.int16))
+    assert torch.equal(gxp3.view(torch.int16), gxp2.view(torch.int16))
+    for a, b in zip(gw_one, gw_w1):
+        a, b = a.float(), b.float()
+        assert torch.all((a - b).abs() <= 2.0 ** -10 * b.abs() + 1e-6), float((a - b).abs().max())
 
 
 def test_grad_guard_poisons_every_shard(cuda):

@@ -27,6 +27,7 @@
 #include "ngp_reduce.h"
 #include "sh_basis.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -68,6 +69,10 @@ constexpr int kOut = 16;        // padded output width (FFMLP pads to 16)
 constexpr int kTileLd = 80;
 constexpr int kTileRows = 32;
 constexpr uint32_t kMaxBwdBlocks = 256;
+
+// Workgroup barrier that orders LDS only: unlike __syncthreads() it does not
+// wait for the wave's outstanding global loads (the next chunk's prefetch).
+NGP_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 NGP_DEV f32x4 mfma(half8 a, half8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -192,12 +197,12 @@ __host__ __device__ inline MatDesc bwd_desc(int q, uint32_t in_dim) {
 }
 
 // acc[nb][mt] = A(frags) · B[nb]
-template <int MT, int KS>
-NGP_DEV void dense(const half8* __restrict__ lds, uint32_t frag0, const half8 (&b)[kNB][KS],
-                   f32x4 (&acc)[kNB][MT]) {
+template <int MT, int KS, int NB>
+NGP_DEV void dense(const half8* __restrict__ lds, uint32_t frag0, const half8 (&b)[NB][KS],
+                   f32x4 (&acc)[NB][MT]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int nb = 0; nb < kNB; ++nb)
+    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[nb][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -206,16 +211,16 @@ NGP_DEV void dense(const half8* __restrict__ lds, uint32_t frag0, const half8 (&
         for (int s = 0; s < KS; ++s) {
             const half8 a = lds[(frag0 + mt * KS + s) * 64 + lane];
 #pragma unroll
-            for (int nb = 0; nb < kNB; ++nb) acc[nb][mt] = mfma(a, b[nb][s], acc[nb][mt]);
+            for (int nb = 0; nb < NB; ++nb) acc[nb][mt] = mfma(a, b[nb][s], acc[nb][mt]);
         }
     }
 }
 
 // accumulator tiles -> activation -> permuted B operand of the next product
-template <int MT, int KS, typename ACT>
-NGP_DEV void pack_act(const f32x4 (&acc)[kNB][MT], ACT act, half8 (&out)[kNB][KS]) {
+template <int MT, int KS, typename ACT, int NB>
+NGP_DEV void pack_act(const f32x4 (&acc)[NB][MT], ACT act, half8 (&out)[NB][KS]) {
 #pragma unroll
-    for (int nb = 0; nb < kNB; ++nb)
+    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             half8 v;
@@ -229,12 +234,12 @@ NGP_DEV void pack_act(const f32x4 (&acc)[kNB][MT], ACT act, half8 (&out)[kNB][KS
 }
 
 // load a [rows, width] fp16 row-major block as natural-K B operands
-template <int KS>
+template <int KS, int NB>
 NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
-                       half8 (&out)[kNB][KS]) {
+                       half8 (&out)[NB][KS]) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int nb = 0; nb < kNB; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
         const uint32_t row = row0 + nb * 16 + c;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -250,9 +255,9 @@ NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_
 
 // First-layer input loaders (natural-K B operands).
 struct InRowMajor {  // [B, width] row-major
-    template <int KS>
+    template <int KS, int NB>
     NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
-                            half8 (&out)[kNB][KS]) const {
+                            half8 (&out)[NB][KS]) const {
         load_rows<KS>(src, width, row0, B, out);
     }
 };
@@ -262,12 +267,12 @@ struct InRowMajor {  // [B, width] row-major
 // group read 64 contiguous bytes per pair.
 struct InPairMajor {
     uint32_t ld;  // allocated rows
-    template <int KS>
+    template <int KS, int NB>
     NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
-                            half8 (&out)[kNB][KS]) const {
+                            half8 (&out)[NB][KS]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-        for (int nb = 0; nb < kNB; ++nb) {
+        for (int nb = 0; nb < NB; ++nb) {
             const uint32_t row = row0 + nb * 16 + c;
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
@@ -288,12 +293,12 @@ struct InPairMajor {
 };
 
 // store accumulator tiles (optionally activated) as fp16 rows [row][16 mt + 4g .. +3]
-template <int MT, typename ACT>
+template <int MT, typename ACT, int NB>
 NGP_DEV void store_tiles(ngp_half* __restrict__ dst, uint32_t width, uint32_t row0, uint32_t B,
-                         const f32x4 (&acc)[kNB][MT], ACT act) {
+                         const f32x4 (&acc)[NB][MT], ACT act) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int nb = 0; nb < kNB; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
         const uint32_t row = row0 + nb * 16 + c;
         if (row >= B) continue;
 #pragma unroll
@@ -569,11 +574,11 @@ k_nerf_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img_s, co
 // K slot j of lane group g holds sample perm_unit(g, j) in BOTH operands.
 typedef short short4v __attribute__((ext_vector_type(4)));
 
-template <int KS, bool PERM>
-NGP_DEV void write_rows(ngp_half* __restrict__ tile, const half8 (&v)[kNB][KS], uint32_t units) {
+template <int KS, bool PERM, int NB>
+NGP_DEV void write_rows(ngp_half* __restrict__ tile, const half8 (&v)[NB][KS], uint32_t units) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int nb = 0; nb < kNB; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
         ngp_half* row = tile + (nb * 16 + c) * kTileLd;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -625,11 +630,11 @@ NGP_DEV void dw_accum(const ngp_half* __restrict__ dT, const ngp_half* __restric
 }
 
 // delta (C layout, MT tiles) * act'(post-activation h, permuted B form) -> permuted B form
-template <int MT, int KS, typename ACT>
-NGP_DEV void pack_delta(const f32x4 (&acc)[kNB][MT], const half8 (&h)[kNB][KS], ACT act,
-                        half8 (&out)[kNB][KS]) {
+template <int MT, int KS, typename ACT, int NB>
+NGP_DEV void pack_delta(const f32x4 (&acc)[NB][MT], const half8 (&h)[NB][KS], ACT act,
+                        half8 (&out)[NB][KS]) {
 #pragma unroll
-    for (int nb = 0; nb < kNB; ++nb)
+    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             half8 v;
@@ -705,20 +710,20 @@ struct BwdLds {
 // gradient, written by the composite kernel).
 struct GiStore {
     ngp_half* gi;
-    template <int IN_MT>
-    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[kNB][IN_MT]) const {
+    template <int IN_MT, int NB>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[NB][IN_MT]) const {
         store_tiles<IN_MT>(gi, in_dim, row0, B, t, ActNone{});
     }
 };
 
 struct GiNerfGeo {
     ngp_half* gh;
-    template <int IN_MT>
-    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t, const f32x4 (&t)[kNB][IN_MT]) const {
+    template <int IN_MT, int NB>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t, const f32x4 (&t)[NB][IN_MT]) const {
         static_assert(IN_MT == 2, "the color network input is 32 wide");  // see launch_bwd
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-        for (int nb = 0; nb < kNB; ++nb) {
+        for (int nb = 0; nb < NB; ++nb) {
             // lane group g holds input columns 16 + 4g .. +3 (tile 1); output
             // columns 4g .. 4g+3 take input columns 15 + 4g .. 18 + 4g
             const ngp_half r0 = (ngp_half)t[nb][1][0], r1 = (ngp_half)t[nb][1][1], r2 = (ngp_half)t[nb][1][2];
@@ -741,11 +746,11 @@ struct GiNerfGeo {
 struct GiPairMajor {
     ngp_half* gi;
     uint32_t ld;
-    template <int IN_MT>
-    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[kNB][IN_MT]) const {
+    template <int IN_MT, int NB>
+    NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[NB][IN_MT]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
-        for (int nb = 0; nb < kNB; ++nb) {
+        for (int nb = 0; nb < NB; ++nb) {
             const uint32_t row = row0 + nb * 16 + c;
             if (row >= B) continue;
 #pragma unroll
@@ -1035,6 +1040,224 @@ k_nerf_bwd(NerfBwdArgs a) {
     }
 }
 
+// ---- two waves per SIMD: a wave pair shares each chunk ----------------------
+// The backward above keeps every dW tile of the network in each wave's
+// registers (176 for the colour network) beside a 32-sample chunk's
+// activations, so it runs one wave per SIMD and each wave's chunk is a
+// dependent chain of MFMAs, conversions and LDS round trips that nothing else
+// on the SIMD hides. Here a workgroup has 8 waves (two per SIMD) and waves
+// 2p, 2p + 1 share pair p's chunk: wave half h recomputes the forward and walks
+// the delta chain for samples [16 h, 16 h + 16) of it (one 16-column block
+// instead of two), writes those rows of the pair's transposing tiles, and,
+// after a workgroup barrier, accumulates HALF of each layer's dW tiles --
+// output tiles [h MTW/2, (h + 1) MTW/2); the last layer's input tiles -- over
+// all 32 samples. Per wave: half the activations and half the accumulators
+// (88 VGPRs for the colour network), the same chunks per workgroup as the
+// one-wave kernel. Input gradients are bit-identical (each row's arithmetic is
+// unchanged); dW is summed in another fixed order.
+constexpr int kPairWaves = 8;
+constexpr int kPairThreads = kPairWaves * 64;
+
+template <int MO, int MI>
+NGP_DEV void dw_accum_at(const ngp_half* __restrict__ dT, int m0, const ngp_half* __restrict__ hT, int n0,
+                         f32x4 (&acc)[MO][MI]) {
+    half8 a[MO], b[MI];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < MO; ++m) a[m] = read_tr(dT, m0 + m);
+#pragma unroll
+    for (int n = 0; n < MI; ++n) b[n] = read_tr(hT, n0 + n);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < MO; ++m)
+#pragma unroll
+        for (int n = 0; n < MI; ++n) acc[m][n] = mfma(a[m], b[n], acc[m][n]);
+}
+
+template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI, typename MAP, typename PRE>
+NGP_DEV void bwd_phase_pair(const half8* __restrict__ fr, ngp_half* __restrict__ tiles, float* __restrict__ img_base,
+                            const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs, XL xl, GI gi_out,
+                            bool want_gi, float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim,
+                            FA act, MAP map, PRE pre) {
+    using N = Net<W, IN_KS, NH>;
+    constexpr int LAST = N::NMAT - 1;
+    constexpr int HM = N::MTW / 2;  // this wave's output tiles of a layer
+    static_assert(N::MTW % 2 == 0, "the pair splits a layer's output tiles in halves");
+    const uint32_t wave = threadIdx.x >> 6, hf = wave & 1u, pair = wave >> 1;
+    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
+    // the pair's tiles; this wave writes rows [16 hf, 16 hf + 16) of them
+    ngp_half* dT = tiles + (size_t)pair * 2 * kTileRows * kTileLd;
+    ngp_half* hT = dT + (size_t)kTileRows * kTileLd;
+    ngp_half* dTw = dT + (size_t)16 * hf * kTileLd;
+    ngp_half* hTw = hT + (size_t)16 * hf * kTileLd;
+
+    uint32_t chunk = map(pair, 0u);
+    half8 xn[1][IN_KS], dn[1][1];
+    xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB + 16 * hf, B, xn);
+    load_rows<1>(grad, kOut, chunk * 16 * kNB + 16 * hf, B, dn);
+    pre();
+
+    f32x4 dw_last[1][HM], dw_hid[NH][HM][N::MTW], dw_first[HM][N::IN_MT];
+    zero_tiles(dw_last);
+#pragma unroll
+    for (int q = 0; q < NH; ++q) zero_tiles(dw_hid[q]);
+    zero_tiles(dw_first);
+
+    // the workgroup's pairs run in lockstep (barriers per matmul); a pair
+    // without a chunk in the last round still meets the barriers
+    const uint32_t rounds = ngp_div_up(nchunks > blockIdx.x ? nchunks - blockIdx.x : 0u,
+                                       gridDim.x * (uint32_t)(kPairWaves / 2));
+    for (uint32_t kc = 1; kc <= rounds; ++kc) {
+        const bool mine = chunk < nchunks;
+        const uint32_t row0 = chunk * 16 * kNB + 16 * hf;
+        half8 x[1][IN_KS], dout[1][1];
+#pragma unroll
+        for (int s = 0; s < IN_KS; ++s) x[0][s] = xn[0][s];
+        dout[0][0] = dn[0][0];
+        const uint32_t next = map(pair, kc);
+        xl.template operator()<IN_KS>(inputs, in_dim, next * 16 * kNB + 16 * hf, B, xn);
+        load_rows<1>(grad, kOut, next * 16 * kNB + 16 * hf, B, dn);
+        half8 h[NH + 1][1][N::KSW];
+        f32x4 a[1][N::MTW];
+        dense<N::MTW, IN_KS>(fr, fwd_desc<W, IN_KS, NH>(0, in_dim).frag0, x, a);
+        pack_act<N::MTW, N::KSW>(a, act, h[0]);
+#pragma unroll
+        for (int q = 1; q <= NH; ++q) {
+            dense<N::MTW, N::KSW>(fr, fwd_desc<W, IN_KS, NH>(q, in_dim).frag0, h[q - 1], a);
+            pack_act<N::MTW, N::KSW>(a, act, h[q]);
+        }
+        write_rows<1, false>(dTw, dout, kOut);
+        write_rows<N::KSW, true>(hTw, h[NH], W);
+        lds_barrier();  // the pair's last-layer tiles are whole
+        dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
+        if (mine) dw_accum_at<1, HM>(dT, 0, hT, (int)hf * HM, dw_last);
+        half8 d[1][N::KSW];
+        pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
+#pragma unroll
+        for (int q = NH; q >= 1; --q) {
+            lds_barrier();  // the pair's reads of the previous tiles are done
+            write_rows<N::KSW, true>(dTw, d, W);
+            write_rows<N::KSW, true>(hTw, h[q - 1], W);
+            lds_barrier();
+            dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
+            if (mine) dw_accum_at<HM, N::MTW>(dT, (int)hf * HM, hT, 0, dw_hid[q - 1]);
+            pack_delta<N::MTW, N::KSW>(a, h[q - 1], act, d);
+        }
+        lds_barrier();
+        write_rows<N::KSW, true>(dTw, d, W);
+        write_rows<IN_KS, false>(hTw, x, in_dim);
+        lds_barrier();
+        f32x4 gi[1][N::IN_MT];
+        if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
+        if (mine) dw_accum_at<HM, N::IN_MT>(dT, (int)hf * HM, hT, 0, dw_first);
+        if (mine && want_gi) gi_out(row0, B, in_dim, gi);
+        lds_barrier();  // the next round's tile writes follow
+        chunk = next;
+    }
+    // fold: a pair's halves are disjoint tiles of one image; pair p folds into
+    // image p & 1 (pairs 0 and 1 store, the others add, in pair order), then
+    // image0 + image1 is the slab row: a fixed summation order
+    constexpr int T_FIRST = N::MTW * N::IN_MT, T_HID = N::MTW * N::MTW, T_LAST = N::MTW;
+    constexpr int NT = T_FIRST + NH * T_HID + T_LAST;
+    float* img = img_base + (size_t)(pair & 1u) * NT * 256;
+    auto fold = [&](auto first) {
+        constexpr bool F = decltype(first)::value;
+        fold_tiles<F>(dw_first, img + (size_t)hf * HM * N::IN_MT * 256);
+#pragma unroll
+        for (int q = 1; q <= NH; ++q)
+            fold_tiles<F>(dw_hid[q - 1], img + ((size_t)T_FIRST + (q - 1) * T_HID + hf * HM * N::MTW) * 256);
+        fold_tiles<F>(dw_last, img + ((size_t)T_FIRST + NH * T_HID + hf * HM) * 256);
+    };
+    __syncthreads();  // fragments and tiles are dead from here on
+    if (pair < 2) fold(std::true_type{});
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t r = 1; r < (uint32_t)kPairWaves / 4; ++r) {
+        if ((pair >> 1) == r) fold(std::false_type{});
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const f32x4* i0 = reinterpret_cast<const f32x4*>(img_base);
+    const f32x4* i1 = i0 + NT * 64;
+    float* slab_row = slab + (size_t)blockIdx.x * nparams;
+    for (int tt = (int)wave; tt < NT; tt += kPairWaves) {
+        int local, mi;
+        uint32_t in_w, out_w, off;
+        if (tt < T_FIRST) {
+            local = tt; mi = N::IN_MT; in_w = in_dim; out_w = W; off = 0;
+        } else if (tt < T_FIRST + NH * T_HID) {
+            const int q = (tt - T_FIRST) / T_HID;
+            local = tt - T_FIRST - q * T_HID; mi = N::MTW; in_w = W; out_w = W;
+            off = fwd_desc<W, IN_KS, NH>(q + 1, in_dim).off;
+        } else {
+            local = tt - T_FIRST - NH * T_HID; mi = N::MTW; in_w = W; out_w = kOut;
+            off = fwd_desc<W, IN_KS, NH>(LAST, in_dim).off;
+        }
+        const uint32_t m = (uint32_t)(local / mi), k = (uint32_t)(local % mi);
+        const f32x4 va = i0[tt * 64 + lane], vb = i1[tt * 64 + lane];
+        const uint32_t i = 16 * k + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t o = 16 * m + 4 * g + r;
+            if (o < out_w && i < in_w) slab_row[off + o * in_w + i] = va[r] + vb[r];
+        }
+    }
+}
+
+// LDS of the pair kernel: [colour fragments][4 pairs' tiles] ... [sigma
+// fragments]; the colour pass's fold images overlay everything before the
+// sigma fragments, the sigma pass's tiles and fold images the same space.
+template <int NHS, int NHC>
+struct NerfBwdPairLds {
+    using LC = BwdLds<64, 1, NHC>;
+    using LS = BwdLds<64, 1, NHS>;
+    static constexpr size_t tile_bytes = (size_t)(kPairWaves / 2) * 2 * kTileRows * kTileLd * 2;
+    static constexpr size_t fold_c = 2 * LC::acc_bytes, fold_s = 2 * LS::acc_bytes;
+    static constexpr size_t cmax(size_t x, size_t y) { return x > y ? x : y; }
+    static constexpr size_t sigma_frags = cmax(cmax(LC::frag_bytes + tile_bytes, fold_c), cmax(fold_s, tile_bytes));
+    static constexpr size_t total = sigma_frags + LS::frag_bytes;
+    static constexpr bool fits = total <= 160 * 1024;
+};
+
+template <int NHS, int NHC>
+__global__ void __launch_bounds__(kPairThreads, 2)
+k_nerf_bwd_pair(NerfBwdArgs a) {
+    using LC = BwdLds<64, 1, NHC>;
+    using LS = BwdLds<64, 1, NHS>;
+    using NL = NerfBwdPairLds<NHS, NHC>;
+    static_assert(NL::fits, "nerf backward (pair) LDS budget exceeded");
+    uint32_t B = a.B;
+    if (a.count) B = *a.count <= 0 ? 0u : min(B, (uint32_t)*a.count);
+    extern __shared__ half8 lds[];
+    half8* sfr = reinterpret_cast<half8*>(reinterpret_cast<char*>(lds) + NL::sigma_frags);
+    ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes);
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t tcall = a.timing && threadIdx.x == 0 ? a.timing[0] : 0u;
+    // pair p's k-th chunk (colour) -- the one-wave kernel's deal with pairs in
+    // place of waves; the sigma pass deals them in reverse pair order, so a
+    // pair with an extra colour chunk has one sigma chunk less
+    bwd_phase_pair<64, 1, NHC>(lds, tiles, reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{},
+                               GiNerfGeo{a.g_h}, true, a.slab_color, a.np_color, B, 32u, ActReLU{},
+                               [=](uint32_t p, uint32_t k) { return b + (p + k * (kPairWaves / 2)) * G; },
+                               [&]() {
+                                   copy_frags<LC::FRAGS, kPairThreads>(lds, a.color_image);
+                                   copy_frags<LS::FRAGS, kPairThreads>(sfr, a.sigma_image);
+                                   __syncthreads();
+                               });
+    __syncthreads();  // the colour pass's geo grads are stored and its fold images read
+    bwd_phase_pair<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
+                               InPairMajor{a.B}, GiPairMajor{a.g_enc, a.B}, true, a.slab_sigma, a.np_sigma, B, 32u,
+                               ActReLU{},
+                               [=](uint32_t p, uint32_t k) { return b + (kPairWaves / 2 - 1 - p + k * (kPairWaves / 2)) * G; },
+                               []() {});
+    if (a.timing && b < NGP_GRID_TIMING_MAX_WG / 4) {
+        __syncthreads();
+        if (threadIdx.x == 0)
+            a.timing[64 + 4 * NGP_GRID_TIMING_RING + (tcall % NGP_GRID_TIMING_RING) * NGP_GRID_TIMING_MAX_WG +
+                     NGP_GRID_TIMING_MAX_WG - 1 - b] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // grad_weights[p] = sum over workgroup rows of the slab, in a fixed order
 // (deterministic; ngp_reduce.h). Block = 64 parameters x 16 row phases.
 // Several networks' slabs in one launch (jobs).
@@ -1219,8 +1442,25 @@ int launch_bwd(const void* grad, const void* in, const void* w, const void* imag
                                       gw_dtype, defer, ws, count, st);
 }
 
+// The pair kernel (two waves per SIMD) where its LDS fits, with
+// NGP_MLP_BWD_PAIR=1; otherwise the one-wave-per-SIMD kernel (same-box A/B).
+inline bool mlp_bwd_pair_enabled() {
+    const char* e = getenv("NGP_MLP_BWD_PAIR");
+    return e && e[0] == '1';
+}
+
 template <int NHS, int NHC>
 int launch_nerf_bwd(const NerfBwdArgs& a, hipStream_t st) {
+    // (a 3-layer sigma network spills at two waves per SIMD: the one-wave kernel)
+    if constexpr (NHS == 1 && NerfBwdPairLds<NHS, NHC>::fits) {
+        if (mlp_bwd_pair_enabled()) {
+            const uint32_t blocks = bwd_blocks(a.B);  // the slab has one row per block either way
+            if (blocks == 0) return NGP_OK;
+            constexpr size_t lds_bytes = NerfBwdPairLds<NHS, NHC>::total;
+            hipLaunchKernelGGL((k_nerf_bwd_pair<NHS, NHC>), dim3(blocks), dim3(kPairThreads), lds_bytes, st, a);
+            return ngp_check_launch("nerf_backward_pair");
+        }
+    }
     if constexpr (!NerfBwdLds<NHS, NHC>::fits) {
         return ngp_set_error(NGP_ERR_UNSUPPORTED, "nerf_backward: networks too large for one launch's LDS");
     } else {
