@@ -39,6 +39,7 @@ import torch.distributed as dist
 import _ngp_native as nat
 
 from .provider import LEGO_BOXES, LEGO_COLORS
+from .zero1 import ShardPlan
 
 _F16 = nat.DTYPE_CODE[torch.float16]
 _F32 = nat.DTYPE_CODE[torch.float32]
@@ -128,13 +129,13 @@ class FusedTrainer:
         # collective each
         self.params = [enc.embeddings, self.sig_net.weights, self.col_net.weights]
         sizes = [p.numel() for p in self.params]
-        starts = np.cumsum([0] + [(n + 7) // 8 * 8 for n in sizes])
-        W = self.world
-        # shard: 64-element aligned chunk per rank (world * chunk >= the layout)
-        self.chunk = chunk = int(-(-int(starts[-1]) // (64 * W)) * 64)
-        self.total = total = chunk * W
         self.rank = dist.get_rank() if self.dp else 0
-        self.lo, self.hi = self.rank * chunk, (self.rank + 1) * chunk
+        # ZeRO-1 layout (nerf/zero1.py): 8-aligned tensors, a 64-aligned chunk per rank
+        self.plan = plan = ShardPlan(sizes, self.world, self.rank)
+        starts = plan.starts + [plan.used]
+        self.chunk = chunk = plan.chunk
+        self.total = total = plan.total
+        self.lo, self.hi = plan.lo, plan.hi
         self.flat_param = z(total)
         self.flat_grad = z(total, dtype=h)
         self.flat_half = z(total, dtype=h)
@@ -221,11 +222,7 @@ class FusedTrainer:
         self._one_bwd = (os.environ.get("NGP_FUSED_SPLIT_BWD") != "1" and sn_.hidden_dim == 64
                          and cn_.hidden_dim == 64 and sn_.input_dim == 32 and cn_.input_dim == 32
                          and 2 <= sn_.num_layers <= 3 and 2 <= cn_.num_layers <= 3)
-        if self.table32:
-            nt = self._starts[1]  # the table, then the two MLPs
-            sec = [(0, nt, False), (nt, chunk - nt, True)]
-        else:
-            sec = [(0, chunk, True)]
+        sec = plan.sections(self.table32)  # the table, then the two MLPs
         self._opt = dict(
             params=_vp_array([nat.ptr(self.flat_param) + 4 * (self.lo + a) for a, _, _ in sec]),
             grads=_vp_array([nat.ptr(self.grad_shard) + 2 * a for a, _, _ in sec]),
@@ -647,19 +644,25 @@ class FusedTrainer:
     # and marched (neither reads a parameter). Per step each rank moves the
     # gradient once and the forward copy once (what one all-reduce moves) and
     # sweeps 1/world of the Adam state.
-    def _reduce(self):
-        if not self.dp:
-            return
-        # the backward's kernels set the per-rank flag: no scan (n = 0)
+    def _guard(self):
+        """GradScaler under sharding: the backward's kernels set the per-rank
+        inf flag (no scan, n = 0); a flagged rank poisons every rank's chunk.
+        The last launch of the network phase (inside its graph)."""
         nat.check(nat.lib().ngp_grad_guard(nat.ptr(self.flat_grad), 0, self.chunk, self.world,
                                            nat.ptr(self.state), nat.stream_of(self.flat_grad)), "grad_guard")
+
+    def _reduce(self):
+        """Averaging reduce-scatter of the (guarded) flat fp16 gradient into
+        this rank's shard. The gradient is cleared for the next backward by the
+        optimizer launch that consumes the shard (`_optimizer`)."""
+        if not self.dp:
+            return
         if self._nccl:
             dist.reduce_scatter_tensor(self.grad_shard, self.flat_grad, op=dist.ReduceOp.AVG)
         else:  # gloo (tests): host-staged
             out = torch.empty(self.chunk, dtype=self.flat_grad.dtype)
             dist.reduce_scatter_tensor(out, self.flat_grad.cpu(), op=dist.ReduceOp.AVG)
             self.grad_shard.copy_(out)
-        self.flat_grad.zero_()  # the next backward accumulates into it
         self._tick("reduce_scatter")
 
     def _gather_half(self, wait):
@@ -792,6 +795,8 @@ class FusedTrainer:
         else:
             self._mlp_backward_split(lib, P, s, M, cnt, img)
         self._grid_backward(lib, P, s, M, cnt, draw, grid_args)
+        if self.dp:
+            self._guard()
 
     def _mlp_backward_split(self, lib, P, s, M, cnt, img):
         chk, sn, cn = nat.check, self.sig_net, self.col_net
@@ -846,7 +851,10 @@ class FusedTrainer:
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         o, chk, N, cnt = self._opt, nat.check, self.N, P(self.counter)
         # world 1 zeroes the grads here; data parallel: the shard is the reduce-scatter's
-        # output and the flat gradient is cleared after the collective read it
+        # output, and the flat gradient (which the collective has read) is cleared
+        # for the next backward in the same graph
+        if self.dp:
+            self.flat_grad.zero_()
         args = (o["n"], o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
                 self.betas[1], self.eps, self.iters, int(not self.dp), 1.0)
         # inside a step (world 1) the found-inf flag was set by the backward's kernels;
@@ -1114,9 +1122,9 @@ class FusedTrainer:
                     continue
                 for key, dst in (("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
                     full = st[i][key].to(self.dev, torch.float32).reshape(-1)
-                    lo, hi = max(a, self.lo), min(a + full.numel(), self.hi)  # this rank's part
+                    lo, hi = self.plan.owned(i)  # this rank's part of tensor i
                     if lo < hi:
-                        dst[lo - self.lo:hi - self.lo].copy_(full[lo - a:hi - a])
+                        dst[a + lo - self.lo:a + hi - self.lo].copy_(full[lo:hi])
                 si[self._S_ADAM] = int(float(st[i]["step"]))
         if "lr_scheduler" in state:
             si[self._S_EPOCH] = int(state["lr_scheduler"]["last_epoch"])
