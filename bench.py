@@ -518,11 +518,24 @@ def adam_bytes(ft):
 
 def launch_bytes(ft, samples, rays):
     """SURVEY §8(d) per-unit bytes of each launch of the world-1 step body
-    (timed_body_steps names): None for the MFMA-bound MLP launches."""
+    (timed_body_steps names): None for the MFMA-bound MLP launches. With the
+    grid forward split in two launches (NGP_ADAM_UNDER_FWD), the table values
+    past the split level are swept by the first one: its bytes are those
+    values' Adam bytes plus its levels' share of the forward's 588 B / sample
+    (12 B of coordinates + 36 B per level)."""
     march = 48 * rays + 32 * samples
-    return {"march_rays_train+adam": adam_bytes(ft) + march, "march_rays_train": march,
-            "step_head": None, "grid_encode_forward": 588 * samples, "grid_encode_backward": 1100 * samples,
-            "composite_loss": (32 + 52) * rays + (24 + 40) * samples, "ffmlp_forward": None, "ffmlp_backward": None}
+    out = {"march_rays_train+adam": adam_bytes(ft) + march, "march_rays_train": march,
+           "step_head": None, "grid_encode_forward": 588 * samples, "grid_encode_backward": 1100 * samples,
+           "composite_loss": (32 + 52) * rays + (24 + 40) * samples, "ffmlp_forward": None, "ffmlp_backward": None}
+    split = getattr(ft, "_fwd_split", None)
+    if split is not None:
+        f, j2 = split
+        late = 28 * int(j2.sizes[0])  # table values: p, m, v read + write, fp16 grad read + clear
+        L = int(ft.enc.num_levels)
+        out["march_rays_train+adam"] = adam_bytes(ft) - late + march
+        out["grid_encode_forward+adam"] = late + (12 + 36 * f) * samples
+        out["grid_encode_forward"] = (12 + 36 * (L - f)) * samples
+    return out
 
 
 def make_trainer(args, model, data, world, dev, dt_gamma, grid_timing=True, distributed=None):
@@ -632,9 +645,12 @@ def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload):
     traffic, src = pmc_traffic(dom, workload)
     out.update(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                traffic=traffic, traffic_source=src, algorithmic_bytes_per_launch=int(b))
-    if dom == "march_rays_train+adam":
-        out["adam_bytes"] = adam_bytes(ft)
-        out["adam_bytes_frac"] = round(adam_bytes(ft) / b, 4)
+    if dom in ("march_rays_train+adam", "grid_encode_forward+adam"):
+        ab = b - {"march_rays_train+adam": 48 * rays + 32 * S}.get(dom, 0)
+        if dom == "grid_encode_forward+adam":
+            ab = 28 * int(ft._fwd_split[1].sizes[0])
+        out["adam_bytes"] = int(ab)
+        out["adam_bytes_frac"] = round(ab / b, 4)
     out["per_launch_ms"] = {k: round(v, 5) for k, v in kernel_ms.items()}
     out["per_launch_frac"] = {k: round(nbytes[k] / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                               for k, v in kernel_ms.items() if nbytes.get(k)}

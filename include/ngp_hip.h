@@ -164,7 +164,10 @@ typedef struct ngp_adam_job {
     float grad_mult;
     void* clear;            /* zeroed by the launch too (the grid backward's bin cursors), or NULL */
     uint32_t clear_bytes;   /* multiple of 16, clear 16-byte aligned */
+    uint32_t flags;         /* NGP_ADAM_JOB_END_LATER: the emit launch leaves the bookkeeping to a
+                               later launch (ngp_grid_encode_forward_fused_adam's end block) */
 } ngp_adam_job;
+#define NGP_ADAM_JOB_END_LATER 1u
 int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const float* rays_d, const uint8_t* grid,
                                        float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
                                        uint32_t C, uint32_t H, uint32_t M, const float* nears,
@@ -444,6 +447,21 @@ typedef struct ngp_adam_table {
 int ngp_grid_table_slices(const int32_t* offsets_host, uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S,
                           uint32_t H, int32_t align_corners, uint32_t* slices_host, uint32_t max_slices);
 /* ngp_grid_encode_forward_fused reading table[*sel] (sel: ngp_fused_table_select). */
+/* The fused step's grid forward over levels [level_lo, level_hi) only, with
+ * (job non-null) the part of the previous step's Adam sweep that job holds
+ * as 256-thread blocks of the same launch, and (end_state non-null) the
+ * deferred GradScaler / LambdaLR / loss bookkeeping of that update as one
+ * block. The caller orders the launches so that no launch's forward reads a
+ * level its own Adam blocks write, and the bookkeeping comes after every
+ * launch carrying Adam (DESIGN.md "Adam under the grid forward"). fp16
+ * outputs, [L, B, C] layout, rows clipped at *count. */
+int ngp_grid_encode_forward_fused_adam(const float* xyz, float bound, const void* embeddings, int32_t emb_dtype,
+                                       const int32_t* offsets, void* outputs, uint32_t B, const int32_t* count,
+                                       uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                       int32_t align_corners, uint32_t interp, uint32_t level_lo, uint32_t level_hi,
+                                       const ngp_adam_job* job, void* state, void* end_state, float growth_factor,
+                                       float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
+                                       const float* loss_ray, uint32_t n_rays, void* stream);
 int ngp_grid_encode_forward_fused_sel(const float* xyz, float bound, const void* table0, const void* table1,
                                       const int32_t* sel, int32_t emb_dtype, const int32_t* offsets,
                                       void* outputs, uint32_t B, const int32_t* count, uint32_t D, uint32_t C,

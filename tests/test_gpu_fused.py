@@ -771,3 +771,40 @@ def test_one_launch_forward_equals_split_forward(cuda, monkeypatch, bound, dt_ga
     assert torch.equal(a[4][1], b[4][1]) and torch.equal(a[4][2], b[4][2])
     assert _rel(a[4][0], b[4][0]) < 1e-3
     assert torch.equal(a[5], b[5])
+
+
+@pytest.mark.parametrize("split_level", [8, 10, 13])
+def test_adam_under_grid_forward_equals_single_sweep(cuda, split_level):
+    """NGP_ADAM_UNDER_FWD=1: the march launch sweeps the table values below
+    the split level (and the MLPs), the grid forward's first launch (levels
+    [0, 8)) sweeps the rest, the second (levels [8, 16)) runs the deferred
+    bookkeeping. Same arithmetic per value, so after eager steps, graph replays
+    and a multi-step graph everything equals the one-sweep step bit for bit:
+    parameters, Adam moments, scaler, loss and the encodings' inputs."""
+    import os
+    out = []
+    for on in ("0", "1"):
+        os.environ["NGP_ADAM_UNDER_FWD"] = on
+        os.environ["NGP_ADAM_SPLIT_LEVEL"] = str(split_level)
+        try:
+            _, _, _, ft = _setup(cuda, num_rays=2048, mean_count=60000, fused_adam=False)
+        finally:
+            del os.environ["NGP_ADAM_UNDER_FWD"], os.environ["NGP_ADAM_SPLIT_LEVEL"]
+        assert (ft._fwd_split is not None) == (on == "1")
+        for _ in range(3):
+            ft.step()
+        ft.capture(warmup=1, multi=3)
+        for _ in range(2):
+            ft.step()
+        ft.run(7)
+        ft.flush()
+        torch.cuda.synchronize()
+        m1, m2 = ft._moments()
+        out.append(([p.detach().clone() for p in ft.params], m1.clone(), m2.clone(), ft.scale, ft.last_loss,
+                    ft.optimizer_steps, ft.enc_out.clone()))
+    a, b = out
+    for x, y in zip(a[0], b[0]):
+        assert torch.equal(x, y)
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert a[3:6] == b[3:6] and a[5] >= 12
+    assert torch.equal(a[6].view(torch.int16), b[6].view(torch.int16))

@@ -60,6 +60,9 @@ SIGNATURES = {
                                           c_vp, c_u32, c_u32, c_f32, c_vp, c_vp, c_vp],
     "ngp_march_rays": [c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32,
                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_grid_encode_forward_fused_adam": [c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
+                                           c_f32, c_u32, c_u32, c_i32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp,
+                                           c_f32, c_f32, c_i32, c_i32, c_vp, c_u32, c_vp],
     "ngp_render_state_bytes": [],
     "ngp_render_count": [c_vp, c_u32],
     "ngp_render_init": [c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
@@ -190,7 +193,11 @@ class AdamJob(ctypes.Structure):
     _fields_ = [("n_tensors", c_i32), ("params", c_vp * 8), ("grads", c_vp * 8), ("exp_avg", c_vp * 8),
                 ("exp_avg_sq", c_vp * 8), ("half_params", c_vp * 8), ("sizes", ctypes.c_uint64 * 8),
                 ("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32), ("iters", c_i32),
-                ("zero_grads", c_i32), ("grad_mult", c_f32), ("clear", c_vp), ("clear_bytes", c_u32)]
+                ("zero_grads", c_i32), ("grad_mult", c_f32), ("clear", c_vp), ("clear_bytes", c_u32),
+                ("flags", c_u32)]
+
+
+ADAM_JOB_END_LATER = 1  # NGP_ADAM_JOB_END_LATER
 
 
 class BatchJob(ctypes.Structure):

@@ -275,23 +275,31 @@ constexpr uint32_t kFwdLevelsPerBlock = 2;
 #endif
 constexpr uint32_t kFwdGroupMajorMin = NGP_FWD_GROUP_MAJOR_MIN;
 
-template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL = kFwdLevelsPerBlock>
-__global__ void __launch_bounds__(256)
-k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
-                const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
-                GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
-                int32_t out_layout, InMap im) {
+// Levels [lo, hi) of the L-level table (the fused step splits the forward
+// in two launches, each beside a part of the optimizer sweep); blk is the
+// block's index in the forward's part of the grid.
+struct LevelRange {
+    uint32_t lo, hi;
+};
+
+template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL>
+NGP_DEV void grid_fwd_pair_block(uint32_t blk, const float* __restrict__ inputs, const E* __restrict__ grid,
+                                 const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B,
+                                 uint32_t L, const GridLevels& lv, uint32_t gridtype, bool align_corners,
+                                 uint32_t interp, int32_t out_layout, const InMap& im, LevelRange lr) {
     using A = Acc<T>;
     using F = typename A::F;
     constexpr uint32_t NR = 1u << (D - 1);
     constexpr bool kGroupMajor = KL == 1;
-    const uint32_t lpx = (L + 7) / 8;                       // levels per XCD
+    const uint32_t lpx = (lr.hi - lr.lo + 7) / 8;           // levels per XCD
     const uint32_t gpx = (lpx + KL - 1) / KL;               // level groups per XCD
-    const uint32_t k = blockIdx.x >> 3;
+    const uint32_t k = blk >> 3;
     const uint32_t nch = (B + 127) / 128;                   // point chunks (grid sized on B)
     const uint32_t grp = kGroupMajor ? k / nch : k % gpx, chunk = kGroupMajor ? k % nch : k / gpx;
-    const uint32_t level0 = (blockIdx.x & 7) + 8 * KL * grp;  // this block: level0, level0 + 8, ...
-    if (level0 >= L) return;
+    const uint32_t level0 = lr.lo + (blk & 7) + 8 * KL * grp;  // this block: level0, level0 + 8, ...
+    if (level0 >= lr.hi) return;
+    const uint32_t Lfull = L;  // the [B, L, C] layout's row width
+    L = lr.hi;                 // the loops below stop at the range's end
     const uint32_t b = chunk * (blockDim.x / 2) + (threadIdx.x >> 1);
     const uint32_t xbit = threadIdx.x & 1;
     const bool live = b < rows_of(B, im);
@@ -375,10 +383,62 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
                 for (uint32_t c = 0; c < C; ++c) res[c] = A::zero();
             }
             T* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C
-                                     : outputs + ((size_t)b * L + level) * C;
+                                     : outputs + ((size_t)b * Lfull + level) * C;
             store_entry<T, C>(out, res);
         }
     }
+}
+
+template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL = kFwdLevelsPerBlock>
+__global__ void __launch_bounds__(256)
+k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
+                const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
+                GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+                int32_t out_layout, InMap im) {
+    grid_fwd_pair_block<T, E, D, C, KL>(blockIdx.x, inputs, grid, offsets, outputs, B, L, lv, gridtype,
+                                        align_corners, interp, out_layout, im, LevelRange{0u, L});
+}
+
+// The fused step's grid forward in two launches (ngp_grid_encode_forward_fused_adam):
+// the first carries the part of the previous step's Adam sweep over the
+// levels the second encodes (blocks [0, nadam): 256-thread Adam blocks, the
+// march launch's sweep, dispatched first so they stream beside the
+// gather-bound forward blocks), the second the deferred GradScaler / LambdaLR /
+// loss bookkeeping of that update (one block, after every Adam block of the
+// earlier launches has read the scaler state). A level's forward never reads
+// a value the same launch's Adam writes.
+struct FwdAdam {
+    ngp_head::TensorList tl;
+    ngp_head::AdamArgs aa;
+    ngp_step::StepState* st;   // null: no Adam blocks
+    uint32_t nadam;
+    ngp_step::StepState* end;  // null: no bookkeeping block
+    ngp_step::ScalerArgs sa;
+    const float* loss_ray;
+    uint32_t n_rays;
+};
+
+template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL>
+__global__ void __launch_bounds__(256)
+k_grid_fwd_adam(const float* __restrict__ inputs, const E* __restrict__ grid,
+                const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
+                GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+                int32_t out_layout, InMap im, LevelRange lr, FwdAdam fa) {
+    const uint32_t nadam = fa.st ? fa.nadam : 0u;
+    if (blockIdx.x < nadam) {
+        ngp_head::adam_sweep_pipe<2>(fa.tl, fa.st, fa.aa, blockIdx.x, nadam, threadIdx.x);
+        return;
+    }
+    uint32_t blk = blockIdx.x - nadam;
+    if (fa.end) {
+        if (blk == 0) {
+            if (fa.end->end_pending) ngp_step::step_end_block(fa.end, fa.sa, nullptr, nullptr, fa.loss_ray, fa.n_rays);
+            return;
+        }
+        --blk;
+    }
+    grid_fwd_pair_block<T, E, D, C, KL>(blk, inputs, grid, offsets, outputs, B, L, lv, gridtype, align_corners,
+                                        interp, out_layout, im, lr);
 }
 
 // ---- scatter-add of one corner's C channels (values already weighted) -----
@@ -1905,6 +1965,70 @@ extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, cons
                                          align_corners != 0, interp, out_layout, ngp_stream(stream), im);
     return fwd_t<ngp_half, float>(xyz, embeddings, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
                                   align_corners != 0, interp, out_layout, ngp_stream(stream), im);
+}
+
+extern "C" int ngp_grid_encode_forward_fused_adam(const float* xyz, float bound, const void* embeddings,
+                                                  int32_t emb_dtype, const int32_t* offsets, void* outputs,
+                                                  uint32_t B, const int32_t* count, uint32_t D, uint32_t C,
+                                                  uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                                  int32_t align_corners, uint32_t interp, uint32_t level_lo,
+                                                  uint32_t level_hi, const ngp_adam_job* job, void* state,
+                                                  void* end_state, float growth_factor, float backoff_factor,
+                                                  int32_t growth_interval, int32_t scaler_enabled,
+                                                  const float* loss_ray, uint32_t n_rays, void* stream) {
+    if (int e = check_common(L, embeddings, offsets, outputs)) return e;
+    NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_forward_fused_adam: null xyz or bound <= 0");
+    NGP_REQUIRE(D == 3 && C == 2, NGP_ERR_UNSUPPORTED, "grid_encode_forward_fused_adam: D 3, C 2 only");
+    NGP_REQUIRE(level_lo < level_hi && level_hi <= L, NGP_ERR_ARG,
+                "grid_encode_forward_fused_adam: levels [%u, %u) of %u", level_lo, level_hi, L);
+    NGP_REQUIRE(emb_dtype == NGP_DTYPE_F32 || emb_dtype == NGP_DTYPE_F16, NGP_ERR_ARG,
+                "grid_encode_forward_fused_adam: emb_dtype %d (F32 or F16)", emb_dtype);
+    NGP_REQUIRE(!job || state, NGP_ERR_ARG, "grid_encode_forward_fused_adam: a job needs the state");
+    NGP_REQUIRE(!end_state || loss_ray, NGP_ERR_ARG, "grid_encode_forward_fused_adam: the bookkeeping needs loss_ray");
+    FwdAdam fa{};
+    if (job) {
+        NGP_REQUIRE(job->n_tensors >= 1 && job->n_tensors <= ngp_head::kMaxTensors, NGP_ERR_ARG,
+                    "grid_encode_forward_fused_adam: 1..%d tensors", ngp_head::kMaxTensors);
+        for (int q = 0; q < job->n_tensors; ++q) {
+            NGP_REQUIRE(((reinterpret_cast<uintptr_t>(job->params[q]) |
+                          reinterpret_cast<uintptr_t>(job->exp_avg[q]) |
+                          reinterpret_cast<uintptr_t>(job->exp_avg_sq[q])) & 15) == 0 &&
+                            (reinterpret_cast<uintptr_t>(job->grads[q]) & 7) == 0 &&
+                            (reinterpret_cast<uintptr_t>(job->half_params[q]) & 7) == 0,
+                        NGP_ERR_ARG, "grid_encode_forward_fused_adam: tensor %d misaligned", q);
+        }
+        fa.tl = ngp_head::make_list(job->n_tensors, job->params, job->grads, job->exp_avg, job->exp_avg_sq,
+                                    job->half_params, job->sizes);
+        fa.aa = ngp_head::AdamArgs{job->lr, job->beta1, job->beta2, job->eps, job->iters, job->zero_grads,
+                                   job->grad_mult, 1};
+        fa.st = static_cast<ngp_step::StepState*>(state);
+        fa.nadam = 3u * ngp_num_cus();  // three 256-thread Adam blocks per CU, as the march launch's
+    }
+    if (end_state) {
+        fa.end = static_cast<ngp_step::StepState*>(end_state);
+        fa.sa = ngp_step::ScalerArgs{growth_factor, backoff_factor, growth_interval, scaler_enabled,
+                                     n_rays ? 1.0f / (float)n_rays : 0.0f};
+        fa.loss_ray = loss_ray;
+        fa.n_rays = n_rays;
+    }
+    if (B == 0) return NGP_OK;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const InMap im{bound, 1.0f / (2.0f * bound), count};
+    const LevelRange lr{level_lo, level_hi};
+    const uint32_t nfwd = 8u * ((level_hi - level_lo + 7) / 8) * ngp_div_up(B, 128);
+    const dim3 grid(nfwd + (fa.st ? fa.nadam : 0u) + (fa.end ? 1u : 0u));
+    hipStream_t st = ngp_stream(stream);
+    const bool ac = align_corners != 0;
+    if (emb_dtype == NGP_DTYPE_F16)
+        k_grid_fwd_adam<ngp_half, ngp_half, 3, 2, 1><<<grid, 256, 0, st>>>(
+            xyz, static_cast<const ngp_half*>(embeddings), offsets, static_cast<ngp_half*>(outputs), B, L, lv, gridtype,
+            ac, interp, 0, im, lr, fa);
+    else
+        k_grid_fwd_adam<ngp_half, float, 3, 2, 1><<<grid, 256, 0, st>>>(
+            xyz, static_cast<const float*>(embeddings), offsets, static_cast<ngp_half*>(outputs), B, L, lv, gridtype,
+            ac, interp, 0, im, lr, fa);
+    return ngp_check_launch("grid_encode_forward_fused_adam");
 }
 
 extern "C" int ngp_grid_encode_forward_fused_sel(const float* xyz, float bound, const void* table0,

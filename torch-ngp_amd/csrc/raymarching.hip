@@ -760,6 +760,7 @@ static_assert((kSegWaves - kMarchAdamWaves) % 4 == 0, "Adam waves form 256-threa
 // instead of in a latency-bound launch of their own.
 struct EmitTail {
     ngp_step::StepState* st;  // null: no tail row
+    bool end;                 // run the bookkeeping (false: a later launch does, NGP_ADAM_JOB_END_LATER)
     ngp_step::ScalerArgs sa;
     const float* loss_ray;
     uint32_t n_rays, groups;  // groups: emit ray groups (gridDim.x may be wider)
@@ -778,7 +779,8 @@ k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     const bool has_tail = tail.st != nullptr;
     if (has_tail && blockIdx.y == 0) {  // the tail row (block-uniform)
         if (blockIdx.x == 0) {
-            if (tail.st->end_pending) ngp_step::step_end_block(tail.st, tail.sa, nullptr, nullptr, tail.loss_ray, tail.n_rays);
+            if (tail.end && tail.st->end_pending)
+                ngp_step::step_end_block(tail.st, tail.sa, nullptr, nullptr, tail.loss_ray, tail.n_rays);
         } else if (blockIdx.x - 1 < (uint32_t)tail.jobs.n) {
             const ngp_pack::PackJob& j = tail.jobs.job[blockIdx.x - 1];
             ngp_pack::build_frags(j.image, j.w, j.m, j.transposed != 0);
@@ -1405,6 +1407,7 @@ extern "C" int ngp_march_rays_train_prebuilt_tail(const float* rays_o, const flo
     NGP_REQUIRE(state && loss_ray, NGP_ERR_ARG, "march_rays_train_prebuilt_tail: null state or loss_ray");
     EmitTail tail{};
     tail.st = static_cast<ngp_step::StepState*>(state);
+    tail.end = true;
     tail.sa = ngp_step::ScalerArgs{growth_factor, backoff_factor, growth_interval, scaler_enabled,
                                    N ? 1.0f / (float)N : 0.0f};
     tail.loss_ray = loss_ray;
@@ -1441,6 +1444,7 @@ extern "C" int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const flo
     }
     EmitTail tail{};
     tail.st = static_cast<ngp_step::StepState*>(state);
+    tail.end = (job->flags & NGP_ADAM_JOB_END_LATER) == 0;
     tail.sa = ngp_step::ScalerArgs{growth_factor, backoff_factor, growth_interval, scaler_enabled,
                                    N ? 1.0f / (float)N : 0.0f};
     tail.loss_ray = loss_ray;

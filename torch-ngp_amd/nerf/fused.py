@@ -256,6 +256,32 @@ class FusedTrainer:
             job.lr, job.beta1, job.beta2, job.eps = self.lr, self.betas[0], self.betas[1], self.eps
             job.iters, job.zero_grads, job.grad_mult = self.iters, 1, 1.0
             self._job = job
+        # ... and (NGP_ADAM_UNDER_FWD=1) the table levels past NGP_ADAM_SPLIT_LEVEL
+        # are swept instead by Adam blocks of the grid forward's first launch
+        # (levels [0, 8)), and the forward of levels [8, L) plus the deferred
+        # bookkeeping run in a second launch: the march launch's sweep is
+        # shorter and the rest of Adam streams beside the gather-bound forward
+        # (DESIGN.md "Adam under the grid forward"). Same arithmetic per value.
+        self._fwd_split = None
+        L = enc.num_levels
+        split = int(os.environ.get("NGP_ADAM_SPLIT_LEVEL", "10"))
+        if (self._march_adam and os.environ.get("NGP_ADAM_UNDER_FWD", "0") == "1" and L == 16
+                and 8 <= split < L and self.table32):
+            x = int(enc.offsets[split].item()) * enc.level_dim  # first table value of level `split`
+            nt = self._starts[1]
+            job, o = self._job, self._opt
+            # the march launch's job: table values [0, x) and the MLP section; its
+            # emit launch leaves the bookkeeping to the forward's second launch
+            job.sizes[0] = x
+            job.flags = nat.ADAM_JOB_END_LATER
+            j2 = nat.AdamJob()
+            j2.n_tensors = 1
+            j2.params[0], j2.grads[0] = o["params"][0] + 4 * x, o["grads"][0] + 2 * x
+            j2.exp_avg[0], j2.exp_avg_sq[0], j2.half_params[0] = o["m"][0] + 4 * x, o["v"][0] + 4 * x, None
+            j2.sizes[0] = nt - x
+            j2.lr, j2.beta1, j2.beta2, j2.eps = self.lr, self.betas[0], self.betas[1], self.eps
+            j2.iters, j2.zero_grads, j2.grad_mult = self.iters, 1, 1.0
+            self._fwd_split = (8, j2)
         # ... and the next batch is drawn while this step's grid backward runs
         # (a column of the bin launch; the batch buffers are dead once the
         # composite has read its targets), so the step starts with the march:
@@ -618,7 +644,7 @@ class FusedTrainer:
             else:
                 self._sample()
             self._march()
-        self._network(draw=self._draw_ahead)
+        self._network(draw=self._draw_ahead, adam_split=pending and self._march_adam)
 
     def _optimizer_head(self):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
@@ -743,7 +769,7 @@ class FusedTrainer:
             nat.check(lib.ngp_march_rays_train_prebuilt(*args, s), "march_rays_train")
         self._tick("march_rays_train+adam" if adam else "march_rays_train")
 
-    def _network(self, draw=False):
+    def _network(self, draw=False, adam_split=False):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         m, e = self.model, self.enc
         M, N, cnt = self.M, self.N, P(self.counter)
@@ -752,7 +778,20 @@ class FusedTrainer:
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
         table, tdt = (self.params[0], _F32) if self.table32 else (self.w_half[0], _F16)
-        if self.fused_adam:  # the current one of the double-buffered table
+        if adam_split and self._fwd_split is not None:
+            # levels [0, f) beside the rest of the previous step's Adam, then
+            # levels [f, L) with the update's deferred bookkeeping
+            f, j2 = self._fwd_split
+            fa = (P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets), P(self.enc_out), M, cnt,
+                  *grid_args[:-1])
+            chk(lib.ngp_grid_encode_forward_fused_adam(*fa, 0, f, ctypes.byref(j2), P(self.state), None, 2.0, 0.5,
+                                                       self.growth_interval, 1, P(self.loss_ray), N, s),
+                "grid_encode_forward_fused_adam")
+            self._tick("grid_encode_forward+adam")
+            chk(lib.ngp_grid_encode_forward_fused_adam(*fa, f, e.num_levels, None, None, P(self.state), 2.0, 0.5,
+                                                       self.growth_interval, 1, P(self.loss_ray), N, s),
+                "grid_encode_forward_fused_end")
+        elif self.fused_adam:  # the current one of the double-buffered table
             chk(lib.ngp_grid_encode_forward_fused_sel(P(self.xyzs), float(m.bound), P(table), P(self.table_b),
                                                       self._table_sel, tdt, P(e.offsets), P(self.enc_out), M, cnt,
                                                       *grid_args[:-1], 0, s), "grid_encode_fused_sel")
