@@ -1,9 +1,9 @@
 #!/bin/bash
 # One iteration on the GPU box: the named test files, probes, then same-box
 # bench A/B legs of an env knob. usage (on the box):
-#   bash tools/gpu_iter.sh TAG "tests/a.py tests/b.py" KNOB
+#   bash tools/gpu_iter.sh TAG "tests/a.py tests/b.py" "KNOB1 KNOB2"
 set -eo pipefail
-TAG=$1; TESTS=$2; KNOB=${3:-}
+TAG=$1; TESTS=$2; KNOBS=${3:-}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 export TMPDIR=/tmp
@@ -15,11 +15,11 @@ fi
 for probe in ${PROBES:-}; do
   timeout -k 10 200 python -u tools/$probe.py > $O/$probe.json 2> $O/$probe.err
 done
-if [ -n "$KNOB" ]; then
+for KNOB in $KNOBS; do
   for rep in 1 2; do
     for v in 0 1; do
       env $KNOB=$v timeout -k 10 200 python -u bench.py --no-cpu --no-legs --no-dp-path --no-render --steps 200 \
-          > $O/ab_${v}_${rep}.json 2> $O/ab_${v}_${rep}.err
+          > $O/ab_${KNOB}_${v}_${rep}.json 2> $O/ab_${KNOB}_${v}_${rep}.err
     done
   done
-fi
+done

@@ -110,7 +110,7 @@ class FusedRenderer:
             self._iteration(i)
 
     def _done(self):
-        st = self.state[:8].view(torch.int32).cpu().numpy()  # slot 0 {count, n_alive, step, pad}
+        st = self.state[:16].view(torch.int32).cpu().numpy()  # slot 0 {count, n_alive, step, pad}
         return st[1] <= 0 or st[2] >= self.max_steps
 
     def capture(self):
