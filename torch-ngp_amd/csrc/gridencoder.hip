@@ -419,14 +419,14 @@ struct FwdAdam {
 };
 
 template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 7)  // <= 72 VGPRs: the forward blocks keep most of their occupancy
 k_grid_fwd_adam(const float* __restrict__ inputs, const E* __restrict__ grid,
                 const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
                 GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
                 int32_t out_layout, InMap im, LevelRange lr, FwdAdam fa) {
     const uint32_t nadam = fa.st ? fa.nadam : 0u;
     if (blockIdx.x < nadam) {
-        ngp_head::adam_sweep_pipe<2>(fa.tl, fa.st, fa.aa, blockIdx.x, nadam, threadIdx.x);
+        ngp_head::adam_sweep_pipe<1>(fa.tl, fa.st, fa.aa, blockIdx.x, nadam, threadIdx.x);
         return;
     }
     uint32_t blk = blockIdx.x - nadam;
@@ -2002,7 +2002,10 @@ extern "C" int ngp_grid_encode_forward_fused_adam(const float* xyz, float bound,
         fa.aa = ngp_head::AdamArgs{job->lr, job->beta1, job->beta2, job->eps, job->iters, job->zero_grads,
                                    job->grad_mult, 1};
         fa.st = static_cast<ngp_step::StepState*>(state);
-        fa.nadam = 3u * ngp_num_cus();  // three 256-thread Adam blocks per CU, as the march launch's
+        // three 256-thread Adam blocks per CU, as the march launch's (NGP_FWD_ADAM_BLOCKS: per CU, A/B)
+        const char* nb = getenv("NGP_FWD_ADAM_BLOCKS");
+        const uint32_t per_cu = nb ? (uint32_t)atoi(nb) : 3u;
+        fa.nadam = (per_cu ? per_cu : 1u) * ngp_num_cus();
     }
     if (end_state) {
         fa.end = static_cast<ngp_step::StepState*>(end_state);
