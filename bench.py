@@ -325,6 +325,20 @@ def dp_path_probe(args, model, data, dev, headline):
         elapsed, used_graph, _ = timed_run(args, ft, 1, dev, steps, 5, 300, 1)
         ms = elapsed / steps * 1e3
         phases = ft.timed_steps(args.kernel_steps)
+        # the whole step (collectives included) captured in one graph, 10 steps per replay
+        whole = None
+        os.environ["NGP_DP_GRAPH"] = "1"
+        try:
+            m3, d3, _, _, _, _, _ = make_workload(args.workload, dev, 1, args.num_rays)
+            ft3, _ = make_trainer(args, m3, d3, 1, dev, dtg, distributed=True)
+            e3, g3, _ = timed_run(args, ft3, 1, dev, steps, 5, 300, args.graph_steps)
+            whole = {"ms_per_step": round(e3 / steps * 1e3, 4), "captured": bool(g3 and ft3._dp_whole is not None),
+                     "graph_steps": ft3._multi}
+            del ft3, m3
+        except Exception as e:  # RCCL capture unsupported: recorded, the three-graph path stands
+            whole = {"error": repr(e)[:300]}
+        finally:
+            del os.environ["NGP_DP_GRAPH"]
         grad_bytes = 2 * ft.total  # the flat fp16 gradient = the fp16 forward copy
         truck_bytes = 2 * _flat_total(22)
         W = 8
@@ -332,6 +346,7 @@ def dp_path_probe(args, model, data, dev, headline):
         budget = W * headline_ms / 6.0  # per-rank step time that still gives 6x at 8 ranks
         out = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "graphs": used_graph,
                "ms_per_step": round(ms, 4), "rays_per_s": round(args.num_rays / (ms * 1e-3), 1),
+               "whole_step_graph": whole,
                "phases_ms": {k: round(v, 5) for k, v in phases.items()},
                "flat_grad_bytes": int(grad_bytes),
                "per_rank_bytes_8_ranks": {
@@ -569,7 +584,7 @@ def timed_run(args, ft, world, dev, steps, warmup, settle, graph_steps):
     used_graph = False
     if args.graph:
         try:
-            ft.capture(multi=graph_steps if not ft.dp else 1)
+            ft.capture(multi=graph_steps if (not ft.dp or ft._dp_graph) else 1)
             ft.run(3 * max(1, graph_steps))
             used_graph = True
         except Exception as e:  # eager launches are the same kernels; record why

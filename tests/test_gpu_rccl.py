@@ -75,8 +75,10 @@ def _run_steps(ft):
                 mean_density=ft.mean_density, dp=ft.dp, nccl=ft._nccl)
 
 
-def _worker(port, q):
+def _worker(port, q, whole_graph=False):
     import sys
+    if whole_graph:  # the whole step, collectives included, in one graph (NGP_DP_GRAPH)
+        os.environ["NGP_DP_GRAPH"] = "1"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "torch-ngp_amd")]
     import torch.distributed as dist
@@ -96,10 +98,11 @@ def _worker(port, q):
         q.put(("error", repr(e), traceback.format_exc(), None))
 
 
-def test_rccl_world1_data_parallel_step_equals_single_process(parity_report):
+@pytest.mark.parametrize("whole_graph", [False, True], ids=["three_graphs", "whole_step_graph"])
+def test_rccl_world1_data_parallel_step_equals_single_process(parity_report, whole_graph):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_worker, args=(_free_port(), q))
+    p = ctx.Process(target=_worker, args=(_free_port(), q, whole_graph))
     p.start()
     status, backend, dp, single = q.get(timeout=300)
     p.join(timeout=60)
@@ -122,5 +125,6 @@ def test_rccl_world1_data_parallel_step_equals_single_process(parity_report):
                               np.argwhere(ne)[:4].tolist())
     assert np.array_equal(dp["m"].view(np.uint32), single["m"].view(np.uint32))
     assert np.array_equal(dp["v"].view(np.uint32), single["v"].view(np.uint32))
-    parity_report(f"RCCL world 1 ZeRO-1 step: {dp['steps']} optimizer steps, params / moments / density grid "
-                  f"bit-identical to the single-process step, loss {dp['loss']:.6f}")
+    parity_report(f"RCCL world 1 ZeRO-1 step ({'one graph per step' if whole_graph else 'three graphs'}): "
+                  f"{dp['steps']} optimizer steps, params / moments / density grid bit-identical to the "
+                  f"single-process step, loss {dp['loss']:.6f}")

@@ -304,6 +304,9 @@ class FusedTrainer:
             self._batch_job = bj
         self.graph = None
         self.graph_multi, self._multi = None, 1  # capture(multi=S): S step bodies in one graph
+        # data parallel over RCCL: NGP_DP_GRAPH=1 captures the whole step, collectives included
+        self._dp_graph = self.dp and os.environ.get("NGP_DP_GRAPH", "0") == "1"
+        self._dp_whole = None
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
@@ -914,6 +917,20 @@ class FusedTrainer:
                                              P(self.loss_ray), P(self.state), s), "fused_optimizer_step")
         self._tick("optimizer")
 
+    def _dp_body(self):
+        """One data-parallel step with an update pending, as one captured
+        sequence: Adam of this rank's shard (+ the gradient clear), the
+        all-gather of the fp16 forward copy on RCCL's stream while the batch is
+        drawn and marched, the network (+ guard), the reduce-scatter."""
+        self._optimizer(defer=True)
+        work = self._gather_half(wait=False)
+        self._sample()
+        self._march()
+        if work is not None:
+            work.wait()
+        self._network()
+        self._reduce()
+
     def step(self):
         """One training iteration (the optimizer half lags by one step, see
         the module docstring)."""
@@ -925,6 +942,8 @@ class FusedTrainer:
                 self.graph.replay()
             else:
                 self._body(self._pending)
+        elif self._dp_whole is not None and self._pending:
+            self._dp_whole.replay()  # the whole step, collectives included (NGP_DP_GRAPH)
         else:
             g = self.graph if self._pending else None
             work = None
@@ -957,7 +976,7 @@ class FusedTrainer:
         update at their head, so after a flush() (update_density, checkpoint,
         read-outs) the first iteration runs as step()."""
         g, S = self.graph_multi, self._multi
-        if g is not None and not self.dp and not self._ring:
+        if g is not None and (not self.dp or self._dp_whole is not None) and not self._ring:
             if not self._pending and k > 0:
                 self.step()
                 k -= 1
@@ -1018,6 +1037,24 @@ class FusedTrainer:
                 with torch.cuda.graph(gm):
                     for _ in range(multi):
                         self._body(True)
+                self.graph_multi, self._multi = gm, multi
+        elif self._dp_graph and self._nccl:
+            # the whole data-parallel step in one graph, the collectives on
+            # RCCL's stream forked from and joined to the capture stream: the
+            # all-gather of the fp16 forward copy beside sample + march, then
+            # the network, the guard and the reduce-scatter (no host round trip
+            # between them; multi=S: S steps per graph as in world 1)
+            self._dp_whole = None
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._dp_body()
+            self._dp_whole = g
+            self.graph_multi, self._multi = None, 1
+            if multi > 1:
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm):
+                    for _ in range(multi):
+                        self._dp_body()
                 self.graph_multi, self._multi = gm, multi
         else:
             graphs = {k: torch.cuda.CUDAGraph() for k in ("opt", "pre", "net")}
