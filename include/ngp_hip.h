@@ -690,6 +690,17 @@ int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, v
  * morton3D(c). */
 int ngp_density_grid_points(const int32_t* coords, const float* noise, uint32_t P, uint32_t ppc, uint32_t C,
                             uint32_t H, float bound, float* xyzs, int32_t* indices, void* stream);
+/* The points [lo, hi) of the same draws (coords required), written to xyzs /
+ * indices [0, hi - lo) in brick order: bucketed by cascade and morton3D(c) >>
+ * shift (bricks of >= 512 cells, at most 8192 buckets), in unspecified order
+ * inside a bucket. The densities' max into tmp_grid does not depend on the
+ * order, so an update gives the same grid as with ngp_density_grid_points,
+ * while a wave's points share the coarse levels' cache lines in the query.
+ * ws: ngp_density_grid_sort_workspace_bytes(C, H) bytes (cleared here). */
+size_t ngp_density_grid_sort_workspace_bytes(uint32_t C, uint32_t H);
+int ngp_density_grid_points_sorted(const int32_t* coords, const float* noise, uint32_t P, uint32_t ppc, uint32_t C,
+                                   uint32_t H, float bound, uint32_t lo, uint32_t hi, void* ws, size_t ws_bytes,
+                                   float* xyzs, int32_t* indices, void* stream);
 /* The densities of the points: sigma network forward on their encodings
  * (pair-major [L][B][2] half, ngp_grid_encode_forward_fused out_layout 0),
  * density = exp(h[:,0]) * density_scale (renderer.py:535-536), written as a

@@ -276,3 +276,64 @@ def test_fused_update_density_matches_restatement(cuda, bound):
     # the marcher's occupancy image follows the new bitfield: a step still marches
     ft.step()
     assert ft.sample_count() > 0
+
+
+@pytest.mark.parametrize("C,H", [(1, 128), (2, 64), (3, 32)])
+def test_sorted_points_are_a_permutation_in_brick_order(cuda, C, H):
+    """ngp_density_grid_points_sorted over [lo, hi) = the same (xyz, index)
+    rows as ngp_density_grid_points' rows lo..hi-1, permuted into brick order
+    (bucket = cascade, morton >> shift non-decreasing); two slices together
+    hold every draw (the data-parallel split)."""
+    import _ngp_native as nat
+    lib, P_ = nat.lib(), nat.ptr
+    H3 = H ** 3
+    ppc = H3 // 2
+    P = C * ppc
+    g = torch.Generator(device="cpu").manual_seed(C * 100 + H)
+    coords = torch.randint(0, H, (P, 3), dtype=torch.int32, generator=g).to(cuda)
+    noise = torch.rand(P, 3, generator=g).to(cuda)
+    xa, ia = torch.zeros(P, 3, device=cuda), torch.zeros(P, dtype=torch.int32, device=cuda)
+    s = nat.stream_of(xa)
+    nat.check(lib.ngp_density_grid_points(P_(coords), P_(noise), P, ppc, C, H, 2.0, P_(xa), P_(ia), s), "points")
+    ws = torch.zeros(int(lib.ngp_density_grid_sort_workspace_bytes(C, H)), dtype=torch.uint8, device=cuda)
+    split = P // 3 + 17
+    xs, is_ = torch.zeros(P, 3, device=cuda), torch.zeros(P, dtype=torch.int32, device=cuda)
+    for lo, hi in ((0, split), (split, P)):
+        nat.check(lib.ngp_density_grid_points_sorted(P_(coords), P_(noise), P, ppc, C, H, 2.0, lo, hi, P_(ws),
+                                                     ws.numel(), P_(xs) + 12 * lo, P_(is_) + 4 * lo, s), "sorted")
+    torch.cuda.synchronize()
+    for lo, hi in ((0, split), (split, P)):
+        ref = np.concatenate([xa[lo:hi].cpu().numpy().view(np.int32), ia[lo:hi, None].cpu().numpy()], 1)
+        got = np.concatenate([xs[lo:hi].cpu().numpy().view(np.int32), is_[lo:hi, None].cpu().numpy()], 1)
+        order = lambda r: r[np.lexsort(r.T[::-1])]  # noqa: E731  rows as a sorted multiset
+        np.testing.assert_array_equal(order(ref), order(got))
+        # brick order: the bucket (cascade * H^3 + morton) >> shift never decreases
+        idx = is_[lo:hi].cpu().numpy().astype(np.int64)
+        cas, mort = idx // H3, idx % H3
+        bits = int(np.ceil(np.log2(H)))
+        shift = min(9, 3 * bits)
+        while shift < 3 * bits and C << (3 * bits - shift) > 8192:
+            shift += 1
+        bucket = cas * (1 << (3 * bits - shift)) + (mort >> shift)
+        assert np.all(np.diff(bucket) >= 0)
+
+
+def test_fused_partial_update_sorted_equals_draw_order(cuda):
+    """A partial update with the brick-ordered query (default) leaves the same
+    density grid, mean and bitfield as the draw-order query, bit for bit."""
+    from nerf.fused import FusedTrainer
+    from nerf.provider import SyntheticLego
+    a = _model(cuda, bound=1)
+    b = copy.deepcopy(a)
+    fa = FusedTrainer(a, SyntheticLego(cuda, num_rays=256), M=20000, seed=5)
+    fb = FusedTrainer(b, SyntheticLego(cuda, num_rays=256), M=20000, seed=5)
+    fb._dens_sorted = False
+    for it in range(4):
+        if it == 2:
+            a.iter_density = b.iter_density = 16
+        fa.update_density()
+        fb.update_density()
+        torch.cuda.synchronize()
+        assert torch.equal(a.density_grid, b.density_grid)
+        assert fa.mean_density == fb.mean_density
+        assert torch.equal(a.density_bitfield, b.density_bitfield)

@@ -39,6 +39,10 @@ def main():
             model.iter_density = 16
             ft.update_density()
     out["update_density_ms"] = wall(updates) / C
+    ft._dens_sorted = False  # partial queries in draw order (A/B of the brick sort)
+    out["update_density_unsorted_ms"] = wall(updates) / C
+    ft._dens_sorted = True
+    out["update_density_sorted_ms"] = wall(updates) / C
     model.density_bitfield.copy_(bits)
     ft.refresh_occupancy()
     ft.run(E)

@@ -134,6 +134,9 @@ SIGNATURES = {
     "ngp_nerf_density_forward": [c_vp, c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_vp, c_vp, c_vp],
     "ngp_density_grid_ema_pack": [c_vp, c_vp, c_u32, c_u32, c_f32, ctypes.c_double, c_vp, c_vp, c_vp],
     "ngp_density_grid_draw_workspace_bytes": [c_u32, c_u32],
+    "ngp_density_grid_sort_workspace_bytes": [c_u32, c_u32],
+    "ngp_density_grid_points_sorted": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_u32, c_vp, c_sz,
+                                       c_vp, c_vp, c_vp],
     "ngp_density_grid_draw": [c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_grid_encode_backward_fused_timing_offset": [c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32, c_vp],
     "ngp_grid_encode_backward_fused_reduce": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
@@ -174,6 +177,7 @@ _RESTYPES = {
     "ngp_grid_encode_backward_fused_workspace_bytes": c_sz,
     "ngp_ffmlp_image_bytes": c_sz,
     "ngp_density_grid_draw_workspace_bytes": c_sz,
+    "ngp_density_grid_sort_workspace_bytes": c_sz,
 }
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}

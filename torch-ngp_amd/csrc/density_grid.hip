@@ -299,7 +299,172 @@ k_density_draw(uint32_t P, uint32_t ppc, uint32_t H, uint32_t seed, uint32_t upd
     for (int j = 0; j < 3; ++j) noise[(size_t)p * 3 + j] = rng_unit(seed, update, p, 1 + j);
 }
 
+// ---- partial-update points in brick order ----------------------------------------
+// The partial update's cells are random draws, so consecutive points of a wave
+// gather unrelated corners in the query's grid forward. tmp_grid is a max over
+// the points, whatever their order, so the points of [lo, hi) are bucketed by
+// their cell's Morton code >> shift (bricks of 2^shift cells, cascade-major):
+// count (a block-private LDS histogram, flushed with one global atomic per
+// nonzero bucket), scan, scatter (LDS ranks + one reservation per nonzero
+// bucket and block). The order inside a bucket is unspecified; each rank sorts
+// only its own slice of the draws, so the union over ranks is the draws.
+constexpr uint32_t kSortThreads = 1024, kSortPerThread = 16, kSortTile = kSortThreads * kSortPerThread;
+constexpr uint32_t kSortMaxBuckets = 8192;
+
+struct SortPlan {
+    uint32_t lo, n, ppc, H, shift, nb;  // nb: buckets per cascade
+};
+
+NGP_DEV uint32_t sort_bucket(const int32_t* __restrict__ coords, uint32_t p, const SortPlan& sp) {
+    const uint32_t cas = p / sp.ppc;
+    const uint32_t m = morton3((uint32_t)coords[(size_t)p * 3], (uint32_t)coords[(size_t)p * 3 + 1],
+                               (uint32_t)coords[(size_t)p * 3 + 2]);
+    return cas * sp.nb + (m >> sp.shift);
+}
+
+__global__ void __launch_bounds__(kSortThreads)
+k_density_sort_count(const int32_t* __restrict__ coords, SortPlan sp, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t hist[kSortMaxBuckets];
+    const uint32_t nbt = sp.nb * ((sp.lo + sp.n - 1) / sp.ppc + 1);  // buckets up to the last point's cascade
+    for (uint32_t b = threadIdx.x; b < nbt; b += kSortThreads) hist[b] = 0;
+    __syncthreads();
+    const uint32_t t0 = blockIdx.x * kSortTile;
+#pragma unroll 4
+    for (uint32_t k = 0; k < kSortPerThread; ++k) {
+        const uint32_t i = t0 + k * kSortThreads + threadIdx.x;
+        if (i < sp.n) atomicAdd(&hist[sort_bucket(coords, sp.lo + i, sp)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbt; b += kSortThreads)
+        if (hist[b]) atomicAdd(&counts[b], hist[b]);
+}
+
+// One workgroup: counts -> exclusive offsets in place.
+__global__ void __launch_bounds__(1024)
+k_density_sort_scan(uint32_t* __restrict__ counts, uint32_t nbt) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nbt; base += 1024) {
+        const uint32_t v = base + t < nbt ? counts[base + t] : 0u;
+        uint32_t incl = v;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t before = carry, all = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 16; ++w) {
+            before += w < wv ? wsum[w] : 0u;
+            all += wsum[w];
+        }
+        if (base + t < nbt) counts[base + t] = before + incl - v;
+        __syncthreads();
+        if (t == 0) carry += all;
+        __syncthreads();
+    }
+}
+
+// Same tiles as the count: each point's rank inside its bucket and block from
+// an LDS atomic, one global reservation per nonzero bucket, then the point
+// (k_density_points' arithmetic) at its slot.
+__global__ void __launch_bounds__(kSortThreads)
+k_density_sort_scatter(const int32_t* __restrict__ coords, const float* __restrict__ noise, SortPlan sp,
+                       CascadeScales cs, uint32_t* __restrict__ cursor, float* __restrict__ xyzs,
+                       int32_t* __restrict__ indices) {
+    __shared__ uint32_t hist[kSortMaxBuckets];
+    const uint32_t nbt = sp.nb * ((sp.lo + sp.n - 1) / sp.ppc + 1);
+    for (uint32_t b = threadIdx.x; b < nbt; b += kSortThreads) hist[b] = 0;
+    __syncthreads();
+    const uint32_t t0 = blockIdx.x * kSortTile;
+    uint32_t bk[kSortPerThread], rk[kSortPerThread];
+#pragma unroll
+    for (uint32_t k = 0; k < kSortPerThread; ++k) {
+        const uint32_t i = t0 + k * kSortThreads + threadIdx.x;
+        bk[k] = i < sp.n ? sort_bucket(coords, sp.lo + i, sp) : 0u;
+        rk[k] = i < sp.n ? atomicAdd(&hist[bk[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbt; b += kSortThreads)
+        if (hist[b]) hist[b] = atomicAdd(&cursor[b], hist[b]);
+    __syncthreads();
+    const float inv = 1.0f / (float)(sp.H - 1);
+#pragma unroll
+    for (uint32_t k = 0; k < kSortPerThread; ++k) {
+        const uint32_t i = t0 + k * kSortThreads + threadIdx.x;
+        if (i >= sp.n) continue;
+        const uint32_t p = sp.lo + i, cas = p / sp.ppc;
+        const uint32_t slot = hist[bk[k]] + rk[k];
+        const float s = cs.s[cas], h = cs.hgs[cas];
+        uint32_t c[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c[j] = (uint32_t)coords[(size_t)p * 3 + j];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            float x = 2.0f * (float)c[j];
+            x = x * inv;
+            x = x - 1.0f;
+            x = x * s;
+            float jt = noise[(size_t)p * 3 + j] * 2.0f;
+            jt = jt - 1.0f;
+            jt = jt * h;
+            xyzs[(size_t)slot * 3 + j] = x + jt;
+        }
+        indices[slot] = (int32_t)(cas * sp.H * sp.H * sp.H + morton3(c[0], c[1], c[2]));
+    }
+}
+
+// shift and buckets per cascade: bricks of >= 2^9 cells, at most
+// kSortMaxBuckets buckets over the cascades
+static SortPlan sort_plan(uint32_t C, uint32_t H, uint32_t ppc, uint32_t lo, uint32_t n) {
+    uint32_t bits = 0;
+    while ((1u << bits) < H) ++bits;
+    const uint32_t mbits = 3 * bits;  // Morton codes of the cube are < 2^mbits
+    uint32_t shift = std::min<uint32_t>(9, mbits);
+    while (shift < mbits && (size_t)C << (mbits - shift) > kSortMaxBuckets) ++shift;
+    return SortPlan{lo, n, ppc, H, shift, 1u << (mbits - shift)};
+}
+
 }  // namespace
+
+extern "C" size_t ngp_density_grid_sort_workspace_bytes(uint32_t C, uint32_t H) {
+    const SortPlan sp = sort_plan(C, H, 1, 0, 1);
+    return (size_t)C * sp.nb * sizeof(uint32_t);
+}
+
+extern "C" int ngp_density_grid_points_sorted(const int32_t* coords, const float* noise, uint32_t P, uint32_t ppc,
+                                              uint32_t C, uint32_t H, float bound, uint32_t lo, uint32_t hi,
+                                              void* ws, size_t ws_bytes, float* xyzs, int32_t* indices,
+                                              void* stream) {
+    NGP_REQUIRE(coords && noise && xyzs && indices && ws, NGP_ERR_ARG,
+                "density_grid_points_sorted: null coords / noise / xyzs / indices / workspace");
+    NGP_REQUIRE(C >= 1 && C <= kMaxCascades && H >= 2 && H <= 1024, NGP_ERR_ARG,
+                "density_grid_points_sorted: cascade %u / grid size %u out of range", C, H);
+    NGP_REQUIRE(ppc > 0 && P == ppc * C && lo <= hi && hi <= P, NGP_ERR_ARG,
+                "density_grid_points_sorted: P = %u is not %u points x %u cascades, or [%u, %u) outside it", P, ppc,
+                C, lo, hi);
+    NGP_REQUIRE(ws_bytes >= ngp_density_grid_sort_workspace_bytes(C, H), NGP_ERR_ARG,
+                "density_grid_points_sorted: workspace of %zu bytes required, got %zu",
+                ngp_density_grid_sort_workspace_bytes(C, H), ws_bytes);
+    if (hi == lo) return NGP_OK;
+    const SortPlan sp = sort_plan(C, H, ppc, lo, hi - lo);
+    hipStream_t st = ngp_stream(stream);
+    const size_t nbt = (size_t)C * sp.nb;
+    if (hipMemsetAsync(ws, 0, nbt * sizeof(uint32_t), st) != hipSuccess)
+        return ngp_set_error(NGP_ERR_HIP, "density_grid_points_sorted: counter clear failed");
+    uint32_t* counts = static_cast<uint32_t*>(ws);
+    const uint32_t blocks = ngp_div_up(sp.n, kSortTile);
+    k_density_sort_count<<<blocks, kSortThreads, 0, st>>>(coords, sp, counts);
+    k_density_sort_scan<<<1, 1024, 0, st>>>(counts, (uint32_t)nbt);
+    k_density_sort_scatter<<<blocks, kSortThreads, 0, st>>>(coords, noise, sp, cascade_scales(C, H, bound), counts,
+                                                            xyzs, indices);
+    return ngp_check_launch("density_grid_points_sorted");
+}
 
 extern "C" int ngp_density_grid_points(const int32_t* coords, const float* noise, uint32_t P, uint32_t ppc,
                                        uint32_t C, uint32_t H, float bound, float* xyzs, int32_t* indices,

@@ -310,6 +310,8 @@ class FusedTrainer:
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
+        # partial updates query their random cells in brick order (NGP_DENSITY_SORT=0: draw order)
+        self._dens_sorted = os.environ.get("NGP_DENSITY_SORT", "1") != "0"
         self._pending = False  # gradients of the last forward/backward not yet applied
 
     def _setup_fused_adam(self, sec):
@@ -407,6 +409,8 @@ class FusedTrainer:
                 tmp=torch.full((C, H3), -1.0, device=dev),
                 stats=torch.zeros(1, dtype=torch.float64, device=dev),
                 ws=torch.zeros(max(wsb, 256), dtype=torch.uint8, device=dev),
+                sort_ws=torch.zeros(max(int(lib.ngp_density_grid_sort_workspace_bytes(C, H)), 256),
+                                    dtype=torch.uint8, device=dev),
                 table=torch.zeros_like(self.params[0], dtype=torch.float16) if self.table32 else None)
         partial = int(m.iter_density >= 16)
         ppc = 2 * (H3 // 4) if partial else H3
@@ -414,10 +418,20 @@ class FusedTrainer:
         nat.check(lib.ngp_density_grid_draw(P_(m.density_grid), C, H, partial, self.density_seed, m.iter_density,
                                             P_(d["coords"]), P_(d["noise"]), P_(d["ws"]), d["ws"].numel(), s),
                   "density_grid_draw")
-        nat.check(lib.ngp_density_grid_points(P_(d["coords"]) if partial else None, P_(d["noise"]), P, ppc, C, H,
-                                              float(m.bound), P_(d["xyzs"]), P_(d["idx"]), s), "density_grid_points")
         lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
         e, n = self.enc, hi - lo
+        if partial and self._dens_sorted:
+            # this rank's slice of the draws in brick order (same max per cell),
+            # at the head of xyzs / idx
+            nat.check(lib.ngp_density_grid_points_sorted(P_(d["coords"]), P_(d["noise"]), P, ppc, C, H,
+                                                         float(m.bound), lo, hi, P_(d["sort_ws"]),
+                                                         d["sort_ws"].numel(), P_(d["xyzs"]), P_(d["idx"]), s),
+                      "density_grid_points_sorted")
+            lo = 0
+        else:
+            nat.check(lib.ngp_density_grid_points(P_(d["coords"]) if partial else None, P_(d["noise"]), P, ppc, C,
+                                                  H, float(m.bound), P_(d["xyzs"]), P_(d["idx"]), s),
+                      "density_grid_points")
         if d["table"] is not None:  # world 1 keeps no fp16 table copy: make one for the query
             d["table"].copy_(self.params[0].detach())
         table = d["table"] if d["table"] is not None else self.w_half[0]
