@@ -14,6 +14,6 @@ i=0
 for PMC in "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_BUSY_CU_CYCLES" "SQ_WAVE_CYCLES SQ_WAVES"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $PMC --output-format csv --kernel-include-regex "$KRE" -d "$O/p$i" -o run -- \
-      python3 bench.py --no-cpu --steps 5 --warmup 3 --settle-steps 0 --kernel-steps 2 > "$O/p$i.log" 2>&1 || echo "pass $i ($PMC) failed rc=$?" >> "$O/failed.txt"
+      python3 bench.py --no-cpu --no-legs --no-dp-path --no-render ${BENCH_ARGS:-} --steps 5 --warmup 3 --settle-steps 0 --kernel-steps 2 > "$O/p$i.log" 2>&1 || echo "pass $i ($PMC) failed rc=$?" >> "$O/failed.txt"
 done
 exit 0

@@ -645,6 +645,9 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #ifndef NGP_MATCH_MAX_BINS
 #define NGP_MATCH_MAX_BINS 64
 #endif
+#ifndef NGP_SOA_ITEMS  // 1: 6-byte items, the values (half2) and entries (u16) in two arrays
+#define NGP_SOA_ITEMS 0
+#endif
 constexpr uint32_t kBinShift = NGP_BIN_SHIFT;
 constexpr uint32_t kBinEntries = 1u << kBinShift;
 constexpr uint32_t kMaxBinsPerLevel = 256;       // the bin kernel's small instantiation
@@ -674,6 +677,7 @@ struct BinPlan {
     // bin, so its result does not depend on the units' order
     uint32_t mslot0[kMaxLevels];     // first slot of the level's bins, or kNoSlot
     uint32_t nmslots;
+    size_t ents_at;                  // NGP_SOA_ITEMS: byte offset of the entry array from the items
 };
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
@@ -1041,7 +1045,13 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
             __builtin_nontemporal_store(*reinterpret_cast<const uint64_t*>(&v),
                                         reinterpret_cast<uint64_t*>(lvl_items + k + bi.x));
 #else
+#if NGP_SOA_ITEMS
+            const size_t slot = (size_t)bp.item0[level] + k + bi.x;
+            reinterpret_cast<ngp_half2*>(items)[slot] = it.v;
+            reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(items) + bp.ents_at)[slot] = (uint16_t)it.e;
+#else
             lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
+#endif
 #endif
         }
     }
@@ -1269,7 +1279,11 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     constexpr uint32_t kOwner = 1, kFresh = 2, kMulti = 4;
     struct Unit {
         uint32_t level, lbin, gb, s0, s1, ne, flags, slot, nunits;
+#if NGP_SOA_ITEMS
+        uint32_t i0;  // the bin's first item slot
+#else
         const uint64_t* src;
+#endif
         ngp_half2* tbl;
     };
     // The unit's bin: the last bin whose first unit is <= u, found 64 ways
@@ -1297,7 +1311,11 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         r.gb = gb;
         r.s0 = seg * kSegItems;
         r.s1 = min(bn[gb] & 0x7fffffffu, r.s0 + kSegItems);
+#if NGP_SOA_ITEMS
+        r.i0 = s_item0[r.level] + r.lbin * s_cap[r.level];
+#else
         r.src = reinterpret_cast<const uint64_t*>(items + s_item0[r.level] + (size_t)r.lbin * s_cap[r.level]);
+#endif
         const uint32_t off0 = s_off[r.level];
         const uint32_t hs = s_off[r.level + 1] - off0;
         const uint32_t e0 = r.lbin * kBinEntries;
@@ -1310,7 +1328,16 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
         for (uint32_t q = 0; q < kAccBatch; ++q) {
             const uint32_t k = k0 + q * kAccThreads + t;
+#if NGP_SOA_ITEMS
+            // (entry, value) as the AoS item's dword pair; clamped loads, value selected away
+            const uint32_t kk = w.i0 + (k < w.s1 ? k : w.s0);
+            const uint32_t v = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(items) + kk);
+            const uint32_t e = __builtin_nontemporal_load(
+                reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(items) + bp.ents_at) + kk);
+            it[q] = k < w.s1 ? ((uint64_t)v << 32) | e : ~0ull;
+#else
             it[q] = k < w.s1 ? __builtin_nontemporal_load(w.src + k) : ~0ull;
+#endif
         }
     };
     // Only a non-fresh owner reads its slice back. No select on the loaded
@@ -1628,6 +1655,7 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
     }
     if (slots >= 0xffffffffull) bp.nlev = 0;  // item offsets are 32-bit: fall back to atomics
     bp.total_bins = bins;
+    bp.ents_at = NGP_SOA_ITEMS ? (size_t)((slots * 4 + 255) / 256 * 256) : 0u;
     return bp;
 }
 
@@ -1638,6 +1666,7 @@ static size_t bin_counters_bytes(const BinPlan& bp) { return ((size_t)bp.total_b
 static size_t bin_items_bytes(const BinPlan& bp) {
     size_t slots = 0;
     for (uint32_t l = 0; l < bp.nlev; ++l) slots += (size_t)bp.nbins[l] * bp.cap[l];
+    if (NGP_SOA_ITEMS) return (slots * 4 + 255) / 256 * 256 + (slots * 2 + 255) / 256 * 256;
     return (slots * sizeof(BinItem) + 255) / 256 * 256;
 }
 static size_t bin_sums_offset(const BinPlan& bp) { return bin_counters_bytes(bp) + 256 + bin_items_bytes(bp); }
