@@ -259,6 +259,33 @@ def test_run_after_flush_replays_multi_step_graph(cuda):
     assert a.optimizer_steps == b.optimizer_steps and a.model.local_step == b.model.local_step
 
 
+def test_first_step_after_flush_replays_its_graph(cuda):
+    """capture() also records the first step after a flush (no update pending,
+    batch drawn ahead); replaying it equals the eager step bit for bit, over
+    several flush points, and counts as one replay each."""
+    _, _, _, a = _setup(cuda)
+    _, _, _, b = _setup(cuda)
+    for t in (a, b):
+        t.step()
+        t.capture(warmup=2)
+    assert a._fresh is not None
+    a._fresh = _CountingGraph(a._fresh)
+    b._fresh = None  # eager after each flush
+    for _ in range(3):
+        for t in (a, b):
+            t.flush()
+            for _ in range(3):
+                t.step()
+    assert a._fresh.replays == 3
+    a.flush()
+    b.flush()
+    torch.cuda.synchronize()
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+    assert torch.equal(a.state, b.state)
+    assert a.optimizer_steps == b.optimizer_steps and a.model.local_step == b.model.local_step
+
+
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
 def test_fused_training_reduces_loss_and_captures(cuda, bound, dt_gamma):
     model, ref, data, ft = _setup(cuda, num_rays=4096, mean_count=100000, bound=bound, dt_gamma=dt_gamma)

@@ -307,6 +307,7 @@ class FusedTrainer:
         # data parallel over RCCL: NGP_DP_GRAPH=1 captures the whole step, collectives included
         self._dp_graph = self.dp and os.environ.get("NGP_DP_GRAPH", "0") == "1"
         self._dp_whole = None
+        self._fresh = None  # world 1: graph of the first step after a flush (capture)
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
@@ -954,6 +955,8 @@ class FusedTrainer:
                 self._ring_i += 1
             elif self.graph is not None and self._pending:
                 self.graph.replay()
+            elif self._fresh is not None and not self._pending and self._ahead:
+                self._fresh.replay()  # captured with the batch drawn ahead; leaves it drawn ahead
             else:
                 self._body(self._pending)
         elif self._dp_whole is not None and self._pending:
@@ -1045,6 +1048,16 @@ class FusedTrainer:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._body(True)
+            # ... and the body of the first step after a flush (no update
+            # pending, the batch drawn ahead by the last backward): so a
+            # training loop's flush points (density updates, read-outs) cost no
+            # eager step
+            self._fresh = None
+            if self._draw_ahead and self._ahead:
+                gf = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gf):
+                    self._body(False)
+                self._fresh = gf
             self.graph_multi, self._multi = None, 1
             if multi > 1:
                 gm = torch.cuda.CUDAGraph()
