@@ -358,6 +358,14 @@ def dp_path_probe(args, model, data, dev, headline):
                "scaling_budget_8_ranks": {"per_rank_ms_for_6x": round(budget, 4),
                                           "compute_ms_world1_dp_path": round(ms, 4),
                                           "exposed_collective_ms_allowed": round(budget - ms, 4)}}
+        # the same step at 8 ranks without its collectives: world 1's collectives are
+        # RCCL's local copies (dropped) and its Adam sweeps 8 shards (7/8 dropped)
+        ph = out["phases_ms"]
+        coll = ph.get("reduce_scatter", 0.0) + ph.get("all_gather", 0.0)
+        est = ms - coll - ph.get("optimizer", 0.0) * (W - 1) / W
+        out["scaling_budget_8_ranks"].update(
+            compute_ms_8_ranks_est=round(est, 4), exposed_collective_ms_allowed_8_ranks=round(budget - est, 4),
+            estimate="graph ms/step - world-1 reduce_scatter/all_gather phases - 7/8 of the optimizer phase")
         del ft, m2
         torch.cuda.empty_cache()
         return out
