@@ -72,7 +72,8 @@ def _run_steps(ft):
                 v=m2[:ft._starts[-1] + ft.params[-1].numel()].cpu().numpy(),
                 steps=ft.optimizer_steps, scale=ft.scale, loss=ft.last_loss,
                 grid=ft.model.density_grid.cpu().numpy(), bits=ft.model.density_bitfield.cpu().numpy(),
-                mean_density=ft.mean_density, dp=ft.dp, nccl=ft._nccl)
+                mean_density=ft.mean_density, dp=ft.dp, nccl=ft._nccl,
+                whole=getattr(ft, "_dp_whole", None) is not None)
 
 
 def _worker(port, q, whole_graph=False):
@@ -109,6 +110,7 @@ def test_rccl_world1_data_parallel_step_equals_single_process(parity_report, who
     assert status == "ok", (backend, dp)
     assert p.exitcode == 0
     assert backend == "nccl" and dp["dp"] and dp["nccl"] and not single["dp"]
+    assert dp["whole"] == whole_graph  # the graph phase replayed the whole-step graph
     assert dp["steps"] == single["steps"] >= 8 and dp["scale"] == single["scale"]
     assert np.isfinite(dp["loss"]) and dp["loss"] == single["loss"]
     for ph in dp["phases"]:  # first phase where the runs part, and by how much

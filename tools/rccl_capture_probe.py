@@ -54,7 +54,10 @@ def main():
                 ref = ref * 2
             torch.cuda.synchronize()
             ok = torch.equal(full, ref + 1) and torch.equal(shard, ref)
-            out[mode] = {"captured": True, "values_ok": bool(ok)}
+            d = lambda a, b: float((a.float() - b.float()).abs().max())  # noqa: E731
+            out[mode] = {"captured": True, "values_ok": bool(ok), "x_vs_ref": d(x, ref),
+                         "shard_vs_ref": d(shard, ref), "full_vs_ref1": d(full, ref + 1),
+                         "head": [x[:4].tolist(), shard[:4].tolist(), full[:4].tolist(), ref[:4].tolist()]}
         except Exception as e:  # noqa: BLE001
             out[mode] = {"captured": False, "error": repr(e)[:400]}
         x.copy_(torch.arange(n, dtype=torch.float16, device=dev) % 97)
