@@ -158,6 +158,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # stdout carries exactly the one JSON line: whatever the libraries print on
+    # file descriptor 1 (RCCL's version banner at communicator init) goes to
+    # stderr, the JSON line to the saved descriptor
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if world > 1 and args.backend == "gloo":
@@ -204,7 +210,10 @@ def main():
         result["cpu_baseline"] = cpu_baseline(model, data, args)
 
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        sys.stdout.flush()
+        line = (json.dumps(result) + "\n").encode()
+        while line:
+            line = line[os.write(json_fd, line):]
     if world > 1:
         dist.destroy_process_group()
 
@@ -772,6 +781,7 @@ def density_cadence(ft, bits, args, cycles=6, every=16):
     model.iter_density = 16  # partial updates, as upstream after the first 16
     ft.run(every)
     torch.cuda.synchronize()
+    eager0 = ft.eager_steps
     t0 = time.perf_counter()
     for _ in range(cycles):
         ft.update_density()
@@ -780,13 +790,29 @@ def density_cadence(ft, bits, args, cycles=6, every=16):
         ft.run(every)
     torch.cuda.synchronize()
     secs = time.perf_counter() - t0
+    eager = ft.eager_steps - eager0
+    # the same cycles again, synchronised after each part (where the time goes)
+    parts = {"update_density": 0.0, "restore": 0.0, "run": 0.0}
+
+    def part(name, fn):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        parts[name] += (time.perf_counter() - t) * 1e3 / cycles
+
+    for _ in range(cycles):
+        part("update_density", ft.update_density)
+        part("restore", lambda: (model.density_bitfield.copy_(bits), ft.refresh_occupancy()))
+        part("run", lambda: ft.run(every))
     model.density_grid.copy_(grid0)
     model.iter_density = it0
     model.density_bitfield.copy_(bits)
     ft.refresh_occupancy()
     ms = secs * 1e3 / (cycles * every)
     return {"ms_per_step": round(ms, 4), "rays_per_s": round(args.num_rays / (ms * 1e-3), 1),
-            "timing": f"{cycles} x [partial update_density + bitfield fixture restore + run({every})], wall"}
+            "timing": f"{cycles} x [partial update_density + bitfield fixture restore + run({every})], wall",
+            "eager_steps": int(eager), "parts_ms_per_cycle_synced": {k: round(v, 4) for k, v in parts.items()}}
 
 
 def density_update_times(model, bits, ft=None, reps=3):

@@ -25,7 +25,7 @@ def main():
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     out = {}
     n = 1 << 20
-    x = torch.arange(n, dtype=torch.float16, device=dev) % 97
+    x = (torch.arange(n, device=dev) % 97).half()
     shard = torch.empty(n, dtype=torch.float16, device=dev)
     full = torch.empty(n, dtype=torch.float16, device=dev)
     # eager first (communicator setup happens outside the capture)
@@ -60,7 +60,7 @@ def main():
                          "head": [x[:4].tolist(), shard[:4].tolist(), full[:4].tolist(), ref[:4].tolist()]}
         except Exception as e:  # noqa: BLE001
             out[mode] = {"captured": False, "error": repr(e)[:400]}
-        x.copy_(torch.arange(n, dtype=torch.float16, device=dev) % 97)
+        x.copy_((torch.arange(n, device=dev) % 97).half())
         torch.cuda.synchronize()
     dist.destroy_process_group()
     print(json.dumps(out))

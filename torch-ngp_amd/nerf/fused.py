@@ -308,6 +308,7 @@ class FusedTrainer:
         self._dp_graph = self.dp and os.environ.get("NGP_DP_GRAPH", "0") == "1"
         self._dp_whole = None
         self._fresh = None  # world 1: graph of the first step after a flush (capture)
+        self.eager_steps = 0  # world 1: steps run as eager launches (not graph replays)
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
@@ -959,6 +960,7 @@ class FusedTrainer:
                 self._fresh.replay()  # captured with the batch drawn ahead; leaves it drawn ahead
             else:
                 self._body(self._pending)
+                self.eager_steps += 1
         elif self._dp_whole is not None and self._pending:
             self._dp_whole.replay()  # the whole step, collectives included (NGP_DP_GRAPH)
         else:
