@@ -782,14 +782,21 @@ def density_cadence(ft, bits, args, cycles=6, every=16):
     ft.run(every)
     torch.cuda.synchronize()
     eager0 = ft.eager_steps
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(cycles + 1)]
+    host = []
     t0 = time.perf_counter()
-    for _ in range(cycles):
+    for c in range(cycles):
+        evs[c].record()
         ft.update_density()
         model.density_bitfield.copy_(bits)
         ft.refresh_occupancy()
         ft.run(every)
+        host.append(time.perf_counter())
+    evs[cycles].record()
     torch.cuda.synchronize()
     secs = time.perf_counter() - t0
+    gpu_cycle = [evs[c].elapsed_time(evs[c + 1]) for c in range(cycles)]
+    host_cycle = [(b - a) * 1e3 for a, b in zip([t0] + host[:-1], host)]
     eager = ft.eager_steps - eager0
     # the same cycles again, synchronised after each part (where the time goes)
     parts = {"update_density": 0.0, "restore": 0.0, "run": 0.0}
@@ -812,7 +819,9 @@ def density_cadence(ft, bits, args, cycles=6, every=16):
     ms = secs * 1e3 / (cycles * every)
     return {"ms_per_step": round(ms, 4), "rays_per_s": round(args.num_rays / (ms * 1e-3), 1),
             "timing": f"{cycles} x [partial update_density + bitfield fixture restore + run({every})], wall",
-            "eager_steps": int(eager), "parts_ms_per_cycle_synced": {k: round(v, 4) for k, v in parts.items()}}
+            "eager_steps": int(eager), "parts_ms_per_cycle_synced": {k: round(v, 4) for k, v in parts.items()},
+            "cycle_ms_gpu_events": [round(v, 3) for v in gpu_cycle],
+            "cycle_ms_host_enqueue": [round(v, 3) for v in host_cycle]}
 
 
 def density_update_times(model, bits, ft=None, reps=3):
