@@ -774,11 +774,18 @@ def density_cadence(ft, bits, args, cycles=6, every=16):
     (partial, device draws; it flushes the pending Adam first), restore the
     benched bitfield fixture (a device copy + the occupancy image rebuild, so
     the steps march the same workload as the headline), run(16) (the first
-    step after the flush eager, then the multi-step graph)]."""
+    step after the flush from its own graph, then the multi-step graph)],
+    after one untimed cycle."""
     model = ft.model
     grid0 = model.density_grid.clone()
     it0 = model.iter_density
     model.iter_density = 16  # partial updates, as upstream after the first 16
+    ft.run(every)
+    # one untimed cycle first: the first call of a code path pays one-time host
+    # costs (buffer allocation, first launches: ~100 ms in tools/cadence_probe2.py)
+    ft.update_density()
+    model.density_bitfield.copy_(bits)
+    ft.refresh_occupancy()
     ft.run(every)
     torch.cuda.synchronize()
     eager0 = ft.eager_steps
