@@ -447,6 +447,64 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
         assert torch.all((a - b).abs() <= 2.0 ** -10 * b.abs() + 1e-6), float((a - b).abs().max())
 
 
+@pytest.mark.parametrize("count", [4700, (256 * 9 + 128) * 32 - 5, (256 * 11 + 17) * 32])
+def test_nerf_backward_half_chunks_equal_whole_chunks(cuda, count):
+    """k_nerf_bwd splits a workgroup's last round of 1 or 2 chunks into
+    16-sample halves (NGP_MLP_BWD_HALVES, default on): input gradients bit for
+    bit against whole chunks only, dW within fp16 rounding of the same sums;
+    the counts give workgroups 1, 2 and 3 chunks in their last round."""
+    import ctypes
+    import os
+
+    import _ngp_native as nat
+    lib, P, s = nat.lib(), nat.ptr, None
+    g = torch.Generator(device="cpu").manual_seed(11)
+    B = 96000
+    cnt = torch.tensor([count, 0], dtype=torch.int32, device=cuda)
+    nets = [(32, 64, 2), (32, 64, 3)]
+    ws = [((torch.rand(h * (i + h * (nl - 1) + 16), generator=g) - 0.5) * 0.3).half().to(cuda) for i, h, nl in nets]
+    imgs = [torch.zeros(int(lib.ngp_ffmlp_image_bytes(i, h, nl)), dtype=torch.uint8, device=cuda)
+            for i, h, nl in nets]
+    arr = lambda ts: (ctypes.c_void_p * len(ts))(*[P(t) if t is not None else None for t in ts])  # noqa: E731
+    u32 = lambda v: (ctypes.c_uint32 * len(v))(*v)  # noqa: E731
+    nat.check(lib.ngp_ffmlp_pack(2, arr(ws), u32([a for a, _, _ in nets]), u32([b for _, b, _ in nets]),
+                                 u32([c for _, _, c in nets]), arr(imgs), s), "pack")
+    xp = torch.randn(16, B, 2, generator=g).half().to(cuda)   # pair-major encodings
+    ci = torch.randn(B, 32, generator=g).half().to(cuda)
+    go = torch.randn(B, 16, generator=g).half().to(cuda)
+    gh0 = torch.randn(B, 16, generator=g).half().to(cuda)
+    wsb = [torch.zeros(int(lib.ngp_ffmlp_backward_workspace_bytes(B, i, 16, h, nl)), dtype=torch.uint8,
+                       device=cuda) for i, h, nl in nets]
+    knob = os.environ.get("NGP_MLP_BWD_HALVES")
+    out = {}
+    try:
+        for v in ("0", "1"):
+            os.environ["NGP_MLP_BWD_HALVES"] = v
+            gh, gx = gh0.clone(), torch.zeros(16, B, 2, dtype=torch.half, device=cuda)
+            wsm = [torch.full_like(w, 7) for w in wsb]
+            nat.check(lib.ngp_nerf_backward(P(go), P(ci), P(imgs[1]), P(gh), P(xp), P(imgs[0]), P(gx), B, P(cnt),
+                                            64, 2, 64, 3, P(wsm[0]), wsm[0].numel(), P(wsm[1]), wsm[1].numel(),
+                                            None, s), "nerf_bwd")
+            gw = [torch.zeros(t.numel(), dtype=torch.half, device=cuda) for t in ws]
+            nat.check(lib.ngp_ffmlp_reduce(2, arr([wsm[1], wsm[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
+                                           u32([3, 2]), arr([gw[1], gw[0]]), 1, None, s), "reduce")
+            torch.cuda.synchronize()
+            out[v] = (gh, gx, gw)
+    finally:
+        if knob is None:
+            os.environ.pop("NGP_MLP_BWD_HALVES", None)
+        else:
+            os.environ["NGP_MLP_BWD_HALVES"] = knob
+    (gh_w, gx_w, gw_w), (gh_h, gx_h, gw_h) = out["0"], out["1"]
+    assert torch.equal(gh_h.view(torch.int16), gh_w.view(torch.int16))
+    assert torch.equal(gx_h.view(torch.int16), gx_w.view(torch.int16))
+    assert int(gx_h[:, count:].view(torch.int16).abs().sum()) == 0  # rows past the count untouched
+    for a, b in zip(gw_h, gw_w):
+        a, b = a.float(), b.float()
+        assert torch.isfinite(a).all() and torch.all((a - b).abs() <= 2.0 ** -10 * b.abs() + 1e-6), \
+            float((a - b).abs().max())
+
+
 def test_grad_guard_poisons_every_shard(cuda):
     """ngp_grad_guard (data-parallel GradScaler guard): an inf/nan anywhere in
     the rank's gradient puts a NaN at the head of every rank's chunk; a finite

@@ -774,17 +774,25 @@ struct GiPairMajor {
 #endif
 
 // One backward pass over the 32-sample chunks a wave takes (map(k): the
-// wave's k-th chunk; a chunk >= the chunk count ends the loop), then the fold
-// of the waves' dW tiles and the workgroup's slab row. fr: the network's
-// fragment image in LDS; tiles: the per-wave staging tiles; img: where the
-// two fold images go (they may overlay fr and tiles, dead by then). pre()
-// runs once the first chunk's loads are issued (a standalone launch copies
-// its fragment image there, so the two latencies overlap).
-template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI, typename MAP, typename PRE>
+// wave's k-th chunk; a chunk >= the chunk count ends the loop), then the
+// wave's half chunk if it has one (half(): the first row of a 16-sample half
+// of a chunk no wave took whole, or kNoHalf), then the fold of the waves' dW
+// tiles and the workgroup's slab row. fr: the network's fragment image in
+// LDS; tiles: the per-wave staging tiles; img: where the two fold images go
+// (they may overlay fr and tiles, dead by then). pre() runs once the first
+// chunk's loads are issued (a standalone launch copies its fragment image
+// there, so the two latencies overlap).
+constexpr uint32_t kNoHalf = 0xffffffffu;
+struct NoHalf {
+    NGP_DEV uint32_t operator()() const { return kNoHalf; }
+};
+
+template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI, typename MAP, typename PRE,
+          typename HALF = NoHalf>
 NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tiles, float* __restrict__ img_base,
                        const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs, XL xl, GI gi_out,
                        bool want_gi, float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim,
-                       FA act, MAP map, PRE pre) {
+                       FA act, MAP map, PRE pre, HALF half = HALF{}) {
     using N = Net<W, IN_KS, NH>;
     constexpr int LAST = N::NMAT - 1;
     MSTAMP(0);
@@ -807,23 +815,13 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
     for (int q = 0; q < NH; ++q) zero_tiles(dw_hid[q]);
     zero_tiles(dw_first);
 
-    // inputs and output gradients of the next chunk are prefetched while the
-    // current one computes (one wave per SIMD: nothing else hides the latency)
-    for (uint32_t kc = 1; chunk < nchunks; ++kc) {
-        const uint32_t row0 = chunk * 16 * kNB;
-        half8 x[kNB][IN_KS], dout[kNB][1];
-#pragma unroll
-        for (int nb = 0; nb < kNB; ++nb) {
-#pragma unroll
-            for (int s = 0; s < IN_KS; ++s) x[nb][s] = xn[nb][s];
-            dout[nb][0] = dn[nb][0];
-        }
-        const uint32_t next = map(kc);
-        xl.template operator()<IN_KS>(inputs, in_dim, next * 16 * kNB, B, xn);
-        load_rows<1>(grad, kOut, next * 16 * kNB, B, dn);
+    // one chunk of NBC 16-sample blocks from row0 (inputs x, output grads
+    // dout): recompute, delta chain, dW accumulation, input grads
+    auto body = [&](auto nbc, uint32_t row0, const auto& x, const auto& dout) {
+        constexpr int NBC = decltype(nbc)::value;
         // recompute the post-activations of every hidden layer
-        half8 h[NH + 1][kNB][N::KSW];
-        f32x4 a[kNB][N::MTW];
+        half8 h[NH + 1][NBC][N::KSW];
+        f32x4 a[NBC][N::MTW];
         dense<N::MTW, IN_KS>(fr, fwd_desc<W, IN_KS, NH>(0, in_dim).frag0, x, a);
         pack_act<N::MTW, N::KSW>(a, act, h[0]);
 #pragma unroll
@@ -846,7 +844,7 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
         dw_accum<1, N::MTW>(dT, hT, dw_last);
         dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
 #endif
-        half8 d[kNB][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
+        half8 d[NBC][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
         pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
 #pragma unroll
         for (int q = NH; q >= 1; --q) {
@@ -864,7 +862,7 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
         // first matmul: dW += d^T . x, and grad_inputs = W_0^T d
         write_rows<N::KSW, true>(dT, d, W);
         write_rows<IN_KS, false>(hT, x, in_dim);
-        f32x4 gi[kNB][N::IN_MT];
+        f32x4 gi[NBC][N::IN_MT];
 #if NGP_MLP_BWD_OVERLAP
         if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
         dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
@@ -873,9 +871,43 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
         if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
 #endif
         if (want_gi) gi_out(row0, B, in_dim, gi);
+    };
+
+    // inputs and output gradients of the next chunk are prefetched while the
+    // current one computes (one wave per SIMD: nothing else hides the latency)
+    for (uint32_t kc = 1; chunk < nchunks; ++kc) {
+        const uint32_t row0 = chunk * 16 * kNB;
+        half8 x[kNB][IN_KS], dout[kNB][1];
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+#pragma unroll
+            for (int s = 0; s < IN_KS; ++s) x[nb][s] = xn[nb][s];
+            dout[nb][0] = dn[nb][0];
+        }
+        const uint32_t next = map(kc);
+        xl.template operator()<IN_KS>(inputs, in_dim, next * 16 * kNB, B, xn);
+        load_rows<1>(grad, kOut, next * 16 * kNB, B, dn);
+        body(std::integral_constant<int, kNB>{}, row0, x, dout);
         MSTAMP(2 + min(nst, 9u));
         ++nst;
         chunk = next;
+    }
+    // the wave's half chunk: 16 samples in rows 0..15 of the transposing
+    // tiles, rows 16..31 zero (the dW products' K runs over all 32 rows)
+    const uint32_t hrow = half();
+    if (hrow != kNoHalf) {
+        half8 x1[1][IN_KS], d1[1][1];
+        xl.template operator()<IN_KS>(inputs, in_dim, hrow, B, x1);
+        load_rows<1>(grad, kOut, hrow, B, d1);
+        asm volatile("" ::: "memory");  // after the last chunk's transposed reads
+        const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        const uint32_t lane = threadIdx.x & 63;
+        for (uint32_t i = lane; i < 16 * kTileLd / 8; i += 64) {
+            reinterpret_cast<half8*>(dT + 16 * kTileLd)[i] = z;
+            reinterpret_cast<half8*>(hT + 16 * kTileLd)[i] = z;
+        }
+        asm volatile("" ::: "memory");
+        body(std::integral_constant<int, 1>{}, hrow, x1, d1);
     }
     MSTAMP(12);
     // fold the waves' register tiles into two LDS dW images (round r: waves
@@ -985,6 +1017,7 @@ struct NerfBwdArgs {
     float* slab_sigma;
     uint32_t np_color, np_sigma, B;
     const int32_t* count;
+    uint32_t halves;  // split a last round of 1 or 2 chunks into 16-sample halves
     // the grid backward's timing ring (NGP_GRID_TIMING, include/ngp_hip.h), or
     // null: workgroup b stores its end (after its last store) in end slot
     // MAX_WG - 1 - b of the call the next bin launch opens (the accumulate's
@@ -1016,22 +1049,33 @@ k_nerf_bwd(NerfBwdArgs a) {
     half8* sfr = reinterpret_cast<half8*>(reinterpret_cast<char*>(lds) + NL::sigma_frags);
     const uint32_t G = gridDim.x, b = blockIdx.x, w = threadIdx.x >> 6;
     const uint32_t tcall = a.timing && threadIdx.x == 0 ? a.timing[0] : 0u;  // requested early
+    // this workgroup's chunks b, b + G, ...: n of them, the j-th in slot j % 4.
+    // When the last round holds r = 1 or 2 chunks (2 or 3 of the 4 waves idle
+    // for a whole chunk), they are split into 2r halves of 16 samples, one per
+    // slot, so the round takes a half chunk's time (NGP_MLP_BWD_HALVES=0: not split)
+    const uint32_t nch = ngp_div_up(B, 16 * kNB);
+    const uint32_t n = b < nch ? (nch - b + G - 1) / G : 0u, r = n % kBwdWaves;
+    const uint32_t nf = a.halves && (r == 1 || r == 2) ? n - r : n;  // chunks taken whole
+    auto map_of = [=](uint32_t slot) {
+        return [=](uint32_t k) { const uint32_t j = slot + k * kBwdWaves; return j < nf ? b + j * G : nch; };
+    };
+    auto half_of = [=](uint32_t slot) {
+        return [=]() { return nf < n && slot < 2 * r ? (b + (nf + slot / 2) * G) * 16 * kNB + 16 * (slot & 1) : kNoHalf; };
+    };
     bwd_phase<64, 1, NHC>(lds, reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes),
                           reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{}, GiNerfGeo{a.g_h},
-                          true, a.slab_color, a.np_color, B, 32u, ActReLU{},
-                          [=](uint32_t k) { return b + (w + k * kBwdWaves) * G; },
+                          true, a.slab_color, a.np_color, B, 32u, ActReLU{}, map_of(w),
                           [&]() {
                               copy_frags<LC::FRAGS, kBwdThreads>(lds, a.color_image);
                               copy_frags<LS::FRAGS, kBwdThreads>(sfr, a.sigma_image);
                               __syncthreads();
-                          });
+                          }, half_of(w));
     // the colour pass's geo grads (global stores of every wave) are complete
     // and its fold images read before the sigma pass loads g_h and reuses LDS
     __syncthreads();
     bwd_phase<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
                           InPairMajor{a.B}, GiPairMajor{a.g_enc, a.B}, true, a.slab_sigma, a.np_sigma, B, 32u,
-                          ActReLU{}, [=](uint32_t k) { return b + (kBwdWaves - 1 - w + k * kBwdWaves) * G; },
-                          []() {});
+                          ActReLU{}, map_of(kBwdWaves - 1 - w), []() {}, half_of(kBwdWaves - 1 - w));
     if (a.timing && b < NGP_GRID_TIMING_MAX_WG / 4) {
         __syncthreads();
         if (threadIdx.x == 0)
@@ -1448,6 +1492,11 @@ inline bool mlp_bwd_pair_enabled() {
     const char* e = getenv("NGP_MLP_BWD_PAIR");
     return e && e[0] == '1';
 }
+// k_nerf_bwd's half-chunk last round (NGP_MLP_BWD_HALVES=0: whole chunks only)
+inline bool mlp_bwd_halves_enabled() {
+    const char* e = getenv("NGP_MLP_BWD_HALVES");
+    return !(e && e[0] == '0');
+}
 
 template <int NHS, int NHC>
 int launch_nerf_bwd(const NerfBwdArgs& a, hipStream_t st) {
@@ -1609,6 +1658,7 @@ extern "C" int ngp_nerf_backward(const void* g_color_out, const void* color_in, 
     a.B = B;
     a.count = count;
     a.timing = timing;
+    a.halves = mlp_bwd_halves_enabled() ? 1u : 0u;
     hipStream_t st = ngp_stream(stream);
     const uint32_t key = (num_layers - 1) * 8 + (num_layers_color - 1);
     switch (key) {
