@@ -6,7 +6,7 @@
 One step = sample 4096 rays of a random training pose -> near/far ->
 march_rays_train -> hash-grid encode -> sigma FFMLP -> trunc_exp -> SH ->
 colour FFMLP -> composite -> MSE -> full backward -> Adam.
---engine fused (default): nerf/fused.py, the step as 11 fused launches in
+--engine fused (default): nerf/fused.py, the step as 8 fused launches in
 one hipGraph; --engine autograd: nerf/train.py, the same step through the
 reference-API autograd Functions (torch glue ops between them).
 The roofline's grid backward is timed by the kernels themselves on the chip's
@@ -328,24 +328,25 @@ def dp_path_probe(args, model, data, dev, headline):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:
         m2, d2, bits2, _, _, _, dtg = make_workload(args.workload, dev, 1, args.num_rays)
+        # the engine's data-parallel step as the N > 1 bench runs it: the whole
+        # step (collectives included) captured in one graph, graph_steps per replay
         ft, _ = make_trainer(args, m2, d2, 1, dev, dtg, distributed=True)
         assert ft.dp and ft._nccl
         steps = max(20, args.steps)
-        elapsed, used_graph, _ = timed_run(args, ft, 1, dev, steps, 5, 300, 1)
+        elapsed, used_graph, _ = timed_run(args, ft, 1, dev, steps, 5, 300, args.graph_steps)
         ms = elapsed / steps * 1e3
+        whole_captured = bool(used_graph and ft._dp_whole is not None)
+        graph_steps = ft._multi
         phases = ft.timed_steps(args.kernel_steps)
-        # the whole step (collectives included) captured in one graph, 10 steps per replay
-        whole = None
-        os.environ["NGP_DP_GRAPH"] = "1"
+        # the three-graph form (NGP_DP_GRAPH=0: collectives between the graphs), for comparison
+        three = None
+        os.environ["NGP_DP_GRAPH"] = "0"
         try:
             m3, d3, _, _, _, _, _ = make_workload(args.workload, dev, 1, args.num_rays)
             ft3, _ = make_trainer(args, m3, d3, 1, dev, dtg, distributed=True)
-            e3, g3, _ = timed_run(args, ft3, 1, dev, steps, 5, 300, args.graph_steps)
-            whole = {"ms_per_step": round(e3 / steps * 1e3, 4), "captured": bool(g3 and ft3._dp_whole is not None),
-                     "graph_steps": ft3._multi}
+            e3, g3, _ = timed_run(args, ft3, 1, dev, steps, 5, 300, 1)
+            three = {"ms_per_step": round(e3 / steps * 1e3, 4), "graphs": bool(g3)}
             del ft3, m3
-        except Exception as e:  # RCCL capture unsupported: recorded, the three-graph path stands
-            whole = {"error": repr(e)[:300]}
         finally:
             del os.environ["NGP_DP_GRAPH"]
         grad_bytes = 2 * ft.total  # the flat fp16 gradient = the fp16 forward copy
@@ -354,8 +355,9 @@ def dp_path_probe(args, model, data, dev, headline):
         headline_ms = headline["ms_per_step"]
         budget = W * headline_ms / 6.0  # per-rank step time that still gives 6x at 8 ranks
         out = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "graphs": used_graph,
+               "whole_step_graph": whole_captured, "graph_steps": graph_steps,
                "ms_per_step": round(ms, 4), "rays_per_s": round(args.num_rays / (ms * 1e-3), 1),
-               "whole_step_graph": whole,
+               "three_graphs": three,
                "phases_ms": {k: round(v, 5) for k, v in phases.items()},
                "flat_grad_bytes": int(grad_bytes),
                "per_rank_bytes_8_ranks": {

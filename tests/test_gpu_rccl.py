@@ -78,8 +78,8 @@ def _run_steps(ft):
 
 def _worker(port, q, whole_graph=False):
     import sys
-    if whole_graph:  # the whole step, collectives included, in one graph (NGP_DP_GRAPH)
-        os.environ["NGP_DP_GRAPH"] = "1"
+    # the whole step, collectives included, in one graph (the default), or three graphs
+    os.environ["NGP_DP_GRAPH"] = "1" if whole_graph else "0"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "torch-ngp_amd")]
     import torch.distributed as dist

@@ -21,8 +21,9 @@ Step order: `step()` runs [optimizer of the PREVIOUS step's gradients ->
 sample -> march -> network], so one graph holds a whole step. Data parallel
 (world > 1, ZeRO-1): [optimizer of this rank's shard] -> all-gather of the
 fp16 forward copy, overlapped with [sample -> march] -> [network] -> guard +
-averaging reduce-scatter of the gradient; the collectives sit between three
-graphs. The arithmetic is the reference's, in the
+averaging reduce-scatter of the gradient, captured as one graph over RCCL
+(the all-gather on RCCL's stream beside sample + march); with gloo or
+NGP_DP_GRAPH=0 the collectives sit between three graphs. The arithmetic is the reference's, in the
 reference's order; only the last step's update stays pending until
 `flush()` (the read-outs below flush first). Running that optimizer on a side
 stream beside sample + march was measured and lost: Adam and the marcher's
@@ -31,6 +32,7 @@ overlapped (profiles/r01u_overlap_trace.txt).
 """
 import ctypes
 import os
+import sys
 
 import numpy as np
 import torch
@@ -304,8 +306,9 @@ class FusedTrainer:
             self._batch_job = bj
         self.graph = None
         self.graph_multi, self._multi = None, 1  # capture(multi=S): S step bodies in one graph
-        # data parallel over RCCL: NGP_DP_GRAPH=1 captures the whole step, collectives included
-        self._dp_graph = self.dp and os.environ.get("NGP_DP_GRAPH", "0") == "1"
+        # data parallel over RCCL: the whole step is captured, collectives included
+        # (NGP_DP_GRAPH=0: three graphs with the collectives between them)
+        self._dp_graph = self.dp and os.environ.get("NGP_DP_GRAPH", "1") != "0"
         self._dp_whole = None
         self._fresh = None  # world 1: graph of the first step after a flush (capture)
         self.eager_steps = 0  # world 1: steps run as eager launches (not graph replays)
@@ -1019,13 +1022,15 @@ class FusedTrainer:
 
     def capture(self, warmup=2, ring=0, multi=1):
         """hipGraph(s) of the step body. World 1: one graph (optimizer of the
-        previous gradients, sample, march, network). Data parallel: three
-        (optimizer | sample + march | network); the collectives between them
-        stay outside. ring=R (world 1): R further copies of the body graph
+        previous gradients, sample, march, network). Data parallel over RCCL:
+        the whole step, collectives included (_dp_body); with gloo or
+        NGP_DP_GRAPH=0, three graphs (optimizer | sample + march | network)
+        with the collectives between them. ring=R (world 1): R further copies of the body graph
         with an event-record node after each launch; step() then replays
         them in turn (instead of the plain graph) and `ring_times` reads the
-        per-launch device times of the last R replays. multi=S (world 1): also
-        a graph of S consecutive step bodies, replayed by run()."""
+        per-launch device times of the last R replays. multi=S (world 1, and
+        the whole data-parallel step): also a graph of S consecutive step
+        bodies, replayed by run()."""
         for _ in range(max(1, warmup)):
             self.step()
         torch.cuda.synchronize()
@@ -1074,17 +1079,25 @@ class FusedTrainer:
             # the network, the guard and the reduce-scatter (no host round trip
             # between them; multi=S: S steps per graph as in world 1)
             self._dp_whole = None
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._dp_body()
-            self._dp_whole = g
             self.graph_multi, self._multi = None, 1
-            if multi > 1:
-                gm = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gm):
-                    for _ in range(multi):
-                        self._dp_body()
-                self.graph_multi, self._multi = gm, multi
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._dp_body()
+                if multi > 1:
+                    gm = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gm):
+                        for _ in range(multi):
+                            self._dp_body()
+                    self.graph_multi, self._multi = gm, multi
+                self._dp_whole = g
+            except RuntimeError as e:  # a stack that cannot capture the collectives: three graphs
+                print(f"FusedTrainer: whole-step capture failed ({e!r:.200}); collectives between graphs",
+                      file=sys.stderr)
+                torch.cuda.synchronize()
+                self._dp_graph = False
+                self.graph_multi, self._multi = None, 1
+                self.capture(warmup=0)
         else:
             graphs = {k: torch.cuda.CUDAGraph() for k in ("opt", "pre", "net")}
             with torch.cuda.graph(graphs["opt"]):
