@@ -505,6 +505,40 @@ def test_nerf_backward_half_chunks_equal_whole_chunks(cuda, count):
             float((a - b).abs().max())
 
 
+@pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
+def test_march_emit_in_launch_equals_emit_launch(cuda, bound, dt_gamma):
+    """The march + Adam launch emits the samples itself (ticketed ray blocks,
+    block totals published as agent-scope words; NGP_MARCH_EMIT_INLINE,
+    default on): samples, rays, counter and the trained parameters equal the
+    separate emit launch's bit for bit, step after step."""
+    import os
+    _, _, _, a = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
+    _, _, _, b = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
+    knob = os.environ.get("NGP_MARCH_EMIT_INLINE")
+    try:
+        for it in range(5):
+            os.environ["NGP_MARCH_EMIT_INLINE"] = "1"
+            a.step()
+            os.environ["NGP_MARCH_EMIT_INLINE"] = "0"
+            b.step()
+            torch.cuda.synchronize()
+            assert torch.equal(a.counter, b.counter), (it, a.counter.tolist(), b.counter.tolist())
+            n = a.sample_count()
+            assert n > 0 and n == b.sample_count()
+            assert torch.equal(a.rays, b.rays)
+            for x, y in ((a.xyzs, b.xyzs), (a.dirs, b.dirs), (a.deltas, b.deltas)):
+                assert torch.equal(x[:n].view(torch.int32), y[:n].view(torch.int32)), it
+    finally:
+        if knob is None:
+            os.environ.pop("NGP_MARCH_EMIT_INLINE", None)
+        else:
+            os.environ["NGP_MARCH_EMIT_INLINE"] = knob
+    a.flush()
+    b.flush()
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+
+
 def test_grad_guard_poisons_every_shard(cuda):
     """ngp_grad_guard (data-parallel GradScaler guard): an inf/nan anywhere in
     the rank's gradient puts a NaN at the head of every rank's chunk; a finite

@@ -671,6 +671,32 @@ NGP_DEV uint32_t march_ray_wave(const Ray& r, const MarchConst& k, const OCC& oc
     return (uint32_t)__builtin_amdgcn_readlane((int)n, 0);
 }
 
+// Sample kk of ray rn at output row p: xyz / dir / delta recomputed from the
+// recorded t with the reference's float ops (raymarching.cu:418-444).
+NGP_DEV void emit_sample(const float* __restrict__ rays_o, const float* __restrict__ rays_d, const MarchConst& k,
+                         const float* __restrict__ nears, const float* __restrict__ noises,
+                         const float* __restrict__ ts, uint32_t rn, uint32_t kk, size_t p, float* __restrict__ xyzs,
+                         float* __restrict__ dirs, float* __restrict__ deltas) {
+    const float* row = ts + (size_t)rn * k.max_steps;
+    const float t = row[kk];
+    // all loads unconditional (a load under the kk == 0 branch made the
+    // compiler wait for each one on the spot)
+    const float tp = row[kk ? kk - 1 : 0u];
+    const float nr = nears[rn], nz = noises[rn];
+    const float prev = kk == 0 ? ray_t0(nr, nz, k) : tp + clampf(tp * k.dt_gamma, k.dt_min, k.dt_max);
+    const float ox = rays_o[rn * 3], oy = rays_o[rn * 3 + 1], oz = rays_o[rn * 3 + 2];
+    const float dx = rays_d[rn * 3], dy = rays_d[rn * 3 + 1], dz = rays_d[rn * 3 + 2];
+    const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
+    xyzs[p * 3 + 0] = clampf(fmaf(t, dx, ox), -k.bound, k.bound);
+    xyzs[p * 3 + 1] = clampf(fmaf(t, dy, oy), -k.bound, k.bound);
+    xyzs[p * 3 + 2] = clampf(fmaf(t, dz, oz), -k.bound, k.bound);
+    dirs[p * 3 + 0] = dx;
+    dirs[p * 3 + 1] = dy;
+    dirs[p * 3 + 2] = dz;
+    deltas[p * 2 + 0] = dt;
+    deltas[p * 2 + 1] = (t + dt) - prev;
+}
+
 // The optimizer update a march launch may carry (ngp_march_rays_train_prebuilt_adam):
 // the march's workgroups keep their 16 waves and their LDS image, waves
 // [0, kMarchAdamWaves) march rays and the rest sweep Adam as virtual
@@ -694,20 +720,53 @@ constexpr uint32_t kMarchAdamWaves = NGP_MARCH_ADAM_WAVES;
 #define NGP_MARCH_ADAM_U 2
 #endif
 
+// The emit inside the march + Adam launch (world 1; ngp_march_rays_train_prebuilt_adam):
+// the march waves finish long before the Adam waves, so they also emit the
+// samples. Each workgroup takes a ticket at its start and marches the ray
+// block [rank * RB, rank * RB + RB), rank = ticket % G; once its block is
+// marched it publishes the block's sample total as one 8-byte agent-scope
+// atomic word ((epoch + 1) << 32 | total, epoch = ticket / G: the words need
+// no reset between launches), and reads the words of every lower rank for
+// its block's first output row. A lower rank's workgroup took its ticket
+// earlier, so it is running or done: no workgroup waits for one that may not
+// be resident. The rows are the emit launch's (ray order), bit for bit.
+constexpr uint32_t kEmitMaxBlockRays = 64;
+struct MarchEmit {
+    uint32_t* ticket;            // null: the emit launch does it; else the workspace's ticket counter
+    unsigned long long* words;   // [G] published block totals
+    int32_t* counter;            // counter[0] = end, counter[1] += N (the last rank)
+    float *xyzs, *dirs, *deltas;
+    uint32_t M, rb;              // output capacity; rays per block (<= kEmitMaxBlockRays)
+};
+
+NGP_DEV unsigned long long agent_load_u64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <uint32_t MW>  // march waves per workgroup (kSegWaves: the whole workgroup)
 __global__ void __launch_bounds__(kSegThreads)
 k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
               const uint8_t* __restrict__ grid, const uint8_t* __restrict__ img, OccLayout L,
               MarchConst k, uint32_t N, const float* __restrict__ nears, const float* __restrict__ fars,
               const float* __restrict__ noises, int32_t* __restrict__ rays, float* __restrict__ ts,
-              const int32_t* __restrict__ counter, uint32_t* __restrict__ scan, MarchAdam ma) {
+              const int32_t* __restrict__ counter, uint32_t* __restrict__ scan, MarchAdam ma, MarchEmit me) {
     extern __shared__ uint4 dyn[];
+    __shared__ uint32_t s_ticket, s_base0, s_arrive, s_ready, s_first;
+    __shared__ uint32_t s_off[kEmitMaxBlockRays + 1];
+    const bool emit = me.ticket != nullptr;  // launch-uniform
     // scan[0] = the offset of the first sample (the reference's counter[0] on entry,
     // raymarching.cu:405); scan[4 + n] = ray n's count (read by k_march_emit)
     if (blockIdx.x == 0 && threadIdx.x == 0) scan[0] = (uint32_t)counter[0];
+    if (emit && threadIdx.x == 0) {
+        s_ticket = atomicAdd(me.ticket, 1u);
+        s_base0 = (uint32_t)counter[0];  // read before this block publishes (the last rank rewrites it)
+        s_arrive = 0;
+        s_ready = 0;
+    }
     uint32_t* sum = reinterpret_cast<uint32_t*>(dyn);
     uint32_t* pre = sum + 4 * L.ngroups;
     const bool lds = L.ngroups > 0 && load_occ_index(img, L, dyn);  // every wave copies (one barrier)
+    if (emit) __syncthreads();  // the ticket (load_occ_index returns before its barrier when the image is too big)
     const uint32_t wave = threadIdx.x >> 6;
     if (MW < kSegWaves && wave >= MW) {  // the Adam waves (workgroup-uniform split, no barrier follows)
         constexpr uint32_t kVirt = (kSegWaves - MW) / 4;  // 256-thread virtual blocks per workgroup
@@ -724,7 +783,11 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
     }
     const OccLds occ_lds{sum, pre, reinterpret_cast<const uint8_t*>(pre + L.ngroups)};
     const OccGlobal occ_glb{grid};
-    for (uint32_t n = blockIdx.x * MW + wave; n < N; n += gridDim.x * MW) {
+    const uint32_t G = gridDim.x;
+    const uint32_t rank = emit ? s_ticket % G : blockIdx.x, epoch1 = emit ? s_ticket / G + 1u : 0u;
+    const uint32_t n0 = emit ? rank * me.rb : 0u, n1 = emit ? min(N, n0 + me.rb) : N;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t n = emit ? n0 + wave : blockIdx.x * MW + wave; n < n1; n += emit ? MW : G * MW) {
         const Ray r = load_ray(rays_o, rays_d, n);
         const float t0 = ray_t0(nears[n], noises[n], k);
         const float far = fars[n];
@@ -737,11 +800,80 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
             cnt = k.C == 1 ? march_ray_wave<true>(r, k, occ_glb, t0, far, row)
                            : march_ray_wave<false>(r, k, occ_glb, t0, far, row);
         }
-        if ((threadIdx.x & 63) == 0) {
+        if (lane == 0) {
             rays[n * 3 + 0] = (int32_t)n;
             rays[n * 3 + 2] = (int32_t)cnt;
             scan[4 + n] = cnt;
+            if (emit) s_off[n - n0] = cnt;
         }
+    }
+    if (!emit) return;
+    // ---- the in-launch emit (march waves only: no workgroup barrier, the Adam
+    // waves are elsewhere; the march waves meet through LDS counters)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's ts rows and counts are out
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    uint32_t last = 0;
+    if (lane == 0) last = atomicAdd(&s_arrive, 1u) == MW - 1 ? 1u : 0u;
+    last = (uint32_t)__builtin_amdgcn_readfirstlane((int)last);
+    const uint32_t nb = n1 > n0 ? n1 - n0 : 0u;
+    if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        // the block's counts -> exclusive offsets (one wave: nb <= 64)
+        const uint32_t c = lane < nb ? s_off[lane] : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        // publish this block's total, then sum the lower ranks' totals
+        if (lane == 0)
+            __hip_atomic_store(me.words + rank, ((unsigned long long)epoch1 << 32) | total, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        // (bounded: a word that never arrives -- a broken launch, not a slow
+        // one: the march itself takes ~20 us -- ends the wait after ~0.1 s
+        // with wrong offsets rather than a hung GPU)
+        uint32_t part = 0;
+        for (uint32_t p = lane; p < rank; p += 64) {
+            unsigned long long v = agent_load_u64(me.words + p);
+            for (uint32_t spin = 0; (uint32_t)(v >> 32) != epoch1 && spin < (1u << 20); ++spin) {
+                __builtin_amdgcn_s_sleep(2);
+                v = agent_load_u64(me.words + p);
+            }
+            part += (uint32_t)v;
+        }
+#pragma unroll
+        for (uint32_t o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        if (lane < nb) s_off[lane] = incl - c;
+        if (lane == 0) {
+            s_off[nb] = total;
+            s_first = s_base0 + part;
+            if (rank == G - 1) {  // every lower rank's total is in: the batch's end (reference :405-406)
+                me.counter[0] = (int32_t)(s_base0 + part + total);
+                me.counter[1] += (int32_t)N;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        for (uint32_t spin = 0; __hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u &&
+                                spin < (1u << 22); ++spin)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    const uint32_t base = s_first, btotal = s_off[nb];
+    const uint32_t t = threadIdx.x;  // 0 .. 64 MW - 1
+    for (uint32_t i = t; i < nb; i += 64 * MW) rays[(size_t)(n0 + i) * 3 + 1] = (int32_t)(base + s_off[i]);
+    for (uint32_t j = t; j < btotal; j += 64 * MW) {
+        uint32_t lo = 0, hi = nb;  // largest ray i with s_off[i] <= j
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_off[mid] <= j) lo = mid; else hi = mid;
+        }
+        if (base + s_off[lo + 1] > me.M) continue;  // whole ray dropped, like the reference
+        emit_sample(rays_o, rays_d, k, nears, noises, ts, n0 + lo, j - s_off[lo], (size_t)base + j, me.xyzs,
+                    me.dirs, me.deltas);
     }
 }
 static_assert((kSegWaves - kMarchAdamWaves) % 4 == 0, "Adam waves form 256-thread virtual blocks");
@@ -835,25 +967,7 @@ k_march_emit(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
         }
         const uint32_t rn = n0 + lo, kk = j - off[lo];
         if (base + off[lo + 1] > M) continue;  // whole ray dropped, like the reference
-        const float* row = ts + (size_t)rn * k.max_steps;
-        const float t = row[kk];
-        // all loads unconditional (a load under the kk == 0 branch made the
-        // compiler wait for each one on the spot)
-        const float tp = row[kk ? kk - 1 : 0u];
-        const float nr = nears[rn], nz = noises[rn];
-        const float prev = kk == 0 ? ray_t0(nr, nz, k) : tp + clampf(tp * k.dt_gamma, k.dt_min, k.dt_max);
-        const float ox = rays_o[rn * 3], oy = rays_o[rn * 3 + 1], oz = rays_o[rn * 3 + 2];
-        const float dx = rays_d[rn * 3], dy = rays_d[rn * 3 + 1], dz = rays_d[rn * 3 + 2];
-        const float dt = clampf(t * k.dt_gamma, k.dt_min, k.dt_max);
-        const size_t p = (size_t)base + j;
-        xyzs[p * 3 + 0] = clampf(fmaf(t, dx, ox), -k.bound, k.bound);
-        xyzs[p * 3 + 1] = clampf(fmaf(t, dy, oy), -k.bound, k.bound);
-        xyzs[p * 3 + 2] = clampf(fmaf(t, dz, oz), -k.bound, k.bound);
-        dirs[p * 3 + 0] = dx;
-        dirs[p * 3 + 1] = dy;
-        dirs[p * 3 + 2] = dz;
-        deltas[p * 2 + 0] = dt;
-        deltas[p * 2 + 1] = (t + dt) - prev;
+        emit_sample(rays_o, rays_d, k, nears, noises, ts, rn, kk, (size_t)base + j, xyzs, dirs, deltas);
     }
 }
 
@@ -1298,11 +1412,22 @@ static size_t march_ts_bytes(uint32_t N, uint32_t max_steps) {
 }
 static size_t march_scan_bytes(uint32_t N) { return ((size_t)(N + 4) * sizeof(uint32_t) + 255) / 256 * 256; }
 
+// the in-launch emit's ticket counter (16 B) and published block totals (8 B per workgroup)
+static size_t march_sync_bytes() { return 256 + 8 * (size_t)kMaxMarchBlocks; }
+
 extern "C" size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_steps, uint32_t C,
                                                         uint32_t H) {
     // the image size does not depend on the grid pointer's alignment
     OccLayout L = occ_layout(nullptr, C, H);
-    return march_ts_bytes(N, max_steps) + march_scan_bytes(N) + occ_image_bytes(L) + occ_scratch_bytes(L);
+    return march_ts_bytes(N, max_steps) + march_scan_bytes(N) + (occ_image_bytes(L) + occ_scratch_bytes(L) + 255) /
+           256 * 256 + march_sync_bytes();
+}
+
+// The march + Adam launch emits the samples itself (MarchEmit) unless
+// NGP_MARCH_EMIT_INLINE=0 or a ray block would exceed kEmitMaxBlockRays.
+static bool march_emit_inline() {
+    const char* e = getenv("NGP_MARCH_EMIT_INLINE");
+    return !(e && e[0] == '0');
 }
 
 static int march_train_impl(const float* rays_o, const float* rays_d, const uint8_t* grid,
@@ -1335,19 +1460,28 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
         k_occ_count<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
         k_occ_compact<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
     }
+    MarchEmit me{};
     if (ma && ma->st) {  // every CU gets a workgroup: the Adam waves sweep 1/gridDim of the parameters each
+        const uint32_t rb = ngp_div_up(N, kMaxMarchBlocks);
+        if (tail && rb <= kEmitMaxBlockRays && march_emit_inline()) {
+            uint8_t* sync = img + (occ_image_bytes(L) + occ_scratch_bytes(L) + 255) / 256 * 256;
+            me = MarchEmit{reinterpret_cast<uint32_t*>(sync), reinterpret_cast<unsigned long long*>(sync + 256),
+                           counter, xyzs, dirs, deltas, M, rb};
+        }
         k_march_train<kMarchAdamWaves><<<kMaxMarchBlocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
-            rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan, *ma);
+            rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan, *ma, me);
     } else {
         k_march_train<kSegWaves><<<blocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
-            rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan, MarchAdam{});
+            rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan, MarchAdam{},
+            MarchEmit{});
     }
     EmitTail et{};
     if (tail) et = *tail;
-    et.groups = groups;
-    const uint32_t gx = tail ? std::max<uint32_t>(groups, 1u + (uint32_t)tail->jobs.n) : groups;
-    k_march_emit<<<dim3(gx, kEmitSplit + (tail ? 1u : 0u)), kMarchThreads, 0, st>>>(
-        rays_o, rays_d, k, N, M, nears, noises, ts, xyzs, dirs, deltas, rays, scan, counter, et);
+    et.groups = me.ticket ? 0u : groups;  // emitted in the march launch: the tail row alone
+    const uint32_t gx = tail ? std::max<uint32_t>(et.groups, 1u + (uint32_t)tail->jobs.n) : groups;
+    const uint32_t gy = me.ticket ? 1u : kEmitSplit + (tail ? 1u : 0u);
+    k_march_emit<<<dim3(gx, gy), kMarchThreads, 0, st>>>(rays_o, rays_d, k, N, M, nears, noises, ts, xyzs, dirs,
+                                                         deltas, rays, scan, counter, et);
     return ngp_check_launch("march_rays_train");
 }
 
