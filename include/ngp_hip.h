@@ -168,6 +168,10 @@ typedef struct ngp_adam_job {
                                later launch (ngp_grid_encode_forward_fused_adam's end block) */
 } ngp_adam_job;
 #define NGP_ADAM_JOB_END_LATER 1u
+/* ... and the emit launch's whole tail row (bookkeeping + MLP fragment packs) is
+ * left to ngp_grid_encode_forward_fused_tail: with the samples emitted by the
+ * march launch itself, the march is then ONE launch */
+#define NGP_ADAM_JOB_TAIL_LATER 2u
 int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const float* rays_d, const uint8_t* grid,
                                        float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
                                        uint32_t C, uint32_t H, uint32_t M, const float* nears,
@@ -455,6 +459,20 @@ int ngp_grid_table_slices(const int32_t* offsets_host, uint32_t B, uint32_t D, u
  * level its own Adam blocks write, and the bookkeeping comes after every
  * launch carrying Adam (DESIGN.md "Adam under the grid forward"). fp16
  * outputs, [L, B, C] layout, rows clipped at *count. */
+/* ngp_grid_encode_forward_fused (out_layout 0) with the fused step's tail as
+ * extra workgroups dispatched first: the deferred GradScaler / LambdaLR / loss
+ * bookkeeping of the update the march launch applied (state; when pending) and
+ * the MLP fragment packs (ngp_ffmlp_pack's arguments; n_nets 0: none). For the
+ * march launch of an ngp_adam_job with NGP_ADAM_JOB_TAIL_LATER. */
+int ngp_grid_encode_forward_fused_tail(const float* xyz, float bound, const void* embeddings, int32_t emb_dtype,
+                                       const int32_t* offsets, void* outputs, uint32_t B, const int32_t* count,
+                                       uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
+                                       int32_t align_corners, uint32_t interp, void* state, float growth_factor,
+                                       float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
+                                       const float* loss_ray, uint32_t n_rays, int32_t n_nets,
+                                       const void* const* mlp_weights, const uint32_t* in_dims,
+                                       const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* images,
+                                       void* stream);
 int ngp_grid_encode_forward_fused_adam(const float* xyz, float bound, const void* embeddings, int32_t emb_dtype,
                                        const int32_t* offsets, void* outputs, uint32_t B, const int32_t* count,
                                        uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,

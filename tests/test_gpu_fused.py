@@ -539,6 +539,40 @@ def test_march_emit_in_launch_equals_emit_launch(cuda, bound, dt_gamma):
         assert torch.equal(x.detach(), y.detach())
 
 
+def test_tail_in_grid_forward_equals_emit_tail(cuda):
+    """The step's tail row (deferred scaler / LR / loss bookkeeping + MLP
+    fragment packs) in the grid forward's launch (NGP_TAIL_IN_FWD, default on:
+    the march is then one launch) against the tail row of the emit launch
+    (=0): parameters, moments and the step state bit for bit, eager and
+    captured, across an overflow-free run."""
+    import os
+    knob = os.environ.get("NGP_TAIL_IN_FWD")
+    try:
+        os.environ["NGP_TAIL_IN_FWD"] = "1"
+        _, _, _, a = _setup(cuda)
+        os.environ["NGP_TAIL_IN_FWD"] = "0"
+        _, _, _, b = _setup(cuda)
+    finally:
+        if knob is None:
+            os.environ.pop("NGP_TAIL_IN_FWD", None)
+        else:
+            os.environ["NGP_TAIL_IN_FWD"] = knob
+    assert a._tail_in_fwd and not b._tail_in_fwd
+    for t in (a, b):
+        for _ in range(3):
+            t.step()
+        t.capture(warmup=1, multi=4)
+        t.run(9)
+        t.flush()
+    torch.cuda.synchronize()
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+    assert torch.equal(a.exp_avg, b.exp_avg) and torch.equal(a.exp_avg_sq, b.exp_avg_sq)
+    assert torch.equal(a.state, b.state)
+    for x, y in zip(a.mlp_img, b.mlp_img):
+        assert torch.equal(x, y)
+
+
 def test_grad_guard_poisons_every_shard(cuda):
     """ngp_grad_guard (data-parallel GradScaler guard): an inf/nan anywhere in
     the rank's gradient puts a NaN at the head of every rank's chunk; a finite

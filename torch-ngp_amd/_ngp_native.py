@@ -63,6 +63,9 @@ SIGNATURES = {
     "ngp_grid_encode_forward_fused_adam": [c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
                                            c_f32, c_u32, c_u32, c_i32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp,
                                            c_f32, c_f32, c_i32, c_i32, c_vp, c_u32, c_vp],
+    "ngp_grid_encode_forward_fused_tail": [c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
+                                           c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_f32, c_f32, c_i32, c_i32, c_vp,
+                                           c_u32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_render_state_bytes": [],
     "ngp_render_count": [c_vp, c_u32],
     "ngp_render_init": [c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
@@ -202,6 +205,7 @@ class AdamJob(ctypes.Structure):
 
 
 ADAM_JOB_END_LATER = 1  # NGP_ADAM_JOB_END_LATER
+ADAM_JOB_TAIL_LATER = 2  # NGP_ADAM_JOB_TAIL_LATER
 
 
 class BatchJob(ctypes.Structure):

@@ -20,6 +20,7 @@
 //   * per-level scale/resolution are computed once on the host (exp2 in double,
 //     rounded to float) and passed as kernel arguments.
 //   * a hashed level's size is a power of two: the modulo becomes a mask.
+#include "ffmlp_pack.h"
 #include "ngp_common.h"
 #include "ngp_dpp.h"
 #include "ngp_head.h"
@@ -397,6 +398,45 @@ k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
                 int32_t out_layout, InMap im) {
     grid_fwd_pair_block<T, E, D, C, KL>(blockIdx.x, inputs, grid, offsets, outputs, B, L, lv, gridtype,
                                         align_corners, interp, out_layout, im, LevelRange{0u, L});
+}
+
+// The fused step's grid forward with the step's tail (ngp_grid_encode_forward_fused_tail):
+// the deferred GradScaler / LambdaLR / loss bookkeeping of the update the march
+// launch applied (one workgroup, when pending) and the MLP fragment packs from
+// the fp16 weights it wrote (one workgroup per pack job), dispatched first,
+// beside the forward blocks; the march launch then needs no emit launch after
+// it. Neither reads what the forward writes, and the next launch (the MLP
+// forward) is the first to read the images or the scale.
+struct FwdTail {
+    ngp_step::StepState* end;  // null: no bookkeeping block
+    ngp_step::ScalerArgs sa;
+    const float* loss_ray;
+    uint32_t n_rays;
+    ngp_pack::PackJobs jobs;
+};
+
+template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL = kFwdLevelsPerBlock>
+__global__ void __launch_bounds__(256)
+k_grid_fwd_tail(const float* __restrict__ inputs, const E* __restrict__ grid,
+                const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
+                GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+                int32_t out_layout, InMap im, FwdTail ft) {
+    uint32_t blk = blockIdx.x;
+    if (ft.end) {
+        if (blk == 0) {
+            if (ft.end->end_pending) ngp_step::step_end_block(ft.end, ft.sa, nullptr, nullptr, ft.loss_ray, ft.n_rays);
+            return;
+        }
+        --blk;
+    }
+    if (blk < (uint32_t)ft.jobs.n) {
+        const ngp_pack::PackJob& j = ft.jobs.job[blk];
+        ngp_pack::build_frags(j.image, j.w, j.m, j.transposed != 0);
+        return;
+    }
+    blk -= (uint32_t)ft.jobs.n;
+    grid_fwd_pair_block<T, E, D, C, KL>(blk, inputs, grid, offsets, outputs, B, L, lv, gridtype, align_corners,
+                                        interp, out_layout, im, LevelRange{0u, L});
 }
 
 // The fused step's grid forward in two launches (ngp_grid_encode_forward_fused_adam):
@@ -2061,6 +2101,58 @@ extern "C" int ngp_grid_encode_forward_fused_adam(const float* xyz, float bound,
             xyz, static_cast<const float*>(embeddings), offsets, static_cast<ngp_half*>(outputs), B, L, lv, gridtype,
             ac, interp, 0, im, lr, fa);
     return ngp_check_launch("grid_encode_forward_fused_adam");
+}
+
+extern "C" int ngp_grid_encode_forward_fused_tail(const float* xyz, float bound, const void* embeddings,
+                                                  int32_t emb_dtype, const int32_t* offsets, void* outputs, uint32_t B,
+                                                  const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
+                                                  uint32_t H, uint32_t gridtype, int32_t align_corners,
+                                                  uint32_t interp, void* state, float growth_factor,
+                                                  float backoff_factor, int32_t growth_interval,
+                                                  int32_t scaler_enabled, const float* loss_ray, uint32_t n_rays,
+                                                  int32_t n_nets, const void* const* mlp_weights,
+                                                  const uint32_t* in_dims, const uint32_t* hidden_dims,
+                                                  const uint32_t* num_layers, void* const* images, void* stream) {
+    if (int e = check_common(L, embeddings, offsets, outputs)) return e;
+    NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_forward_fused_tail: null xyz or bound <= 0");
+    NGP_REQUIRE(D == 3 && C == 2, NGP_ERR_UNSUPPORTED, "grid_encode_forward_fused_tail: D 3, C 2 only");
+    NGP_REQUIRE(emb_dtype == NGP_DTYPE_F32 || emb_dtype == NGP_DTYPE_F16, NGP_ERR_ARG,
+                "grid_encode_forward_fused_tail: emb_dtype %d (F32 or F16)", emb_dtype);
+    NGP_REQUIRE(!state || loss_ray, NGP_ERR_ARG, "grid_encode_forward_fused_tail: the bookkeeping needs loss_ray");
+    FwdTail ft{};
+    if (state) {
+        ft.end = static_cast<ngp_step::StepState*>(state);
+        ft.sa = ngp_step::ScalerArgs{growth_factor, backoff_factor, growth_interval, scaler_enabled,
+                                     n_rays ? 1.0f / (float)n_rays : 0.0f};
+        ft.loss_ray = loss_ray;
+        ft.n_rays = n_rays;
+    }
+    if (n_nets > 0)
+        if (int e = ngp_pack::build_jobs(n_nets, mlp_weights, in_dims, hidden_dims, num_layers, images, ft.jobs))
+            return e;
+    GridLevels lv;
+    make_levels(lv, L, S, H);
+    const InMap im{bound, 1.0f / (2.0f * bound), count};
+    const bool ac = align_corners != 0;
+    const bool gm = B >= kFwdGroupMajorMin;
+    const uint32_t kl = gm ? 1u : kFwdLevelsPerBlock;
+    const uint32_t nfwd = B ? 8u * (((L + 7) / 8 + kl - 1) / kl) * ngp_div_up(B, 128) : 0u;
+    const dim3 grid(nfwd + (ft.end ? 1u : 0u) + (uint32_t)ft.jobs.n);
+    if (grid.x == 0) return NGP_OK;
+    hipStream_t st = ngp_stream(stream);
+    ngp_half* o = static_cast<ngp_half*>(outputs);
+#define NGP_FWD_TAIL(E_)                                                                                          \
+    (gm ? k_grid_fwd_tail<ngp_half, E_, 3, 2, 1><<<grid, 256, 0, st>>>(xyz, static_cast<const E_*>(embeddings),   \
+                                                                        offsets, o, B, L, lv, gridtype, ac, interp, \
+                                                                        0, im, ft)                                  \
+        : k_grid_fwd_tail<ngp_half, E_, 3, 2><<<grid, 256, 0, st>>>(xyz, static_cast<const E_*>(embeddings), offsets, \
+                                                                     o, B, L, lv, gridtype, ac, interp, 0, im, ft))
+    if (emb_dtype == NGP_DTYPE_F16)
+        NGP_FWD_TAIL(ngp_half);
+    else
+        NGP_FWD_TAIL(float);
+#undef NGP_FWD_TAIL
+    return ngp_check_launch("grid_encode_forward_fused_tail");
 }
 
 extern "C" int ngp_grid_encode_forward_fused_sel(const float* xyz, float bound, const void* table0,

@@ -1463,7 +1463,7 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
     MarchEmit me{};
     if (ma && ma->st) {  // every CU gets a workgroup: the Adam waves sweep 1/gridDim of the parameters each
         const uint32_t rb = ngp_div_up(N, kMaxMarchBlocks);
-        if (tail && rb <= kEmitMaxBlockRays && march_emit_inline()) {
+        if (rb <= kEmitMaxBlockRays && march_emit_inline()) {
             uint8_t* sync = img + (occ_image_bytes(L) + occ_scratch_bytes(L) + 255) / 256 * 256;
             me = MarchEmit{reinterpret_cast<uint32_t*>(sync), reinterpret_cast<unsigned long long*>(sync + 256),
                            counter, xyzs, dirs, deltas, M, rb};
@@ -1475,6 +1475,7 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
             rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan, MarchAdam{},
             MarchEmit{});
     }
+    if (me.ticket && !tail) return ngp_check_launch("march_rays_train");  // emitted, no tail: one launch
     EmitTail et{};
     if (tail) et = *tail;
     et.groups = me.ticket ? 0u : groups;  // emitted in the march launch: the tail row alone
@@ -1597,9 +1598,12 @@ extern "C" int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const flo
                 "march_rays_train_prebuilt_adam: clear must be 16-byte aligned, a multiple of 16 bytes");
     ma.clear = static_cast<uint4*>(job->clear);
     ma.clear16 = job->clear ? job->clear_bytes / 16 : 0u;
+    // NGP_ADAM_JOB_TAIL_LATER: the bookkeeping and the packs ride in the next
+    // launch (ngp_grid_encode_forward_fused_tail)
+    const bool later = (job->flags & NGP_ADAM_JOB_TAIL_LATER) != 0;
     return march_train_impl(rays_o, rays_d, grid, bound, dt_gamma, max_steps, N, C, H, M, nears, fars,
                             xyzs, dirs, deltas, rays, counter, noises, workspace, workspace_bytes, false,
-                            stream, &tail, &ma);
+                            stream, later ? nullptr : &tail, &ma);
 }
 
 extern "C" int ngp_composite_rays_train_forward(const float* sigmas, const float* rgbs,

@@ -284,6 +284,13 @@ class FusedTrainer:
             j2.lr, j2.beta1, j2.beta2, j2.eps = self.lr, self.betas[0], self.betas[1], self.eps
             j2.iters, j2.zero_grads, j2.grad_mult = self.iters, 1, 1.0
             self._fwd_split = (8, j2)
+        # ... and (NGP_TAIL_IN_FWD, default on; with the Adam sweep whole in the
+        # march launch) the march launch emits its samples itself and leaves the
+        # bookkeeping + MLP packs row to the grid forward's launch: no emit launch
+        self._tail_in_fwd = (self._march_adam and self._fwd_split is None
+                             and os.environ.get("NGP_TAIL_IN_FWD", "1") != "0")
+        if self._tail_in_fwd:
+            self._job.flags |= nat.ADAM_JOB_TAIL_LATER
         # ... and the next batch is drawn while this step's grid backward runs
         # (a column of the bin launch; the batch buffers are dead once the
         # composite has read its targets), so the step starts with the march:
@@ -813,6 +820,14 @@ class FusedTrainer:
             chk(lib.ngp_grid_encode_forward_fused_adam(*fa, f, e.num_levels, None, None, P(self.state), 2.0, 0.5,
                                                        self.growth_interval, 1, P(self.loss_ray), N, s),
                 "grid_encode_forward_fused_end")
+        elif adam_split and self._tail_in_fwd:
+            # + the update's deferred bookkeeping and the MLP packs (the march
+            # launch emitted the samples and left its tail row to this launch)
+            chk(lib.ngp_grid_encode_forward_fused_tail(P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets),
+                                                       P(self.enc_out), M, cnt, *grid_args[:-1], P(self.state), 2.0,
+                                                       0.5, self.growth_interval, 1, P(self.loss_ray), N, 2, pk["w"],
+                                                       pk["ins"], pk["hid"], pk["nl"], pk["img"], s),
+                "grid_encode_forward_fused_tail")
         elif self.fused_adam:  # the current one of the double-buffered table
             chk(lib.ngp_grid_encode_forward_fused_sel(P(self.xyzs), float(m.bound), P(table), P(self.table_b),
                                                       self._table_sel, tdt, P(e.offsets), P(self.enc_out), M, cnt,
