@@ -508,8 +508,8 @@ def test_nerf_backward_half_chunks_equal_whole_chunks(cuda, count):
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
 def test_march_emit_in_launch_equals_emit_launch(cuda, bound, dt_gamma):
     """The march + Adam launch emits the samples itself (ticketed ray blocks,
-    block totals published as agent-scope words; NGP_MARCH_EMIT_INLINE,
-    default on): samples, rays, counter and the trained parameters equal the
+    block totals published as agent-scope words; NGP_MARCH_EMIT_INLINE=1):
+    samples, rays, counter and the trained parameters equal the
     separate emit launch's bit for bit, step after step."""
     import os
     _, _, _, a = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
@@ -541,9 +541,9 @@ def test_march_emit_in_launch_equals_emit_launch(cuda, bound, dt_gamma):
 
 def test_tail_in_grid_forward_equals_emit_tail(cuda):
     """The step's tail row (deferred scaler / LR / loss bookkeeping + MLP
-    fragment packs) in the grid forward's launch (NGP_TAIL_IN_FWD, default on:
-    the march is then one launch) against the tail row of the emit launch
-    (=0): parameters, moments and the step state bit for bit, eager and
+    fragment packs) in the grid forward's launch (NGP_TAIL_IN_FWD=1; with the
+    in-launch emit the march is then one launch) against the tail row of the
+    emit launch (=0): parameters, moments and the step state bit for bit, eager and
     captured, across an overflow-free run."""
     import os
     knob = os.environ.get("NGP_TAIL_IN_FWD")
