@@ -15,10 +15,13 @@ fi
 for probe in ${PROBES:-}; do
   timeout -k 10 200 python -u tools/$probe.py > $O/$probe.json 2> $O/$probe.err
 done
+# a knob "A+B" sets both A and B to the value
 for KNOB in $KNOBS; do
   for rep in 1 2; do
     for v in 0 1; do
-      env $KNOB=$v timeout -k 10 200 python -u bench.py --no-cpu --no-legs --no-dp-path --no-render --steps 200 \
+      ENVS=""
+      for K in ${KNOB//+/ }; do ENVS="$ENVS $K=$v"; done
+      env $ENVS timeout -k 10 200 python -u bench.py --no-cpu --no-legs --no-dp-path --no-render --steps 200 \
           > $O/ab_${KNOB}_${v}_${rep}.json 2> $O/ab_${KNOB}_${v}_${rep}.err
     done
   done
