@@ -1423,11 +1423,11 @@ extern "C" size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_
            256 * 256 + march_sync_bytes();
 }
 
-// The march + Adam launch emits the samples itself (MarchEmit) with
-// NGP_MARCH_EMIT_INLINE=1, unless a ray block would exceed kEmitMaxBlockRays.
+// The march + Adam launch emits the samples itself (MarchEmit) unless
+// NGP_MARCH_EMIT_INLINE=0 or a ray block would exceed kEmitMaxBlockRays.
 static bool march_emit_inline() {
     const char* e = getenv("NGP_MARCH_EMIT_INLINE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 static int march_train_impl(const float* rays_o, const float* rays_d, const uint8_t* grid,

@@ -284,12 +284,12 @@ class FusedTrainer:
             j2.lr, j2.beta1, j2.beta2, j2.eps = self.lr, self.betas[0], self.betas[1], self.eps
             j2.iters, j2.zero_grads, j2.grad_mult = self.iters, 1, 1.0
             self._fwd_split = (8, j2)
-        # ... and (NGP_TAIL_IN_FWD=1; with the Adam sweep whole in the march
-        # launch) the march launch leaves the bookkeeping + MLP packs row to the
-        # grid forward's launch; with NGP_MARCH_EMIT_INLINE=1 it also emits its
-        # samples itself: no emit launch
+        # ... and (with the Adam sweep whole in the march launch) the march
+        # launch emits its samples itself and leaves the bookkeeping + MLP packs
+        # row to the grid forward's launch: no emit launch (NGP_TAIL_IN_FWD=0:
+        # the tail row in the emit launch; NGP_MARCH_EMIT_INLINE=0: the emit launch)
         self._tail_in_fwd = (self._march_adam and self._fwd_split is None
-                             and os.environ.get("NGP_TAIL_IN_FWD", "0") == "1")
+                             and os.environ.get("NGP_TAIL_IN_FWD", "1") != "0")
         if self._tail_in_fwd:
             self._job.flags |= nat.ADAM_JOB_TAIL_LATER
         # ... and the next batch is drawn while this step's grid backward runs
