@@ -872,7 +872,9 @@ def density_update_times(model, bits, ft=None, reps=3):
 
 
 _PMC_KERNELS = {"grid_encode_backward": ("k_grid_bwd_bin", "k_grid_bin_accum"),
-                "grid_encode_forward": ("k_grid_fwd_pair",),
+                # the step's forward carries the tail (k_grid_fwd_tail); k_grid_fwd_pair
+                # also counts the density update's 2M-point queries
+                "grid_encode_forward": ("k_grid_fwd_tail",),
                 "march_rays_train+adam": ("void k_march_train<4u>", "k_march_emit")}
 
 

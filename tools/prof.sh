@@ -12,9 +12,11 @@ mkdir -p "$O"
 cd "$R"
 [ -n "${SKIP_TRACE:-}" ] || timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- \
     python3 bench.py --no-cpu --no-legs --no-dp-path --no-render ${BENCH_ARGS:-} --steps 30 --warmup 10 > "$O/trace.log" 2>&1
-# PMC passes on eager steps (--no-graph): the counters of graph-replayed dispatches
-# read a fraction of the bytes (r05j: the bin launch's writes 2-5 MB in replays
-# against 52-57 MB in the eager steps of the same run, for the same samples)
+# PMC passes on eager steps (--no-graph). The per-launch bytes follow the
+# training state: as the field trains, samples behind early-terminated rays get
+# a zero gradient and produce no grid-backward items (r05m: the bin launch
+# writes 52-59 MB in the first steps, 2-6 MB after a few hundred), and the
+# summary's median is over the whole run
 KRE='k_grid_bwd|k_grid_bin|k_grid_fwd|k_adam|k_mlp|k_nerf_fwd|k_nerf_bwd|k_march|k_composite|k_glue'
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex "$KRE" -d "$O/fetch" -o run -- \
     python3 bench.py --no-cpu --no-legs --no-dp-path --no-render ${BENCH_ARGS:-} --no-graph --steps 5 --warmup 3 --settle-steps 0 > "$O/fetch.log" 2>&1

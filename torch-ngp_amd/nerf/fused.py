@@ -297,11 +297,18 @@ class FusedTrainer:
         # composite has read its targets), so the step starts with the march:
         # no head launch. The march + Adam launch clears the bin cursors.
         # NGP_DRAW_AHEAD=0: the head launch draws the batch.
-        self._draw_ahead = (self._march_adam and not self._split_reduce
+        # Data parallel too (round 5): the bin launch draws the next batch, the
+        # step clears the bin cursors itself, and the deferred bookkeeping and the
+        # MLP packs ride in the grid forward's launch (_dp_tail): no head launch
+        # and no pack launch per step.
+        self._draw_ahead = ((self._march_adam or self.dp) and not self._split_reduce
                             and os.environ.get("NGP_DRAW_AHEAD", "1") != "0")
+        self._dp_tail = self.dp and os.environ.get("NGP_TAIL_IN_FWD", "1") != "0"
         self._ahead = False  # the batch buffers hold the next step's batch
-        if self._draw_ahead:
+        self._pre_ahead = None  # data parallel: the batch state the "pre" graph was captured in
+        if self._draw_ahead and self._march_adam:
             self._job.clear, self._job.clear_bytes = nat.ptr(self.grid_ws), self._grid_counter_bytes
+        if self._draw_ahead:
             m_, d_, bj = self.model, self.data, nat.BatchJob()
             bj.poses, bj.n_poses, bj.intrinsics4 = nat.ptr(d_.poses), d_.poses.shape[0], ctypes.addressof(self._intr)
             bj.H, bj.W, bj.N = d_.H, d_.W, self.N
@@ -821,6 +828,14 @@ class FusedTrainer:
             chk(lib.ngp_grid_encode_forward_fused_adam(*fa, f, e.num_levels, None, None, P(self.state), 2.0, 0.5,
                                                        self.growth_interval, 1, P(self.loss_ray), N, s),
                 "grid_encode_forward_fused_end")
+        elif self.dp and self._dp_tail:
+            # + the deferred bookkeeping of the shard update (when the head did
+            # not run it: batch drawn ahead) and the MLP packs of the gathered weights
+            chk(lib.ngp_grid_encode_forward_fused_tail(P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets),
+                                                       P(self.enc_out), M, cnt, *grid_args[:-1], P(self.state), 2.0,
+                                                       0.5, self.growth_interval, 1, P(self.loss_ray), N, 2, pk["w"],
+                                                       pk["ins"], pk["hid"], pk["nl"], pk["img"], s),
+                "grid_encode_forward_fused_tail")
         elif adam_split and self._tail_in_fwd:
             # + the update's deferred bookkeeping and the MLP packs (the march
             # launch emitted the samples and left its tail row to this launch)
@@ -839,7 +854,7 @@ class FusedTrainer:
                 "grid_encode_fused")
         self._tick("grid_encode_forward")
         sn, cn, img, pk = self.sig_net, self.col_net, self.mlp_img, self._pk
-        if self.dp:  # after the all-gather of the fp16 forward copy (see _sample)
+        if self.dp and not self._dp_tail:  # after the all-gather of the fp16 forward copy (see _sample)
             chk(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
         if self._one_fwd:  # both networks in one launch (ngp_nerf_forward)
             chk(lib.ngp_nerf_forward(P(self.enc_out), P(img[0]), P(img[1]), M, cnt, sn.hidden_dim, sn.num_layers,
@@ -959,12 +974,22 @@ class FusedTrainer:
         drawn and marched, the network (+ guard), the reduce-scatter."""
         self._optimizer(defer=True)
         work = self._gather_half(wait=False)
-        self._sample()
-        self._march()
+        self._dp_pre()
         if work is not None:
             work.wait()
-        self._network()
+        self._network(draw=self._draw_ahead)
         self._reduce()
+
+    def _dp_pre(self):
+        """Data parallel, before the all-gather is joined: the batch (drawn
+        ahead by the last backward: only the bin cursors are cleared; else the
+        head launch draws it) and the march."""
+        if self._ahead:
+            if self._grid_counter_bytes:
+                self.grid_ws[:self._grid_counter_bytes].zero_()
+        else:
+            self._sample()
+        self._march()
 
     def step(self):
         """One training iteration (the optimizer half lags by one step, see
@@ -980,7 +1005,7 @@ class FusedTrainer:
             else:
                 self._body(self._pending)
                 self.eager_steps += 1
-        elif self._dp_whole is not None and self._pending:
+        elif self._dp_whole is not None and self._pending and self._ahead == self._pre_ahead:
             self._dp_whole.replay()  # the whole step, collectives included (NGP_DP_GRAPH)
         else:
             g = self.graph if self._pending else None
@@ -991,17 +1016,18 @@ class FusedTrainer:
                 else:
                     self._optimizer(defer=True)
                 work = self._gather_half(wait=False)
+            if g and self._ahead != self._pre_ahead:  # captured in the other batch state
+                g = None
             if g:
                 g["pre"].replay()
             else:
-                self._sample()
-                self._march()
+                self._dp_pre()
             if work is not None:
                 work.wait()
             if g:
                 g["net"].replay()
             else:
-                self._network()
+                self._network(draw=self._draw_ahead)
             self._reduce()
         self._pending = True
         self.model.local_step += 1
@@ -1015,7 +1041,9 @@ class FusedTrainer:
         read-outs) the first iteration runs as step()."""
         g, S = self.graph_multi, self._multi
         if g is not None and (not self.dp or self._dp_whole is not None) and not self._ring:
-            if not self._pending and k > 0:
+            # single steps until the state is the graph's: an update pending
+            # (after a flush) and, data parallel, the batch state it was captured in
+            while k > 0 and (not self._pending or (self.dp and self._ahead != self._pre_ahead)):
                 self.step()
                 k -= 1
             for _ in range(k // S):
@@ -1096,6 +1124,7 @@ class FusedTrainer:
             # between them; multi=S: S steps per graph as in world 1)
             self._dp_whole = None
             self.graph_multi, self._multi = None, 1
+            self._pre_ahead = self._ahead  # the batch state the graph assumes (and leaves)
             try:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
@@ -1118,11 +1147,11 @@ class FusedTrainer:
             graphs = {k: torch.cuda.CUDAGraph() for k in ("opt", "pre", "net")}
             with torch.cuda.graph(graphs["opt"]):
                 self._optimizer(defer=True)
+            self._pre_ahead = self._ahead
             with torch.cuda.graph(graphs["pre"]):
-                self._sample()
-                self._march()
+                self._dp_pre()
             with torch.cuda.graph(graphs["net"]):
-                self._network()
+                self._network(draw=self._draw_ahead)
             self.graph = graphs
         # capture recorded the launches without running them: the pending
         # update is still pending and the next step() replays it first
