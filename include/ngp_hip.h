@@ -420,6 +420,15 @@ int ngp_grid_encode_backward_fused_reduce_batch(const void* grad, const float* x
                                                 const uint32_t* in_dims, const uint32_t* hidden_dims,
                                                 const uint32_t* num_layers, void* const* grad_weights,
                                                 int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream);
+/* ngp_grid_encode_backward_fused_reduce_batch over the rows live_rows[0 ..
+ * *live_count) (the sample rows of xyz and of the [L, B, C] grad). */
+int ngp_grid_encode_backward_fused_reduce_batch_live(
+    const void* grad, const float* xyz, float bound, const int32_t* offsets, void* grad_embeddings, uint32_t B,
+    const int32_t* live_rows, const int32_t* live_count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+    uint32_t gridtype, int32_t align_corners, uint32_t interp, const int32_t* offsets_host, void* workspace,
+    size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite, int32_t n_nets, void* const* mlp_workspaces,
+    const uint32_t* mlp_Bs, const uint32_t* in_dims, const uint32_t* hidden_dims, const uint32_t* num_layers,
+    void* const* grad_weights, int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream);
 /* Fused Adam over the hash table (world 1; torch.optim.Adam + GradScaler of
  * nerf/utils.py:975-978 / main_nerf.py:194 on the table, inside the grid
  * backward). The table's fp32 parameters and Adam moments are double
@@ -552,6 +561,15 @@ int ngp_nerf_backward(const void* g_color_out, const void* color_in, const void*
                       uint32_t hidden_dim, uint32_t num_layers, uint32_t hidden_dim_color,
                       uint32_t num_layers_color, void* sigma_workspace, size_t sigma_workspace_bytes,
                       void* color_workspace, size_t color_workspace_bytes, uint32_t* timing, void* stream);
+/* ngp_nerf_backward over the rows live_rows[0 .. *live_count) only (see
+ * ngp_nerf_composite_loss_live): input gradients are written for those rows,
+ * the others are left as they were. */
+int ngp_nerf_backward_live(const void* g_color_out, const void* color_in, const void* color_image, void* g_h,
+                           const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
+                           const int32_t* live_rows, const int32_t* live_count, uint32_t hidden_dim,
+                           uint32_t num_layers, uint32_t hidden_dim_color, uint32_t num_layers_color,
+                           void* sigma_workspace, size_t sigma_workspace_bytes, void* color_workspace,
+                           size_t color_workspace_bytes, uint32_t* timing, void* stream);
 /* Sums the deferred dW partials of n backward calls (same B and shapes as
  * those calls) into grad_weights[k], in one launch (n <= 4). nonfinite
  * (nullable): set to 1 when a written grad is inf/nan (GradScaler's check). */
@@ -582,6 +600,21 @@ int ngp_nerf_composite_loss(const float* sigma, const void* color_out, const voi
                             uint32_t gt_channels, const float* bg, void* state,
                             void* grad_color_out, void* grad_h_sigma, float* out_image,
                             float* out_ws, float* loss_ray, void* stream);
+/* ngp_nerf_composite_loss plus the step's live rows: every row whose written
+ * gradient (the colour logits' and the density's) is nonzero in some
+ * component, listed in ray order in live_rows [M] (live_total[0] of them);
+ * ray_rows [M] and live_cnt [N] are scratch (each ray's live rows in its own
+ * row range, and their count). The other rows' gradients are exactly zero, so
+ * the backwards may skip them (ngp_nerf_backward_live,
+ * ngp_grid_encode_backward_fused_reduce_batch_live): the products with a zero
+ * row are zeros (instant-ngp compacts its samples before the backward the same
+ * way). Two launches. */
+int ngp_nerf_composite_loss_live(const float* sigma, const void* color_out, const void* h_sigma,
+                                 const float* deltas, const int32_t* rays, uint32_t M, uint32_t N, float T_thresh,
+                                 float density_scale, const float* gt, uint32_t gt_channels, const float* bg,
+                                 void* state, void* grad_color_out, void* grad_h_sigma, float* out_image,
+                                 float* out_ws, float* loss_ray, int32_t* ray_rows, int32_t* live_cnt,
+                                 int32_t* live_rows, int32_t* live_total, void* stream);
 /* scaler_enabled of the optimizer entries: GradScaler off; on, with its inf
  * check as a sweep over the grads; on, with the check already made by the
  * kernels that wrote the grads into the state's flag (ngp_fused_inf_flag). */

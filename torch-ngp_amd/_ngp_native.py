@@ -52,6 +52,10 @@ SIGNATURES = {
                                                     c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz,
                                                     c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                     c_vp, c_vp],
+    "ngp_grid_encode_backward_fused_reduce_batch_live": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_vp,
+                                                         c_u32, c_u32, c_u32, c_f32, c_u32, c_u32, c_i32, c_u32,
+                                                         c_vp, c_vp, c_sz, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp,
+                                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "ngp_march_rays_train": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_composite_rays_train_forward": [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_vp, c_vp,
@@ -121,6 +125,8 @@ SIGNATURES = {
                                 c_vp, c_vp, c_i32, c_u32, c_vp, c_sz, c_vp],
     "ngp_nerf_backward": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_u32,
                           c_vp, c_sz, c_vp, c_sz, c_vp, c_vp],
+    "ngp_nerf_backward_live": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_u32, c_u32,
+                               c_u32, c_vp, c_sz, c_vp, c_sz, c_vp, c_vp],
     "ngp_ffmlp_reduce": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
     "ngp_fused_state_bytes": [],
     "ngp_fused_state_init": [c_vp, c_f32, c_vp],
@@ -130,6 +136,9 @@ SIGNATURES = {
     "ngp_nerf_glue_backward": [c_vp, c_vp, c_u32, c_vp, c_vp],
     "ngp_nerf_composite_loss": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
                                 c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_nerf_composite_loss_live": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
+                                     c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp],
     "ngp_fused_optimizer_step": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
                                  c_i32, c_i32, c_f32, c_f32, c_f32, c_i32, c_i32, c_u32, c_vp, c_vp,
                                  c_vp, c_vp, c_vp],

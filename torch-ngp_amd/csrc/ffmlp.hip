@@ -103,6 +103,9 @@ NGP_DEV void copy_frags(half8* __restrict__ lds, const half8* __restrict__ image
 // a row index that is always readable (rows past B read row B - 1 and the
 // caller zeroes the value): loads without branches, see copy_frags
 NGP_DEV uint32_t clamp_row(uint32_t row, uint32_t B) { return row < B ? row : (B ? B - 1 : 0u); }
+// A row list (the live rows of a step, see ngp_nerf_composite_loss_live): row r of
+// the B rows an MLP call processes is map[r]; null: r itself.
+NGP_DEV uint32_t map_row(const int32_t* map, uint32_t r) { return map ? (uint32_t)map[r] : r; }
 
 // Activation enum of ffmlp.py:89-96 / utils.h:29-37.
 enum Act : uint32_t { kReLU = 0, kExp = 1, kSine = 2, kSigmoid = 3, kSquareplus = 4, kSoftplus = 5, kNone = 6 };
@@ -236,7 +239,7 @@ NGP_DEV void pack_act(const f32x4 (&acc)[NB][MT], ACT act, half8 (&out)[NB][KS])
 // load a [rows, width] fp16 row-major block as natural-K B operands
 template <int KS, int NB>
 NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
-                       half8 (&out)[NB][KS]) {
+                       half8 (&out)[NB][KS], const int32_t* map = nullptr) {
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
@@ -245,7 +248,7 @@ NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_
         for (int s = 0; s < KS; ++s) {
             const uint32_t col = 32 * s + 8 * g;
             const bool ok = row < B && col < width;
-            const half8 v = *reinterpret_cast<const half8*>(src + (size_t)clamp_row(row, B) * width +
+            const half8 v = *reinterpret_cast<const half8*>(src + (size_t)map_row(map, clamp_row(row, B)) * width +
                                                             (col < width ? col : 0u));
             const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
             out[nb][s] = ok ? v : z;
@@ -255,10 +258,11 @@ NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_
 
 // First-layer input loaders (natural-K B operands).
 struct InRowMajor {  // [B, width] row-major
+    const int32_t* map = nullptr;  // row list, or null
     template <int KS, int NB>
     NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
                             half8 (&out)[NB][KS]) const {
-        load_rows<KS>(src, width, row0, B, out);
+        load_rows<KS>(src, width, row0, B, out, map);
     }
 };
 // [width / 2][ld][2]: column pairs stored pair-major, the hash grid's
@@ -267,6 +271,7 @@ struct InRowMajor {  // [B, width] row-major
 // group read 64 contiguous bytes per pair.
 struct InPairMajor {
     uint32_t ld;  // allocated rows
+    const int32_t* map = nullptr;  // row list, or null
     template <int KS, int NB>
     NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
                             half8 (&out)[NB][KS]) const {
@@ -278,7 +283,7 @@ struct InPairMajor {
             for (int s = 0; s < KS; ++s) {
                 const uint32_t col = 32 * s + 8 * g;
                 const bool ok = row < B && col < width;
-                const uint32_t rr = clamp_row(row, B), cc = col < width ? col : 0u;
+                const uint32_t rr = map_row(map, clamp_row(row, B)), cc = col < width ? col : 0u;
                 half8 v;
 #pragma unroll
                 for (int p = 0; p < 4; ++p) {
@@ -718,6 +723,7 @@ struct GiStore {
 
 struct GiNerfGeo {
     ngp_half* gh;
+    const int32_t* map = nullptr;  // row list, or null
     template <int IN_MT, int NB>
     NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t, const f32x4 (&t)[NB][IN_MT]) const {
         static_assert(IN_MT == 2, "the color network input is 32 wide");  // see launch_bwd
@@ -730,7 +736,7 @@ struct GiNerfGeo {
             const uint32_t pv = __shfl((uint32_t)__builtin_bit_cast(uint16_t, (ngp_half)t[nb][1][3]), lane - 16, 64);
             const uint32_t row = row0 + nb * 16 + c;
             if (row >= B) continue;
-            ngp_half* d = gh + (size_t)row * kOut + 4 * g;
+            ngp_half* d = gh + (size_t)map_row(map, row) * kOut + 4 * g;
             if (g == 0) {
                 d[1] = r0;
                 d[2] = r1;
@@ -746,6 +752,7 @@ struct GiNerfGeo {
 struct GiPairMajor {
     ngp_half* gi;
     uint32_t ld;
+    const int32_t* map = nullptr;  // row list, or null
     template <int IN_MT, int NB>
     NGP_DEV void operator()(uint32_t row0, uint32_t B, uint32_t in_dim, const f32x4 (&t)[NB][IN_MT]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
@@ -753,14 +760,15 @@ struct GiPairMajor {
         for (int nb = 0; nb < NB; ++nb) {
             const uint32_t row = row0 + nb * 16 + c;
             if (row >= B) continue;
+            const uint32_t pr = map_row(map, row);
 #pragma unroll
             for (int mt = 0; mt < IN_MT; ++mt) {
                 const uint32_t col = 16 * mt + 4 * g;
                 if (col >= in_dim) continue;
                 const uint32_t p = col / 2;
-                *reinterpret_cast<ngp_half2*>(gi + ((size_t)p * ld + row) * 2) =
+                *reinterpret_cast<ngp_half2*>(gi + ((size_t)p * ld + pr) * 2) =
                     ngp_half2{(ngp_half)t[nb][mt][0], (ngp_half)t[nb][mt][1]};
-                *reinterpret_cast<ngp_half2*>(gi + ((size_t)(p + 1) * ld + row) * 2) =
+                *reinterpret_cast<ngp_half2*>(gi + ((size_t)(p + 1) * ld + pr) * 2) =
                     ngp_half2{(ngp_half)t[nb][mt][2], (ngp_half)t[nb][mt][3]};
             }
         }
@@ -800,7 +808,7 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
     uint32_t chunk = map(0u);
     half8 xn[kNB][IN_KS], dn[kNB][1];
     xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
-    load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn);  // output activation ignored (ffmlp.cu:783)
+    load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn, xl.map);  // output activation ignored (ffmlp.cu:783)
     pre();
     MSTAMP(1);
     [[maybe_unused]] uint32_t nst = 0;
@@ -886,7 +894,7 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
         }
         const uint32_t next = map(kc);
         xl.template operator()<IN_KS>(inputs, in_dim, next * 16 * kNB, B, xn);
-        load_rows<1>(grad, kOut, next * 16 * kNB, B, dn);
+        load_rows<1>(grad, kOut, next * 16 * kNB, B, dn, xl.map);
         body(std::integral_constant<int, kNB>{}, row0, x, dout);
         MSTAMP(2 + min(nst, 9u));
         ++nst;
@@ -898,7 +906,7 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
     if (hrow != kNoHalf) {
         half8 x1[1][IN_KS], d1[1][1];
         xl.template operator()<IN_KS>(inputs, in_dim, hrow, B, x1);
-        load_rows<1>(grad, kOut, hrow, B, d1);
+        load_rows<1>(grad, kOut, hrow, B, d1, xl.map);
         asm volatile("" ::: "memory");  // after the last chunk's transposed reads
         const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint32_t lane = threadIdx.x & 63;
@@ -1018,6 +1026,7 @@ struct NerfBwdArgs {
     uint32_t np_color, np_sigma, B;
     const int32_t* count;
     uint32_t halves;  // split a last round of 1 or 2 chunks into 16-sample halves
+    const int32_t* rows;  // the rows to run (*count of them), or null: rows [0, *count)
     // the grid backward's timing ring (NGP_GRID_TIMING, include/ngp_hip.h), or
     // null: workgroup b stores its end (after its last store) in end slot
     // MAX_WG - 1 - b of the call the next bin launch opens (the accumulate's
@@ -1063,7 +1072,8 @@ k_nerf_bwd(NerfBwdArgs a) {
         return [=]() { return nf < n && slot < 2 * r ? (b + (nf + slot / 2) * G) * 16 * kNB + 16 * (slot & 1) : kNoHalf; };
     };
     bwd_phase<64, 1, NHC>(lds, reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes),
-                          reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{}, GiNerfGeo{a.g_h},
+                          reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{a.rows},
+                          GiNerfGeo{a.g_h, a.rows},
                           true, a.slab_color, a.np_color, B, 32u, ActReLU{}, map_of(w),
                           [&]() {
                               copy_frags<LC::FRAGS, kBwdThreads>(lds, a.color_image);
@@ -1074,8 +1084,8 @@ k_nerf_bwd(NerfBwdArgs a) {
     // and its fold images read before the sigma pass loads g_h and reuses LDS
     __syncthreads();
     bwd_phase<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
-                          InPairMajor{a.B}, GiPairMajor{a.g_enc, a.B}, true, a.slab_sigma, a.np_sigma, B, 32u,
-                          ActReLU{}, map_of(kBwdWaves - 1 - w), []() {}, half_of(kBwdWaves - 1 - w));
+                          InPairMajor{a.B, a.rows}, GiPairMajor{a.g_enc, a.B, a.rows}, true, a.slab_sigma, a.np_sigma,
+                          B, 32u, ActReLU{}, map_of(kBwdWaves - 1 - w), []() {}, half_of(kBwdWaves - 1 - w));
     if (a.timing && b < NGP_GRID_TIMING_MAX_WG / 4) {
         __syncthreads();
         if (threadIdx.x == 0)
@@ -1138,7 +1148,7 @@ NGP_DEV void bwd_phase_pair(const half8* __restrict__ fr, ngp_half* __restrict__
     uint32_t chunk = map(pair, 0u);
     half8 xn[1][IN_KS], dn[1][1];
     xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB + 16 * hf, B, xn);
-    load_rows<1>(grad, kOut, chunk * 16 * kNB + 16 * hf, B, dn);
+    load_rows<1>(grad, kOut, chunk * 16 * kNB + 16 * hf, B, dn, xl.map);
     pre();
 
     f32x4 dw_last[1][HM], dw_hid[NH][HM][N::MTW], dw_first[HM][N::IN_MT];
@@ -1160,7 +1170,7 @@ NGP_DEV void bwd_phase_pair(const half8* __restrict__ fr, ngp_half* __restrict__
         dout[0][0] = dn[0][0];
         const uint32_t next = map(pair, kc);
         xl.template operator()<IN_KS>(inputs, in_dim, next * 16 * kNB + 16 * hf, B, xn);
-        load_rows<1>(grad, kOut, next * 16 * kNB + 16 * hf, B, dn);
+        load_rows<1>(grad, kOut, next * 16 * kNB + 16 * hf, B, dn, xl.map);
         half8 h[NH + 1][1][N::KSW];
         f32x4 a[1][N::MTW];
         dense<N::MTW, IN_KS>(fr, fwd_desc<W, IN_KS, NH>(0, in_dim).frag0, x, a);
@@ -1280,8 +1290,8 @@ k_nerf_bwd_pair(NerfBwdArgs a) {
     // pair p's k-th chunk (colour) -- the one-wave kernel's deal with pairs in
     // place of waves; the sigma pass deals them in reverse pair order, so a
     // pair with an extra colour chunk has one sigma chunk less
-    bwd_phase_pair<64, 1, NHC>(lds, tiles, reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{},
-                               GiNerfGeo{a.g_h}, true, a.slab_color, a.np_color, B, 32u, ActReLU{},
+    bwd_phase_pair<64, 1, NHC>(lds, tiles, reinterpret_cast<float*>(lds), a.g_color_out, a.color_in,
+                               InRowMajor{a.rows}, GiNerfGeo{a.g_h, a.rows}, true, a.slab_color, a.np_color, B, 32u, ActReLU{},
                                [=](uint32_t p, uint32_t k) { return b + (p + k * (kPairWaves / 2)) * G; },
                                [&]() {
                                    copy_frags<LC::FRAGS, kPairThreads>(lds, a.color_image);
@@ -1290,7 +1300,8 @@ k_nerf_bwd_pair(NerfBwdArgs a) {
                                });
     __syncthreads();  // the colour pass's geo grads are stored and its fold images read
     bwd_phase_pair<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
-                               InPairMajor{a.B}, GiPairMajor{a.g_enc, a.B}, true, a.slab_sigma, a.np_sigma, B, 32u,
+                               InPairMajor{a.B, a.rows}, GiPairMajor{a.g_enc, a.B, a.rows}, true, a.slab_sigma,
+                               a.np_sigma, B, 32u,
                                ActReLU{},
                                [=](uint32_t p, uint32_t k) { return b + (kPairWaves / 2 - 1 - p + k * (kPairWaves / 2)) * G; },
                                []() {});
@@ -1623,12 +1634,13 @@ extern "C" int ngp_nerf_forward(const void* enc, const void* sigma_image, const 
  * workspaces (ngp_ffmlp_backward_workspace_bytes of each network) for
  * ngp_ffmlp_reduce, as NGP_FFMLP_DEFER_REDUCE. Input gradients equal the two
  * calls bit for bit; dW is summed in another order. */
-extern "C" int ngp_nerf_backward(const void* g_color_out, const void* color_in, const void* color_image,
-                                 void* g_h, const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
-                                 const int32_t* count, uint32_t hidden_dim, uint32_t num_layers,
-                                 uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
-                                 size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
-                                 uint32_t* timing, void* stream) {
+static int nerf_backward_impl(const void* g_color_out, const void* color_in, const void* color_image,
+                              void* g_h, const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
+                              const int32_t* count, const int32_t* rows, uint32_t hidden_dim, uint32_t num_layers,
+                              uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
+                              size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
+                              uint32_t* timing, void* stream) {
+    NGP_REQUIRE(!rows || count, NGP_ERR_ARG, "nerf_backward_live: a row list needs its count");
     NGP_REQUIRE(hidden_dim == 64 && hidden_dim_color == 64, NGP_ERR_UNSUPPORTED,
                 "nerf_backward: 64-wide networks only on this build, got %u / %u", hidden_dim, hidden_dim_color);
     NGP_REQUIRE(num_layers >= 2 && num_layers <= 3 && num_layers_color >= 2 && num_layers_color <= 3,
@@ -1659,6 +1671,7 @@ extern "C" int ngp_nerf_backward(const void* g_color_out, const void* color_in, 
     a.count = count;
     a.timing = timing;
     a.halves = mlp_bwd_halves_enabled() ? 1u : 0u;
+    a.rows = rows;
     hipStream_t st = ngp_stream(stream);
     const uint32_t key = (num_layers - 1) * 8 + (num_layers_color - 1);
     switch (key) {
@@ -1667,6 +1680,29 @@ extern "C" int ngp_nerf_backward(const void* g_color_out, const void* color_in, 
         case 2 * 8 + 1: return launch_nerf_bwd<2, 1>(a, st);
         default: return launch_nerf_bwd<2, 2>(a, st);
     }
+}
+
+extern "C" int ngp_nerf_backward(const void* g_color_out, const void* color_in, const void* color_image,
+                                 void* g_h, const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
+                                 const int32_t* count, uint32_t hidden_dim, uint32_t num_layers,
+                                 uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
+                                 size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
+                                 uint32_t* timing, void* stream) {
+    return nerf_backward_impl(g_color_out, color_in, color_image, g_h, enc, sigma_image, g_enc, B, count, nullptr,
+                              hidden_dim, num_layers, hidden_dim_color, num_layers_color, sigma_workspace,
+                              sigma_workspace_bytes, color_workspace, color_workspace_bytes, timing, stream);
+}
+
+extern "C" int ngp_nerf_backward_live(const void* g_color_out, const void* color_in, const void* color_image,
+                                      void* g_h, const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
+                                      const int32_t* live_rows, const int32_t* live_count, uint32_t hidden_dim,
+                                      uint32_t num_layers, uint32_t hidden_dim_color, uint32_t num_layers_color,
+                                      void* sigma_workspace, size_t sigma_workspace_bytes, void* color_workspace,
+                                      size_t color_workspace_bytes, uint32_t* timing, void* stream) {
+    NGP_REQUIRE(live_rows && live_count, NGP_ERR_ARG, "nerf_backward_live: null row list or count");
+    return nerf_backward_impl(g_color_out, color_in, color_image, g_h, enc, sigma_image, g_enc, B, live_count,
+                              live_rows, hidden_dim, num_layers, hidden_dim_color, num_layers_color, sigma_workspace,
+                              sigma_workspace_bytes, color_workspace, color_workspace_bytes, timing, stream);
 }
 
 extern "C" int ngp_nerf_density_forward(const void* inputs, const void* weights, const void* image, uint32_t B,

@@ -109,7 +109,10 @@ struct InMap {
     // double-buffered table (fused Adam): grid = *sel ? alt : grid
     const void* alt = nullptr;
     const int32_t* sel = nullptr;
+    // backward over a row list (the step's live rows): row b is rows[b], b < *count
+    const int32_t* rows = nullptr;
 };
+NGP_DEV uint32_t phys_row(const InMap& m, uint32_t b) { return m.rows ? (uint32_t)m.rows[b] : b; }
 template <typename E>
 NGP_DEV const E* select_table(const E* grid, const InMap& m) {
     return m.sel && *m.sel ? static_cast<const E*>(m.alt) : grid;
@@ -547,10 +550,11 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
     const int lane = (int)(threadIdx.x & 63);
 
     bool valid = b < rows_of(B, im);
+    const uint32_t pb = valid ? phys_row(im, b) : 0u;  // the sample's row
     float x[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; d++) {
-        x[d] = valid ? inputs[(size_t)b * D + d] : 0.5f;
+        x[d] = valid ? inputs[(size_t)pb * D + d] : 0.5f;
         if (valid && im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
         if (x[d] < 0 || x[d] > 1) valid = false;  // grad is zero-initialised
     }
@@ -575,8 +579,8 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 
     F gcur[C];
     if (valid) {
-        const T* gp = grad_layout == 0 ? grad + ((size_t)level * B + b) * C
-                                       : grad + ((size_t)b * L + level) * C;
+        const T* gp = grad_layout == 0 ? grad + ((size_t)level * B + pb) * C
+                                       : grad + ((size_t)pb * L + level) * C;
         load_entry<T, C>(gp, gcur);
     } else {
 #pragma unroll
@@ -841,7 +845,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // the sample's coordinates and this level's grad are loaded together (the
     // grad of an out-of-bounds sample is discarded below): loads gated on the
     // previous coordinate's bounds check went out one round trip at a time
-    const uint32_t bl = in_rows ? b : 0u;
+    const uint32_t bl = in_rows ? phys_row(im, b) : 0u;  // the sample's row
     float x[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; d++) x[d] = inputs[(size_t)bl * D + d];
@@ -2211,7 +2215,7 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
                    uint32_t gridtype, int32_t align_corners, uint32_t interp, const int32_t* offsets_host,
                    void* workspace, size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
                    const AccAdam& ad, void* stream, const ngp_reduce::ReduceJobs* rj = nullptr,
-                   uint32_t nred = 0, const BinLego* blp = nullptr) {
+                   uint32_t nred = 0, const BinLego* blp = nullptr, const int32_t* rows = nullptr) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
     const bool zeroed = (grad_layout & NGP_GRID_GRAD_ZEROED) != 0;
     const bool external = (grad_layout & NGP_GRID_CURSORS_EXTERNAL) != 0;
@@ -2225,7 +2229,8 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
     if (B == 0) return NGP_OK;
     GridLevels lv;
     make_levels(lv, L, S, H);
-    const InMap im{bound, 1.0f / (2.0f * bound), count};
+    InMap im{bound, 1.0f / (2.0f * bound), count};
+    im.rows = rows;
     hipStream_t st = ngp_stream(stream);
     const bool ac = align_corners != 0;
     BinPlan bp{};
@@ -2364,13 +2369,13 @@ extern "C" int ngp_grid_encode_backward_fused_reduce(const void* grad, const flo
                           AccAdam{}, stream, &rj, nred);
 }
 
-extern "C" int ngp_grid_encode_backward_fused_reduce_batch(
+static int reduce_batch_impl(
     const void* grad, const float* xyz, float bound, const int32_t* offsets, void* grad_embeddings, uint32_t B,
     const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
     int32_t align_corners, uint32_t interp, const int32_t* offsets_host, void* workspace, size_t workspace_bytes,
     int32_t grad_layout, int32_t* nonfinite, int32_t n_nets, void* const* mlp_workspaces, const uint32_t* mlp_Bs,
     const uint32_t* in_dims, const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* grad_weights,
-    int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream) {
+    int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream, const int32_t* rows) {
     NGP_REQUIRE(job && job->state && job->counter && job->poses && job->N > 0 && job->n_poses > 0, NGP_ERR_ARG,
                 "grid_encode_backward_fused_reduce_batch: incomplete batch job");
     NGP_REQUIRE(job->nboxes >= 0 && job->nboxes <= ngp_head::kMaxBoxes, NGP_ERR_ARG,
@@ -2403,11 +2408,38 @@ extern "C" int ngp_grid_encode_backward_fused_reduce_batch(
             return e;
         return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                               align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout,
-                              nonfinite, AccAdam{}, stream, nullptr, 0, &bl);
+                              nonfinite, AccAdam{}, stream, nullptr, 0, &bl, rows);
     }
     return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                           align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
-                          AccAdam{}, stream, &rj, nred, &bl);
+                          AccAdam{}, stream, &rj, nred, &bl, rows);
+}
+
+extern "C" int ngp_grid_encode_backward_fused_reduce_batch(
+    const void* grad, const float* xyz, float bound, const int32_t* offsets, void* grad_embeddings, uint32_t B,
+    const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
+    int32_t align_corners, uint32_t interp, const int32_t* offsets_host, void* workspace, size_t workspace_bytes,
+    int32_t grad_layout, int32_t* nonfinite, int32_t n_nets, void* const* mlp_workspaces, const uint32_t* mlp_Bs,
+    const uint32_t* in_dims, const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* grad_weights,
+    int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream) {
+    return reduce_batch_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
+                             align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
+                             n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims, num_layers, grad_weights,
+                             mlp_nonfinite, job, stream, nullptr);
+}
+
+extern "C" int ngp_grid_encode_backward_fused_reduce_batch_live(
+    const void* grad, const float* xyz, float bound, const int32_t* offsets, void* grad_embeddings, uint32_t B,
+    const int32_t* live_rows, const int32_t* live_count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
+    uint32_t gridtype, int32_t align_corners, uint32_t interp, const int32_t* offsets_host, void* workspace,
+    size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite, int32_t n_nets, void* const* mlp_workspaces,
+    const uint32_t* mlp_Bs, const uint32_t* in_dims, const uint32_t* hidden_dims, const uint32_t* num_layers,
+    void* const* grad_weights, int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream) {
+    NGP_REQUIRE(live_rows && live_count, NGP_ERR_ARG, "grid_encode_backward_fused_reduce_batch_live: null row list");
+    return reduce_batch_impl(grad, xyz, bound, offsets, grad_embeddings, B, live_count, D, C, L, S, H, gridtype,
+                             align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
+                             n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims, num_layers, grad_weights,
+                             mlp_nonfinite, job, stream, live_rows);
 }
 
 extern "C" int ngp_grid_encode_backward_fused_adam(const void* grad, const float* xyz, float bound,

@@ -199,7 +199,8 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
                  const float* __restrict__ gt, const float* __restrict__ bg, LossArgs la,
                  StepState* __restrict__ st, ngp_half* __restrict__ grad_color_out,
                  ngp_half* __restrict__ grad_h, float* __restrict__ out_image,
-                 float* __restrict__ out_ws, float* __restrict__ loss_ray) {
+                 float* __restrict__ out_ws, float* __restrict__ loss_ray, int32_t* __restrict__ ray_rows,
+                 int32_t* __restrict__ live_cnt) {
     typedef _Float16 half8 __attribute__((ext_vector_type(8)));
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t n = blockIdx.x * kLossWaves + (threadIdx.x >> 6);
@@ -293,6 +294,7 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
 
     // ---- backward (composite_rays_train_backward) + activation backward
     if (!valid) {
+        if (live_cnt && lane == 0) live_cnt[n] = 0;
         // a ray dropped for overflowing M still owns rows [offset, M): zero their grads
         for (uint32_t k = offset + lane; k < min(offset + num_steps, M); k += 64) {
             const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -304,6 +306,7 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     }
     float S = 0.0f, tacc = 0.0f, rr = 0, rg = 0, rb = 0, rd = 0;
     bool stopped = false;
+    uint32_t nlive = 0;  // rows of this ray with a nonzero gradient so far (listed in ray_rows)
     for (uint32_t base = 0; base < num_steps; base += 64) {
         bool stop = false;
         Chunk c{};
@@ -337,6 +340,7 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
         const float pb = rb + scan_incl(c.w * c.c2, lane);
         const float pd = rd + scan_incl(c.w * c.t, lane);
         rr = lane63(pr); rg = lane63(pg); rb = lane63(pb); rd = lane63(pd);
+        bool lv = false;
         if (c.ok) {
             const uint32_t i = offset + base + lane;
             float gc0 = 0, gc1 = 0, gc2 = 0, gs = 0;
@@ -355,9 +359,66 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
             go[0] = o0;
             go[1] = o1;
             // sigmas = ds * trunc_exp(h0): grad_h0 = (gs * ds) * exp(clamp(h0, -15, 15)), -> half
-            grad_h[(size_t)i * 16] = ngp_f2h((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
+            const ngp_half gh0 = ngp_f2h((gs * la.density_scale) * expf(fminf(fmaxf(h0, -15.0f), 15.0f)));
+            grad_h[(size_t)i * 16] = gh0;
+            // a row whose gradient is zero in every component contributes
+            // nothing to any weight or table gradient (the backward's products
+            // with it are zeros): the others are listed below, in ray order
+            lv = (float)o0[0] != 0.0f || (float)o0[1] != 0.0f || (float)o0[2] != 0.0f || (float)gh0 != 0.0f;
+        }
+        if (ray_rows) {  // every lane of the wave takes part
+            const uint64_t m = __ballot(lv);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (lv) ray_rows[offset + nlive + below] = (int32_t)(offset + base + lane);
+            nlive += (uint32_t)__popcll(m);
         }
         stopped = stopped || stop;
+    }
+    if (live_cnt && lane == 0) live_cnt[n] = (int32_t)nlive;
+}
+
+// The live rows of a step as one list in ray order: each workgroup sums the
+// live counts of every ray before its block of rays (all N counts are read by
+// every workgroup: a few KB from L2), then copies its rays' rows from their
+// per-ray slots; block 0 writes the total.
+constexpr uint32_t kLiveThreads = 256, kLiveRaysPerBlock = 64;
+__global__ void __launch_bounds__(kLiveThreads)
+k_live_compact(const int32_t* __restrict__ rays, const int32_t* __restrict__ live_cnt, const int32_t* __restrict__ ray_rows,
+               uint32_t N, int32_t* __restrict__ live_rows, int32_t* __restrict__ live_total) {
+    __shared__ uint32_t wsum[kLiveThreads / 64];
+    __shared__ uint32_t s_off[kLiveRaysPerBlock + 1];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t r0 = blockIdx.x * kLiveRaysPerBlock, r1 = min(N, r0 + kLiveRaysPerBlock);
+    // sum of the counts of rays [0, r0) (and, block 0: of all rays)
+    const uint32_t upto = blockIdx.x == 0 ? N : r0;
+    uint32_t part = 0;
+    for (uint32_t i = t; i < upto; i += kLiveThreads) part += (uint32_t)live_cnt[i];
+#pragma unroll
+    for (uint32_t o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (lane == 0) wsum[wv] = part;
+    __syncthreads();
+    const uint32_t before = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (blockIdx.x == 0 && t == 0) *live_total = (int32_t)before;
+    // this block's rays: exclusive offsets (one wave)
+    if (wv == 0) {
+        const uint32_t r = r0 + lane;
+        const uint32_t c = r < r1 ? (uint32_t)live_cnt[r] : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+        }
+        s_off[lane] = (blockIdx.x == 0 ? 0u : before) + incl - c;
+        if (lane == 63) s_off[64] = (blockIdx.x == 0 ? 0u : before) + incl;
+    }
+    __syncthreads();
+    // copy: a wave per ray
+    for (uint32_t r = r0 + wv; r < r1; r += kLiveThreads / 64) {
+        const uint32_t dst = s_off[r - r0], cnt = s_off[r - r0 + 1] - dst;
+        const uint32_t src = (uint32_t)rays[(size_t)r * 3 + 1];
+        for (uint32_t k = lane; k < cnt; k += 64) live_rows[dst + k] = ray_rows[src + k];
     }
 }
 
@@ -634,8 +695,40 @@ extern "C" int ngp_nerf_composite_loss(const float* sigma, const void* color_out
     k_composite_loss<<<ngp_div_up(N, kLossWaves), kLossWaves * 64, 0, ngp_stream(stream)>>>(
         sigma, (const ngp_half*)color_out, (const ngp_half*)h_sigma, deltas, rays, M, N, gt, bg, la,
         static_cast<StepState*>(state), (ngp_half*)grad_color_out, (ngp_half*)grad_h_sigma, out_image,
-        out_ws, loss_ray);
+        out_ws, loss_ray, nullptr, nullptr);
     return ngp_check_launch("nerf_composite_loss");
+}
+
+extern "C" int ngp_nerf_composite_loss_live(const float* sigma, const void* color_out, const void* h_sigma,
+                                            const float* deltas, const int32_t* rays, uint32_t M, uint32_t N,
+                                            float T_thresh, float density_scale, const float* gt,
+                                            uint32_t gt_channels, const float* bg, void* state,
+                                            void* grad_color_out, void* grad_h_sigma, float* out_image,
+                                            float* out_ws, float* loss_ray, int32_t* ray_rows, int32_t* live_cnt,
+                                            int32_t* live_rows, int32_t* live_total, void* stream) {
+    NGP_REQUIRE(loss_ray, NGP_ERR_ARG, "composite_loss_live: loss_ray [N] buffer required");
+    NGP_REQUIRE(gt_channels == 3 || gt_channels == 4, NGP_ERR_ARG, "composite_loss_live: gt must be RGB or RGBA");
+    NGP_REQUIRE(ray_rows && live_cnt && live_rows && live_total, NGP_ERR_ARG,
+                "composite_loss_live: null ray_rows [M] / live_cnt [N] / live_rows [M] / live_total");
+    hipStream_t st = ngp_stream(stream);
+    if (N == 0) {
+        if (hipMemsetAsync(live_total, 0, sizeof(int32_t), st) != hipSuccess)
+            return ngp_set_error(NGP_ERR_HIP, "composite_loss_live: memset failed");
+        return NGP_OK;
+    }
+    LossArgs la;
+    la.T_thresh = T_thresh;
+    la.density_scale = density_scale;
+    la.inv_n = 1.0f / (float)N;
+    la.inv_c = 1.0f / 3.0f;
+    la.gt_channels = gt_channels;
+    k_composite_loss<<<ngp_div_up(N, kLossWaves), kLossWaves * 64, 0, st>>>(
+        sigma, (const ngp_half*)color_out, (const ngp_half*)h_sigma, deltas, rays, M, N, gt, bg, la,
+        static_cast<StepState*>(state), (ngp_half*)grad_color_out, (ngp_half*)grad_h_sigma, out_image,
+        out_ws, loss_ray, ray_rows, live_cnt);
+    k_live_compact<<<ngp_div_up(N, kLiveRaysPerBlock), kLiveThreads, 0, st>>>(rays, live_cnt, ray_rows, N, live_rows,
+                                                                              live_total);
+    return ngp_check_launch("nerf_composite_loss_live");
 }
 
 extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* const* grads,

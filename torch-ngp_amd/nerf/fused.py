@@ -319,6 +319,18 @@ class FusedTrainer:
             bj.nears, bj.fars, bj.noises = nat.ptr(self.nears), nat.ptr(self.fars), nat.ptr(self.noises)
             bj.counter, bj.step_counter = nat.ptr(self.counter), nat.ptr(m_.step_counter)
             self._batch_job = bj
+        # the backwards over the live rows only (NGP_LIVE_ROWS=1): rows whose
+        # gradient the composite left zero in every component (behind a ray's
+        # early termination, or underflowed to zero in fp16) are skipped by the
+        # MLP and grid backwards, as instant-ngp compacts its samples before
+        # the backward; needs the one-launch MLP backward and the draw-ahead
+        # bin launch (where the list is consumed)
+        self._live = (os.environ.get("NGP_LIVE_ROWS", "0") == "1" and self._one_bwd and self._draw_ahead
+                      and not self.fused_adam and not self._split_reduce)
+        if self._live:
+            i32 = torch.int32
+            self._live_bufs = dict(ray_rows=z(M, dtype=i32), cnt=z(N, dtype=i32), rows=z(M, dtype=i32),
+                                   total=z(4, dtype=i32))
         self.graph = None
         self.graph_multi, self._multi = None, 1  # capture(multi=S): S step bodies in one graph
         # data parallel over RCCL: the whole step is captured, collectives included
@@ -871,18 +883,39 @@ class FusedTrainer:
                                            cn.hidden_dim, cn.num_layers, _RELU, _NONE, P(self.color_out), s),
                 "color_mlp")
             self._tick("ffmlp_forward_color")
-        chk(lib.ngp_nerf_composite_loss(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
-                                        P(self.rays), M, N, self.T_thresh, float(m.density_scale),
-                                        P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
-                                        P(self.g_h), None, None, P(self.loss_ray), s), "composite_loss")
+        # the live rows (a nonzero gradient) listed by the composite: both
+        # backwards then run over them only (the other rows' products are zeros)
+        live = self._live and draw
+        if live:
+            lv = self._live_bufs
+            chk(lib.ngp_nerf_composite_loss_live(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
+                                                 P(self.rays), M, N, self.T_thresh, float(m.density_scale),
+                                                 P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
+                                                 P(self.g_h), None, None, P(self.loss_ray), P(lv["ray_rows"]),
+                                                 P(lv["cnt"]), P(lv["rows"]), P(lv["total"]), s),
+                "composite_loss_live")
+        else:
+            chk(lib.ngp_nerf_composite_loss(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
+                                            P(self.rays), M, N, self.T_thresh, float(m.density_scale),
+                                            P(self.rgba), 4, P(self.bg), P(self.state), P(self.g_color_out),
+                                            P(self.g_h), None, None, P(self.loss_ray), s), "composite_loss")
         self._tick("composite_loss")
         if self._one_bwd:  # both networks' backward in one launch (ngp_nerf_backward)
-            chk(lib.ngp_nerf_backward(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
-                                      P(self.enc_out), P(img[0]), P(self.g_enc), M, cnt, sn.hidden_dim,
-                                      sn.num_layers, cn.hidden_dim, cn.num_layers, P(self.mlp_ws[0]),
-                                      self.mlp_ws[0].numel(), P(self.mlp_ws[1]), self.mlp_ws[1].numel(),
-                                      P(self.grid_ws) + self._grid_timing_at if self._grid_timing_at else None, s),
-                "nerf_backward")
+            timing = P(self.grid_ws) + self._grid_timing_at if self._grid_timing_at else None
+            if live:
+                chk(lib.ngp_nerf_backward_live(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
+                                               P(self.enc_out), P(img[0]), P(self.g_enc), M, P(lv["rows"]),
+                                               P(lv["total"]), sn.hidden_dim, sn.num_layers, cn.hidden_dim,
+                                               cn.num_layers, P(self.mlp_ws[0]), self.mlp_ws[0].numel(),
+                                               P(self.mlp_ws[1]), self.mlp_ws[1].numel(), timing, s),
+                    "nerf_backward_live")
+            else:
+                chk(lib.ngp_nerf_backward(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
+                                          P(self.enc_out), P(img[0]), P(self.g_enc), M, cnt, sn.hidden_dim,
+                                          sn.num_layers, cn.hidden_dim, cn.num_layers, P(self.mlp_ws[0]),
+                                          self.mlp_ws[0].numel(), P(self.mlp_ws[1]), self.mlp_ws[1].numel(),
+                                          timing, s),
+                    "nerf_backward")
             self._tick("ffmlp_backward")
         else:
             self._mlp_backward_split(lib, P, s, M, cnt, img)
@@ -918,6 +951,17 @@ class FusedTrainer:
                     "grid_backward_fused_adam")
             else:
                 chk(lib.ngp_grid_encode_backward_fused(*bargs, s), "grid_backward_fused")
+        elif draw and self._live:
+            # over the live rows (the MLP backward wrote g_enc for those only)
+            lv = self._live_bufs
+            largs = (P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets), P(self.grads[0]), M, P(lv["rows"]),
+                     P(lv["total"]), *grid_args[:-1], self._offsets_host, P(self.grid_ws), self.grid_ws.numel(),
+                     self._grid_flags, self._inf_flag)
+            chk(lib.ngp_grid_encode_backward_fused_reduce_batch_live(*largs, 2, pk["ws"], pk["B"], pk["ins"],
+                                                                     pk["hid"], pk["nl"], pk["gw"], self._inf_flag,
+                                                                     ctypes.byref(self._batch_job), s),
+                "grid_backward_fused_reduce_batch_live")
+            self._ahead = True
         elif draw:
             # + the next step's batch, as another column of the bin launch
             chk(lib.ngp_grid_encode_backward_fused_reduce_batch(*bargs, 2, pk["ws"], pk["B"], pk["ins"], pk["hid"],
