@@ -573,6 +573,59 @@ def test_tail_in_grid_forward_equals_emit_tail(cuda):
         assert torch.equal(x, y)
 
 
+def test_live_row_backwards_equal_all_row_backwards(cuda):
+    """The backwards over the live rows only (NGP_LIVE_ROWS=1: the composite
+    lists the rows with a nonzero gradient, the MLP backward and the grid bin
+    kernel walk that list) against the backwards over every row (=0): the loss
+    and the encoding gradient of each live row bit for bit, the grid gradient
+    bit for bit (dead rows add exact zeros, live rows keep their order), the
+    MLP weight gradients to fp16-accumulation tolerance (other 32-row chunks);
+    then eager and captured runs stay within tolerance of each other."""
+    import os
+    knob = os.environ.get("NGP_LIVE_ROWS")
+    try:
+        os.environ["NGP_LIVE_ROWS"] = "1"
+        _, _, _, a = _setup(cuda)
+        os.environ["NGP_LIVE_ROWS"] = "0"
+        _, _, _, b = _setup(cuda)
+    finally:
+        if knob is None:
+            os.environ.pop("NGP_LIVE_ROWS", None)
+        else:
+            os.environ["NGP_LIVE_ROWS"] = knob
+    assert a._live and not b._live
+    a.step()
+    b.step()
+    torch.cuda.synchronize()
+    n = a.sample_count()
+    assert n > 0 and n == b.sample_count()
+    lv = a._live_bufs
+    total = int(lv["total"][0])
+    rows = lv["rows"][:total].long()
+    gh, gc = b.g_h[:n].float(), b.g_color_out[:n].float()
+    live_ref = torch.nonzero((gh != 0).any(dim=1) | (gc != 0).any(dim=1)).flatten()
+    assert 0 < total <= n
+    assert torch.equal(torch.sort(rows).values, live_ref), (total, live_ref.numel())
+    ea, eb = a.g_enc.view(16, -1, 2), b.g_enc.view(16, -1, 2)
+    assert torch.equal(ea[:, rows].view(torch.int16), eb[:, rows].view(torch.int16))
+    assert torch.equal(a.grads[0].view(torch.int16) if a.grads[0].dtype == torch.float16 else a.grads[0],
+                       b.grads[0].view(torch.int16) if b.grads[0].dtype == torch.float16 else b.grads[0])
+    for x, y in zip(a.grads[1:], b.grads[1:]):
+        x, y = x.float(), y.float()
+        assert torch.isfinite(x).all() and _rel(x, y) < 1e-3, _rel(x, y)
+    assert a.last_loss == b.last_loss  # (flushes: after the gradient checks)
+    for t in (a, b):
+        for _ in range(3):
+            t.step()
+        t.capture(warmup=1, multi=4)
+        t.run(9)
+        t.flush()
+    torch.cuda.synchronize()
+    for x, y in zip(a.params, b.params):
+        assert torch.isfinite(x).all() and _rel(x.detach(), y.detach()) < 1e-3, _rel(x.detach(), y.detach())
+    assert abs(a.last_loss - b.last_loss) <= 1e-3 * abs(b.last_loss)
+
+
 def test_grad_guard_poisons_every_shard(cuda):
     """ngp_grad_guard (data-parallel GradScaler guard): an inf/nan anywhere in
     the rank's gradient puts a NaN at the head of every rank's chunk; a finite
