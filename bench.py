@@ -195,6 +195,9 @@ def main():
     spr = result["config"]["samples_per_step"] / args.num_rays
     result["samples_per_ray"] = round(spr, 2)
     result["samples_per_s"] = round(result["value"] * spr, 1)
+    if args.engine == "fused" and ft.live_fraction() is not None:
+        # the backwards walk only these rows (the rest carry a zero gradient)
+        result["live_rows_frac"] = round(ft.live_fraction(), 4)
     if world == 1 and args.engine == "fused":
         ft.flush()
         if args.render:
@@ -550,16 +553,18 @@ def adam_bytes(ft):
     return int((28 if ft.table32 else 30) * n_tab + 30 * n_mlp)
 
 
-def launch_bytes(ft, samples, rays):
+def launch_bytes(ft, samples, rays, live=None):
     """SURVEY §8(d) per-unit bytes of each launch of the world-1 step body
-    (timed_body_steps names): None for the MFMA-bound MLP launches. With the
+    (timed_body_steps names): None for the MFMA-bound MLP launches. The grid
+    backward's 1,100 B are per LIVE sample when the backwards walk only the
+    rows with a nonzero gradient (NGP_LIVE_ROWS; `live` = their count). With the
     grid forward split in two launches (NGP_ADAM_UNDER_FWD), the table values
     past the split level are swept by the first one: its bytes are those
     values' Adam bytes plus its levels' share of the forward's 588 B / sample
     (12 B of coordinates + 36 B per level)."""
     march = 48 * rays + 32 * samples
     out = {"march_rays_train+adam": adam_bytes(ft) + march, "march_rays_train": march,
-           "step_head": None, "grid_encode_forward": 588 * samples, "grid_encode_backward": 1100 * samples,
+           "step_head": None, "grid_encode_forward": 588 * samples, "grid_encode_backward": 1100 * (samples if live is None else live),
            "composite_loss": (32 + 52) * rays + (24 + 40) * samples, "ffmlp_forward": None, "ffmlp_backward": None}
     split = getattr(ft, "_fwd_split", None)
     if split is not None:
@@ -656,20 +661,21 @@ def grid_roofline(grid_clock, steps, workload):
             "launch_ms_min_median_max": [round(float(v), 5) for v in (min(ms), np.median(ms), max(ms))]}
 
 
-def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload):
+def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload, live=None):
     """The step's longest launch (over all launches of the body, timed with
     HIP events between the launches of eager body steps on the launch stream,
     the sample counts of those same steps): its algorithmic bytes (SURVEY
     §8(d)) over its mean duration. World 1 that is the march launch carrying
     the previous step's Adam; `adam_bytes_frac` is Adam's share of its bytes."""
     S = float(np.mean(counts))
-    nbytes = launch_bytes(ft, S, rays)
+    nbytes = launch_bytes(ft, S, rays, live)
     dom = max(kernel_ms, key=lambda k: kernel_ms[k])
     out = {"kernel": dom, "timing": "eager_body_events", "launches_timed": len(per_step[dom]),
            "avg_launch_ms": round(kernel_ms[dom], 5),
            "share_of_launch_time": round(kernel_ms[dom] / sum(kernel_ms.values()), 4)}
     if nbytes.get(dom) is None:  # an MLP launch: MFMA-bound
-        flops = 110592 * S / 2
+        # forward 36,864 FLOP / sample, backward twice that per live sample
+        flops = 36864 * S if "forward" in dom else 73728 * (S if live is None else live)
         ach = flops / (kernel_ms[dom] * 1e-3) / 1e12
         out.update(bound="mfma", achieved=round(ach, 2), peak=FP16_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                    frac=round(ach / FP16_MFMA_PEAK_TFLOPS, 4), traffic=None)
@@ -709,15 +715,18 @@ def run_fused(args, model, data, bits, world, dev):
         kernel_ms, per_step, counts = ft.timed_steps(args.kernel_steps, with_counts=True)
     counts = [min(int(c), ft.M) for c in counts]
     rows = float(np.mean(counts))
+    # the rows the backwards walk (NGP_LIVE_ROWS: those with a nonzero gradient)
+    lc = getattr(ft, "body_live_counts", None) if world == 1 else None
+    live = float(np.mean(lc)) if lc else None
     grid = grid_roofline(grid_clock, args.steps, args.workload)
     if world == 1:
-        roofline = launch_roofline(ft, kernel_ms, per_step, counts, args.num_rays, args.workload)
+        roofline = launch_roofline(ft, kernel_ms, per_step, counts, args.num_rays, args.workload, live)
     else:  # the data-parallel step's phases include collectives: the grid backward names the roofline
         roofline = grid
     mlp_ms = sum(v for k, v in kernel_ms.items() if k.startswith("ffmlp"))
-    ffmlp_flops = 110592 * rows
+    ffmlp_flops = 36864 * rows + 73728 * (rows if live is None else live)
     step_bytes = whole_step_bytes(rows, args.num_rays, sum(p.numel() for p in model.parameters()),
-                                  int(model.encoder.embeddings.numel()))
+                                  int(model.encoder.embeddings.numel()), live)
 
     density = density_update_times(model, bits, ft)
     cadence = density_cadence(ft, bits, args) if world == 1 else None
@@ -755,6 +764,7 @@ def run_fused(args, model, data, bits, world, dev):
         "roofline_grid_encode": grid,
         "kernels_ms": {k: round(v, 5) for k, v in kernel_ms.items()},
         "kernel_samples": counts,
+        "kernel_live_rows": lc or None,
         "ffmlp_mfma": {"flops_per_step": int(ffmlp_flops), "ms": round(mlp_ms, 5),
                         "tflops": round(ffmlp_flops / (mlp_ms * 1e-3) / 1e12, 2) if mlp_ms > 0 else None,
                         "peak_tflops": FP16_MFMA_PEAK_TFLOPS},
@@ -878,13 +888,14 @@ _PMC_KERNELS = {"grid_encode_backward": ("k_grid_bwd_bin", "k_grid_bin_accum"),
                 "march_rays_train+adam": ("void k_march_train<4u>", "k_march_emit")}
 
 
-def whole_step_bytes(samples, rays, n_params, n_table):
+def whole_step_bytes(samples, rays, n_params, n_table, live=None):
     """Algorithmic HBM bytes of one step per SURVEY §8(d): grid forward 588 B and
     backward 1,100 B per sample (+ the fp16 table grad's zero fill, 2 B per table
     value), march 48 B/ray + 32 B/sample, composite forward 32 B/ray + 24
     B/sample and backward 52 B/ray + 40 B/sample, SH 76 B/direction, dense Adam
-    28 B/parameter."""
-    return (588 * samples + 1100 * samples + 2 * n_table + 48 * rays + 32 * samples + 32 * rays + 24 * samples
+    28 B/parameter. The backward's bytes are per live sample when the
+    backwards walk only those (`live`, NGP_LIVE_ROWS)."""
+    return (588 * samples + 1100 * (samples if live is None else live) + 2 * n_table + 48 * rays + 32 * samples + 32 * rays + 24 * samples
             + 52 * rays + 40 * samples + 76 * samples + 28 * n_params)
 
 

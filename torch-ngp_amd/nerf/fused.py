@@ -319,13 +319,13 @@ class FusedTrainer:
             bj.nears, bj.fars, bj.noises = nat.ptr(self.nears), nat.ptr(self.fars), nat.ptr(self.noises)
             bj.counter, bj.step_counter = nat.ptr(self.counter), nat.ptr(m_.step_counter)
             self._batch_job = bj
-        # the backwards over the live rows only (NGP_LIVE_ROWS=1): rows whose
+        # the backwards over the live rows only (NGP_LIVE_ROWS, default on): rows whose
         # gradient the composite left zero in every component (behind a ray's
         # early termination, or underflowed to zero in fp16) are skipped by the
         # MLP and grid backwards, as instant-ngp compacts its samples before
         # the backward; needs the one-launch MLP backward and the draw-ahead
         # bin launch (where the list is consumed)
-        self._live = (os.environ.get("NGP_LIVE_ROWS", "0") == "1" and self._one_bwd and self._draw_ahead
+        self._live = (os.environ.get("NGP_LIVE_ROWS", "1") != "0" and self._one_bwd and self._draw_ahead
                       and not self.fused_adam and not self._split_reduce)
         if self._live:
             i32 = torch.int32
@@ -635,6 +635,8 @@ class FusedTrainer:
             torch.cuda.synchronize()
             ev, self._events = self._events, None
             counts.append(self.sample_count())
+            if self._live:
+                self.body_live_counts.append(int(self._live_bufs["total"][0]))
             for (_, a), (name, b) in zip(ev[:-1], ev[1:]):
                 acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
                 per.setdefault(name, []).append(a.elapsed_time(b))
@@ -652,6 +654,7 @@ class FusedTrainer:
         if not self._pending:
             self.step()
         per, counts = {}, []
+        self.body_live_counts = []  # the live rows of those steps (NGP_LIVE_ROWS)
         for _ in range(k):
             torch.cuda.synchronize()
             torch.cuda._sleep(4_000_000)
@@ -1206,6 +1209,15 @@ class FusedTrainer:
 
     def _state_i(self):
         return self.state.view(torch.int32)
+
+    def live_fraction(self):
+        """Live rows (a nonzero gradient) over samples in the last step the
+        backwards ran over the live rows only (NGP_LIVE_ROWS), else None."""
+        if not self._live:
+            return None
+        torch.cuda.synchronize()
+        n = self.sample_count()
+        return int(self._live_bufs["total"][0]) / max(n, 1)
 
     @property
     def last_loss(self):
