@@ -635,8 +635,6 @@ class FusedTrainer:
             torch.cuda.synchronize()
             ev, self._events = self._events, None
             counts.append(self.sample_count())
-            if self._live:
-                self.body_live_counts.append(int(self._live_bufs["total"][0]))
             for (_, a), (name, b) in zip(ev[:-1], ev[1:]):
                 acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
                 per.setdefault(name, []).append(a.elapsed_time(b))
@@ -665,6 +663,8 @@ class FusedTrainer:
             torch.cuda.synchronize()
             ev, self._events = self._events, None
             counts.append(self.sample_count())
+            if self._live:
+                self.body_live_counts.append(int(self._live_bufs["total"][0]))
             for (_, a), (name, b) in zip(ev[:-1], ev[1:]):
                 per.setdefault(name, []).append(a.elapsed_time(b))
         return {n: float(np.mean(v)) for n, v in per.items()}, per, counts
