@@ -379,46 +379,67 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
 }
 
 // The live rows of a step as one list in ray order: each workgroup sums the
-// live counts of every ray before its block of rays (all N counts are read by
-// every workgroup: a few KB from L2), then copies its rays' rows from their
-// per-ray slots; block 0 writes the total.
+// live counts of every ray before its block of 64 rays (16-byte loads, all of
+// a thread's issued together: one round trip for up to 4,096 rays), scans its
+// own rays' counts, then every thread copies list positions (a binary search
+// over the block's offsets, the row loads independent of each other); the
+// last block writes the total. A latency-bound launch: every step is one
+// round trip, nothing waits on another workgroup.
 constexpr uint32_t kLiveThreads = 256, kLiveRaysPerBlock = 64;
 __global__ void __launch_bounds__(kLiveThreads)
 k_live_compact(const int32_t* __restrict__ rays, const int32_t* __restrict__ live_cnt, const int32_t* __restrict__ ray_rows,
                uint32_t N, int32_t* __restrict__ live_rows, int32_t* __restrict__ live_total) {
     __shared__ uint32_t wsum[kLiveThreads / 64];
-    __shared__ uint32_t s_off[kLiveRaysPerBlock + 1];
+    __shared__ uint32_t s_off[kLiveRaysPerBlock + 1], s_src[kLiveRaysPerBlock];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t r0 = blockIdx.x * kLiveRaysPerBlock, r1 = min(N, r0 + kLiveRaysPerBlock);
-    // sum of the counts of rays [0, r0) (and, block 0: of all rays)
-    const uint32_t upto = blockIdx.x == 0 ? N : r0;
+    // this block's rays (wave 0): their counts and first rows, requested with the sums below
+    uint32_t c = 0, src = 0;
+    if (wv == 0 && r0 + lane < r1) {
+        c = (uint32_t)live_cnt[r0 + lane];
+        src = (uint32_t)rays[(size_t)(r0 + lane) * 3 + 1];
+    }
+    // sum of the counts of rays [0, r0): r0 is a multiple of 64, so whole int4 groups
+    const int4* cnt4 = reinterpret_cast<const int4*>(live_cnt);
+    const uint32_t g4 = r0 / 4;
     uint32_t part = 0;
-    for (uint32_t i = t; i < upto; i += kLiveThreads) part += (uint32_t)live_cnt[i];
+    for (uint32_t b = 0; b < g4; b += 4 * kLiveThreads) {
+        int4 v[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t g = b + q * kLiveThreads + t;
+            v[q] = g < g4 ? cnt4[g] : int4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) part += (uint32_t)(v[q].x + v[q].y + v[q].z + v[q].w);
+    }
 #pragma unroll
     for (uint32_t o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
     if (lane == 0) wsum[wv] = part;
-    __syncthreads();
-    const uint32_t before = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    if (blockIdx.x == 0 && t == 0) *live_total = (int32_t)before;
-    // this block's rays: exclusive offsets (one wave)
+    // this block's rays: exclusive offsets (wave 0)
     if (wv == 0) {
-        const uint32_t r = r0 + lane;
-        const uint32_t c = r < r1 ? (uint32_t)live_cnt[r] : 0u;
         uint32_t incl = c;
 #pragma unroll
         for (uint32_t o = 1; o < 64; o <<= 1) {
             const uint32_t u = __shfl_up(incl, o, 64);
             if (lane >= o) incl += u;
         }
-        s_off[lane] = (blockIdx.x == 0 ? 0u : before) + incl - c;
-        if (lane == 63) s_off[64] = (blockIdx.x == 0 ? 0u : before) + incl;
+        s_off[lane] = incl - c;
+        s_src[lane] = src;
+        if (lane == 63) s_off[64] = incl;
     }
     __syncthreads();
-    // copy: a wave per ray
-    for (uint32_t r = r0 + wv; r < r1; r += kLiveThreads / 64) {
-        const uint32_t dst = s_off[r - r0], cnt = s_off[r - r0 + 1] - dst;
-        const uint32_t src = (uint32_t)rays[(size_t)r * 3 + 1];
-        for (uint32_t k = lane; k < cnt; k += 64) live_rows[dst + k] = ray_rows[src + k];
+    const uint32_t before = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    const uint32_t btotal = s_off[64];
+    if (t == 0 && r1 == N) *live_total = (int32_t)(before + btotal);
+    // copy: list position before + j <- the row of ray i (largest i with s_off[i] <= j)
+    for (uint32_t j = t; j < btotal; j += kLiveThreads) {
+        uint32_t lo = 0, hi = kLiveRaysPerBlock;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_off[mid] <= j) lo = mid; else hi = mid;
+        }
+        live_rows[before + j] = ray_rows[s_src[lo] + (j - s_off[lo])];
     }
 }
 
@@ -710,6 +731,8 @@ extern "C" int ngp_nerf_composite_loss_live(const float* sigma, const void* colo
     NGP_REQUIRE(gt_channels == 3 || gt_channels == 4, NGP_ERR_ARG, "composite_loss_live: gt must be RGB or RGBA");
     NGP_REQUIRE(ray_rows && live_cnt && live_rows && live_total, NGP_ERR_ARG,
                 "composite_loss_live: null ray_rows [M] / live_cnt [N] / live_rows [M] / live_total");
+    NGP_REQUIRE((reinterpret_cast<uintptr_t>(live_cnt) & 15) == 0, NGP_ERR_ARG,
+                "composite_loss_live: live_cnt must be 16-byte aligned");
     hipStream_t st = ngp_stream(stream);
     if (N == 0) {
         if (hipMemsetAsync(live_total, 0, sizeof(int32_t), st) != hipSuccess)
