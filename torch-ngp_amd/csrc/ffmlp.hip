@@ -62,6 +62,7 @@ constexpr int kBwdWaves = NGP_MLP_BWD_WAVES;
 constexpr int kBwdThreads = kBwdWaves * 64;
 static_assert(kBwdWaves % 2 == 0 && kBwdWaves <= 16, "the dW fold pairs waves (two LDS images)");
 constexpr int kNB = 2;          // 16-sample column blocks per wave step (32 samples)
+static_assert(16 * kNB == ngp_reduce::kBwdChunkRows, "the reduce's live-row slab count assumes 32-row chunks");
 constexpr int kOut = 16;        // padded output width (FFMLP pads to 16)
 // Per-wave staging tiles of the dW products: [32 samples][units], row pitch
 // 80 halves (40 dwords: the 8 rows one 32-lane half of a transposed read
@@ -1071,6 +1072,9 @@ k_nerf_bwd(NerfBwdArgs a) {
     auto half_of = [=](uint32_t slot) {
         return [=]() { return nf < n && slot < 2 * r ? (b + (nf + slot / 2) * G) * 16 * kNB + 16 * (slot & 1) : kNoHalf; };
     };
+    // live rows: the workgroups past the slab rows the reduce reads have no
+    // chunk and skip both passes (ngp_reduce::live_slab_rows)
+    if (!a.rows || b < ngp_reduce::live_slab_rows((int32_t)B, G)) {
     bwd_phase<64, 1, NHC>(lds, reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes),
                           reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{a.rows},
                           GiNerfGeo{a.g_h, a.rows},
@@ -1086,6 +1090,7 @@ k_nerf_bwd(NerfBwdArgs a) {
     bwd_phase<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
                           InPairMajor{a.B, a.rows}, GiPairMajor{a.g_enc, a.B, a.rows}, true, a.slab_sigma, a.np_sigma,
                           B, 32u, ActReLU{}, map_of(kBwdWaves - 1 - w), []() {}, half_of(kBwdWaves - 1 - w));
+    }
     if (a.timing && b < NGP_GRID_TIMING_MAX_WG / 4) {
         __syncthreads();
         if (threadIdx.x == 0)
@@ -1832,6 +1837,12 @@ uint32_t ngp_reduce::build_reduce_jobs(int32_t n, void* const* workspaces, const
     }
     rj.block0[rj.n] = blocks;
     return blocks;
+}
+
+int ngp_reduce::launch_slab_reduce(const ReduceJobs& rj, uint32_t blocks, void* stream) {
+    if (blocks == 0) return NGP_OK;
+    hipLaunchKernelGGL(k_slab_reduce<ngp_half>, dim3(blocks), dim3(64 * kReducePhases), 0, ngp_stream(stream), rj);
+    return ngp_check_launch("ffmlp_reduce");
 }
 
 extern "C" int ngp_ffmlp_reduce(int32_t n, void* const* workspaces, const uint32_t* Bs, const uint32_t* in_dims,

@@ -2396,6 +2396,7 @@ static int reduce_batch_impl(
     ngp_reduce::ReduceJobs rj{};
     const uint32_t nred = ngp_reduce::build_reduce_jobs(n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims,
                                                         num_layers, grad_weights, mlp_nonfinite, rj);
+    if (rows) rj.live = count;  // the slabs of ngp_nerf_backward_live over the same live rows
     bool binned = false;
     if (workspace && offsets_host && C == 2 && D == 3 && L >= 1 && L <= kMaxLevels) {
         GridLevels lv;
@@ -2403,9 +2404,7 @@ static int reduce_batch_impl(
         binned = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B).nlev > 0;
     }
     if (!binned) {  // no bin launch to carry the reduce: it goes first, on its own
-        if (int e = ngp_ffmlp_reduce(n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims, num_layers, grad_weights,
-                                     NGP_DTYPE_F16, mlp_nonfinite, stream))
-            return e;
+        if (int e = ngp_reduce::launch_slab_reduce(rj, nred, stream)) return e;
         return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                               align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout,
                               nonfinite, AccAdam{}, stream, nullptr, 0, &bl, rows);

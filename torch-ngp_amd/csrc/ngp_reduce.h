@@ -19,6 +19,17 @@ namespace ngp_reduce {
 
 constexpr int kReducePhases = 16;  // row phases of one 64-parameter block
 constexpr int kMaxReduceJobs = 4;
+constexpr uint32_t kBwdChunkRows = 32;  // rows of one backward chunk (ffmlp.hip: 16 * kNB)
+// The slab rows a live-row backward (ngp_nerf_backward_live) writes: its
+// workgroup b takes chunks b, b + G, ..., so with nch chunks only rows < nch
+// hold partials; rows up to the next multiple of 4 phases are written too
+// (zeros), so the reduce's sums keep their association and its result is the
+// all-rows sum bit for bit (the rows skipped would add +0.0).
+NGP_DEV uint32_t live_slab_rows(int32_t live_count, uint32_t rows) {
+    const uint32_t nch = live_count <= 0 ? 0u : ((uint32_t)live_count + kBwdChunkRows - 1) / kBwdChunkRows;
+    const uint32_t g = 4u * kReducePhases;
+    return min(rows, (nch + g - 1) / g * g);
+}
 struct ReduceJobs {
     int n;
     const float* slab[kMaxReduceJobs];
@@ -26,6 +37,7 @@ struct ReduceJobs {
     uint32_t rows[kMaxReduceJobs], np[kMaxReduceJobs];
     uint32_t block0[kMaxReduceJobs + 1];
     int32_t* nonfinite;  // nullable: set when a written grad is inf/nan (GradScaler's check)
+    const int32_t* live;  // nullable: the live-row count of a live-row backward (live_slab_rows)
 };
 
 // grad_weights[p] = sum over the slab rows, in a fixed order: row phase ph
@@ -40,7 +52,7 @@ NGP_DEV void slab_reduce_block(const ReduceJobs& jobs, uint32_t blk, float (*par
     int j = 0;
     while (j + 1 < jobs.n && blk >= jobs.block0[j + 1]) ++j;
     const float* __restrict__ slab = jobs.slab[j];
-    const uint32_t rows = jobs.rows[j], n = jobs.np[j];
+    const uint32_t rows = jobs.live ? live_slab_rows(*jobs.live, jobs.rows[j]) : jobs.rows[j], n = jobs.np[j];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t p = (blk - jobs.block0[j]) * 64 + lane;
 #pragma unroll
@@ -75,5 +87,7 @@ NGP_DEV void slab_reduce_block(const ReduceJobs& jobs, uint32_t blk, float (*par
 uint32_t build_reduce_jobs(int32_t n, void* const* workspaces, const uint32_t* Bs, const uint32_t* in_dims,
                            const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* grad_weights,
                            int32_t* nonfinite, ReduceJobs& rj);
+// The reduce of built jobs as its own launch (fp16 grads); NGP_OK or an error code.
+int launch_slab_reduce(const ReduceJobs& rj, uint32_t blocks, void* stream);
 
 }  // namespace ngp_reduce
