@@ -924,6 +924,8 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
     // image0 + image1 as the slab row: a fixed summation order, so dW is
     // bit-reproducible. Images are tile-major (fold_tiles): first layer's
     // MTW x IN_MT tiles, each hidden layer's MTW x MTW, the last layer's 1 x MTW.
+    // A later round whose two waves took no rows adds only zeros: it is
+    // skipped (x + 0.0 == x, so the row is the same bit for bit).
     constexpr int T_FIRST = N::MTW * N::IN_MT, T_HID = N::MTW * N::MTW, T_LAST = N::MTW;
     constexpr int NT = T_FIRST + NH * T_HID + T_LAST;
         float* img = img_base + (size_t)(wave & 1) * NT * 256;
@@ -934,13 +936,19 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
         for (int q = 1; q <= NH; ++q) fold_tiles<F>(dw_hid[q - 1], img + (T_FIRST + (q - 1) * T_HID) * 256);
         fold_tiles<F>(dw_last, img + (T_FIRST + NH * T_HID) * 256);
     };
-    __syncthreads();  // fragments and tiles are dead from here on
-    if (wave < 2) fold(std::true_type{});
+    __shared__ uint32_t s_took[kBwdWaves];  // each wave writes its own slot before the barrier below
+    if ((threadIdx.x & 63) == 0) s_took[wave] = nst != 0 || hrow != kNoHalf ? 1u : 0u;
+    // fragments and tiles are dead from here on; a full barrier: the waves'
+    // input-gradient stores are complete for the workgroup (the NeRF
+    // backward's sigma pass reads the colour pass's), the later ones order LDS only
     __syncthreads();
+    if (wave < 2) fold(std::true_type{});
+    lds_barrier();
 #pragma unroll 1
     for (uint32_t r = 1; r < (uint32_t)kBwdWaves / 2; ++r) {
+        if ((s_took[2 * r] | s_took[2 * r + 1]) == 0u) continue;  // workgroup-uniform
         if ((wave >> 1) == r) fold(std::false_type{});
-        __syncthreads();
+        lds_barrier();
     }
     MSTAMP(13);
     // slab row = image0 + image1 in the unpadded [out][in] layout: per tile a
@@ -1085,8 +1093,10 @@ k_nerf_bwd(NerfBwdArgs a) {
                               __syncthreads();
                           }, half_of(w));
     // the colour pass's geo grads (global stores of every wave) are complete
-    // and its fold images read before the sigma pass loads g_h and reuses LDS
-    __syncthreads();
+    // (the fold's first barrier) and its fold images read before the sigma
+    // pass loads g_h and reuses LDS: an LDS-only barrier, so the colour slab
+    // row's stores need not land first
+    lds_barrier();
     bwd_phase<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
                           InPairMajor{a.B, a.rows}, GiPairMajor{a.g_enc, a.B, a.rows}, true, a.slab_sigma, a.np_sigma,
                           B, 32u, ActReLU{}, map_of(kBwdWaves - 1 - w), []() {}, half_of(kBwdWaves - 1 - w));
