@@ -570,6 +570,20 @@ int ngp_nerf_backward_live(const void* g_color_out, const void* color_in, const 
                            uint32_t num_layers, uint32_t hidden_dim_color, uint32_t num_layers_color,
                            void* sigma_workspace, size_t sigma_workspace_bytes, void* color_workspace,
                            size_t color_workspace_bytes, uint32_t* timing, void* stream);
+/* ngp_nerf_backward_live with the list joined in the same launch from the
+ * per-ray lists of ngp_nerf_composite_loss_ray_lists (rays [N, 3] of the march,
+ * live_cnt [N], ray_rows [M]): each workgroup scans the N counts and writes
+ * the list positions of its own chunks into live_rows [M]; workgroup 0 writes
+ * live_total[0]. live_rows / live_total then feed
+ * ngp_grid_encode_backward_fused_reduce_batch_live as after
+ * ngp_nerf_composite_loss_live. 1 <= N <= 4096. */
+int ngp_nerf_backward_live_list(const void* g_color_out, const void* color_in, const void* color_image, void* g_h,
+                                const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
+                                const int32_t* rays, uint32_t N, const int32_t* live_cnt, const int32_t* ray_rows,
+                                int32_t* live_rows, int32_t* live_total, uint32_t hidden_dim, uint32_t num_layers,
+                                uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
+                                size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
+                                uint32_t* timing, void* stream);
 /* Sums the deferred dW partials of n backward calls (same B and shapes as
  * those calls) into grad_weights[k], in one launch (n <= 4). nonfinite
  * (nullable): set to 1 when a written grad is inf/nan (GradScaler's check). */
@@ -615,6 +629,16 @@ int ngp_nerf_composite_loss_live(const float* sigma, const void* color_out, cons
                                  void* state, void* grad_color_out, void* grad_h_sigma, float* out_image,
                                  float* out_ws, float* loss_ray, int32_t* ray_rows, int32_t* live_cnt,
                                  int32_t* live_rows, int32_t* live_total, void* stream);
+/* ngp_nerf_composite_loss plus each ray's live rows, listed in the ray's own
+ * row range of ray_rows [M] (live_cnt [N] of them), not yet joined: the
+ * one-launch form of ngp_nerf_composite_loss_live, whose list
+ * ngp_nerf_backward_live_list joins in its own launch. */
+int ngp_nerf_composite_loss_ray_lists(const float* sigma, const void* color_out, const void* h_sigma,
+                                      const float* deltas, const int32_t* rays, uint32_t M, uint32_t N,
+                                      float T_thresh, float density_scale, const float* gt, uint32_t gt_channels,
+                                      const float* bg, void* state, void* grad_color_out, void* grad_h_sigma,
+                                      float* out_image, float* out_ws, float* loss_ray, int32_t* ray_rows,
+                                      int32_t* live_cnt, void* stream);
 /* scaler_enabled of the optimizer entries: GradScaler off; on, with its inf
  * check as a sweep over the grads; on, with the check already made by the
  * kernels that wrote the grads into the state's flag (ngp_fused_inf_flag). */

@@ -626,6 +626,45 @@ def test_live_row_backwards_equal_all_row_backwards(cuda):
     assert abs(a.last_loss - b.last_loss) <= 1e-3 * abs(b.last_loss)
 
 
+def test_live_list_in_backward_launch_equals_compact_launch(cuda):
+    """The live-row list joined inside the MLP backward's launch
+    (NGP_LIVE_LIST=1: every workgroup scans the per-ray counts and writes its
+    own chunks' list positions) against its own k_live_compact launch (=0):
+    the list, its length, every gradient and, after eager and captured runs,
+    parameters and moments bit for bit."""
+    import os
+    knob = os.environ.get("NGP_LIVE_LIST")
+    try:
+        os.environ["NGP_LIVE_LIST"] = "1"
+        _, _, _, a = _setup(cuda)
+        os.environ["NGP_LIVE_LIST"] = "0"
+        _, _, _, b = _setup(cuda)
+    finally:
+        if knob is None:
+            os.environ.pop("NGP_LIVE_LIST", None)
+        else:
+            os.environ["NGP_LIVE_LIST"] = knob
+    assert a._live_list and b._live and not b._live_list
+    for it in range(3):
+        a.step()
+        b.step()
+        torch.cuda.synchronize()
+        ta, tb = int(a._live_bufs["total"][0]), int(b._live_bufs["total"][0])
+        assert ta == tb > 0, (it, ta, tb)
+        assert torch.equal(a._live_bufs["rows"][:ta], b._live_bufs["rows"][:tb]), it
+        for x, y in zip(a.grads, b.grads):
+            assert torch.equal(x.view(torch.int16) if x.dtype == torch.float16 else x,
+                               y.view(torch.int16) if y.dtype == torch.float16 else y), it
+    for t in (a, b):
+        t.capture(warmup=1, multi=4)
+        t.run(8)
+        t.flush()
+    torch.cuda.synchronize()
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+    assert torch.equal(a.exp_avg, b.exp_avg) and torch.equal(a.exp_avg_sq, b.exp_avg_sq)
+
+
 def test_grad_guard_poisons_every_shard(cuda):
     """ngp_grad_guard (data-parallel GradScaler guard): an inf/nan anywhere in
     the rank's gradient puts a NaN at the head of every rank's chunk; a finite

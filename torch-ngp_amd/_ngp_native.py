@@ -136,6 +136,10 @@ SIGNATURES = {
     "ngp_nerf_glue_backward": [c_vp, c_vp, c_u32, c_vp, c_vp],
     "ngp_nerf_composite_loss": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
                                 c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_nerf_composite_loss_ray_lists": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
+                                          c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "ngp_nerf_backward_live_list": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp,
+                                    c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_sz, c_vp, c_sz, c_vp, c_vp],
     "ngp_nerf_composite_loss_live": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
                                      c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      c_vp],

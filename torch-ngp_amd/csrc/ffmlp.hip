@@ -1036,6 +1036,15 @@ struct NerfBwdArgs {
     const int32_t* count;
     uint32_t halves;  // split a last round of 1 or 2 chunks into 16-sample halves
     const int32_t* rows;  // the rows to run (*count of them), or null: rows [0, *count)
+    // the list made in this launch (ngp_nerf_backward_live_list; list_cnt null:
+    // none): each workgroup joins the composite's per-ray lists (list_cnt [N]
+    // rows at ray_rows[rays[n][1]]) up to its chunks, writes those positions of
+    // `rows` (the bin kernel reads the whole list) and runs them
+    const int32_t* list_cnt;
+    const int32_t* list_rays;
+    const int32_t* list_src;
+    int32_t* list_total;
+    uint32_t list_n;
     // the grid backward's timing ring (NGP_GRID_TIMING, include/ngp_hip.h), or
     // null: workgroup b stores its end (after its last store) in end slot
     // MAX_WG - 1 - b of the call the next bin launch opens (the accumulate's
@@ -1053,6 +1062,68 @@ struct NerfBwdLds {
     static constexpr size_t total = sigma_frags + LS::frag_bytes;
     static constexpr bool fits = total <= 160 * 1024 && LS::total <= sigma_frags;
 };
+// the in-launch list's per-ray offsets and first rows, past the kernel's LDS
+constexpr uint32_t kListMaxRays = 4096;
+constexpr uint32_t kListPerThread = (kListMaxRays + kBwdThreads - 1) / kBwdThreads;
+
+// The prologue of the in-launch list (NerfBwdArgs::list_cnt): the exclusive
+// offsets of every ray's live rows (their counts and first rows requested
+// together, one round trip), then this workgroup's chunk positions of the list
+// (b + j G for j < n), each row one independent load. Returns the list length.
+NGP_DEV uint32_t nerf_bwd_list(const NerfBwdArgs& a, uint32_t* off, uint32_t* src, uint32_t b, uint32_t G) {
+    __shared__ uint32_t s_wsum[kBwdWaves];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, N = a.list_n;
+    const uint32_t r0 = t * kListPerThread;
+    uint32_t c[kListPerThread], sr[kListPerThread];
+#pragma unroll
+    for (uint32_t k = 0; k < kListPerThread; ++k) {
+        const uint32_t r = r0 + k;
+        c[k] = r < N ? (uint32_t)a.list_cnt[r] : 0u;
+        sr[k] = r < N ? (uint32_t)a.list_rays[(size_t)r * 3 + 1] : 0u;
+    }
+    uint32_t mine = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kListPerThread; ++k) mine += c[k];
+    uint32_t incl = mine;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) s_wsum[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - mine, total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kBwdWaves; ++k) {
+        run += k < w ? s_wsum[k] : 0u;
+        total += s_wsum[k];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kListPerThread; ++k) {
+        if (r0 + k < N) {
+            off[r0 + k] = run;
+            src[r0 + k] = sr[k];
+        }
+        run += c[k];
+    }
+    __syncthreads();
+    const uint32_t nch = ngp_div_up(total, ngp_reduce::kBwdChunkRows);
+    const uint32_t n = b < nch ? (nch - b + G - 1) / G : 0u;
+    for (uint32_t k = t; k < n * ngp_reduce::kBwdChunkRows; k += kBwdThreads) {
+        const uint32_t p = (b + (k / ngp_reduce::kBwdChunkRows) * G) * ngp_reduce::kBwdChunkRows +
+                           k % ngp_reduce::kBwdChunkRows;
+        if (p >= total) continue;
+        uint32_t lo = 0, hi = N;  // the last ray whose offset is <= p (it holds p: later rays start past it)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (off[mid] <= p) lo = mid; else hi = mid;
+        }
+        const_cast<int32_t*>(a.rows)[p] = a.list_src[src[lo] + (p - off[lo])];
+    }
+    if (b == 0 && t == 0) *a.list_total = (int32_t)total;
+    __syncthreads();  // this workgroup's positions of the list are stored before its passes read them
+    return total;
+}
 
 template <int NHS, int NHC>
 __global__ void __launch_bounds__(kBwdThreads)
@@ -1067,6 +1138,10 @@ k_nerf_bwd(NerfBwdArgs a) {
     half8* sfr = reinterpret_cast<half8*>(reinterpret_cast<char*>(lds) + NL::sigma_frags);
     const uint32_t G = gridDim.x, b = blockIdx.x, w = threadIdx.x >> 6;
     const uint32_t tcall = a.timing && threadIdx.x == 0 ? a.timing[0] : 0u;  // requested early
+    if (a.list_cnt) {  // launch-uniform
+        uint32_t* off = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + NL::total);
+        B = min(a.B, nerf_bwd_list(a, off, off + kListMaxRays, b, G));
+    }
     // this workgroup's chunks b, b + G, ...: n of them, the j-th in slot j % 4.
     // When the last round holds r = 1 or 2 chunks (2 or 3 of the 4 waves idle
     // for a whole chunk), they are split into 2r halves of 16 samples, one per
@@ -1542,7 +1617,16 @@ int launch_nerf_bwd(const NerfBwdArgs& a, hipStream_t st) {
         const uint32_t blocks = bwd_blocks(a.B);
         if (blocks == 0) return NGP_OK;
         constexpr size_t lds_bytes = NerfBwdLds<NHS, NHC>::total;
-        hipLaunchKernelGGL((k_nerf_bwd<NHS, NHC>), dim3(blocks), dim3(kBwdThreads), lds_bytes, st, a);
+        constexpr size_t list_bytes = lds_bytes + 2 * sizeof(uint32_t) * kListMaxRays;
+        if (a.list_cnt) {
+            if constexpr (list_bytes + 1024 > 160 * 1024) {
+                return ngp_set_error(NGP_ERR_UNSUPPORTED, "nerf_backward_live_list: no LDS left for the list");
+            } else {
+                hipLaunchKernelGGL((k_nerf_bwd<NHS, NHC>), dim3(blocks), dim3(kBwdThreads), list_bytes, st, a);
+            }
+        } else {
+            hipLaunchKernelGGL((k_nerf_bwd<NHS, NHC>), dim3(blocks), dim3(kBwdThreads), lds_bytes, st, a);
+        }
         return ngp_check_launch("nerf_backward");
     }
 }
@@ -1649,13 +1733,19 @@ extern "C" int ngp_nerf_forward(const void* enc, const void* sigma_image, const 
  * workspaces (ngp_ffmlp_backward_workspace_bytes of each network) for
  * ngp_ffmlp_reduce, as NGP_FFMLP_DEFER_REDUCE. Input gradients equal the two
  * calls bit for bit; dW is summed in another order. */
+struct ListIn {  // the in-launch list's inputs (ngp_nerf_backward_live_list), or all null
+    const int32_t *cnt = nullptr, *rays = nullptr, *src = nullptr;
+    int32_t* total = nullptr;
+    uint32_t n = 0;
+};
+
 static int nerf_backward_impl(const void* g_color_out, const void* color_in, const void* color_image,
                               void* g_h, const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
                               const int32_t* count, const int32_t* rows, uint32_t hidden_dim, uint32_t num_layers,
                               uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
                               size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
-                              uint32_t* timing, void* stream) {
-    NGP_REQUIRE(!rows || count, NGP_ERR_ARG, "nerf_backward_live: a row list needs its count");
+                              uint32_t* timing, void* stream, const ListIn& list = ListIn{}) {
+    NGP_REQUIRE(!rows || count || list.cnt, NGP_ERR_ARG, "nerf_backward_live: a row list needs its count");
     NGP_REQUIRE(hidden_dim == 64 && hidden_dim_color == 64, NGP_ERR_UNSUPPORTED,
                 "nerf_backward: 64-wide networks only on this build, got %u / %u", hidden_dim, hidden_dim_color);
     NGP_REQUIRE(num_layers >= 2 && num_layers <= 3 && num_layers_color >= 2 && num_layers_color <= 3,
@@ -1687,7 +1777,14 @@ static int nerf_backward_impl(const void* g_color_out, const void* color_in, con
     a.timing = timing;
     a.halves = mlp_bwd_halves_enabled() ? 1u : 0u;
     a.rows = rows;
+    a.list_cnt = list.cnt;
+    a.list_rays = list.rays;
+    a.list_src = list.src;
+    a.list_total = list.total;
+    a.list_n = list.n;
     hipStream_t st = ngp_stream(stream);
+    if (list.cnt && mlp_bwd_pair_enabled())
+        return ngp_set_error(NGP_ERR_UNSUPPORTED, "nerf_backward_live_list: not with NGP_MLP_BWD_PAIR=1");
     const uint32_t key = (num_layers - 1) * 8 + (num_layers_color - 1);
     switch (key) {
         case 1 * 8 + 1: return launch_nerf_bwd<1, 1>(a, st);
@@ -1718,6 +1815,30 @@ extern "C" int ngp_nerf_backward_live(const void* g_color_out, const void* color
     return nerf_backward_impl(g_color_out, color_in, color_image, g_h, enc, sigma_image, g_enc, B, live_count,
                               live_rows, hidden_dim, num_layers, hidden_dim_color, num_layers_color, sigma_workspace,
                               sigma_workspace_bytes, color_workspace, color_workspace_bytes, timing, stream);
+}
+
+extern "C" int ngp_nerf_backward_live_list(const void* g_color_out, const void* color_in, const void* color_image,
+                                           void* g_h, const void* enc, const void* sigma_image, void* g_enc,
+                                           uint32_t B, const int32_t* rays, uint32_t N, const int32_t* live_cnt,
+                                           const int32_t* ray_rows, int32_t* live_rows, int32_t* live_total,
+                                           uint32_t hidden_dim, uint32_t num_layers, uint32_t hidden_dim_color,
+                                           uint32_t num_layers_color, void* sigma_workspace,
+                                           size_t sigma_workspace_bytes, void* color_workspace,
+                                           size_t color_workspace_bytes, uint32_t* timing, void* stream) {
+    NGP_REQUIRE(rays && live_cnt && ray_rows && live_rows && live_total, NGP_ERR_ARG,
+                "nerf_backward_live_list: null rays / live_cnt / ray_rows / live_rows / live_total");
+    NGP_REQUIRE(N >= 1 && N <= kListMaxRays, NGP_ERR_UNSUPPORTED,
+                "nerf_backward_live_list: 1..%u rays per call, got %u (use ngp_nerf_composite_loss_live + "
+                "ngp_nerf_backward_live)", kListMaxRays, N);
+    ListIn list;
+    list.cnt = live_cnt;
+    list.rays = rays;
+    list.src = ray_rows;
+    list.total = live_total;
+    list.n = N;
+    return nerf_backward_impl(g_color_out, color_in, color_image, g_h, enc, sigma_image, g_enc, B, nullptr,
+                              live_rows, hidden_dim, num_layers, hidden_dim_color, num_layers_color, sigma_workspace,
+                              sigma_workspace_bytes, color_workspace, color_workspace_bytes, timing, stream, list);
 }
 
 extern "C" int ngp_nerf_density_forward(const void* inputs, const void* weights, const void* image, uint32_t B,

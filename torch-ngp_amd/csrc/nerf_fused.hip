@@ -754,6 +754,31 @@ extern "C" int ngp_nerf_composite_loss_live(const float* sigma, const void* colo
     return ngp_check_launch("nerf_composite_loss_live");
 }
 
+extern "C" int ngp_nerf_composite_loss_ray_lists(const float* sigma, const void* color_out, const void* h_sigma,
+                                                 const float* deltas, const int32_t* rays, uint32_t M, uint32_t N,
+                                                 float T_thresh, float density_scale, const float* gt,
+                                                 uint32_t gt_channels, const float* bg, void* state,
+                                                 void* grad_color_out, void* grad_h_sigma, float* out_image,
+                                                 float* out_ws, float* loss_ray, int32_t* ray_rows,
+                                                 int32_t* live_cnt, void* stream) {
+    NGP_REQUIRE(loss_ray, NGP_ERR_ARG, "composite_loss_ray_lists: loss_ray [N] buffer required");
+    NGP_REQUIRE(gt_channels == 3 || gt_channels == 4, NGP_ERR_ARG,
+                "composite_loss_ray_lists: gt must be RGB or RGBA");
+    NGP_REQUIRE(ray_rows && live_cnt, NGP_ERR_ARG, "composite_loss_ray_lists: null ray_rows [M] / live_cnt [N]");
+    if (N == 0) return NGP_OK;
+    LossArgs la;
+    la.T_thresh = T_thresh;
+    la.density_scale = density_scale;
+    la.inv_n = 1.0f / (float)N;
+    la.inv_c = 1.0f / 3.0f;
+    la.gt_channels = gt_channels;
+    k_composite_loss<<<ngp_div_up(N, kLossWaves), kLossWaves * 64, 0, ngp_stream(stream)>>>(
+        sigma, (const ngp_half*)color_out, (const ngp_half*)h_sigma, deltas, rays, M, N, gt, bg, la,
+        static_cast<StepState*>(state), (ngp_half*)grad_color_out, (ngp_half*)grad_h_sigma, out_image,
+        out_ws, loss_ray, ray_rows, live_cnt);
+    return ngp_check_launch("nerf_composite_loss_ray_lists");
+}
+
 extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* const* grads,
                                         float* const* exp_avg, float* const* exp_avg_sq,
                                         void* const* half_params, const uint64_t* sizes, float lr,

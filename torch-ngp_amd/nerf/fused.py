@@ -327,6 +327,11 @@ class FusedTrainer:
         # bin launch (where the list is consumed)
         self._live = (os.environ.get("NGP_LIVE_ROWS", "1") != "0" and self._one_bwd and self._draw_ahead
                       and not self.fused_adam and not self._split_reduce)
+        # the list joined inside the MLP backward's launch (NGP_LIVE_LIST=1;
+        # default: its own k_live_compact launch after the composite, which
+        # measured faster: profiles/r05p_live_rows_ab.txt, r05y)
+        self._live_list = (self._live and os.environ.get("NGP_LIVE_LIST", "0") == "1" and N <= 4096
+                           and os.environ.get("NGP_MLP_BWD_PAIR") != "1")
         if self._live:
             i32 = torch.int32
             self._live_bufs = dict(ray_rows=z(M, dtype=i32), cnt=z(N, dtype=i32), rows=z(M, dtype=i32),
@@ -889,7 +894,15 @@ class FusedTrainer:
         # the live rows (a nonzero gradient) listed by the composite: both
         # backwards then run over them only (the other rows' products are zeros)
         live = self._live and draw
-        if live:
+        if live and self._live_list:
+            lv = self._live_bufs
+            chk(lib.ngp_nerf_composite_loss_ray_lists(P(self.sigma), P(self.color_out), P(self.h_sigma),
+                                                      P(self.deltas), P(self.rays), M, N, self.T_thresh,
+                                                      float(m.density_scale), P(self.rgba), 4, P(self.bg),
+                                                      P(self.state), P(self.g_color_out), P(self.g_h), None, None,
+                                                      P(self.loss_ray), P(lv["ray_rows"]), P(lv["cnt"]), s),
+                "composite_loss_ray_lists")
+        elif live:
             lv = self._live_bufs
             chk(lib.ngp_nerf_composite_loss_live(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
                                                  P(self.rays), M, N, self.T_thresh, float(m.density_scale),
@@ -905,7 +918,15 @@ class FusedTrainer:
         self._tick("composite_loss")
         if self._one_bwd:  # both networks' backward in one launch (ngp_nerf_backward)
             timing = P(self.grid_ws) + self._grid_timing_at if self._grid_timing_at else None
-            if live:
+            if live and self._live_list:
+                chk(lib.ngp_nerf_backward_live_list(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
+                                                    P(self.enc_out), P(img[0]), P(self.g_enc), M, P(self.rays), N,
+                                                    P(lv["cnt"]), P(lv["ray_rows"]), P(lv["rows"]), P(lv["total"]),
+                                                    sn.hidden_dim, sn.num_layers, cn.hidden_dim, cn.num_layers,
+                                                    P(self.mlp_ws[0]), self.mlp_ws[0].numel(), P(self.mlp_ws[1]),
+                                                    self.mlp_ws[1].numel(), timing, s),
+                    "nerf_backward_live_list")
+            elif live:
                 chk(lib.ngp_nerf_backward_live(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
                                                P(self.enc_out), P(img[0]), P(self.g_enc), M, P(lv["rows"]),
                                                P(lv["total"]), sn.hidden_dim, sn.num_layers, cn.hidden_dim,
