@@ -8,6 +8,10 @@
 
 #include <cfloat>
 
+#ifndef NGP_ADAM_NT
+#define NGP_ADAM_NT 0
+#endif
+
 namespace ngp_head {
 
 using ngp_step::StepState;
@@ -341,16 +345,30 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
         const int k = find_tensor(tl, c0);
         return find_tensor(tl, c1 - 1) == k && c1 - tl.start[k] <= tl.size[k] ? k : -1;
     };
+    // NGP_ADAM_NT (same-box A/B builds): 1 = the moments and grads streamed
+    // nontemporal (read once per step), 2 = the parameters too
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    auto ld_f4 = [](const float* q, bool nt) {
+        if (!nt) return *reinterpret_cast<const float4*>(q);
+        const f4v x = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(q));
+        return float4{x[0], x[1], x[2], x[3]};
+    };
+    auto st_f4 = [](float* q, float4 x, bool nt) {
+        if (nt) __builtin_nontemporal_store(f4v{x.x, x.y, x.z, x.w}, reinterpret_cast<f4v*>(q));
+        else *reinterpret_cast<float4*>(q) = x;
+    };
+    constexpr bool kNtMV = NGP_ADAM_NT >= 1, kNtP = NGP_ADAM_NT >= 2;
     auto load = [&](uint64_t c, int k, Buf& b) {  // unconditional: past the end reads the chunk's first group
         const uint64_t c0 = c * kChunk, c1 = min(c0 + kChunk, total), first = c0 - tl.start[k];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t off = first + tid * 4 + u * (kChunk / U);
             const uint64_t lo = off + tl.start[k] < c1 ? off : first;
-            b.p[u] = *reinterpret_cast<const float4*>(tl.p[k] + lo);
-            b.m[u] = *reinterpret_cast<const float4*>(tl.m[k] + lo);
-            b.v[u] = *reinterpret_cast<const float4*>(tl.v[k] + lo);
-            b.g[u] = *reinterpret_cast<const half4*>(tl.g[k] + lo);
+            b.p[u] = ld_f4(tl.p[k] + lo, kNtP);
+            b.m[u] = ld_f4(tl.m[k] + lo, kNtMV);
+            b.v[u] = ld_f4(tl.v[k] + lo, kNtMV);
+            b.g[u] = kNtMV ? __builtin_nontemporal_load(reinterpret_cast<const half4*>(tl.g[k] + lo))
+                           : *reinterpret_cast<const half4*>(tl.g[k] + lo);
         }
     };
     auto apply = [&](uint64_t c, int k, Buf& b) {
@@ -364,14 +382,17 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
                 ngp_step::adam_update(b.p[u].y, b.m[u].y, b.v[u].y, (float)b.g[u][1], ac, aa.beta1, aa.beta2, aa.eps);
                 ngp_step::adam_update(b.p[u].z, b.m[u].z, b.v[u].z, (float)b.g[u][2], ac, aa.beta1, aa.beta2, aa.eps);
                 ngp_step::adam_update(b.p[u].w, b.m[u].w, b.v[u].w, (float)b.g[u][3], ac, aa.beta1, aa.beta2, aa.eps);
-                *reinterpret_cast<float4*>(tl.p[k] + off) = b.p[u];
-                *reinterpret_cast<float4*>(tl.m[k] + off) = b.m[u];
-                *reinterpret_cast<float4*>(tl.v[k] + off) = b.v[u];
+                st_f4(tl.p[k] + off, b.p[u], kNtP);
+                st_f4(tl.m[k] + off, b.m[u], kNtMV);
+                st_f4(tl.v[k] + off, b.v[u], kNtMV);
                 if (tl.ph[k])
                     *reinterpret_cast<half4*>(tl.ph[k] + off) =
                         half4{(ngp_half)b.p[u].x, (ngp_half)b.p[u].y, (ngp_half)b.p[u].z, (ngp_half)b.p[u].w};
             }
-            if (aa.zero_grads) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
+            if (aa.zero_grads) {
+                if (kNtMV) __builtin_nontemporal_store(half4{0, 0, 0, 0}, reinterpret_cast<half4*>(tl.g[k] + off));
+                else *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
+            }
         }
     };
     auto seam = [&](uint64_t c) {  // per element (the few chunks across a tensor boundary)
