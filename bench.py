@@ -252,7 +252,11 @@ def run_leg(args, name, dev):
     out = {"workload": desc, "rays_per_s": round(rays_s, 1), "ms_per_step": round(elapsed / args.leg_steps * 1e3, 4),
            "steps": args.leg_steps, "samples_per_ray": round(counts / args.num_rays, 2),
            "samples_per_s": round(rays_s * counts / args.num_rays, 1), "mean_count_M": mean_count,
-           "hipgraph": used_graph, "grid_encode_backward": grid_roofline(grid_clock, args.leg_steps, name)}
+           "hipgraph": used_graph,
+           "grid_encode_backward": grid_roofline(grid_clock, args.leg_steps, name,
+                                                 counts if getattr(ft, "_live", False) else None)}
+    if ft.live_fraction() is not None:
+        out["live_rows_frac"] = round(ft.live_fraction(), 4)
     del ft, model
     torch.cuda.empty_cache()
     return out
@@ -643,7 +647,7 @@ def timed_run(args, ft, world, dev, steps, warmup, settle, graph_steps):
     return elapsed, used_graph, grid_clock
 
 
-def grid_roofline(grid_clock, steps, workload):
+def grid_roofline(grid_clock, steps, workload, all_samples=None):
     """The grid backward (bin + accumulate) on its own clock over the timed
     region's graph replays: 1,100 B per sample x the samples of
     exactly those launches / their summed spans (NGP_GRID_TIMING). north_star's
@@ -654,11 +658,21 @@ def grid_roofline(grid_clock, steps, workload):
     calls = len(ms)
     achieved = 1100 * sum(samp) / (sum(ms) * 1e-3) / 1e9
     traffic, src = pmc_traffic("grid_encode_backward", workload)
-    return {"kernel": "grid_encode_backward", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-            "algorithmic_bytes_per_launch": int(1100 * sum(samp) / calls), "timing": "device_clock_timed_region",
-            "launches_timed": calls, "samples_timed": int(sum(samp)), "avg_launch_ms": round(sum(ms) / calls, 5),
-            "launch_ms_min_median_max": [round(float(v), 5) for v in (min(ms), np.median(ms), max(ms))]}
+    out = {"kernel": "grid_encode_backward", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+           "algorithmic_bytes_per_launch": int(1100 * sum(samp) / calls), "timing": "device_clock_timed_region",
+           "launches_timed": calls, "samples_timed": int(sum(samp)), "avg_launch_ms": round(sum(ms) / calls, 5),
+           "launch_ms_min_median_max": [round(float(v), 5) for v in (min(ms), np.median(ms), max(ms))]}
+    if all_samples:
+        # the backward walks only the live rows (NGP_LIVE_ROWS): samples_timed
+        # counts those, the bytes above are theirs. Beside it, the reference's
+        # work (its backward reads every sample's gradient) over the same time:
+        # an equivalent rate, not bytes this kernel moved
+        eq = 1100 * all_samples * calls / (sum(ms) * 1e-3) / 1e9
+        out["rows"] = "live (a nonzero gradient)"
+        out["all_samples_per_launch"] = int(all_samples)
+        out["reference_equivalent_frac"] = round(eq / HBM_PEAK_GBS, 4)
+    return out
 
 
 def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload, live=None):
@@ -718,7 +732,8 @@ def run_fused(args, model, data, bits, world, dev):
     # the rows the backwards walk (NGP_LIVE_ROWS: those with a nonzero gradient)
     lc = getattr(ft, "body_live_counts", None) if world == 1 else None
     live = float(np.mean(lc)) if lc else None
-    grid = grid_roofline(grid_clock, args.steps, args.workload)
+    grid = grid_roofline(grid_clock, args.steps, args.workload,
+                         samples_per_step if getattr(ft, "_live", False) else None)
     if world == 1:
         roofline = launch_roofline(ft, kernel_ms, per_step, counts, args.num_rays, args.workload, live)
     else:  # the data-parallel step's phases include collectives: the grid backward names the roofline

@@ -14,11 +14,12 @@ cd "$R"
     python3 bench.py --no-cpu --no-legs --no-dp-path --no-render ${BENCH_ARGS:-} --steps 30 --warmup 10 > "$O/trace.log" 2>&1
 # PMC passes on eager steps (--no-graph). The per-launch bytes follow the
 # training state: as the field trains, samples behind early-terminated rays get
-# a zero gradient and produce no grid-backward items (r05m: the bin launch
-# writes 52-59 MB in the first steps, 2-6 MB after a few hundred), and the
-# summary's median is over the whole run
-KRE='k_grid_bwd|k_grid_bin|k_grid_fwd|k_adam|k_mlp|k_nerf_fwd|k_nerf_bwd|k_march|k_composite|k_glue'
+# a zero gradient (r05m: the bin launch writes 52-59 MB in the first steps, 2-6
+# MB after a few hundred), and the backwards walk only the live rows. The
+# summary's median is over the whole run, so the passes settle 300 steps
+# first: the median is the trained regime the bench times
+KRE='k_grid_bwd|k_grid_bin|k_grid_fwd|k_adam|k_mlp|k_nerf_fwd|k_nerf_bwd|k_march|k_composite|k_glue|k_live'
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex "$KRE" -d "$O/fetch" -o run -- \
-    python3 bench.py --no-cpu --no-legs --no-dp-path --no-render ${BENCH_ARGS:-} --no-graph --steps 5 --warmup 3 --settle-steps 0 > "$O/fetch.log" 2>&1
+    python3 bench.py --no-cpu --no-legs --no-dp-path --no-render ${BENCH_ARGS:-} --no-graph --steps 5 --warmup 3 --settle-steps ${PMC_SETTLE:-300} > "$O/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex "$KRE" -d "$O/write" -o run -- \
-    python3 bench.py --no-cpu --no-legs --no-dp-path --no-render ${BENCH_ARGS:-} --no-graph --steps 5 --warmup 3 --settle-steps 0 > "$O/write.log" 2>&1
+    python3 bench.py --no-cpu --no-legs --no-dp-path --no-render ${BENCH_ARGS:-} --no-graph --steps 5 --warmup 3 --settle-steps ${PMC_SETTLE:-300} > "$O/write.log" 2>&1
