@@ -101,6 +101,39 @@ NGP_DEV void copy_frags(half8* __restrict__ lds, const half8* __restrict__ image
     }
 }
 
+#ifndef NGP_BWD_COPY2  // same-box A/B builds only: 1 batches the two image copies (r05ac: no change, 23.3 us both)
+#define NGP_BWD_COPY2 0
+#endif
+// Two images copied with every load of both issued before the first LDS
+// store: one round trip instead of two (the NeRF backward's prologue).
+template <int F1, int F2, int THREADS>
+NGP_DEV void copy_frags2(half8* __restrict__ lds1, const half8* __restrict__ image1, half8* __restrict__ lds2,
+                         const half8* __restrict__ image2) {
+    constexpr int T1 = F1 * 64, P1 = (T1 + THREADS - 1) / THREADS;
+    constexpr int T2 = F2 * 64, P2 = (T2 + THREADS - 1) / THREADS;
+    half8 v1[P1], v2[P2];
+#pragma unroll
+    for (int k = 0; k < P1; ++k) {
+        const int t = k * THREADS + (int)threadIdx.x;
+        v1[k] = image1[(k + 1) * THREADS <= T1 ? t : min(t, T1 - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < P2; ++k) {
+        const int t = k * THREADS + (int)threadIdx.x;
+        v2[k] = image2[(k + 1) * THREADS <= T2 ? t : min(t, T2 - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < P1; ++k) {
+        const int t = k * THREADS + (int)threadIdx.x;
+        if ((k + 1) * THREADS <= T1 || t < T1) lds1[t] = v1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < P2; ++k) {
+        const int t = k * THREADS + (int)threadIdx.x;
+        if ((k + 1) * THREADS <= T2 || t < T2) lds2[t] = v2[k];
+    }
+}
+
 // a row index that is always readable (rows past B read row B - 1 and the
 // caller zeroes the value): loads without branches, see copy_frags
 NGP_DEV uint32_t clamp_row(uint32_t row, uint32_t B) { return row < B ? row : (B ? B - 1 : 0u); }
@@ -1163,8 +1196,12 @@ k_nerf_bwd(NerfBwdArgs a) {
                           GiNerfGeo{a.g_h, a.rows},
                           true, a.slab_color, a.np_color, B, 32u, ActReLU{}, map_of(w),
                           [&]() {
+#if NGP_BWD_COPY2
+                              copy_frags2<LC::FRAGS, LS::FRAGS, kBwdThreads>(lds, a.color_image, sfr, a.sigma_image);
+#else
                               copy_frags<LC::FRAGS, kBwdThreads>(lds, a.color_image);
                               copy_frags<LS::FRAGS, kBwdThreads>(sfr, a.sigma_image);
+#endif
                               __syncthreads();
                           }, half_of(w));
     // the colour pass's geo grads (global stores of every wave) are complete
