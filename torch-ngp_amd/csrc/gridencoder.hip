@@ -269,13 +269,15 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
 // its 128 points: the point is loaded once and the KL levels' gathers are all
 // in flight together.
 //
-// Large batches (the density-grid update's 1-2M query points, B >= kFwdGroupMajorMin)
-// run level-group-major with one level per block instead: an XCD then works
-// through all points of level j before level j + 8, and its L2 holds one level
-// table at a time (two hashed fp16 tables are its whole 4 MiB). Same values.
+// Very large batches (B >= kFwdGroupMajorMin, 2^22) run level-group-major with
+// one level per block instead: an XCD then works through all points of level
+// j before level j + 8, and its L2 holds one level table at a time (two hashed
+// fp16 tables are its whole 4 MiB). Same values. The density-grid update's
+// 1-2M query points measured faster level-interleaved (r05ad: full update
+// 0.655-0.668 -> 0.600-0.609 ms, partial unchanged), hence the threshold.
 constexpr uint32_t kFwdLevelsPerBlock = 2;
 #ifndef NGP_FWD_GROUP_MAJOR_MIN  // same-box A/B builds only (tools/variants.sh)
-#define NGP_FWD_GROUP_MAJOR_MIN (1u << 19)
+#define NGP_FWD_GROUP_MAJOR_MIN (1u << 22)
 #endif
 constexpr uint32_t kFwdGroupMajorMin = NGP_FWD_GROUP_MAJOR_MIN;
 
