@@ -11,6 +11,9 @@
 #ifndef NGP_ADAM_NT
 #define NGP_ADAM_NT 0
 #endif
+#ifndef NGP_ADAM_ALT
+#define NGP_ADAM_ALT 0
+#endif
 
 namespace ngp_head {
 
@@ -412,16 +415,21 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
             if (aa.zero_grads) tl.g[kk][off] = (ngp_half)0.0f;
         }
     };
+    // NGP_ADAM_ALT (same-box A/B builds): every other update sweeps the chunks
+    // in reverse, so it starts where the last one ended (the lines most
+    // recently written, likeliest still in the memory-side cache)
+    const bool rev = NGP_ADAM_ALT && (st->iter & 1);
+    auto at = [&](uint64_t i) { return rev ? nchunks - 1 - i : i; };
     Buf a{}, b{};
     uint64_t c = blk;
-    int ka = c < nchunks ? whole(c) : -1;
-    if (ka >= 0) load(c, ka, a);
+    int ka = c < nchunks ? whole(at(c)) : -1;
+    if (ka >= 0) load(at(c), ka, a);
     while (c < nchunks) {
         const uint64_t cn = c + nblk;
-        const int kb = cn < nchunks ? whole(cn) : -1;
-        if (kb >= 0) load(cn, kb, b);  // in flight while this chunk computes
-        if (ka >= 0) apply(c, ka, a);
-        else seam(c);
+        const int kb = cn < nchunks ? whole(at(cn)) : -1;
+        if (kb >= 0) load(at(cn), kb, b);  // in flight while this chunk computes
+        if (ka >= 0) apply(at(c), ka, a);
+        else seam(at(c));
         a = b;
         ka = kb;
         c = cn;
