@@ -125,6 +125,41 @@ def test_oracle_composite_backward_matches_reference_autograd():
     _grad_close(g_rgb, f["d_rgb"], "d rgb")
 
 
+def test_oracle_composite_backward_is_zero_past_termination():
+    """The premise of the live-row backwards (nerf/fused.py NGP_LIVE_ROWS): the
+    reference's composite backward stops at a ray's early termination
+    (`if (T < T_thresh) break;`, raymarching.cu:680), so every sample past it
+    has an exactly zero sigma and rgb gradient. Checked on the oracle's
+    restatement with dense rays that terminate inside their samples."""
+    rng = np.random.default_rng(7)
+    N, S, T_thresh = 64, 96, 1e-4
+    counts = rng.integers(1, S + 1, N)
+    offsets = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    rays = np.stack([np.arange(N), offsets, counts], 1).astype(np.int32)
+    M = int(counts.sum())
+    sigma = rng.uniform(0.0, 60.0, M).astype(np.float32)
+    rgb = rng.uniform(0.0, 1.0, (M, 3)).astype(np.float32)
+    deltas = np.stack([rng.uniform(0.005, 0.02, M), rng.uniform(0.005, 0.02, M)], 1).astype(np.float32)
+    ws, depth, image = oracle.composite_rays_train_forward(sigma, rgb, deltas, rays, T_thresh)
+    g_ws = rng.normal(size=N).astype(np.float32)
+    g_sig, g_rgb = oracle.composite_rays_train_backward(g_ws, np.zeros(N, np.float32),
+                                                        rng.normal(size=(N, 3)).astype(np.float32), sigma, rgb,
+                                                        deltas, rays, ws, depth, image, T_thresh)
+    terminated = 0
+    for n in range(N):
+        o, c = int(offsets[n]), int(counts[n])
+        T, stop = 1.0, c
+        for k in range(c):  # the first sample after which T < T_thresh (float32, as the kernel)
+            T = np.float32(T) * np.float32(1.0 - (1.0 - np.exp(np.float32(-sigma[o + k] * deltas[o + k, 0]))))
+            if T < T_thresh:
+                stop = k + 1
+                break
+        terminated += stop < c
+        assert not g_sig[o + stop:o + c].any() and not g_rgb[o + stop:o + c].any(), n
+        assert g_rgb[o:o + stop].any(), n  # the live samples do carry a gradient
+    assert terminated > N // 2  # most rays end early: the rows the live-row backwards skip
+
+
 @pytest.mark.gpu
 def test_hip_composite_backward_matches_reference_autograd(cuda, parity_report):
     """The HIP composite_rays_train backward through the reference-API autograd
