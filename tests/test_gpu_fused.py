@@ -573,7 +573,8 @@ def test_tail_in_grid_forward_equals_emit_tail(cuda):
         assert torch.equal(x, y)
 
 
-def test_live_row_backwards_equal_all_row_backwards(cuda):
+@pytest.mark.parametrize("bound,dt_gamma,occ", [(1, 0.0, "boxes"), (2, 1 / 128, "boxes"), (1, 0.0, "ball")])
+def test_live_row_backwards_equal_all_row_backwards(cuda, bound, dt_gamma, occ):
     """The backwards over the live rows only (NGP_LIVE_ROWS=1: the composite
     lists the rows with a nonzero gradient, the MLP backward and the grid bin
     kernel walk that list) against the backwards over every row (=0): the loss
@@ -585,9 +586,9 @@ def test_live_row_backwards_equal_all_row_backwards(cuda):
     knob = os.environ.get("NGP_LIVE_ROWS")
     try:
         os.environ["NGP_LIVE_ROWS"] = "1"
-        _, _, _, a = _setup(cuda)
+        _, _, _, a = _setup(cuda, bound=bound, dt_gamma=dt_gamma, occ=occ)
         os.environ["NGP_LIVE_ROWS"] = "0"
-        _, _, _, b = _setup(cuda)
+        _, _, _, b = _setup(cuda, bound=bound, dt_gamma=dt_gamma, occ=occ)
     finally:
         if knob is None:
             os.environ.pop("NGP_LIVE_ROWS", None)
