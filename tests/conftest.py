@@ -11,9 +11,12 @@ for p in (ROOT, PKG):
 
 # The -m gpu run stops at the first failure (-x), so the tests that establish
 # the coverage rows run first: the benched step against the oracle on every
-# BASELINE config, the reference's own gradcheck, the reference-executed
-# golden fixtures, then the RCCL data-parallel path. The rest keep their order.
-FIRST = ["test_gpu_e2e_oracle.py", "test_gradcheck.py", "test_golden_reference.py", "test_gpu_rccl.py"]
+# BASELINE config, the reference operator surface (every _backend entry point
+# against the oracle), the render loop, the reference's own gradcheck, the
+# reference-executed golden fixtures, then the RCCL data-parallel path. The
+# rest keep their order.
+FIRST = ["test_gpu_e2e_oracle.py", "test_gpu_parity.py", "test_gpu_render.py", "test_gradcheck.py",
+         "test_golden_reference.py", "test_gpu_rccl.py"]
 
 _REPORT = []
 

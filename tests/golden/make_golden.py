@@ -21,6 +21,13 @@ not):
                        encoding, the same layout as freqencoder's CUDA op with
                        max_freq_log2 = degree - 1, N_freqs = degree): outputs
                        and input grads for a seeded output grad
+  * NeRFRenderer.update_extra_state / mark_untrained_grid — nerf/renderer.py
+                       :433-598 (density-grid EMA, packbits, mean_density,
+                       mean_count; the frustum mark) on a stub `self` with an
+                       analytic density, raymarching.morton3D / _invert /
+                       packbits bound to the oracle's CPU restatements; the
+                       update's torch draws are served by a recording proxy
+                       (below) and stored with the results
 
 Only the class / function definitions are extracted (ast) and executed; the
 scripts' module-level CUDA code never runs. Usage:
@@ -275,6 +282,134 @@ def freq_fixture():
     np.savez_compressed(os.path.join(HERE, "freq_reference.npz"), **res)
 
 
+class _DrawProxy:
+    """Stands in for the `torch` module inside the exec'd update_extra_state:
+    every attribute is torch's, except the three draws, which are served from
+    a seeded numpy generator and recorded in call order:
+      * randint(0, H, (N, 3)): distinct cells (a random subset of H^3);
+      * randint(0, n_occ, [N]): distinct occupied picks where there are enough,
+        wrapping around otherwise;
+      * rand_like(x): k / 2^16 with k a hash of the row's cell, cascade and
+        update, so a cell drawn twice in one update gets the same noise row and
+        density, and upstream's index_put (which keeps an arbitrary duplicate)
+        and the build's scatter-max agree.
+    The values are exactly representable, so they travel as uint16 / int32."""
+
+    def __init__(self, seed, H, bound_of):
+        self._rng = np.random.default_rng(seed)
+        self._H, self._bound_of = H, bound_of
+        self.draws = []
+        self.update = 0
+        self.cas = 0
+
+    def __getattr__(self, name):
+        return getattr(torch, name)
+
+    def randint(self, low, high, size, **kw):
+        n = int(np.prod(size))
+        if len(size) == 2:  # cells
+            H = self._H
+            cells = self._rng.choice(H ** 3, size=size[0], replace=False)
+            out = np.stack([cells // (H * H), (cells // H) % H, cells % H], -1)
+        else:  # picks into the occupied list
+            perm = self._rng.permutation(int(high))
+            out = np.resize(perm, n)
+        t = torch.from_numpy(out.astype(np.int64)).reshape(size)
+        self.draws.append(("randint", out.astype(np.int32).reshape(size)))
+        return t
+
+    def rand_like(self, x):
+        H = self._H
+        bound = self._bound_of(self.cas)
+        hgs = bound / H
+        c = torch.round((x / (bound - hgs) + 1) * (H - 1) / 2).to(torch.int64).numpy()  # the rows' cells
+        key = (c[:, 0] * H + c[:, 1]) * H + c[:, 2] + (self.cas * 7919 + self.update * 104729) * H ** 3
+        k = np.empty((x.shape[0], 3), np.uint16)
+        for j in range(3):
+            h = (key * 0x9E3779B1 + (j + 1) * 0x85EBCA77) & 0xFFFFFFFF
+            h ^= h >> 15
+            h = (h * 0x2C1B3C6D) & 0xFFFFFFFF
+            h ^= h >> 12
+            k[:, j] = (h & 0xFFFF).astype(np.uint16)
+        self.draws.append(("rand", k))
+        self.cas += 1
+        return torch.from_numpy(k.astype(np.float32) * np.float32(2.0 ** -16))
+
+
+def density_fixture():
+    """update_extra_state (renderer.py:498-598) x 4 (2 full, 2 partial) and
+    mark_untrained_grid (:433-496) on stubs: bound 2 / cascade 2 and bound 1 /
+    cascade 1, grid 16^3. The density is an analytic blob (so no network is
+    involved): sigma = 30 exp(-|x - c|^2 / 0.35)."""
+    import types
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE))))
+    import oracle
+    rm = types.SimpleNamespace(
+        morton3D=lambda c: torch.from_numpy(oracle.morton3D(c.numpy())),
+        morton3D_invert=lambda i: torch.from_numpy(oracle.morton3D_invert(i.numpy())),
+        packbits=lambda g, th, bf: torch.from_numpy(oracle.packbits(g.numpy(), float(th))))
+    util = extract(os.path.join(REF, "nerf/utils.py"), {"custom_meshgrid"})
+    H = 16
+    out = {"H": np.int32(H)}
+    for tag, bound, thresh in (("b2", 2, 10.0), ("b1", 1, 0.5)):
+        cascade = 1 + int(np.ceil(np.log2(bound)))
+        proxy = _DrawProxy(17 + bound, H, lambda cas: min(2 ** cas, bound))
+        ns = {"raymarching": rm, "custom_meshgrid": util["custom_meshgrid"]}
+        upd = extract_method(os.path.join(REF, "nerf/renderer.py"), "NeRFRenderer", "update_extra_state", ns)
+        upd.__globals__["torch"] = proxy
+        mark = extract_method(os.path.join(REF, "nerf/renderer.py"), "NeRFRenderer", "mark_untrained_grid", ns)
+        centre = torch.tensor([0.15, -0.1, 0.05]) * bound
+
+        def density(x):
+            return {"sigma": 30.0 * torch.exp(-((x - centre) ** 2).sum(-1) / (0.35 * bound * bound))}
+
+        stub = types.SimpleNamespace(
+            cuda_ray=True, grid_size=H, cascade=cascade, bound=bound, density_scale=1.0, density_thresh=thresh,
+            density_grid=torch.zeros(cascade, H ** 3), density_bitfield=torch.zeros(cascade * H ** 3 // 8,
+                                                                                     dtype=torch.uint8),
+            iter_density=0, mean_density=0.0, mean_count=-1, local_step=0,
+            step_counter=torch.zeros(16, 2, dtype=torch.int32), density=density)
+        # mark_untrained_grid: cameras on half a ring looking at the origin
+        # (narrow field of view: the far corners stay unseen)
+        poses = []
+        for k in range(4):
+            th = np.pi * k / 3
+            eye = np.array([np.cos(th), np.sin(th), 0.5]) * 2.2 * bound
+            z = -eye / np.linalg.norm(eye)  # the mark's frustum test looks along +z (renderer.py:482)
+            x = np.cross([0.0, 0.0, 1.0], z)
+            x /= np.linalg.norm(x)
+            y = np.cross(z, x)
+            p = np.eye(4)
+            p[:3, 0], p[:3, 1], p[:3, 2], p[:3, 3] = x, y, z, eye
+            poses.append(p)
+        poses = np.stack(poses).astype(np.float32)
+        intr = (40.0, 40.0, 10.0, 9.0)
+        mark(stub, torch.from_numpy(poses), intr, S=64)
+        out[f"{tag}_poses"], out[f"{tag}_intrinsics"] = poses, np.array(intr, np.float32)
+        out[f"{tag}_marked"] = stub.density_grid.numpy().copy()
+        counts = np.arange(1, 17, dtype=np.int32) * 1000 + bound * 7
+        for u in range(4):
+            if u == 2:
+                stub.iter_density = 16  # partial updates from here on
+            stub.step_counter[:, 0] = torch.from_numpy(counts + u)
+            stub.local_step = (5, 16, 30, 0)[u]
+            proxy.update, proxy.cas = u, 0
+            n0 = len(proxy.draws)
+            upd(stub)
+            kinds = [k for k, _ in proxy.draws[n0:]]
+            out[f"{tag}_u{u}_kinds"] = np.array([0 if k == "randint" else 1 for k in kinds], np.int8)
+            for j, (k, v) in enumerate(proxy.draws[n0:]):
+                out[f"{tag}_u{u}_d{j}"] = v
+            out[f"{tag}_u{u}_step_counter"] = stub.step_counter.numpy().copy()
+            out[f"{tag}_u{u}_grid"] = stub.density_grid.numpy().copy()
+            out[f"{tag}_u{u}_bitfield"] = stub.density_bitfield.numpy().copy()
+            out[f"{tag}_u{u}_mean_density"] = np.float64(stub.mean_density)
+            out[f"{tag}_u{u}_mean_count"] = np.int64(stub.mean_count)
+            out[f"{tag}_u{u}_local_step"] = np.int64(stub.local_step)
+    np.savez_compressed(os.path.join(HERE, "density_reference.npz"), **out)
+
+
 if __name__ == "__main__":
     sh_fixture()
     mlp_fixture()
@@ -284,4 +419,5 @@ if __name__ == "__main__":
     get_rays_fixture()
     nerf_matrix_fixture()
     freq_fixture()
+    density_fixture()
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

@@ -656,13 +656,18 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 //                    bin, summed exactly in an LDS image of int64 fixed-point
 //                    counts of the bin's entries. A unit that owns its bin
 //                    stores the slice (per entry, or per item for small units
-//                    of a cleared grad); bins with several units flush each
-//                    image with packed fp16 atomics (coalesced, one per entry
-//                    per unit).
+//                    of a cleared grad); the units of a bin with several add
+//                    their images into the bin's int64 slot and the last to
+//                    arrive stores the slice.
 // Contributions are rounded to half once per run (the reference rounds each
 // term, gridencoder.cu:325) and summed exactly. Items past a bin's capacity
-// fall back to direct atomics. Levels with more than kMaxBinsPerLevelBig bins
-// (or past the plan's kMaxTotalBins) use k_grid_bwd.
+// (a concentrated sample cloud) are added as the same int64 counts into a
+// spill image of the table with integer atomics, and the bin's first unit
+// folds its slice of the spill image into its own before storing: every sum
+// is exact and independent of arrival order in every regime, so the result
+// is one fp16 rounding of the exact sum of the rounded runs, bit-identical
+// from launch to launch. Levels with more than kMaxBinsPerLevelBig bins (or
+// past the plan's kMaxTotalBins) use k_grid_bwd.
 // The NGP_* macros exist only for same-box A/B builds (tools/variants.sh).
 #ifndef NGP_BIN_SHIFT
 #define NGP_BIN_SHIFT 12
@@ -682,17 +687,8 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 #ifndef NGP_SPARSE_Q
 #define NGP_SPARSE_Q 4
 #endif
-#ifndef NGP_NT_ITEMS  // same-box A/B builds only: nontemporal item stores
-#define NGP_NT_ITEMS 0
-#endif
-#ifndef NGP_MULTI_UNITS  // 0: bins of several units flush with fp16 atomics (order-dependent rounding)
-#define NGP_MULTI_UNITS 1
-#endif
 #ifndef NGP_MATCH_MAX_BINS
 #define NGP_MATCH_MAX_BINS 64
-#endif
-#ifndef NGP_SOA_ITEMS  // 1: 6-byte items, the values (half2) and entries (u16) in two arrays
-#define NGP_SOA_ITEMS 0
 #endif
 constexpr uint32_t kBinShift = NGP_BIN_SHIFT;
 constexpr uint32_t kBinEntries = 1u << kBinShift;
@@ -723,7 +719,7 @@ struct BinPlan {
     // bin, so its result does not depend on the units' order
     uint32_t mslot0[kMaxLevels];     // first slot of the level's bins, or kNoSlot
     uint32_t nmslots;
-    size_t ents_at;                  // NGP_SOA_ITEMS: byte offset of the entry array from the items
+    uint32_t spill_entries;          // table entries of the binned levels (the spill image's size)
 };
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
@@ -733,12 +729,12 @@ struct BinItem {  // 8 bytes: the accumulate kernel reads items as one dword pai
 };
 static_assert(sizeof(BinItem) == 8, "BinItem layout");
 
-// Is the fp16 sum old + v (what a packed fp16 atomic stores) finite in both
-// channels? The float sum of two halves rounds to the same half as the
-// half-precision add.
-NGP_DEV bool half2_sum_finite(ngp_half2 old, ngp_half2 v) {
-    const ngp_half a = (ngp_half)((float)old[0] + (float)v[0]), b = (ngp_half)((float)old[1] + (float)v[1]);
-    return __builtin_isfinite((float)a) && __builtin_isfinite((float)b);
+// An fp16 value as a signed count of 2^-24 (every finite fp16 is one:
+// (1024 + m) << (e - 1) for normals, m for subnormals); |x| < 2^41.
+NGP_DEV int64_t half_fixed24(uint32_t bits) {
+    const uint32_t e = (bits >> 10) & 31u, m = bits & 1023u;
+    const int64_t mag = e ? (int64_t)(1024u | m) << (e - 1) : (int64_t)m;
+    return (bits & 0x8000u) ? -mag : mag;
 }
 
 NGP_DEV uint32_t lanes_below(uint64_t m) {
@@ -790,8 +786,9 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
                InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
                int32_t grad_layout, int32_t* __restrict__ nonfinite, ngp_reduce::ReduceJobs rj, uint32_t nred,
-               uint32_t* __restrict__ timing, BinLego next_batch) {
-    constexpr uint32_t C = 2, NC = 1u << D, NW = kBinPts / 64;
+               uint32_t* __restrict__ timing, BinLego next_batch, unsigned long long* __restrict__ spill,
+               uint32_t* __restrict__ spill_bad) {
+    constexpr uint32_t NC = 1u << D, NW = kBinPts / 64;
     constexpr uint32_t BPT = (NBMAX + kBinPts - 1) / kBinPts;  // bins per thread in the reservation step
     __shared__ uint32_t cnt[NBMAX], soff[NBMAX + 1], wsum[NW];
     __shared__ uint2 binfo[NBMAX];  // (slot - stage index, end of the bin's in-capacity stage run)
@@ -1078,54 +1075,36 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     BSTAMP(3);
     const uint32_t total = soff[nb];
     BinItem* lvl_items = items + bp.item0[level];
-    ngp_half* gg = grad_grid + (size_t)off0 * C;
     // in-capacity items: plain stores, back to back (with the overflow path's
     // returning atomics in the same loop the compiler waited for every
     // store's completion before the next)
     for (uint32_t k = threadIdx.x; k < total; k += kBinPts) {
         const BinItem it = stage[k];
         const uint2 bi = binfo[it.e >> 16];
-        if (k < bi.y) {
-#if NGP_NT_ITEMS  // streamed once (the accumulate reads them nontemporally): keep them out of the caches
-            const BinItem v{it.e & 0xffffu, it.v};
-            __builtin_nontemporal_store(*reinterpret_cast<const uint64_t*>(&v),
-                                        reinterpret_cast<uint64_t*>(lvl_items + k + bi.x));
-#else
-#if NGP_SOA_ITEMS
-            const size_t slot = (size_t)bp.item0[level] + k + bi.x;
-            reinterpret_cast<ngp_half2*>(items)[slot] = it.v;
-            reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(items) + bp.ents_at)[slot] = (uint16_t)it.e;
-#else
-            lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
-#endif
-#endif
-        }
+        if (k < bi.y) lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
     }
+    // Past a bin's capacity: the item's exact int64 counts go into the spill
+    // image (integer atomics, so the sum does not depend on the arrival
+    // order); the bin's first accumulate unit folds them in. A non-finite
+    // item cannot be carried by the integers: it marks the bin instead.
     for (uint32_t k = threadIdx.x; s_over && k < total; k += kBinPts) {
         const BinItem it = stage[k];
         const uint32_t bin = it.e >> 16;
         const uint2 bi = binfo[bin];
-        if (k >= bi.y) {  // past the bin's capacity
-            const size_t e = (size_t)bin * kBinEntries + (it.e & 0xffffu);
-            ngp_half2* p = reinterpret_cast<ngp_half2*>(gg + e * C);
-            if (nonfinite) {  // the returning atomic: the entry's new value is checked
-                const ngp_half2 o = __builtin_amdgcn_global_atomic_fadd_v2f16(p, it.v);
-                if (!half2_sum_finite(o, it.v)) atomicOr(nonfinite, 1);
+        if (k >= bi.y) {
+            const uint32_t vb = __builtin_bit_cast(uint32_t, it.v);
+            if (((vb >> 10) & 31u) == 31u || ((vb >> 26) & 31u) == 31u) {
+                spill_bad[bp.bin0[level] + bin] = 1u;  // benign race: every writer stores 1
+                if (nonfinite) atomicOr(nonfinite, 1);
             } else {
-                __builtin_amdgcn_global_atomic_fadd_v2f16(p, it.v);
+                const size_t e = (size_t)off0 + (size_t)bin * kBinEntries + (it.e & 0xffffu);
+                atomicAdd(spill + 2 * e, (unsigned long long)half_fixed24(vb & 0xffffu));
+                atomicAdd(spill + 2 * e + 1, (unsigned long long)half_fixed24(vb >> 16));
             }
         }
     }
     BSTAMP(4);
     BRSTAMP(9);
-}
-
-// An fp16 value as a signed count of 2^-24 (every finite fp16 is one:
-// (1024 + m) << (e - 1) for normals, m for subnormals); |x| < 2^41.
-NGP_DEV int64_t half_fixed24(uint32_t bits) {
-    const uint32_t e = (bits >> 10) & 31u, m = bits & 1023u;
-    const int64_t mag = e ? (int64_t)(1024u | m) << (e - 1) : (int64_t)m;
-    return (bits & 0x8000u) ? -mag : mag;
 }
 
 // Persistent accumulation: every workgroup reads all bins' counts, forms the
@@ -1136,8 +1115,10 @@ NGP_DEV int64_t half_fixed24(uint32_t bits) {
 // integer LDS atomics: ds_add_u64 costs ~15 cycles per wave-instruction on
 // gfx950 against ~195 for ds_add_f32 / ds_pk_add_f16 (tools/lds_atomic_probe).
 // All item loads of a batch are issued before its adds. The image is then
-// written to the fp16 table: a plain 16-byte read-modify-write when the unit
-// is its bin's only one, packed fp16 atomics otherwise. A non-finite item
+// written to the fp16 table when the unit is its bin's only one; the units of
+// a bin with several add their images into the bin's int64 slot and the last
+// to arrive writes the table. The first unit of a bin whose items ran past its
+// capacity folds the bin's slice of the spill image in first. A non-finite item
 // (inf / NaN: fp16 overflow under the loss scale) cannot be carried by the
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
@@ -1176,7 +1157,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                  const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
                  bool external, AccAdam ad, unsigned long long* __restrict__ msums,
                  uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing,
-                 int32_t* __restrict__ reset_counter) {
+                 int32_t* __restrict__ reset_counter, unsigned long long* __restrict__ spill,
+                 uint32_t* __restrict__ spill_bad) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     // [entry][channel]; a channel-planar image (8-byte lane stride for the
     // 64-bit atomics instead of 16) measured the same
@@ -1265,7 +1247,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             if (j0 + j >= per || b >= nbins) break;
             while (level + 1 < nlev && b >= s_bin0[level + 1]) ++level;
             const uint32_t n = min(cv[j], s_cap[level]);
-            bn[b] = n | (cv[j] > s_cap[level] ? 0x80000000u : 0u);  // top bit: items went atomic
+            bn[b] = n | (cv[j] > s_cap[level] ? 0x80000000u : 0u);  // top bit: items spilled
             const uint32_t nu = (n + kSegItems - 1) / kSegItems;      // n: the clipped count
             upre[b] = nu;
             mine += nu;
@@ -1321,15 +1303,12 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // No bool members: with them the struct lived in scratch memory (a
     // private-segment load and store per unit, waited on like any other).
     // flags; fresh: the table slice is known to be zero; multi: one of several
-    // units of a bin of a zeroed grad, finished through the bin's int64 slot
-    constexpr uint32_t kOwner = 1, kFresh = 2, kMulti = 4;
+    // units of a bin, finished through the bin's int64 slot; spill: the bin's
+    // first unit, and items of the bin went to the spill image
+    constexpr uint32_t kOwner = 1, kFresh = 2, kMulti = 4, kSpill = 8;
     struct Unit {
         uint32_t level, lbin, gb, s0, s1, ne, flags, slot, nunits;
-#if NGP_SOA_ITEMS
-        uint32_t i0;  // the bin's first item slot
-#else
         const uint64_t* src;
-#endif
         ngp_half2* tbl;
     };
     // The unit's bin: the last bin whose first unit is <= u, found 64 ways
@@ -1350,18 +1329,15 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         const bool owner = r.nunits == 1;
         r.level = 63u - (uint32_t)__builtin_clzll(__ballot(lane < nlev && s_bin0[lane] <= gb));
         r.lbin = gb - s_bin0[r.level];
-        const bool clean = ZEROED && (bn[gb] >> 31) == 0;  // zeroed grad, no items went atomic
+        // several units: the bin's count passed kSegItems, so its capacity
+        // did and the plan gave its level int64 slots
         r.slot = s_mslot0[r.level] == kNoSlot ? kNoSlot : s_mslot0[r.level] + r.lbin;
-        r.flags = (owner ? kOwner : 0u) | (owner && clean ? kFresh : 0u) |
-                  (NGP_MULTI_UNITS && !owner && clean && r.slot != kNoSlot ? kMulti : 0u);
+        r.flags = (owner ? kOwner : kMulti) | (owner && ZEROED ? kFresh : 0u) |
+                  ((bn[gb] >> 31) != 0 && seg == 0 ? kSpill : 0u);
         r.gb = gb;
         r.s0 = seg * kSegItems;
         r.s1 = min(bn[gb] & 0x7fffffffu, r.s0 + kSegItems);
-#if NGP_SOA_ITEMS
-        r.i0 = s_item0[r.level] + r.lbin * s_cap[r.level];
-#else
         r.src = reinterpret_cast<const uint64_t*>(items + s_item0[r.level] + (size_t)r.lbin * s_cap[r.level]);
-#endif
         const uint32_t off0 = s_off[r.level];
         const uint32_t hs = s_off[r.level + 1] - off0;
         const uint32_t e0 = r.lbin * kBinEntries;
@@ -1374,16 +1350,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
         for (uint32_t q = 0; q < kAccBatch; ++q) {
             const uint32_t k = k0 + q * kAccThreads + t;
-#if NGP_SOA_ITEMS
-            // (entry, value) as the AoS item's dword pair; clamped loads, value selected away
-            const uint32_t kk = w.i0 + (k < w.s1 ? k : w.s0);
-            const uint32_t v = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(items) + kk);
-            const uint32_t e = __builtin_nontemporal_load(
-                reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(items) + bp.ents_at) + kk);
-            it[q] = k < w.s1 ? ((uint64_t)v << 32) | e : ~0ull;
-#else
             it[q] = k < w.s1 ? __builtin_nontemporal_load(w.src + k) : ~0ull;
-#endif
         }
     };
     // Only a non-fresh owner reads its slice back. No select on the loaded
@@ -1457,7 +1424,26 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             load_batch(cur, k0, it);
         }
         STAMP(sb + 1, __builtin_amdgcn_s_memtime());
-        const bool sparse = (cur.flags & kFresh) && cur.s1 - cur.s0 <= kSparseMax;
+        if (cur.flags & kSpill) {
+            // the bin's spilled items: add its slice of the spill image (one
+            // entry per lane, after every item add has landed) and clear it
+            lds_barrier();
+            unsigned long long* sp = spill + 2 * ebase;
+#pragma unroll 1
+            for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
+                const ulonglong2 x = reinterpret_cast<const ulonglong2*>(sp)[e];
+                if (x.x | x.y) {
+                    acc[e * C] += x.x;
+                    acc[e * C + 1] += x.y;
+                    reinterpret_cast<ulonglong2*>(sp)[e] = ulonglong2{0ull, 0ull};
+                }
+            }
+            if (t == 0 && spill_bad[cur.gb]) {
+                bad = true;
+                spill_bad[cur.gb] = 0u;
+            }
+        }
+        const bool sparse = (cur.flags & (kFresh | kSpill)) == kFresh && cur.s1 - cur.s0 <= kSparseMax;
         uint32_t ent[kSparseQ];  // sparse: this lane's items' entries (0xffffffff: none)
 #pragma unroll
         for (uint32_t q = 0; q < kSparseQ; ++q) ent[q] = it[q] == ~0ull ? 0xffffffffu : (uint32_t)it[q];
@@ -1591,7 +1577,13 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                 for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
                     const int64_t x0 = (int64_t)atomicExch(sums + 2 * e, 0ull);
                     const int64_t x1 = (int64_t)atomicExch(sums + 2 * e + 1, 0ull);
-                    const ngp_half2 n{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
+                    float o0 = 0.0f, o1 = 0.0f;  // a grad that was not zeroed: added to
+                    if (!ZEROED && (x0 != 0 || x1 != 0)) {
+                        const ngp_half2 o = cur.tbl[e];
+                        o0 = (float)o[0];
+                        o1 = (float)o[1];
+                    }
+                    const ngp_half2 n{(ngp_half)(o0 + (float)x0 * q24), (ngp_half)(o1 + (float)x1 * q24)};
                     inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
                     if (adam_bin) {
                         float2 pp = a_sp[ebase + e], mm = a_sm[ebase + e], vv = a_sv[ebase + e];
@@ -1622,20 +1614,6 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                 const ngp_half2 n{(ngp_half)((float)o[0] + (float)x0 * q24), (ngp_half)((float)o[1] + (float)x1 * q24)};
                 inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
                 cur.tbl[e] = n;
-            }
-        } else {
-            need_zero = true;
-            for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
-                const ulonglong2 xx = acc_entry(e);
-                const int64_t x0 = (int64_t)xx.x, x1 = (int64_t)xx.y;
-                if (x0 == 0 && x1 == 0) continue;
-                const ngp_half2 v{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
-                if (nonfinite) {  // the returning atomic: the entry's new value is checked
-                    const ngp_half2 o = __builtin_amdgcn_global_atomic_fadd_v2f16(cur.tbl + e, v);
-                    inf_out |= !half2_sum_finite(o, v);
-                } else {
-                    __builtin_amdgcn_global_atomic_fadd_v2f16(cur.tbl + e, v);
-                }
             }
         }
         // a NaN grad marks a bad unit for a caller without the flag (a flagged
@@ -1701,18 +1679,18 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
     }
     if (slots >= 0xffffffffull) bp.nlev = 0;  // item offsets are 32-bit: fall back to atomics
     bp.total_bins = bins;
-    bp.ents_at = NGP_SOA_ITEMS ? (size_t)((slots * 4 + 255) / 256 * 256) : 0u;
+    bp.spill_entries = bp.nlev ? (uint32_t)offsets_host[bp.nlev] : 0u;
     return bp;
 }
 
 static size_t bin_counters_bytes(const BinPlan& bp) { return ((size_t)bp.total_bins * 4 + 255) / 256 * 256; }
 
 // workspace: [bin cursors][retire counter][items][int64 sums of the multi-unit
-// slots][their arrival counters]
+// slots][their arrival counters][timing ring][spill image: int64 counts per
+// binned table entry and channel][spill marks per bin]
 static size_t bin_items_bytes(const BinPlan& bp) {
     size_t slots = 0;
     for (uint32_t l = 0; l < bp.nlev; ++l) slots += (size_t)bp.nbins[l] * bp.cap[l];
-    if (NGP_SOA_ITEMS) return (slots * 4 + 255) / 256 * 256 + (slots * 2 + 255) / 256 * 256;
     return (slots * sizeof(BinItem) + 255) / 256 * 256;
 }
 static size_t bin_sums_offset(const BinPlan& bp) { return bin_counters_bytes(bp) + 256 + bin_items_bytes(bp); }
@@ -1723,8 +1701,15 @@ static size_t bin_arrive_offset(const BinPlan& bp) {
 static size_t bin_timing_offset(const BinPlan& bp) {
     return bin_arrive_offset(bp) + ((size_t)bp.nmslots * 4 + 255) / 256 * 256;
 }
+static size_t bin_spill_offset(const BinPlan& bp) {
+    return bin_timing_offset(bp) + ((size_t)(kTimingEnds + NGP_GRID_TIMING_RING * NGP_GRID_TIMING_MAX_WG) * 4 + 255) /
+                                       256 * 256;
+}
+static size_t bin_spill_bad_offset(const BinPlan& bp) {
+    return bin_spill_offset(bp) + (size_t)bp.spill_entries * 2 * sizeof(unsigned long long);
+}
 static size_t bin_workspace_bytes(const BinPlan& bp) {
-    return bin_timing_offset(bp) + (size_t)(kTimingEnds + NGP_GRID_TIMING_RING * NGP_GRID_TIMING_MAX_WG) * 4;
+    return bin_spill_bad_offset(bp) + ((size_t)bp.total_bins * 4 + 255) / 256 * 256;
 }
 
 template <typename T, uint32_t D, uint32_t C>
@@ -2252,6 +2237,8 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         uint32_t* timing =
             timed ? reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_timing_offset(bp)) : nullptr;
         uint32_t* marrive = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_arrive_offset(bp));
+        auto* spill = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + bin_spill_offset(bp));
+        auto* spill_bad = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_spill_bad_offset(bp));
         // (level, point block) + one column of slab-reduce blocks when merged
         const ngp_reduce::ReduceJobs rjv = rj ? *rj : ngp_reduce::ReduceJobs{};
         if (!rj) nred = 0;
@@ -2264,11 +2251,11 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         if (nbmax <= kMaxBinsPerLevel)
             k_grid_bwd_bin<3, kMaxBinsPerLevel><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl);
+                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad);
         else
             k_grid_bwd_bin<3, kMaxBinsPerLevelBig><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl);
+                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad);
         // two persistent workgroups per CU while both fit the CU's LDS (the
         // 64 KiB image + two words per bin), else one
         const size_t dyn = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
@@ -2277,11 +2264,11 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         if (zeroed)
             k_grid_bin_accum<true><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
-                marrive, timing, reset);
+                marrive, timing, reset, spill, spill_bad);
         else
             k_grid_bin_accum<false><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
-                marrive, timing, reset);
+                marrive, timing, reset, spill, spill_bad);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
