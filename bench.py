@@ -639,6 +639,11 @@ def timed_run(args, ft, world, dev, steps, warmup, settle, graph_steps):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # a bounded cross-workgroup wait of the in-launch emit that ran out would
+    # have made some step's sample offsets wrong: such a run is not a result
+    err = ft.device_errors()
+    if err:
+        raise RuntimeError(f"march emit wait timed out during the run (error word {err:#x})")
     grid_clock = ft.grid_timing(last=steps)  # the timed region's grid backwards (<= 256 of them)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)

@@ -104,6 +104,13 @@ int ngp_packbits(const float* grid, uint32_t N, float density_thresh, uint8_t* b
  * N * max_steps, plus an occupancy image of ~C * H^3 / 6 bytes), e.g. from
  * the caller's caching allocator. */
 size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_steps, uint32_t C, uint32_t H);
+/* Byte offset, inside that workspace, of a u32 error word the fused march +
+ * Adam launch's in-launch emit sets when one of its bounded cross-workgroup
+ * waits ran out (bit 0: a lower block's sample total, bit 1: the block's own
+ * offsets); the offsets it wrote are then wrong. Sticky; the caller reads and
+ * clears it (FusedTrainer.device_errors). No reference counterpart: the
+ * reference's march (raymarching.cu:405-406) takes its offsets with atomics. */
+size_t ngp_march_rays_train_error_offset(uint32_t N, uint32_t max_steps, uint32_t C, uint32_t H);
 int ngp_march_rays_train(const float* rays_o, const float* rays_d, const uint8_t* grid,
                          float bound, float dt_gamma, uint32_t max_steps, uint32_t N, uint32_t C,
                          uint32_t H, uint32_t M, const float* nears, const float* fars,

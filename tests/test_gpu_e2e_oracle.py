@@ -14,7 +14,8 @@ autocast casts restated). Two comparisons:
   and the three parameter gradients.
 
 Configs: Config 2 (Lego, bound 1, one cascade, dt_gamma 0), the Fox-shaped
-Config 3 (bound 2, two cascades, dt_gamma 1/128) and Config 5's single-GPU
+Config 3 (bound 2, two cascades, dt_gamma 1/128, the bench leg's Fox-shaped
+occupancy: >= 20 samples per ray, cascade-1 samples) and Config 5's single-GPU
 shapes (Truck: 1920x1080 images, L16 log2T 22 = 39,625,280 table entries, the
 binned backward's 1,024-bin levels with per-item flushes; bound 1).
 
@@ -38,12 +39,15 @@ pytestmark = pytest.mark.gpu
 def _setup(cuda, bound, dt_gamma, log2T=19, hw=(800, 800), num_rays=1024, mean_count=80000):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
-    from nerf.provider import SyntheticLego, lego_bitfield
+    from nerf.provider import SyntheticLego, fox_bitfield, lego_bitfield
     torch.manual_seed(0)
     model = NeRFNetwork(bound=bound, cuda_ray=True, density_thresh=10, log2_hashmap_size=log2T).to(cuda)
     with torch.no_grad():  # a non-trivial field: larger table values than the 1e-4 init
         model.encoder.embeddings.normal_(0, 0.05)
-    bits = lego_bitfield(cascade=model.cascade, bound=float(bound))
+    # bound 2: the Fox-shaped occupancy the bench's Config-3 leg marches (~30
+    # samples per ray, cascade-1 cells); the Lego boxes at bound 2 give ~3
+    occ = fox_bitfield if bound == 2 else lego_bitfield
+    bits = occ(cascade=model.cascade, bound=float(bound))
     model.density_bitfield.copy_(torch.from_numpy(bits).to(cuda))
     data = SyntheticLego(cuda, H=hw[0], W=hw[1], num_rays=num_rays)
     M = mean_count + 128 - mean_count % 128
@@ -132,6 +136,10 @@ def test_fused_step_stages_match_oracle(cuda, parity_report, bound, dt_gamma, lo
         assert ft.enc.embeddings.shape[0] == (39625280 if log2T == 22 else 6119864)
     n = _fused_batch(ft)
     assert n > 1000
+    if bound == 2:  # Config 3 marches: >= 20 samples / ray, some in cascade 1 (|x|max > 1, mip_from_pos)
+        assert n >= 20 * ft.N, n / ft.N
+        outer = int((np.abs(_np(ft.xyzs)[:n]).max(-1) > 1.0).sum())
+        assert outer > 0.05 * n, outer
     inp = _oracle_inputs(ft)
     # ---- march (bit-exact: counts, ray offsets, samples)
     aabb = np.array([-bound] * 3 + [bound] * 3, np.float32)

@@ -300,6 +300,7 @@ def test_fused_training_reduces_loss_and_captures(cuda, bound, dt_gamma):
     late = ft.last_loss
     assert np.isfinite(late) and late < losses[0], (losses, late)
     assert ft.optimizer_steps >= 60
+    assert ft.device_errors() == 0  # no in-launch emit wait ran out
 
 
 def test_mlp_fused_epilogues_match_unfused(cuda):

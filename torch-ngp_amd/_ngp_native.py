@@ -37,6 +37,7 @@ SIGNATURES = {
     "ngp_morton3D_invert": [c_vp, c_u32, c_vp, c_vp],
     "ngp_packbits": [c_vp, c_u32, c_f32, c_vp, c_vp],
     "ngp_march_rays_train_workspace_bytes": [c_u32, c_u32, c_u32, c_u32],
+    "ngp_march_rays_train_error_offset": [c_u32, c_u32, c_u32, c_u32],
     "ngp_march_occupancy_build": [c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_sz, c_vp],
     "ngp_march_rays_train_prebuilt": [c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32, c_u32, c_u32,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp],
@@ -187,6 +188,7 @@ _RESTYPES = {
     "ngp_grid_encode_backward_fused_counter_bytes": c_sz,
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
     "ngp_march_rays_train_workspace_bytes": c_sz,
+    "ngp_march_rays_train_error_offset": c_sz,
     "ngp_fused_state_bytes": c_sz,
     "ngp_render_state_bytes": c_sz,
     "ngp_render_count": c_vp,

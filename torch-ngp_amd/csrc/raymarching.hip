@@ -733,6 +733,7 @@ constexpr uint32_t kMarchAdamWaves = NGP_MARCH_ADAM_WAVES;
 constexpr uint32_t kEmitMaxBlockRays = 64;
 struct MarchEmit {
     uint32_t* ticket;            // null: the emit launch does it; else the workspace's ticket counter
+    uint32_t* error;             // bit 0: a lower rank's total never arrived, bit 1: the block's offsets never did
     unsigned long long* words;   // [G] published block totals
     int32_t* counter;            // counter[0] = end, counter[1] += N (the last rank)
     float *xyzs, *dirs, *deltas;
@@ -833,16 +834,20 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
                                __HIP_MEMORY_SCOPE_AGENT);
         // (bounded: a word that never arrives -- a broken launch, not a slow
         // one: the march itself takes ~20 us -- ends the wait after ~0.1 s
-        // with wrong offsets rather than a hung GPU)
+        // with wrong offsets rather than a hung GPU, and records it in the
+        // workspace's error word, which the host reads: ngp_march_rays_train_error)
         uint32_t part = 0;
+        bool lost = false;
         for (uint32_t p = lane; p < rank; p += 64) {
             unsigned long long v = agent_load_u64(me.words + p);
             for (uint32_t spin = 0; (uint32_t)(v >> 32) != epoch1 && spin < (1u << 20); ++spin) {
                 __builtin_amdgcn_s_sleep(2);
                 v = agent_load_u64(me.words + p);
             }
+            lost |= (uint32_t)(v >> 32) != epoch1;
             part += (uint32_t)v;
         }
+        if (__ballot(lost) && lane == 0) atomicOr(me.error, 1u);
 #pragma unroll
         for (uint32_t o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
         if (lane < nb) s_off[lane] = incl - c;
@@ -860,6 +865,8 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
         for (uint32_t spin = 0; __hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u &&
                                 spin < (1u << 22); ++spin)
             __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u && lane == 0)
+            atomicOr(me.error, 2u);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     const uint32_t base = s_first, btotal = s_off[nb];
@@ -1423,6 +1430,14 @@ extern "C" size_t ngp_march_rays_train_workspace_bytes(uint32_t N, uint32_t max_
            256 * 256 + march_sync_bytes();
 }
 
+// The in-launch emit's error word (MarchEmit::error; 0 = none), from the
+// workspace's sync header: sticky until the caller clears it.
+extern "C" size_t ngp_march_rays_train_error_offset(uint32_t N, uint32_t max_steps, uint32_t C, uint32_t H) {
+    const OccLayout L = occ_layout(nullptr, C, H);
+    return march_ts_bytes(N, max_steps) + march_scan_bytes(N) +
+           (occ_image_bytes(L) + occ_scratch_bytes(L) + 255) / 256 * 256 + 4;
+}
+
 // The march + Adam launch emits the samples itself (MarchEmit) unless
 // NGP_MARCH_EMIT_INLINE=0 or a ray block would exceed kEmitMaxBlockRays.
 static bool march_emit_inline() {
@@ -1465,8 +1480,8 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
         const uint32_t rb = ngp_div_up(N, kMaxMarchBlocks);
         if (rb <= kEmitMaxBlockRays && march_emit_inline()) {
             uint8_t* sync = img + (occ_image_bytes(L) + occ_scratch_bytes(L) + 255) / 256 * 256;
-            me = MarchEmit{reinterpret_cast<uint32_t*>(sync), reinterpret_cast<unsigned long long*>(sync + 256),
-                           counter, xyzs, dirs, deltas, M, rb};
+            me = MarchEmit{reinterpret_cast<uint32_t*>(sync), reinterpret_cast<uint32_t*>(sync) + 1,
+                           reinterpret_cast<unsigned long long*>(sync + 256), counter, xyzs, dirs, deltas, M, rb};
         }
         k_march_train<kMarchAdamWaves><<<kMaxMarchBlocks, kSegThreads, L.ngroups ? kMarchLdsBytes : 0, st>>>(
             rays_o, rays_d, grid, img, L, k, N, nears, fars, noises, rays, ts, counter, scan, *ma, me);

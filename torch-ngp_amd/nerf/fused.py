@@ -1147,7 +1147,7 @@ class FusedTrainer:
         per-launch device times of the last R replays. multi=S (world 1, and
         the whole data-parallel step): also a graph of S consecutive step
         bodies, replayed by run()."""
-        for _ in range(max(1, warmup)):
+        for _ in range(warmup):
             self.step()
         torch.cuda.synchronize()
         if ring and not self.dp:
@@ -1197,6 +1197,7 @@ class FusedTrainer:
             self._dp_whole = None
             self.graph_multi, self._multi = None, 1
             self._pre_ahead = self._ahead  # the batch state the graph assumes (and leaves)
+            err = None
             try:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
@@ -1208,13 +1209,23 @@ class FusedTrainer:
                             self._dp_body()
                     self.graph_multi, self._multi = gm, multi
                 self._dp_whole = g
-            except RuntimeError as e:  # a stack that cannot capture the collectives: three graphs
-                print(f"FusedTrainer: whole-step capture failed ({e!r:.200}); collectives between graphs",
-                      file=sys.stderr)
-                torch.cuda.synchronize()
+            except RuntimeError as e:  # a stack that cannot capture the collectives
+                err = e
+            # every rank takes the same form: a capture that failed on one rank
+            # only would otherwise leave the ranks issuing different collective
+            # sequences. Capture records without running, so no
+            # collective of a step has run on any rank yet.
+            torch.cuda.synchronize()
+            ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=self.dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0:
+                print(f"FusedTrainer: whole-step capture failed on {'this' if err is not None else 'another'} rank "
+                      f"({err!r:.200}); collectives between graphs on every rank", file=sys.stderr)
+                self._dp_whole = None
                 self._dp_graph = False
                 self.graph_multi, self._multi = None, 1
-                self.capture(warmup=0)
+                self._ahead = self._pre_ahead  # the batch state before the recording
+                self.capture(warmup=0)  # the three graphs, no extra step
         else:
             graphs = {k: torch.cuda.CUDAGraph() for k in ("opt", "pre", "net")}
             with torch.cuda.graph(graphs["opt"]):
@@ -1262,6 +1273,18 @@ class FusedTrainer:
     def sample_count(self):
         """Samples of the last step's batch."""
         return int(self._recent_counts(1)[0].item())
+
+    def device_errors(self, clear=True):
+        """The in-launch emit's error word (ngp_march_rays_train_error_offset:
+        a bounded cross-workgroup wait ran out, so some step's sample offsets
+        were wrong); 0 when every step was sound. A host sync."""
+        m = self.model
+        at = int(nat.lib().ngp_march_rays_train_error_offset(self.N, self.max_steps, m.cascade, m.grid_size))
+        w = self.march_ws[at:at + 4].view(torch.int32)
+        v = int(w.item())
+        if clear and v:
+            w.zero_()
+        return v
 
     # ------------------------------------------------------ checkpoints
     # StepState as int32 words: 0 scale (f32), 4 growth tracker, 6 Adam steps,
