@@ -345,17 +345,12 @@ def dp_path_probe(args, model, data, dev, headline):
         whole_captured = bool(used_graph and ft._dp_whole is not None)
         graph_steps = ft._multi
         phases = ft.timed_steps(args.kernel_steps)
-        # the three-graph form (NGP_DP_GRAPH=0: collectives between the graphs), for comparison
-        three = None
-        os.environ["NGP_DP_GRAPH"] = "0"
-        try:
-            m3, d3, _, _, _, _, _ = make_workload(args.workload, dev, 1, args.num_rays)
-            ft3, _ = make_trainer(args, m3, d3, 1, dev, dtg, distributed=True)
-            e3, g3, _ = timed_run(args, ft3, 1, dev, steps, 5, 300, 1)
-            three = {"ms_per_step": round(e3 / steps * 1e3, 4), "graphs": bool(g3)}
-            del ft3, m3
-        finally:
-            del os.environ["NGP_DP_GRAPH"]
+        # the three-graph form (dp_graph=False: collectives between the graphs), for comparison
+        m3, d3, _, _, _, _, _ = make_workload(args.workload, dev, 1, args.num_rays)
+        ft3, _ = make_trainer(args, m3, d3, 1, dev, dtg, distributed=True, options=dict(dp_graph=False))
+        e3, g3, _ = timed_run(args, ft3, 1, dev, steps, 5, 300, 1)
+        three = {"ms_per_step": round(e3 / steps * 1e3, 4), "graphs": bool(g3)}
+        del ft3, m3
         grad_bytes = 2 * ft.total  # the flat fp16 gradient = the fp16 forward copy
         truck_bytes = 2 * _flat_total(22)
         W = 8
@@ -561,32 +556,20 @@ def launch_bytes(ft, samples, rays, live=None):
     """SURVEY §8(d) per-unit bytes of each launch of the world-1 step body
     (timed_body_steps names): None for the MFMA-bound MLP launches. The grid
     backward's 1,100 B are per LIVE sample when the backwards walk only the
-    rows with a nonzero gradient (NGP_LIVE_ROWS; `live` = their count). With the
-    grid forward split in two launches (NGP_ADAM_UNDER_FWD), the table values
-    past the split level are swept by the first one: its bytes are those
-    values' Adam bytes plus its levels' share of the forward's 588 B / sample
-    (12 B of coordinates + 36 B per level)."""
+    rows with a nonzero gradient (options live_rows; `live` = their count)."""
     march = 48 * rays + 32 * samples
     out = {"march_rays_train+adam": adam_bytes(ft) + march, "march_rays_train": march,
            "step_head": None, "grid_encode_forward": 588 * samples, "grid_encode_backward": 1100 * (samples if live is None else live),
            "composite_loss": (32 + 52) * rays + (24 + 40) * samples, "ffmlp_forward": None, "ffmlp_backward": None}
-    split = getattr(ft, "_fwd_split", None)
-    if split is not None:
-        f, j2 = split
-        late = 28 * int(j2.sizes[0])  # table values: p, m, v read + write, fp16 grad read + clear
-        L = int(ft.enc.num_levels)
-        out["march_rays_train+adam"] = adam_bytes(ft) - late + march
-        out["grid_encode_forward+adam"] = late + (12 + 36 * f) * samples
-        out["grid_encode_forward"] = (12 + 36 * (L - f)) * samples
     return out
 
 
-def make_trainer(args, model, data, world, dev, dt_gamma, grid_timing=True, distributed=None):
+def make_trainer(args, model, data, world, dev, dt_gamma, grid_timing=True, distributed=None, options=None):
     """A FusedTrainer with its sample buffer sized as upstream sizes it
     (mean_count = measured counts x 1.25, update_extra_state)."""
     from nerf.fused import FusedTrainer
     dp = world > 1 if distributed is None else distributed
-    probe = FusedTrainer(model, data, M=args.num_rays * 64, distributed=dp, dt_gamma=dt_gamma)
+    probe = FusedTrainer(model, data, M=args.num_rays * 64, distributed=dp, dt_gamma=dt_gamma, options=options)
     counts = []
     for _ in range(4):
         probe.step()
@@ -599,7 +582,8 @@ def make_trainer(args, model, data, world, dev, dt_gamma, grid_timing=True, dist
     probe.flush()  # data parallel: every rank's shard of the masters gathered back
     del probe
     torch.cuda.empty_cache()
-    ft = FusedTrainer(model, data, M=mean_count, distributed=dp, dt_gamma=dt_gamma, grid_timing=grid_timing)
+    ft = FusedTrainer(model, data, M=mean_count, distributed=dp, dt_gamma=dt_gamma, grid_timing=grid_timing,
+                      options=options)
     return ft, mean_count
 
 
@@ -669,7 +653,7 @@ def grid_roofline(grid_clock, steps, workload, all_samples=None):
            "launches_timed": calls, "samples_timed": int(sum(samp)), "avg_launch_ms": round(sum(ms) / calls, 5),
            "launch_ms_min_median_max": [round(float(v), 5) for v in (min(ms), np.median(ms), max(ms))]}
     if all_samples:
-        # the backward walks only the live rows (NGP_LIVE_ROWS): samples_timed
+        # the backward walks only the live rows (options live_rows): samples_timed
         # counts those, the bytes above are theirs. Beside it, the reference's
         # work (its backward reads every sample's gradient) over the same time:
         # an equivalent rate, not bytes this kernel moved
@@ -734,7 +718,7 @@ def run_fused(args, model, data, bits, world, dev):
         kernel_ms, per_step, counts = ft.timed_steps(args.kernel_steps, with_counts=True)
     counts = [min(int(c), ft.M) for c in counts]
     rows = float(np.mean(counts))
-    # the rows the backwards walk (NGP_LIVE_ROWS: those with a nonzero gradient)
+    # the rows the backwards walk (options live_rows: those with a nonzero gradient)
     lc = getattr(ft, "body_live_counts", None) if world == 1 else None
     live = float(np.mean(lc)) if lc else None
     grid = grid_roofline(grid_clock, args.steps, args.workload,
@@ -914,7 +898,7 @@ def whole_step_bytes(samples, rays, n_params, n_table, live=None):
     value), march 48 B/ray + 32 B/sample, composite forward 32 B/ray + 24
     B/sample and backward 52 B/ray + 40 B/sample, SH 76 B/direction, dense Adam
     28 B/parameter. The backward's bytes are per live sample when the
-    backwards walk only those (`live`, NGP_LIVE_ROWS)."""
+    backwards walk only those (`live`, options live_rows)."""
     return (588 * samples + 1100 * (samples if live is None else live) + 2 * n_table + 48 * rays + 32 * samples + 32 * rays + 24 * samples
             + 52 * rays + 40 * samples + 76 * samples + 28 * n_params)
 

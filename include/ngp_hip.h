@@ -171,14 +171,15 @@ typedef struct ngp_adam_job {
     float grad_mult;
     void* clear;            /* zeroed by the launch too (the grid backward's bin cursors), or NULL */
     uint32_t clear_bytes;   /* multiple of 16, clear 16-byte aligned */
-    uint32_t flags;         /* NGP_ADAM_JOB_END_LATER: the emit launch leaves the bookkeeping to a
-                               later launch (ngp_grid_encode_forward_fused_adam's end block) */
+    uint32_t flags;         /* NGP_ADAM_JOB_TAIL_LATER | NGP_ADAM_JOB_EMIT_LAUNCH (below) or 0 */
 } ngp_adam_job;
-#define NGP_ADAM_JOB_END_LATER 1u
 /* ... and the emit launch's whole tail row (bookkeeping + MLP fragment packs) is
  * left to ngp_grid_encode_forward_fused_tail: with the samples emitted by the
  * march launch itself, the march is then ONE launch */
 #define NGP_ADAM_JOB_TAIL_LATER 2u
+/* ... and the samples are emitted by the march's own emit launch instead of
+ * inside the march + Adam launch (the in-launch emit's equivalence tests) */
+#define NGP_ADAM_JOB_EMIT_LAUNCH 4u
 int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const float* rays_d, const uint8_t* grid,
                                        float bound, float dt_gamma, uint32_t max_steps, uint32_t N,
                                        uint32_t C, uint32_t H, uint32_t M, const float* nears,
@@ -436,45 +437,6 @@ int ngp_grid_encode_backward_fused_reduce_batch_live(
     size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite, int32_t n_nets, void* const* mlp_workspaces,
     const uint32_t* mlp_Bs, const uint32_t* in_dims, const uint32_t* hidden_dims, const uint32_t* num_layers,
     void* const* grad_weights, int32_t* mlp_nonfinite, const ngp_batch_job* job, void* stream);
-/* Fused Adam over the hash table (world 1; torch.optim.Adam + GradScaler of
- * nerf/utils.py:975-978 / main_nerf.py:194 on the table, inside the grid
- * backward). The table's fp32 parameters and Adam moments are double
- * buffered: buffers [state cur] are current, an update writes the other ones
- * and the step's GradScaler bookkeeping makes them current unless the step is
- * skipped (an inf/nan anywhere), so a skip leaves the table untouched as
- * torch's does. The accumulate applies Adam to every slice it owns (one work
- * unit per bin of a zeroed grad: the slice's exact sums, rounded to the fp16
- * grad torch would see, unscaled) and tags the bin in `done`; the optimizer
- * entries (*_db) then update the other slices from the fp16 grad buffer.
- * slices: nslices x (first entry, entries, bin or 0xffffffff) covering the
- * table (ngp_grid_table_slices); done: one word per bin (zero-filled once). */
-typedef struct ngp_adam_table {
-    float* params[2];
-    float* exp_avg[2];
-    float* exp_avg_sq[2];
-    void* grad;               /* fp16 [sum_T * C] */
-    uint64_t size;            /* sum_T * C: values per buffer */
-    uint32_t* done;
-    const uint32_t* slices;   /* device */
-    uint32_t nslices;
-    uint32_t channels;        /* C (2) */
-    float lr, beta1, beta2, eps;
-    int32_t iters;            /* LambdaLR: lr * 0.1 ** min(epoch / iters, 1) */
-} ngp_adam_table;
-/* The table's slices (host array of 3 * max_slices words): the binned
- * backward's bins in bin order, then the levels it does not bin in slices of
- * <= 4096 entries (bin 0xffffffff). Returns their number, or < 0. */
-int ngp_grid_table_slices(const int32_t* offsets_host, uint32_t B, uint32_t D, uint32_t C, uint32_t L, float S,
-                          uint32_t H, int32_t align_corners, uint32_t* slices_host, uint32_t max_slices);
-/* ngp_grid_encode_forward_fused reading table[*sel] (sel: ngp_fused_table_select). */
-/* The fused step's grid forward over levels [level_lo, level_hi) only, with
- * (job non-null) the part of the previous step's Adam sweep that job holds
- * as 256-thread blocks of the same launch, and (end_state non-null) the
- * deferred GradScaler / LambdaLR / loss bookkeeping of that update as one
- * block. The caller orders the launches so that no launch's forward reads a
- * level its own Adam blocks write, and the bookkeeping comes after every
- * launch carrying Adam (DESIGN.md "Adam under the grid forward"). fp16
- * outputs, [L, B, C] layout, rows clipped at *count. */
 /* ngp_grid_encode_forward_fused (out_layout 0) with the fused step's tail as
  * extra workgroups dispatched first: the deferred GradScaler / LambdaLR / loss
  * bookkeeping of the update the march launch applied (state; when pending) and
@@ -489,29 +451,6 @@ int ngp_grid_encode_forward_fused_tail(const float* xyz, float bound, const void
                                        const void* const* mlp_weights, const uint32_t* in_dims,
                                        const uint32_t* hidden_dims, const uint32_t* num_layers, void* const* images,
                                        void* stream);
-int ngp_grid_encode_forward_fused_adam(const float* xyz, float bound, const void* embeddings, int32_t emb_dtype,
-                                       const int32_t* offsets, void* outputs, uint32_t B, const int32_t* count,
-                                       uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H, uint32_t gridtype,
-                                       int32_t align_corners, uint32_t interp, uint32_t level_lo, uint32_t level_hi,
-                                       const ngp_adam_job* job, void* state, void* end_state, float growth_factor,
-                                       float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
-                                       const float* loss_ray, uint32_t n_rays, void* stream);
-int ngp_grid_encode_forward_fused_sel(const float* xyz, float bound, const void* table0, const void* table1,
-                                      const int32_t* sel, int32_t emb_dtype, const int32_t* offsets,
-                                      void* outputs, uint32_t B, const int32_t* count, uint32_t D, uint32_t C,
-                                      uint32_t L, float S, uint32_t H, uint32_t gridtype, int32_t align_corners,
-                                      uint32_t interp, int32_t out_layout, void* stream);
-/* ngp_grid_encode_backward_fused (grad_layout must carry NGP_GRID_GRAD_ZEROED)
- * with Adam applied by the accumulate to the slices it owns (see
- * ngp_adam_table); grad_embeddings == at->grad receives only the other
- * slices' grads. state: the fused step's StepState. */
-int ngp_grid_encode_backward_fused_adam(const void* grad, const float* xyz, float bound,
-                                        const int32_t* offsets, void* grad_embeddings, uint32_t B,
-                                        const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
-                                        uint32_t H, uint32_t gridtype, int32_t align_corners,
-                                        uint32_t interp, const int32_t* offsets_host, void* workspace,
-                                        size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
-                                        const ngp_adam_table* at, void* state, void* stream);
 /* Weight-fragment images (forward + transposed, per matmul) of n networks in
  * one launch; image k needs ngp_ffmlp_image_bytes of its network. The
  * forward/backward *_rows calls below take the image (nullable: the weights
@@ -577,20 +516,6 @@ int ngp_nerf_backward_live(const void* g_color_out, const void* color_in, const 
                            uint32_t num_layers, uint32_t hidden_dim_color, uint32_t num_layers_color,
                            void* sigma_workspace, size_t sigma_workspace_bytes, void* color_workspace,
                            size_t color_workspace_bytes, uint32_t* timing, void* stream);
-/* ngp_nerf_backward_live with the list joined in the same launch from the
- * per-ray lists of ngp_nerf_composite_loss_ray_lists (rays [N, 3] of the march,
- * live_cnt [N], ray_rows [M]): each workgroup scans the N counts and writes
- * the list positions of its own chunks into live_rows [M]; workgroup 0 writes
- * live_total[0]. live_rows / live_total then feed
- * ngp_grid_encode_backward_fused_reduce_batch_live as after
- * ngp_nerf_composite_loss_live. 1 <= N <= 4096. */
-int ngp_nerf_backward_live_list(const void* g_color_out, const void* color_in, const void* color_image, void* g_h,
-                                const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
-                                const int32_t* rays, uint32_t N, const int32_t* live_cnt, const int32_t* ray_rows,
-                                int32_t* live_rows, int32_t* live_total, uint32_t hidden_dim, uint32_t num_layers,
-                                uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
-                                size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
-                                uint32_t* timing, void* stream);
 /* Sums the deferred dW partials of n backward calls (same B and shapes as
  * those calls) into grad_weights[k], in one launch (n <= 4). nonfinite
  * (nullable): set to 1 when a written grad is inf/nan (GradScaler's check). */
@@ -636,16 +561,6 @@ int ngp_nerf_composite_loss_live(const float* sigma, const void* color_out, cons
                                  void* state, void* grad_color_out, void* grad_h_sigma, float* out_image,
                                  float* out_ws, float* loss_ray, int32_t* ray_rows, int32_t* live_cnt,
                                  int32_t* live_rows, int32_t* live_total, void* stream);
-/* ngp_nerf_composite_loss plus each ray's live rows, listed in the ray's own
- * row range of ray_rows [M] (live_cnt [N] of them), not yet joined: the
- * one-launch form of ngp_nerf_composite_loss_live, whose list
- * ngp_nerf_backward_live_list joins in its own launch. */
-int ngp_nerf_composite_loss_ray_lists(const float* sigma, const void* color_out, const void* h_sigma,
-                                      const float* deltas, const int32_t* rays, uint32_t M, uint32_t N,
-                                      float T_thresh, float density_scale, const float* gt, uint32_t gt_channels,
-                                      const float* bg, void* state, void* grad_color_out, void* grad_h_sigma,
-                                      float* out_image, float* out_ws, float* loss_ray, int32_t* ray_rows,
-                                      int32_t* live_cnt, void* stream);
 /* scaler_enabled of the optimizer entries: GradScaler off; on, with its inf
  * check as a sweep over the grads; on, with the check already made by the
  * kernels that wrote the grads into the state's flag (ngp_fused_inf_flag). */
@@ -656,13 +571,6 @@ int ngp_nerf_composite_loss_ray_lists(const float* sigma, const void* color_out,
  * reads; local != 0: the data-parallel guard's per-rank flag), for the
  * nonfinite arguments of the grid backward and the MLP reduce. */
 int32_t* ngp_fused_inf_flag(void* state, int32_t local);
-/* The state's current-table word (ngp_adam_table double buffer). */
-int32_t* ngp_fused_table_select(void* state);
-/* out fp16 [entries * C] = half(params[cur]) of the double-buffered table. */
-int ngp_fused_table_to_half(const ngp_adam_table* at, const void* state, void* out, uint64_t n, void* stream);
-/* Make buffer 0 current (copy buffer 1's params / moments over it when it is
- * the current one) and set cur = 0: host read-outs then see buffer 0. */
-int ngp_fused_table_normalize(const ngp_adam_table* at, void* state, uint64_t n, void* stream);
 /* Adam (+ GradScaler inf check/unscale/update, LambdaLR 0.1^(epoch/iters))
  * over n_tensors fp32 params with fp16 grads; half_params[k] (nullable) is
  * refreshed with half(p) after the update; grads are zeroed when zero_grads;
@@ -717,32 +625,6 @@ int ngp_fused_optimizer_update_head(int32_t n_tensors, float* const* params, voi
                                     float* rays_d, float* rgba, float* bg, float* nears, float* fars,
                                     float* noises, int32_t* counter, int32_t* step_counter, void* clear,
                                     uint32_t clear_bytes, void* stream);
-
-/* The three optimizer entries above with the hash table double buffered and
- * updated by the grid backward (ngp_adam_table): the tensor lists hold the
- * other parameters (the MLPs, updated in place as before); the table's slices
- * the accumulate did not update are updated here, from at->grad, into the
- * other buffer, which the bookkeeping then makes current (skipped steps: not). */
-int ngp_fused_optimizer_step_db(int32_t n_tensors, float* const* params, void* const* grads,
-                                float* const* exp_avg, float* const* exp_avg_sq, void* const* half_params,
-                                const uint64_t* sizes, float lr, float beta1, float beta2, float eps,
-                                int32_t iters, int32_t zero_grads, float grad_mult, float growth_factor,
-                                float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
-                                uint32_t num_rays, const int32_t* counter, int32_t* step_counter,
-                                const float* loss_ray, void* state, const ngp_adam_table* at, void* stream);
-int ngp_fused_optimizer_update_db(int32_t n_tensors, float* const* params, void* const* grads,
-                                  float* const* exp_avg, float* const* exp_avg_sq, void* const* half_params,
-                                  const uint64_t* sizes, float lr, float beta1, float beta2, float eps,
-                                  int32_t iters, int32_t zero_grads, float grad_mult, int32_t scaler_enabled,
-                                  void* state, const ngp_adam_table* at, void* stream);
-int ngp_fused_optimizer_update_head_db(
-    int32_t n_tensors, float* const* params, void* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
-    void* const* half_params, const uint64_t* sizes, float lr, float beta1, float beta2, float eps, int32_t iters,
-    int32_t zero_grads, float grad_mult, int32_t scaler_enabled, void* state, const float* poses, uint32_t n_poses,
-    const float* intrinsics4, uint32_t H, uint32_t W, uint32_t N, const float* boxes, int32_t nboxes,
-    const float* aabb6, float min_near, uint32_t seed, float* rays_o, float* rays_d, float* rgba, float* bg,
-    float* nears, float* fars, float* noises, int32_t* counter, int32_t* step_counter, void* clear,
-    uint32_t clear_bytes, const ngp_adam_table* at, void* stream);
 
 /* Data-parallel GradScaler guard for the sharded optimizer (nerf/fused.py,
  * world > 1), run on each rank's own fp16 gradient before the averaging

@@ -126,7 +126,7 @@ def test_oracle_composite_backward_matches_reference_autograd():
 
 
 def test_oracle_composite_backward_is_zero_past_termination():
-    """The premise of the live-row backwards (nerf/fused.py NGP_LIVE_ROWS): the
+    """The premise of the live-row backwards (nerf/fused.py options live_rows): the
     reference's composite backward stops at a ray's early termination
     (`if (T < T_thresh) break;`, raymarching.cu:680), so every sample past it
     has an exactly zero sigma and rgb gradient. Checked on the oracle's

@@ -51,9 +51,8 @@ def _setup(cuda, bound, dt_gamma, log2T=19, hw=(800, 800), num_rays=1024, mean_c
     model.density_bitfield.copy_(torch.from_numpy(bits).to(cuda))
     data = SyntheticLego(cuda, H=hw[0], W=hw[1], num_rays=num_rays)
     M = mean_count + 128 - mean_count % 128
-    # fused_adam off: the table grads are materialised for the comparison (the
-    # fused update equals the unfused one bit for bit: tests/test_gpu_fused.py)
-    return FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma, fused_adam=False)
+    # the table grads are materialised in grads[0] for the comparison
+    return FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma)
 
 
 def _np(t):

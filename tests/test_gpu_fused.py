@@ -15,8 +15,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0, fused_adam=None, occ="boxes",
-           grid_timing=None):
+def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0, occ="boxes", grid_timing=False,
+           options=None):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield, sphere_bitfield
@@ -30,7 +30,7 @@ def _setup(cuda, num_rays=1024, mean_count=30000, bound=1, dt_gamma=0.0, fused_a
     data = SyntheticLego(cuda, num_rays=num_rays)
     M = mean_count + 128 - mean_count % 128  # what run_cuda's align=128 makes of mean_count
     ref.mean_count = mean_count
-    ft = FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma, fused_adam=fused_adam, grid_timing=grid_timing)
+    ft = FusedTrainer(model, data, M=M, seed=3, dt_gamma=dt_gamma, grid_timing=grid_timing, options=options)
     return model, ref, data, ft
 
 
@@ -81,8 +81,7 @@ def test_lego_sampler(cuda):
 # shape (bound 2, two cascades, dt_gamma 1/128: the serially marched rays)
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
 def test_fused_forward_backward_matches_autograd(cuda, bound, dt_gamma):
-    # fused_adam off: every table grad is materialised (test_fused_adam_* checks the fused update)
-    model, ref, data, ft = _setup(cuda, bound=bound, dt_gamma=dt_gamma, fused_adam=False)
+    model, ref, data, ft = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
     assert model.cascade == (1 if bound == 1 else 2)
     ft._sample()
     ft.noises.zero_()  # the autograd call below marches with perturb=False
@@ -105,7 +104,7 @@ def test_fused_forward_backward_matches_autograd(cuda, bound, dt_gamma):
 
 
 def test_fused_optimizer_matches_torch_adam_and_scaler(cuda):
-    model, ref, data, ft = _setup(cuda, fused_adam=False)
+    model, ref, data, ft = _setup(cuda)
     ft._sample()
     ft._forward_backward()
     torch.cuda.synchronize()
@@ -191,7 +190,7 @@ def test_pipelined_steps_match_serial_steps(cuda):
         assert torch.equal(x.detach(), y.detach())
     assert a.optimizer_steps == b.optimizer_steps
     # every batch's sample count; `a` drew its next batch during the last backward
-    # (NGP_DRAW_AHEAD), which recorded the last count in step_counter already
+    # (options draw_ahead), which recorded the last count in step_counter already
     assert torch.equal(a._recent_counts(9), b._recent_counts(9))
     assert (a._recent_counts(9) > 0).all()
     # the scaler / loss bookkeeping (deferred into the march emit launch in world 1)
@@ -420,42 +419,17 @@ def test_mlp_fused_epilogues_match_unfused(cuda):
     for a, b in zip(gw_one, gw_two):
         a, b = a.float(), b.float()
         assert torch.all((a - b).abs() <= 2.0 ** -10 * b.abs() + 1e-6), float((a - b).abs().max())
-    # the pair kernel (NGP_MLP_BWD_PAIR=1: two waves per SIMD, a wave pair per
-    # chunk) against the one-wave-per-SIMD kernel (=0): the same input
-    # gradients bit for bit, dW within fp16 rounding of the same sums
-    import os
-    knob = os.environ.get("NGP_MLP_BWD_PAIR")
-    os.environ["NGP_MLP_BWD_PAIR"] = "0" if knob == "1" else "1"
-    try:
-        gh3, gxp3 = gh0.clone(), torch.zeros_like(gx_ref)
-        ws1 = [torch.full_like(w, 7) for w in wsb]
-        nat.check(lib.ngp_nerf_backward(P(go), P(ci), P(imgs[1]), P(gh3), P(xp), P(imgs[0]), P(gxp3), B, P(cnt),
-                                        64, 2, 64, 3, P(ws1[0]), ws1[0].numel(), P(ws1[1]), ws1[1].numel(), None,
-                                        s), "nerf_bwd_one_wave")
-        gw_w1 = [torch.zeros_like(t) for t in gw_ref]
-        nat.check(lib.ngp_ffmlp_reduce(2, arr([ws1[1], ws1[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
-                                       u32([3, 2]), arr([gw_w1[1], gw_w1[0]]), 1, None, s), "reduce")
-        torch.cuda.synchronize()
-    finally:
-        if knob is None:
-            del os.environ["NGP_MLP_BWD_PAIR"]
-        else:
-            os.environ["NGP_MLP_BWD_PAIR"] = knob
-    assert torch.equal(gh3.view(torch.int16), gh2.view(torch.int16))
-    assert torch.equal(gxp3.view(torch.int16), gxp2.view(torch.int16))
-    for a, b in zip(gw_one, gw_w1):
-        a, b = a.float(), b.float()
-        assert torch.all((a - b).abs() <= 2.0 ** -10 * b.abs() + 1e-6), float((a - b).abs().max())
 
 
 @pytest.mark.parametrize("count", [4700, (256 * 9 + 128) * 32 - 5, (256 * 11 + 17) * 32])
-def test_nerf_backward_half_chunks_equal_whole_chunks(cuda, count):
+def test_nerf_backward_half_chunks_equal_two_calls(cuda, count):
     """k_nerf_bwd splits a workgroup's last round of 1 or 2 chunks into
-    16-sample halves (NGP_MLP_BWD_HALVES, default on): input gradients bit for
-    bit against whole chunks only, dW within fp16 rounding of the same sums;
-    the counts give workgroups 1, 2 and 3 chunks in their last round."""
+    16-sample halves: against the two per-network calls (colour backward with
+    its geo-feature epilogue, then the sigma backward on the pair-major
+    encodings; whole chunks), input gradients bit for bit and dW within fp16
+    rounding of the same sums; the counts give workgroups 1, 2 and 3 chunks in
+    their last round."""
     import ctypes
-    import os
 
     import _ngp_native as nat
     lib, P, s = nat.lib(), nat.ptr, None
@@ -476,31 +450,29 @@ def test_nerf_backward_half_chunks_equal_whole_chunks(cuda, count):
     gh0 = torch.randn(B, 16, generator=g).half().to(cuda)
     wsb = [torch.zeros(int(lib.ngp_ffmlp_backward_workspace_bytes(B, i, 16, h, nl)), dtype=torch.uint8,
                        device=cuda) for i, h, nl in nets]
-    knob = os.environ.get("NGP_MLP_BWD_HALVES")
-    out = {}
-    try:
-        for v in ("0", "1"):
-            os.environ["NGP_MLP_BWD_HALVES"] = v
-            gh, gx = gh0.clone(), torch.zeros(16, B, 2, dtype=torch.half, device=cuda)
-            wsm = [torch.full_like(w, 7) for w in wsb]
-            nat.check(lib.ngp_nerf_backward(P(go), P(ci), P(imgs[1]), P(gh), P(xp), P(imgs[0]), P(gx), B, P(cnt),
-                                            64, 2, 64, 3, P(wsm[0]), wsm[0].numel(), P(wsm[1]), wsm[1].numel(),
-                                            None, s), "nerf_bwd")
-            gw = [torch.zeros(t.numel(), dtype=torch.half, device=cuda) for t in ws]
-            nat.check(lib.ngp_ffmlp_reduce(2, arr([wsm[1], wsm[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
-                                           u32([3, 2]), arr([gw[1], gw[0]]), 1, None, s), "reduce")
-            torch.cuda.synchronize()
-            out[v] = (gh, gx, gw)
-    finally:
-        if knob is None:
-            os.environ.pop("NGP_MLP_BWD_HALVES", None)
-        else:
-            os.environ["NGP_MLP_BWD_HALVES"] = knob
-    (gh_w, gx_w, gw_w), (gh_h, gx_h, gw_h) = out["0"], out["1"]
-    assert torch.equal(gh_h.view(torch.int16), gh_w.view(torch.int16))
-    assert torch.equal(gx_h.view(torch.int16), gx_w.view(torch.int16))
-    assert int(gx_h[:, count:].view(torch.int16).abs().sum()) == 0  # rows past the count untouched
-    for a, b in zip(gw_h, gw_w):
+    # two calls
+    gh_t, gx_t = gh0.clone(), torch.zeros(16, B, 2, dtype=torch.half, device=cuda)
+    nat.check(lib.ngp_ffmlp_backward_rows(P(go), P(ci), P(ws[1]), P(imgs[1]), B, P(cnt), 32, 16, 64, 3, 0, P(gh_t),
+                                          None, 1, 3, P(wsb[1]), wsb[1].numel(), s), "b_geo")
+    nat.check(lib.ngp_ffmlp_backward_rows(P(gh_t), P(xp), P(ws[0]), P(imgs[0]), B, P(cnt), 32, 16, 64, 2, 0,
+                                          P(gx_t), None, 1, 5, P(wsb[0]), wsb[0].numel(), s), "b_pair_defer")
+    gw_t = [torch.zeros(t.numel(), dtype=torch.half, device=cuda) for t in ws]
+    nat.check(lib.ngp_ffmlp_reduce(2, arr([wsb[1], wsb[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
+                                   u32([3, 2]), arr([gw_t[1], gw_t[0]]), 1, None, s), "reduce")
+    # one launch
+    gh, gx = gh0.clone(), torch.zeros(16, B, 2, dtype=torch.half, device=cuda)
+    wsm = [torch.full_like(w, 7) for w in wsb]  # stale slab contents must not leak through
+    nat.check(lib.ngp_nerf_backward(P(go), P(ci), P(imgs[1]), P(gh), P(xp), P(imgs[0]), P(gx), B, P(cnt),
+                                    64, 2, 64, 3, P(wsm[0]), wsm[0].numel(), P(wsm[1]), wsm[1].numel(), None, s),
+              "nerf_bwd")
+    gw = [torch.zeros(t.numel(), dtype=torch.half, device=cuda) for t in ws]
+    nat.check(lib.ngp_ffmlp_reduce(2, arr([wsm[1], wsm[0]]), u32([B, B]), u32([32, 32]), u32([64, 64]),
+                                   u32([3, 2]), arr([gw[1], gw[0]]), 1, None, s), "reduce")
+    torch.cuda.synchronize()
+    assert torch.equal(gh[:count].view(torch.int16), gh_t[:count].view(torch.int16))
+    assert torch.equal(gx[:, :count].view(torch.int16), gx_t[:, :count].view(torch.int16))
+    assert int(gx[:, count:].view(torch.int16).abs().sum()) == 0  # rows past the count untouched
+    for a, b in zip(gw, gw_t):
         a, b = a.float(), b.float()
         assert torch.isfinite(a).all() and torch.all((a - b).abs() <= 2.0 ** -10 * b.abs() + 1e-6), \
             float((a - b).abs().max())
@@ -509,55 +481,36 @@ def test_nerf_backward_half_chunks_equal_whole_chunks(cuda, count):
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
 def test_march_emit_in_launch_equals_emit_launch(cuda, bound, dt_gamma):
     """The march + Adam launch emits the samples itself (ticketed ray blocks,
-    block totals published as agent-scope words; NGP_MARCH_EMIT_INLINE=1):
-    samples, rays, counter and the trained parameters equal the
-    separate emit launch's bit for bit, step after step."""
-    import os
+    block totals published as agent-scope words; the default) against the
+    separate emit launch (options emit_inline=False): samples, rays, counter
+    and the trained parameters bit for bit, step after step."""
     _, _, _, a = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
-    _, _, _, b = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
-    knob = os.environ.get("NGP_MARCH_EMIT_INLINE")
-    try:
-        for it in range(5):
-            os.environ["NGP_MARCH_EMIT_INLINE"] = "1"
-            a.step()
-            os.environ["NGP_MARCH_EMIT_INLINE"] = "0"
-            b.step()
-            torch.cuda.synchronize()
-            assert torch.equal(a.counter, b.counter), (it, a.counter.tolist(), b.counter.tolist())
-            n = a.sample_count()
-            assert n > 0 and n == b.sample_count()
-            assert torch.equal(a.rays, b.rays)
-            for x, y in ((a.xyzs, b.xyzs), (a.dirs, b.dirs), (a.deltas, b.deltas)):
-                assert torch.equal(x[:n].view(torch.int32), y[:n].view(torch.int32)), it
-    finally:
-        if knob is None:
-            os.environ.pop("NGP_MARCH_EMIT_INLINE", None)
-        else:
-            os.environ["NGP_MARCH_EMIT_INLINE"] = knob
+    _, _, _, b = _setup(cuda, bound=bound, dt_gamma=dt_gamma, options=dict(emit_inline=False))
+    for it in range(5):
+        a.step()
+        b.step()
+        torch.cuda.synchronize()
+        assert torch.equal(a.counter, b.counter), (it, a.counter.tolist(), b.counter.tolist())
+        n = a.sample_count()
+        assert n > 0 and n == b.sample_count()
+        assert torch.equal(a.rays, b.rays)
+        for x, y in ((a.xyzs, b.xyzs), (a.dirs, b.dirs), (a.deltas, b.deltas)):
+            assert torch.equal(x[:n].view(torch.int32), y[:n].view(torch.int32)), it
     a.flush()
     b.flush()
     for x, y in zip(a.params, b.params):
         assert torch.equal(x.detach(), y.detach())
+    assert a.device_errors() == 0
 
 
 def test_tail_in_grid_forward_equals_emit_tail(cuda):
     """The step's tail row (deferred scaler / LR / loss bookkeeping + MLP
-    fragment packs) in the grid forward's launch (NGP_TAIL_IN_FWD=1; with the
+    fragment packs) in the grid forward's launch (the default; with the
     in-launch emit the march is then one launch) against the tail row of the
-    emit launch (=0): parameters, moments and the step state bit for bit, eager and
-    captured, across an overflow-free run."""
-    import os
-    knob = os.environ.get("NGP_TAIL_IN_FWD")
-    try:
-        os.environ["NGP_TAIL_IN_FWD"] = "1"
-        _, _, _, a = _setup(cuda)
-        os.environ["NGP_TAIL_IN_FWD"] = "0"
-        _, _, _, b = _setup(cuda)
-    finally:
-        if knob is None:
-            os.environ.pop("NGP_TAIL_IN_FWD", None)
-        else:
-            os.environ["NGP_TAIL_IN_FWD"] = knob
+    emit launch (options tail_in_fwd=False): parameters, moments and the step
+    state bit for bit, eager and captured, across an overflow-free run."""
+    _, _, _, a = _setup(cuda)
+    _, _, _, b = _setup(cuda, options=dict(tail_in_fwd=False))
     assert a._tail_in_fwd and not b._tail_in_fwd
     for t in (a, b):
         for _ in range(3):
@@ -576,25 +529,16 @@ def test_tail_in_grid_forward_equals_emit_tail(cuda):
 
 @pytest.mark.parametrize("bound,dt_gamma,occ", [(1, 0.0, "boxes"), (2, 1 / 128, "boxes"), (1, 0.0, "ball")])
 def test_live_row_backwards_equal_all_row_backwards(cuda, bound, dt_gamma, occ):
-    """The backwards over the live rows only (NGP_LIVE_ROWS=1: the composite
+    """The backwards over the live rows only (the default: the composite
     lists the rows with a nonzero gradient, the MLP backward and the grid bin
-    kernel walk that list) against the backwards over every row (=0): the loss
+    kernel walk that list) against the backwards over every row (options
+    live_rows=False): the loss
     and the encoding gradient of each live row bit for bit, the grid gradient
     bit for bit (dead rows add exact zeros, live rows keep their order), the
     MLP weight gradients to fp16-accumulation tolerance (other 32-row chunks);
     then eager and captured runs stay within tolerance of each other."""
-    import os
-    knob = os.environ.get("NGP_LIVE_ROWS")
-    try:
-        os.environ["NGP_LIVE_ROWS"] = "1"
-        _, _, _, a = _setup(cuda, bound=bound, dt_gamma=dt_gamma, occ=occ)
-        os.environ["NGP_LIVE_ROWS"] = "0"
-        _, _, _, b = _setup(cuda, bound=bound, dt_gamma=dt_gamma, occ=occ)
-    finally:
-        if knob is None:
-            os.environ.pop("NGP_LIVE_ROWS", None)
-        else:
-            os.environ["NGP_LIVE_ROWS"] = knob
+    _, _, _, a = _setup(cuda, bound=bound, dt_gamma=dt_gamma, occ=occ)
+    _, _, _, b = _setup(cuda, bound=bound, dt_gamma=dt_gamma, occ=occ, options=dict(live_rows=False))
     assert a._live and not b._live
     a.step()
     b.step()
@@ -626,45 +570,6 @@ def test_live_row_backwards_equal_all_row_backwards(cuda, bound, dt_gamma, occ):
     for x, y in zip(a.params, b.params):
         assert torch.isfinite(x).all() and _rel(x.detach(), y.detach()) < 1e-3, _rel(x.detach(), y.detach())
     assert abs(a.last_loss - b.last_loss) <= 1e-3 * abs(b.last_loss)
-
-
-def test_live_list_in_backward_launch_equals_compact_launch(cuda):
-    """The live-row list joined inside the MLP backward's launch
-    (NGP_LIVE_LIST=1: every workgroup scans the per-ray counts and writes its
-    own chunks' list positions) against its own k_live_compact launch (=0):
-    the list, its length, every gradient and, after eager and captured runs,
-    parameters and moments bit for bit."""
-    import os
-    knob = os.environ.get("NGP_LIVE_LIST")
-    try:
-        os.environ["NGP_LIVE_LIST"] = "1"
-        _, _, _, a = _setup(cuda)
-        os.environ["NGP_LIVE_LIST"] = "0"
-        _, _, _, b = _setup(cuda)
-    finally:
-        if knob is None:
-            os.environ.pop("NGP_LIVE_LIST", None)
-        else:
-            os.environ["NGP_LIVE_LIST"] = knob
-    assert a._live_list and b._live and not b._live_list
-    for it in range(3):
-        a.step()
-        b.step()
-        torch.cuda.synchronize()
-        ta, tb = int(a._live_bufs["total"][0]), int(b._live_bufs["total"][0])
-        assert ta == tb > 0, (it, ta, tb)
-        assert torch.equal(a._live_bufs["rows"][:ta], b._live_bufs["rows"][:tb]), it
-        for x, y in zip(a.grads, b.grads):
-            assert torch.equal(x.view(torch.int16) if x.dtype == torch.float16 else x,
-                               y.view(torch.int16) if y.dtype == torch.float16 else y), it
-    for t in (a, b):
-        t.capture(warmup=1, multi=4)
-        t.run(8)
-        t.flush()
-    torch.cuda.synchronize()
-    for x, y in zip(a.params, b.params):
-        assert torch.equal(x.detach(), y.detach())
-    assert torch.equal(a.exp_avg, b.exp_avg) and torch.equal(a.exp_avg_sq, b.exp_avg_sq)
 
 
 def test_grad_guard_poisons_every_shard(cuda):
@@ -778,64 +683,11 @@ def test_checkpoint_after_update_density_has_reference_bookkeeping(cuda):
     assert ft.mean_density == 12.5 and ft.mean_count == 777 and ft.checkpoint()["mean_count"] == 777
 
 
-def _fused_adam_run(ft):
-    for _ in range(3):  # eager
-        ft.step()
-    ft.capture(warmup=1)
-    for _ in range(5):  # graph replays
-        ft.step()
-    ft.flush()
-    ft.state.view(torch.float32)[0] = 2.0 ** 40  # the next two steps overflow: skipped, scale backs off
-    ft.step()
-    ft.step()
-    ft.flush()
-    assert ft.scale == 2.0 ** 38
-    ft.state.view(torch.float32)[0] = 4096.0
-    ft.update_density()
-    for _ in range(4):
-        ft.step()
-    ft.flush()
-    torch.cuda.synchronize()
-    m1, m2 = ft._moments()
-    return ([p.detach().clone() for p in ft.params], m1.clone(), m2.clone(), ft.optimizer_steps, ft.scale,
-            ft.last_loss, ft.model.density_bitfield.clone())
-
-
-@pytest.mark.parametrize("bound,dt_gamma,num_rays,occ", [(1, 0.0, 1024, "boxes"), (2, 1 / 128, 1024, "boxes"),
-                                                         (1, 0.0, 4096, "ball")], ids=["lego", "fox", "dense"])
-def test_fused_adam_equals_unfused(cuda, bound, dt_gamma, num_rays, occ):
-    """The table's Adam inside the grid backward (fused_adam: double-buffered
-    p / m / v, the accumulate updates the slices it owns, the step's optimizer
-    launch the rest, the bookkeeping makes the new buffer current) against the
-    unfused optimizer over materialised fp16 table grads: bit-identical
-    parameters, Adam moments, scaler state and loss, through eager steps, graph
-    replays, two overflowing (skipped) steps, a density update and more steps.
-    The dense case (4096 rays through a ball: bins of the coarse levels hold
-    several work units) covers the bins finished through their int64 slot."""
-    mc = 400000 if occ == "ball" else 30000
-    _, _, _, a = _setup(cuda, num_rays=num_rays, mean_count=mc, bound=bound, dt_gamma=dt_gamma, fused_adam=True,
-                        occ=occ)
-    _, _, _, b = _setup(cuda, num_rays=num_rays, mean_count=mc, bound=bound, dt_gamma=dt_gamma, fused_adam=False,
-                        occ=occ)
-    assert a.fused_adam and not b.fused_adam
-    ra, rb = _fused_adam_run(a), _fused_adam_run(b)
-    assert ra[3] == rb[3] >= 10 and ra[4] == rb[4] and ra[5] == rb[5]
-    for x, y, what in zip(ra[0], rb[0], ("table", "sigma", "color")):
-        ne = (x.view(torch.int32) != y.view(torch.int32))
-        assert not ne.any(), (what, int(ne.sum()), float((x - y).abs().max()))
-    for x, y, what in ((ra[1], rb[1], "exp_avg"), (ra[2], rb[2], "exp_avg_sq")):
-        assert torch.equal(x.view(torch.int32), y.view(torch.int32)), what
-    assert torch.equal(ra[6], rb[6])
-    assert int(a.grads[0].abs().sum()) == 0  # every table grad left cleared for the next step
-    if occ == "ball":  # ~330K samples: level 0's two bins get ~35K items each (3 work units)
-        assert a.sample_count() > 250000
-
-
 def test_grid_backward_is_deterministic(cuda):
     """The binned backward sums every bin exactly (int64 fixed point), also
     the bins several work units share (their partial sums meet in an int64
     slot): two backward passes of one batch give bit-identical table grads."""
-    _, _, _, ft = _setup(cuda, num_rays=4096, mean_count=400000, fused_adam=False, occ="ball")
+    _, _, _, ft = _setup(cuda, num_rays=4096, mean_count=400000, occ="ball")
     ft._sample()
     ft._forward_backward()
     g1 = ft.grads[0].clone()
@@ -849,10 +701,10 @@ def test_grid_backward_is_deterministic(cuda):
 
 
 def test_grid_backward_self_timing_counts_graph_replays(cuda):
-    """NGP_GRID_TIMING (the bench's roofline clock): every grid backward of
+    """grid_timing (NGP_GRID_TIMING; the bench's roofline clock): every grid backward of
     the captured step opens a ring entry with its samples and the accumulate
     closes it; the spans are positive and a step's worth."""
-    _, _, _, ft = _setup(cuda, num_rays=4096, mean_count=120000, fused_adam=False, grid_timing=True)
+    _, _, _, ft = _setup(cuda, num_rays=4096, mean_count=120000, grid_timing=True)
     assert ft._grid_timing_at > ft._grid_counter_bytes
     ft.step()
     ft.capture(warmup=1)
@@ -992,16 +844,15 @@ def test_grid_forward_fp32_table_equals_fp16_copy(cuda):
 
 
 @pytest.mark.parametrize("bound,dt_gamma", [(1, 0.0), (2, 1 / 128)])
-def test_one_launch_forward_equals_split_forward(cuda, monkeypatch, bound, dt_gamma):
+def test_one_launch_forward_equals_split_forward(cuda, bound, dt_gamma):
     """ngp_nerf_forward (sigma + colour networks in one launch) against the
     two launches (ngp_nerf_sigma_forward + ngp_ffmlp_forward_rows) on the same
     batch: h, sigma, color_in, rgb logits, loss and the MLP gradients
     bit-identical."""
     outs = []
-    for split in ("1", "0"):
-        monkeypatch.setenv("NGP_FUSED_SPLIT_FWD", split)
-        model, ref, data, ft = _setup(cuda, bound=bound, dt_gamma=dt_gamma)
-        assert ft._one_fwd == (split == "0")
+    for split in (True, False):
+        model, ref, data, ft = _setup(cuda, bound=bound, dt_gamma=dt_gamma, options=dict(split_fwd=split))
+        assert ft._one_fwd == (not split)
         ft._sample()
         ft._forward_backward()
         torch.cuda.synchronize()
@@ -1013,45 +864,7 @@ def test_one_launch_forward_equals_split_forward(cuda, monkeypatch, bound, dt_ga
     assert n0 == n1
     for name, x, y in zip(["h", "sigma", "color_in", "color_out"], a[:4], b[:4]):
         assert torch.equal(x, y), name
-    # MLP grads: fixed-order slab reduce; the table grad's shared bins add by
-    # fp16 atomics in arrival order
-    assert torch.equal(a[4][1], b[4][1]) and torch.equal(a[4][2], b[4][2])
-    assert _rel(a[4][0], b[4][0]) < 1e-3
+    # MLP grads: fixed-order slab reduce; the table grad: exact bin sums
+    for x, y in zip(a[4], b[4]):
+        assert torch.equal(x.view(torch.int16), y.view(torch.int16))
     assert torch.equal(a[5], b[5])
-
-
-@pytest.mark.parametrize("split_level", [8, 10, 13])
-def test_adam_under_grid_forward_equals_single_sweep(cuda, split_level):
-    """NGP_ADAM_UNDER_FWD=1: the march launch sweeps the table values below
-    the split level (and the MLPs), the grid forward's first launch (levels
-    [0, 8)) sweeps the rest, the second (levels [8, 16)) runs the deferred
-    bookkeeping. Same arithmetic per value, so after eager steps, graph replays
-    and a multi-step graph everything equals the one-sweep step bit for bit:
-    parameters, Adam moments, scaler, loss and the encodings' inputs."""
-    import os
-    out = []
-    for on in ("0", "1"):
-        os.environ["NGP_ADAM_UNDER_FWD"] = on
-        os.environ["NGP_ADAM_SPLIT_LEVEL"] = str(split_level)
-        try:
-            _, _, _, ft = _setup(cuda, num_rays=2048, mean_count=60000, fused_adam=False)
-        finally:
-            del os.environ["NGP_ADAM_UNDER_FWD"], os.environ["NGP_ADAM_SPLIT_LEVEL"]
-        assert (ft._fwd_split is not None) == (on == "1")
-        for _ in range(3):
-            ft.step()
-        ft.capture(warmup=1, multi=3)
-        for _ in range(2):
-            ft.step()
-        ft.run(7)
-        ft.flush()
-        torch.cuda.synchronize()
-        m1, m2 = ft._moments()
-        out.append(([p.detach().clone() for p in ft.params], m1.clone(), m2.clone(), ft.scale, ft.last_loss,
-                    ft.optimizer_steps, ft.enc_out.clone()))
-    a, b = out
-    for x, y in zip(a[0], b[0]):
-        assert torch.equal(x, y)
-    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
-    assert a[3:6] == b[3:6] and a[5] >= 12
-    assert torch.equal(a[6].view(torch.int16), b[6].view(torch.int16))

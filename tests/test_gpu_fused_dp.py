@@ -97,9 +97,7 @@ def _equiv_worker(rank, world, port, q):
         with torch.no_grad():
             model.encoder.embeddings.normal_(0, 0.05)
         model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
-        # world 1: the table grads are read and replaced below, so they must be materialised (no fused Adam)
-        return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, seed=seed, distributed=distributed,
-                            fused_adam=False)
+        return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, seed=seed, distributed=distributed)
 
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)

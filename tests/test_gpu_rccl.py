@@ -32,7 +32,7 @@ def _free_port():
     return p
 
 
-def _trainer(dev, distributed):
+def _trainer(dev, distributed, whole_graph=True):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield
@@ -41,7 +41,8 @@ def _trainer(dev, distributed):
     with torch.no_grad():
         model.encoder.embeddings.normal_(0, 0.05)
     model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
-    return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, distributed=distributed)
+    return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, distributed=distributed,
+                        options=dict(dp_graph=whole_graph))
 
 
 def _snap(ft):
@@ -78,8 +79,6 @@ def _run_steps(ft):
 
 def _worker(port, q, whole_graph=False):
     import sys
-    # the whole step, collectives included, in one graph (the default), or three graphs
-    os.environ["NGP_DP_GRAPH"] = "1" if whole_graph else "0"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "torch-ngp_amd")]
     import torch.distributed as dist
@@ -89,7 +88,8 @@ def _worker(port, q, whole_graph=False):
     try:
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
         backend = dist.get_backend()
-        dp = _run_steps(_trainer(dev, True))
+        # the whole step, collectives included, in one graph (the default), or three graphs
+        dp = _run_steps(_trainer(dev, True, whole_graph))
         single = _run_steps(_trainer(dev, False))
         dist.barrier()
         dist.destroy_process_group()

@@ -1,5 +1,5 @@
 """Phase clocks of the one-launch NeRF backward (k_nerf_bwd) in the trained
-regime (live rows only, NGP_LIVE_ROWS), diagnostic build with -DNGP_STAMPS
+regime (live rows only, options live_rows), diagnostic build with -DNGP_STAMPS
 (SRCS=ffmlp bash tools/variants.sh stamps "-DNGP_STAMPS"): per wave and pass,
 s_memtime at entry, after the first loads + fragment copy, after each chunk,
 after the half chunk, after the fold, after the slab row.

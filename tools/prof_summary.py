@@ -35,9 +35,9 @@ def main(tag, out=None):
     spin = next((i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]), len(rows))
     name = lambda i: rows[i]["Kernel_Name"] if i < len(rows) else ""  # noqa: E731
     # a step starts with k_adam_head (merged optimizer + batch launch) or, with
-    # NGP_FUSED_SPLIT_HEAD=1 / older builds, k_adam_multi followed by k_step_head
-    # or (NGP_MARCH_ADAM, Adam inside the march launch) k_step_head alone, or
-    # (NGP_DRAW_AHEAD: the batch drawn in the previous bin launch) the march +
+    # options split_head / older builds, k_adam_multi followed by k_step_head
+    # or (march_adam, Adam inside the march launch) k_step_head alone, or
+    # (draw_ahead: the batch drawn in the previous bin launch) the march +
     # Adam launch k_march_train<4> itself
     starts = [i for i in range(spin) if "k_adam_head" in name(i) or
               ("k_adam_multi" in name(i) and "k_step_head" in name(i + 1)) or

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Build variant libngp_hip.so files that differ only in compile-time NGP_*
-# knobs, for same-box A/B via NGP_HIP_LIB (tools/ab_env.sh, tools/ab_variants.sh).
+# Build variant libngp_hip.so files that differ only in compile-time -D
+# defines (a change under test, or -DNGP_STAMPS), for same-box A/B via NGP_HIP_LIB (tools/ab_env.sh, tools/ab_variants.sh).
 # SRCS names the sources rebuilt with the knobs (default gridencoder; e.g.
 # SRCS="nerf_fused density_grid" for ngp_head.h knobs); the rest come from
 # the objects of a normal build (build/obj). Runs on the CPU host.
-# usage: [SRCS="a b"] bash tools/variants.sh NAME "-DNGP_SEG_ITEMS=8192 ..." [NAME2 "DEFS2" ...]
+# usage: [SRCS="a b"] bash tools/variants.sh NAME "-DNGP_STAMPS ..." [NAME2 "DEFS2" ...]
 set -eo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 OBJ=$R/build/obj

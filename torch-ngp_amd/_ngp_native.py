@@ -65,9 +65,6 @@ SIGNATURES = {
                                           c_vp, c_u32, c_u32, c_f32, c_vp, c_vp, c_vp],
     "ngp_march_rays": [c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_u32, c_u32, c_u32,
                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
-    "ngp_grid_encode_forward_fused_adam": [c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
-                                           c_f32, c_u32, c_u32, c_i32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp,
-                                           c_f32, c_f32, c_i32, c_i32, c_vp, c_u32, c_vp],
     "ngp_grid_encode_forward_fused_tail": [c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
                                            c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_f32, c_f32, c_i32, c_i32, c_vp,
                                            c_u32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
@@ -137,10 +134,6 @@ SIGNATURES = {
     "ngp_nerf_glue_backward": [c_vp, c_vp, c_u32, c_vp, c_vp],
     "ngp_nerf_composite_loss": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
                                 c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
-    "ngp_nerf_composite_loss_ray_lists": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
-                                          c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
-    "ngp_nerf_backward_live_list": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp,
-                                    c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_sz, c_vp, c_sz, c_vp, c_vp],
     "ngp_nerf_composite_loss_live": [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_f32, c_f32, c_vp,
                                      c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      c_vp],
@@ -159,31 +152,10 @@ SIGNATURES = {
     "ngp_grid_encode_backward_fused_reduce": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
                                               c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_i32, c_vp,
                                               c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
-    # fused table Adam (ngp_adam_table, double-buffered hash table)
-    "ngp_grid_table_slices": [c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32, c_vp, c_u32],
-    "ngp_grid_encode_forward_fused_sel": [c_vp, c_f32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_u32, c_vp, c_u32,
-                                          c_u32, c_u32, c_f32, c_u32, c_u32, c_i32, c_u32, c_i32, c_vp],
-    "ngp_grid_encode_backward_fused_adam": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
-                                            c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_i32, c_vp,
-                                            c_vp, c_vp, c_vp],
-    "ngp_fused_table_select": [c_vp],
-    "ngp_fused_table_to_half": [c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp],
-    "ngp_fused_table_normalize": [c_vp, c_vp, ctypes.c_uint64, c_vp],
-    "ngp_fused_optimizer_step_db": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
-                                    c_i32, c_i32, c_f32, c_f32, c_f32, c_i32, c_i32, c_u32, c_vp, c_vp,
-                                    c_vp, c_vp, c_vp, c_vp],
-    "ngp_fused_optimizer_update_db": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
-                                      c_i32, c_i32, c_f32, c_i32, c_vp, c_vp, c_vp],
-    "ngp_fused_optimizer_update_head_db": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32,
-                                           c_i32, c_i32, c_f32, c_i32, c_vp,
-                                           c_vp, c_u32, c_vp, c_u32, c_u32, c_u32, c_vp, c_i32, c_vp, c_f32, c_u32,
-                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp,
-                                           c_vp],
 }
 _RESTYPES = {
     "ngp_last_error": ctypes.c_char_p,
     "ngp_fused_inf_flag": c_vp,
-    "ngp_fused_table_select": c_vp,
     "ngp_grid_encode_backward_fused_timing_offset": c_sz,
     "ngp_grid_encode_backward_fused_counter_bytes": c_sz,
     "ngp_ffmlp_backward_workspace_bytes": c_sz,
@@ -201,14 +173,6 @@ _RESTYPES = {
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}
 
 
-class AdamTable(ctypes.Structure):
-    """ngp_adam_table (include/ngp_hip.h): the double-buffered hash table of
-    the fused Adam."""
-    _fields_ = [("params", c_vp * 2), ("exp_avg", c_vp * 2), ("exp_avg_sq", c_vp * 2), ("grad", c_vp),
-                ("size", ctypes.c_uint64), ("done", c_vp), ("slices", c_vp), ("nslices", c_u32),
-                ("channels", c_u32), ("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32),
-                ("iters", c_i32)]
-
 class AdamJob(ctypes.Structure):
     """ngp_adam_job (include/ngp_hip.h): the optimizer update a march launch
     carries (ngp_march_rays_train_prebuilt_adam)."""
@@ -219,8 +183,8 @@ class AdamJob(ctypes.Structure):
                 ("flags", c_u32)]
 
 
-ADAM_JOB_END_LATER = 1  # NGP_ADAM_JOB_END_LATER
 ADAM_JOB_TAIL_LATER = 2  # NGP_ADAM_JOB_TAIL_LATER
+ADAM_JOB_EMIT_LAUNCH = 4  # NGP_ADAM_JOB_EMIT_LAUNCH
 
 
 class BatchJob(ctypes.Structure):

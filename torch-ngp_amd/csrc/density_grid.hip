@@ -308,10 +308,7 @@ k_density_draw(uint32_t P, uint32_t ppc, uint32_t H, uint32_t seed, uint32_t upd
 // nonzero bucket), scan, scatter (LDS ranks + one reservation per nonzero
 // bucket and block). The order inside a bucket is unspecified; each rank sorts
 // only its own slice of the draws, so the union over ranks is the draws.
-#ifndef NGP_SORT_PER_THREAD  // same-box A/B builds: points per thread of the count / scatter tiles
-#define NGP_SORT_PER_THREAD 16
-#endif
-constexpr uint32_t kSortThreads = 1024, kSortPerThread = NGP_SORT_PER_THREAD,
+constexpr uint32_t kSortThreads = 1024, kSortPerThread = 16,
                    kSortTile = kSortThreads * kSortPerThread;
 constexpr uint32_t kSortMaxBuckets = 8192;
 

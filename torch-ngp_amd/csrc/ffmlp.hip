@@ -42,23 +42,14 @@ using ngp_pack::perm_unit;
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef NGP_MLP_FWD_WAVES  // same-box A/B builds only (tools/variants.sh)
-#define NGP_MLP_FWD_WAVES 4
-#endif
-constexpr int kWaves = NGP_MLP_FWD_WAVES;  // forward: waves per workgroup (sharing one fragment copy)
+constexpr int kWaves = 4;  // forward: waves per workgroup (sharing one fragment copy)
 constexpr int kThreads = kWaves * 64;
 // Backward: waves per workgroup sharing one fragment image. The dW tiles
 // live in registers for the whole chunk loop (176 of them for the colour
 // network), which leaves room for one wave per SIMD: at 8 waves per workgroup
 // (two per SIMD, 256 registers each) the compiler spills 362 (colour) / 78
 // (sigma) VGPRs.
-#ifndef NGP_MLP_BWD_WAVES
-#define NGP_MLP_BWD_WAVES 4
-#endif
-#ifndef NGP_MLP_BWD_OVERLAP  // see k_mlp_bwd's chunk loop (0: same-box A/B builds)
-#define NGP_MLP_BWD_OVERLAP 1
-#endif
-constexpr int kBwdWaves = NGP_MLP_BWD_WAVES;
+constexpr int kBwdWaves = 4;
 constexpr int kBwdThreads = kBwdWaves * 64;
 static_assert(kBwdWaves % 2 == 0 && kBwdWaves <= 16, "the dW fold pairs waves (two LDS images)");
 constexpr int kNB = 2;          // 16-sample column blocks per wave step (32 samples)
@@ -101,9 +92,6 @@ NGP_DEV void copy_frags(half8* __restrict__ lds, const half8* __restrict__ image
     }
 }
 
-#ifndef NGP_BWD_COPY2  // same-box A/B builds only: 1 batches the two image copies (r05ac: no change, 23.3 us both)
-#define NGP_BWD_COPY2 0
-#endif
 // Two images copied with every load of both issued before the first LDS
 // store: one round trip instead of two (the NeRF backward's prologue).
 template <int F1, int F2, int THREADS>
@@ -875,43 +863,28 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
         // product (register operands + fragment reads) is issued BEFORE the
         // dW product that reads the tiles back, so its MFMAs cover the tile
         // round trip (LDS executes one wave's operations in order, the reads
-        // see the stores). NGP_MLP_BWD_OVERLAP=0: the dW product first.
+        // see the stores).
         // last matmul: dW += dout^T . h[NH]
         write_rows<1, false>(dT, dout, kOut);
         write_rows<N::KSW, true>(hT, h[NH], W);
-#if NGP_MLP_BWD_OVERLAP
         dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
         dw_accum<1, N::MTW>(dT, hT, dw_last);
-#else
-        dw_accum<1, N::MTW>(dT, hT, dw_last);
-        dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
-#endif
         half8 d[NBC][N::KSW];  // delta of a matmul's pre-activation output, permuted B form
         pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
 #pragma unroll
         for (int q = NH; q >= 1; --q) {
             write_rows<N::KSW, true>(dT, d, W);
             write_rows<N::KSW, true>(hT, h[q - 1], W);
-#if NGP_MLP_BWD_OVERLAP
             dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
             dw_accum<N::MTW, N::MTW>(dT, hT, dw_hid[q - 1]);
-#else
-            dw_accum<N::MTW, N::MTW>(dT, hT, dw_hid[q - 1]);
-            dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
-#endif
             pack_delta<N::MTW, N::KSW>(a, h[q - 1], act, d);
         }
         // first matmul: dW += d^T . x, and grad_inputs = W_0^T d
         write_rows<N::KSW, true>(dT, d, W);
         write_rows<IN_KS, false>(hT, x, in_dim);
         f32x4 gi[NBC][N::IN_MT];
-#if NGP_MLP_BWD_OVERLAP
         if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
         dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
-#else
-        dw_accum<N::MTW, N::IN_MT>(dT, hT, dw_first);
-        if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
-#endif
         if (want_gi) gi_out(row0, B, in_dim, gi);
     };
 
@@ -1010,11 +983,7 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t o = 16 * m + 4 * g + r;
-#if NGP_NT_SLAB  // streamed once by the reduce: keep the slab out of the caches
-            if (o < out_w && i < in_w) __builtin_nontemporal_store(a[r] + b[r], slab_row + off + o * in_w + i);
-#else
             if (o < out_w && i < in_w) slab_row[off + o * in_w + i] = a[r] + b[r];
-#endif
         }
     }
     MSTAMP(14);
@@ -1067,17 +1036,7 @@ struct NerfBwdArgs {
     float* slab_sigma;
     uint32_t np_color, np_sigma, B;
     const int32_t* count;
-    uint32_t halves;  // split a last round of 1 or 2 chunks into 16-sample halves
     const int32_t* rows;  // the rows to run (*count of them), or null: rows [0, *count)
-    // the list made in this launch (ngp_nerf_backward_live_list; list_cnt null:
-    // none): each workgroup joins the composite's per-ray lists (list_cnt [N]
-    // rows at ray_rows[rays[n][1]]) up to its chunks, writes those positions of
-    // `rows` (the bin kernel reads the whole list) and runs them
-    const int32_t* list_cnt;
-    const int32_t* list_rays;
-    const int32_t* list_src;
-    int32_t* list_total;
-    uint32_t list_n;
     // the grid backward's timing ring (NGP_GRID_TIMING, include/ngp_hip.h), or
     // null: workgroup b stores its end (after its last store) in end slot
     // MAX_WG - 1 - b of the call the next bin launch opens (the accumulate's
@@ -1095,69 +1054,6 @@ struct NerfBwdLds {
     static constexpr size_t total = sigma_frags + LS::frag_bytes;
     static constexpr bool fits = total <= 160 * 1024 && LS::total <= sigma_frags;
 };
-// the in-launch list's per-ray offsets and first rows, past the kernel's LDS
-constexpr uint32_t kListMaxRays = 4096;
-constexpr uint32_t kListPerThread = (kListMaxRays + kBwdThreads - 1) / kBwdThreads;
-
-// The prologue of the in-launch list (NerfBwdArgs::list_cnt): the exclusive
-// offsets of every ray's live rows (their counts and first rows requested
-// together, one round trip), then this workgroup's chunk positions of the list
-// (b + j G for j < n), each row one independent load. Returns the list length.
-NGP_DEV uint32_t nerf_bwd_list(const NerfBwdArgs& a, uint32_t* off, uint32_t* src, uint32_t b, uint32_t G) {
-    __shared__ uint32_t s_wsum[kBwdWaves];
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, N = a.list_n;
-    const uint32_t r0 = t * kListPerThread;
-    uint32_t c[kListPerThread], sr[kListPerThread];
-#pragma unroll
-    for (uint32_t k = 0; k < kListPerThread; ++k) {
-        const uint32_t r = r0 + k;
-        c[k] = r < N ? (uint32_t)a.list_cnt[r] : 0u;
-        sr[k] = r < N ? (uint32_t)a.list_rays[(size_t)r * 3 + 1] : 0u;
-    }
-    uint32_t mine = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kListPerThread; ++k) mine += c[k];
-    uint32_t incl = mine;
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += u;
-    }
-    if (lane == 63) s_wsum[w] = incl;
-    __syncthreads();
-    uint32_t run = incl - mine, total = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kBwdWaves; ++k) {
-        run += k < w ? s_wsum[k] : 0u;
-        total += s_wsum[k];
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kListPerThread; ++k) {
-        if (r0 + k < N) {
-            off[r0 + k] = run;
-            src[r0 + k] = sr[k];
-        }
-        run += c[k];
-    }
-    __syncthreads();
-    const uint32_t nch = ngp_div_up(total, ngp_reduce::kBwdChunkRows);
-    const uint32_t n = b < nch ? (nch - b + G - 1) / G : 0u;
-    for (uint32_t k = t; k < n * ngp_reduce::kBwdChunkRows; k += kBwdThreads) {
-        const uint32_t p = (b + (k / ngp_reduce::kBwdChunkRows) * G) * ngp_reduce::kBwdChunkRows +
-                           k % ngp_reduce::kBwdChunkRows;
-        if (p >= total) continue;
-        uint32_t lo = 0, hi = N;  // the last ray whose offset is <= p (it holds p: later rays start past it)
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (off[mid] <= p) lo = mid; else hi = mid;
-        }
-        const_cast<int32_t*>(a.rows)[p] = a.list_src[src[lo] + (p - off[lo])];
-    }
-    if (b == 0 && t == 0) *a.list_total = (int32_t)total;
-    __syncthreads();  // this workgroup's positions of the list are stored before its passes read them
-    return total;
-}
-
 template <int NHS, int NHC>
 __global__ void __launch_bounds__(kBwdThreads)
 k_nerf_bwd(NerfBwdArgs a) {
@@ -1171,17 +1067,13 @@ k_nerf_bwd(NerfBwdArgs a) {
     half8* sfr = reinterpret_cast<half8*>(reinterpret_cast<char*>(lds) + NL::sigma_frags);
     const uint32_t G = gridDim.x, b = blockIdx.x, w = threadIdx.x >> 6;
     const uint32_t tcall = a.timing && threadIdx.x == 0 ? a.timing[0] : 0u;  // requested early
-    if (a.list_cnt) {  // launch-uniform
-        uint32_t* off = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + NL::total);
-        B = min(a.B, nerf_bwd_list(a, off, off + kListMaxRays, b, G));
-    }
     // this workgroup's chunks b, b + G, ...: n of them, the j-th in slot j % 4.
     // When the last round holds r = 1 or 2 chunks (2 or 3 of the 4 waves idle
     // for a whole chunk), they are split into 2r halves of 16 samples, one per
-    // slot, so the round takes a half chunk's time (NGP_MLP_BWD_HALVES=0: not split)
+    // slot, so the round takes a half chunk's time
     const uint32_t nch = ngp_div_up(B, 16 * kNB);
     const uint32_t n = b < nch ? (nch - b + G - 1) / G : 0u, r = n % kBwdWaves;
-    const uint32_t nf = a.halves && (r == 1 || r == 2) ? n - r : n;  // chunks taken whole
+    const uint32_t nf = r == 1 || r == 2 ? n - r : n;  // chunks taken whole
     auto map_of = [=](uint32_t slot) {
         return [=](uint32_t k) { const uint32_t j = slot + k * kBwdWaves; return j < nf ? b + j * G : nch; };
     };
@@ -1196,12 +1088,8 @@ k_nerf_bwd(NerfBwdArgs a) {
                           GiNerfGeo{a.g_h, a.rows},
                           true, a.slab_color, a.np_color, B, 32u, ActReLU{}, map_of(w),
                           [&]() {
-#if NGP_BWD_COPY2
-                              copy_frags2<LC::FRAGS, LS::FRAGS, kBwdThreads>(lds, a.color_image, sfr, a.sigma_image);
-#else
                               copy_frags<LC::FRAGS, kBwdThreads>(lds, a.color_image);
                               copy_frags<LS::FRAGS, kBwdThreads>(sfr, a.sigma_image);
-#endif
                               __syncthreads();
                           }, half_of(w));
     // the colour pass's geo grads (global stores of every wave) are complete
@@ -1213,225 +1101,6 @@ k_nerf_bwd(NerfBwdArgs a) {
                           InPairMajor{a.B, a.rows}, GiPairMajor{a.g_enc, a.B, a.rows}, true, a.slab_sigma, a.np_sigma,
                           B, 32u, ActReLU{}, map_of(kBwdWaves - 1 - w), []() {}, half_of(kBwdWaves - 1 - w));
     }
-    if (a.timing && b < NGP_GRID_TIMING_MAX_WG / 4) {
-        __syncthreads();
-        if (threadIdx.x == 0)
-            a.timing[64 + 4 * NGP_GRID_TIMING_RING + (tcall % NGP_GRID_TIMING_RING) * NGP_GRID_TIMING_MAX_WG +
-                     NGP_GRID_TIMING_MAX_WG - 1 - b] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    }
-}
-
-// ---- two waves per SIMD: a wave pair shares each chunk ----------------------
-// The backward above keeps every dW tile of the network in each wave's
-// registers (176 for the colour network) beside a 32-sample chunk's
-// activations, so it runs one wave per SIMD and each wave's chunk is a
-// dependent chain of MFMAs, conversions and LDS round trips that nothing else
-// on the SIMD hides. Here a workgroup has 8 waves (two per SIMD) and waves
-// 2p, 2p + 1 share pair p's chunk: wave half h recomputes the forward and walks
-// the delta chain for samples [16 h, 16 h + 16) of it (one 16-column block
-// instead of two), writes those rows of the pair's transposing tiles, and,
-// after a workgroup barrier, accumulates HALF of each layer's dW tiles --
-// output tiles [h MTW/2, (h + 1) MTW/2); the last layer's input tiles -- over
-// all 32 samples. Per wave: half the activations and half the accumulators
-// (88 VGPRs for the colour network), the same chunks per workgroup as the
-// one-wave kernel. Input gradients are bit-identical (each row's arithmetic is
-// unchanged); dW is summed in another fixed order.
-constexpr int kPairWaves = 8;
-constexpr int kPairThreads = kPairWaves * 64;
-
-template <int MO, int MI>
-NGP_DEV void dw_accum_at(const ngp_half* __restrict__ dT, int m0, const ngp_half* __restrict__ hT, int n0,
-                         f32x4 (&acc)[MO][MI]) {
-    half8 a[MO], b[MI];
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int m = 0; m < MO; ++m) a[m] = read_tr(dT, m0 + m);
-#pragma unroll
-    for (int n = 0; n < MI; ++n) b[n] = read_tr(hT, n0 + n);
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int m = 0; m < MO; ++m)
-#pragma unroll
-        for (int n = 0; n < MI; ++n) acc[m][n] = mfma(a[m], b[n], acc[m][n]);
-}
-
-template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI, typename MAP, typename PRE>
-NGP_DEV void bwd_phase_pair(const half8* __restrict__ fr, ngp_half* __restrict__ tiles, float* __restrict__ img_base,
-                            const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs, XL xl, GI gi_out,
-                            bool want_gi, float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim,
-                            FA act, MAP map, PRE pre) {
-    using N = Net<W, IN_KS, NH>;
-    constexpr int LAST = N::NMAT - 1;
-    constexpr int HM = N::MTW / 2;  // this wave's output tiles of a layer
-    static_assert(N::MTW % 2 == 0, "the pair splits a layer's output tiles in halves");
-    const uint32_t wave = threadIdx.x >> 6, hf = wave & 1u, pair = wave >> 1;
-    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
-    // the pair's tiles; this wave writes rows [16 hf, 16 hf + 16) of them
-    ngp_half* dT = tiles + (size_t)pair * 2 * kTileRows * kTileLd;
-    ngp_half* hT = dT + (size_t)kTileRows * kTileLd;
-    ngp_half* dTw = dT + (size_t)16 * hf * kTileLd;
-    ngp_half* hTw = hT + (size_t)16 * hf * kTileLd;
-
-    uint32_t chunk = map(pair, 0u);
-    half8 xn[1][IN_KS], dn[1][1];
-    xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB + 16 * hf, B, xn);
-    load_rows<1>(grad, kOut, chunk * 16 * kNB + 16 * hf, B, dn, xl.map);
-    pre();
-
-    f32x4 dw_last[1][HM], dw_hid[NH][HM][N::MTW], dw_first[HM][N::IN_MT];
-    zero_tiles(dw_last);
-#pragma unroll
-    for (int q = 0; q < NH; ++q) zero_tiles(dw_hid[q]);
-    zero_tiles(dw_first);
-
-    // the workgroup's pairs run in lockstep (barriers per matmul); a pair
-    // without a chunk in the last round still meets the barriers
-    const uint32_t rounds = ngp_div_up(nchunks > blockIdx.x ? nchunks - blockIdx.x : 0u,
-                                       gridDim.x * (uint32_t)(kPairWaves / 2));
-    for (uint32_t kc = 1; kc <= rounds; ++kc) {
-        const bool mine = chunk < nchunks;
-        const uint32_t row0 = chunk * 16 * kNB + 16 * hf;
-        half8 x[1][IN_KS], dout[1][1];
-#pragma unroll
-        for (int s = 0; s < IN_KS; ++s) x[0][s] = xn[0][s];
-        dout[0][0] = dn[0][0];
-        const uint32_t next = map(pair, kc);
-        xl.template operator()<IN_KS>(inputs, in_dim, next * 16 * kNB + 16 * hf, B, xn);
-        load_rows<1>(grad, kOut, next * 16 * kNB + 16 * hf, B, dn, xl.map);
-        half8 h[NH + 1][1][N::KSW];
-        f32x4 a[1][N::MTW];
-        dense<N::MTW, IN_KS>(fr, fwd_desc<W, IN_KS, NH>(0, in_dim).frag0, x, a);
-        pack_act<N::MTW, N::KSW>(a, act, h[0]);
-#pragma unroll
-        for (int q = 1; q <= NH; ++q) {
-            dense<N::MTW, N::KSW>(fr, fwd_desc<W, IN_KS, NH>(q, in_dim).frag0, h[q - 1], a);
-            pack_act<N::MTW, N::KSW>(a, act, h[q]);
-        }
-        write_rows<1, false>(dTw, dout, kOut);
-        write_rows<N::KSW, true>(hTw, h[NH], W);
-        lds_barrier();  // the pair's last-layer tiles are whole
-        dense<N::MTW, 1>(fr, bwd_desc<W, IN_KS, NH>(LAST, in_dim).frag0 + N::FWD_FRAGS, dout, a);
-        if (mine) dw_accum_at<1, HM>(dT, 0, hT, (int)hf * HM, dw_last);
-        half8 d[1][N::KSW];
-        pack_delta<N::MTW, N::KSW>(a, h[NH], act, d);
-#pragma unroll
-        for (int q = NH; q >= 1; --q) {
-            lds_barrier();  // the pair's reads of the previous tiles are done
-            write_rows<N::KSW, true>(dTw, d, W);
-            write_rows<N::KSW, true>(hTw, h[q - 1], W);
-            lds_barrier();
-            dense<N::MTW, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(q, in_dim).frag0 + N::FWD_FRAGS, d, a);
-            if (mine) dw_accum_at<HM, N::MTW>(dT, (int)hf * HM, hT, 0, dw_hid[q - 1]);
-            pack_delta<N::MTW, N::KSW>(a, h[q - 1], act, d);
-        }
-        lds_barrier();
-        write_rows<N::KSW, true>(dTw, d, W);
-        write_rows<IN_KS, false>(hTw, x, in_dim);
-        lds_barrier();
-        f32x4 gi[1][N::IN_MT];
-        if (want_gi) dense<N::IN_MT, N::KSW>(fr, bwd_desc<W, IN_KS, NH>(0, in_dim).frag0 + N::FWD_FRAGS, d, gi);
-        if (mine) dw_accum_at<HM, N::IN_MT>(dT, (int)hf * HM, hT, 0, dw_first);
-        if (mine && want_gi) gi_out(row0, B, in_dim, gi);
-        lds_barrier();  // the next round's tile writes follow
-        chunk = next;
-    }
-    // fold: a pair's halves are disjoint tiles of one image; pair p folds into
-    // image p & 1 (pairs 0 and 1 store, the others add, in pair order), then
-    // image0 + image1 is the slab row: a fixed summation order
-    constexpr int T_FIRST = N::MTW * N::IN_MT, T_HID = N::MTW * N::MTW, T_LAST = N::MTW;
-    constexpr int NT = T_FIRST + NH * T_HID + T_LAST;
-    float* img = img_base + (size_t)(pair & 1u) * NT * 256;
-    auto fold = [&](auto first) {
-        constexpr bool F = decltype(first)::value;
-        fold_tiles<F>(dw_first, img + (size_t)hf * HM * N::IN_MT * 256);
-#pragma unroll
-        for (int q = 1; q <= NH; ++q)
-            fold_tiles<F>(dw_hid[q - 1], img + ((size_t)T_FIRST + (q - 1) * T_HID + hf * HM * N::MTW) * 256);
-        fold_tiles<F>(dw_last, img + ((size_t)T_FIRST + NH * T_HID + hf * HM) * 256);
-    };
-    __syncthreads();  // fragments and tiles are dead from here on
-    if (pair < 2) fold(std::true_type{});
-    __syncthreads();
-#pragma unroll 1
-    for (uint32_t r = 1; r < (uint32_t)kPairWaves / 4; ++r) {
-        if ((pair >> 1) == r) fold(std::false_type{});
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-    const f32x4* i0 = reinterpret_cast<const f32x4*>(img_base);
-    const f32x4* i1 = i0 + NT * 64;
-    float* slab_row = slab + (size_t)blockIdx.x * nparams;
-    for (int tt = (int)wave; tt < NT; tt += kPairWaves) {
-        int local, mi;
-        uint32_t in_w, out_w, off;
-        if (tt < T_FIRST) {
-            local = tt; mi = N::IN_MT; in_w = in_dim; out_w = W; off = 0;
-        } else if (tt < T_FIRST + NH * T_HID) {
-            const int q = (tt - T_FIRST) / T_HID;
-            local = tt - T_FIRST - q * T_HID; mi = N::MTW; in_w = W; out_w = W;
-            off = fwd_desc<W, IN_KS, NH>(q + 1, in_dim).off;
-        } else {
-            local = tt - T_FIRST - NH * T_HID; mi = N::MTW; in_w = W; out_w = kOut;
-            off = fwd_desc<W, IN_KS, NH>(LAST, in_dim).off;
-        }
-        const uint32_t m = (uint32_t)(local / mi), k = (uint32_t)(local % mi);
-        const f32x4 va = i0[tt * 64 + lane], vb = i1[tt * 64 + lane];
-        const uint32_t i = 16 * k + c;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t o = 16 * m + 4 * g + r;
-            if (o < out_w && i < in_w) slab_row[off + o * in_w + i] = va[r] + vb[r];
-        }
-    }
-}
-
-// LDS of the pair kernel: [colour fragments][4 pairs' tiles] ... [sigma
-// fragments]; the colour pass's fold images overlay everything before the
-// sigma fragments, the sigma pass's tiles and fold images the same space.
-template <int NHS, int NHC>
-struct NerfBwdPairLds {
-    using LC = BwdLds<64, 1, NHC>;
-    using LS = BwdLds<64, 1, NHS>;
-    static constexpr size_t tile_bytes = (size_t)(kPairWaves / 2) * 2 * kTileRows * kTileLd * 2;
-    static constexpr size_t fold_c = 2 * LC::acc_bytes, fold_s = 2 * LS::acc_bytes;
-    static constexpr size_t cmax(size_t x, size_t y) { return x > y ? x : y; }
-    static constexpr size_t sigma_frags = cmax(cmax(LC::frag_bytes + tile_bytes, fold_c), cmax(fold_s, tile_bytes));
-    static constexpr size_t total = sigma_frags + LS::frag_bytes;
-    static constexpr bool fits = total <= 160 * 1024;
-};
-
-template <int NHS, int NHC>
-__global__ void __launch_bounds__(kPairThreads, 2)
-k_nerf_bwd_pair(NerfBwdArgs a) {
-    using LC = BwdLds<64, 1, NHC>;
-    using LS = BwdLds<64, 1, NHS>;
-    using NL = NerfBwdPairLds<NHS, NHC>;
-    static_assert(NL::fits, "nerf backward (pair) LDS budget exceeded");
-    uint32_t B = a.B;
-    if (a.count) B = *a.count <= 0 ? 0u : min(B, (uint32_t)*a.count);
-    extern __shared__ half8 lds[];
-    half8* sfr = reinterpret_cast<half8*>(reinterpret_cast<char*>(lds) + NL::sigma_frags);
-    ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes);
-    const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t tcall = a.timing && threadIdx.x == 0 ? a.timing[0] : 0u;
-    // pair p's k-th chunk (colour) -- the one-wave kernel's deal with pairs in
-    // place of waves; the sigma pass deals them in reverse pair order, so a
-    // pair with an extra colour chunk has one sigma chunk less
-    bwd_phase_pair<64, 1, NHC>(lds, tiles, reinterpret_cast<float*>(lds), a.g_color_out, a.color_in,
-                               InRowMajor{a.rows}, GiNerfGeo{a.g_h, a.rows}, true, a.slab_color, a.np_color, B, 32u, ActReLU{},
-                               [=](uint32_t p, uint32_t k) { return b + (p + k * (kPairWaves / 2)) * G; },
-                               [&]() {
-                                   copy_frags<LC::FRAGS, kPairThreads>(lds, a.color_image);
-                                   copy_frags<LS::FRAGS, kPairThreads>(sfr, a.sigma_image);
-                                   __syncthreads();
-                               });
-    __syncthreads();  // the colour pass's geo grads are stored and its fold images read
-    bwd_phase_pair<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
-                               InPairMajor{a.B, a.rows}, GiPairMajor{a.g_enc, a.B, a.rows}, true, a.slab_sigma,
-                               a.np_sigma, B, 32u,
-                               ActReLU{},
-                               [=](uint32_t p, uint32_t k) { return b + (kPairWaves / 2 - 1 - p + k * (kPairWaves / 2)) * G; },
-                               []() {});
     if (a.timing && b < NGP_GRID_TIMING_MAX_WG / 4) {
         __syncthreads();
         if (threadIdx.x == 0)
@@ -1624,51 +1293,20 @@ int launch_bwd(const void* grad, const void* in, const void* w, const void* imag
                                       gw_dtype, defer, ws, count, st);
 }
 
-// The pair kernel (two waves per SIMD) where its LDS fits, with
-// NGP_MLP_BWD_PAIR=1; otherwise the one-wave-per-SIMD kernel (same-box A/B).
-inline bool mlp_bwd_pair_enabled() {
-    const char* e = getenv("NGP_MLP_BWD_PAIR");
-    return e && e[0] == '1';
-}
-// k_nerf_bwd's half-chunk last round (NGP_MLP_BWD_HALVES=0: whole chunks only)
-inline bool mlp_bwd_halves_enabled() {
-    const char* e = getenv("NGP_MLP_BWD_HALVES");
-    return !(e && e[0] == '0');
-}
-
 template <int NHS, int NHC>
 int launch_nerf_bwd(const NerfBwdArgs& a, hipStream_t st) {
-    // (a 3-layer sigma network spills at two waves per SIMD: the one-wave kernel)
-    if constexpr (NHS == 1 && NerfBwdPairLds<NHS, NHC>::fits) {
-        if (mlp_bwd_pair_enabled()) {
-            const uint32_t blocks = bwd_blocks(a.B);  // the slab has one row per block either way
-            if (blocks == 0) return NGP_OK;
-            constexpr size_t lds_bytes = NerfBwdPairLds<NHS, NHC>::total;
-            hipLaunchKernelGGL((k_nerf_bwd_pair<NHS, NHC>), dim3(blocks), dim3(kPairThreads), lds_bytes, st, a);
-            return ngp_check_launch("nerf_backward_pair");
-        }
-    }
     if constexpr (!NerfBwdLds<NHS, NHC>::fits) {
         return ngp_set_error(NGP_ERR_UNSUPPORTED, "nerf_backward: networks too large for one launch's LDS");
     } else {
         const uint32_t blocks = bwd_blocks(a.B);
         if (blocks == 0) return NGP_OK;
         constexpr size_t lds_bytes = NerfBwdLds<NHS, NHC>::total;
-        constexpr size_t list_bytes = lds_bytes + 2 * sizeof(uint32_t) * kListMaxRays;
-        if (a.list_cnt) {
-            if constexpr (list_bytes + 1024 > 160 * 1024) {
-                return ngp_set_error(NGP_ERR_UNSUPPORTED, "nerf_backward_live_list: no LDS left for the list");
-            } else {
-                hipLaunchKernelGGL((k_nerf_bwd<NHS, NHC>), dim3(blocks), dim3(kBwdThreads), list_bytes, st, a);
-            }
-        } else {
-            hipLaunchKernelGGL((k_nerf_bwd<NHS, NHC>), dim3(blocks), dim3(kBwdThreads), lds_bytes, st, a);
-        }
+        hipLaunchKernelGGL((k_nerf_bwd<NHS, NHC>), dim3(blocks), dim3(kBwdThreads), lds_bytes, st, a);
         return ngp_check_launch("nerf_backward");
     }
 }
 
-#define NGP_MLP_DISPATCH(FN, ...)                                                              \
+#define MLP_DISPATCH(FN, ...)                                                              \
     do {                                                                                        \
         const int ks = (int)((in_dim + 31) / 32);                                                \
         const int nh = (int)num_layers - 1;                                                     \
@@ -1684,12 +1322,12 @@ int launch_nerf_bwd(const NerfBwdArgs& a, hipStream_t st) {
     } while (0)
 
 size_t image_bytes(uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers) {
-    NGP_MLP_DISPATCH(image_bytes_t);
+    MLP_DISPATCH(image_bytes_t);
 }
 
 int pack_one(PackJobs& jobs, const void* w, uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers,
              void* image) {
-    NGP_MLP_DISPATCH(add_pack_jobs, jobs, w, in_dim, image);
+    MLP_DISPATCH(add_pack_jobs, jobs, w, in_dim, image);
 }
 
 }  // namespace
@@ -1702,7 +1340,7 @@ extern "C" int ngp_ffmlp_forward(const void* inputs, const void* weights, uint32
     if (int e = check_shape(B, in_dim, output_dim, hidden_dim, num_layers)) return e;
     if (B == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
-    NGP_MLP_DISPATCH(launch_fwd, inputs, weights, nullptr, B, in_dim, activation, output_activation,
+    MLP_DISPATCH(launch_fwd, inputs, weights, nullptr, B, in_dim, activation, output_activation,
                      forward_buffer, outputs, nullptr, st);
 }
 
@@ -1716,7 +1354,7 @@ extern "C" int ngp_ffmlp_forward_rows(const void* inputs, const void* weights, c
     if (int e = check_shape(B, in_dim, output_dim, hidden_dim, num_layers)) return e;
     if (B == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
-    NGP_MLP_DISPATCH(launch_fwd, inputs, weights, image, B, in_dim, activation, output_activation,
+    MLP_DISPATCH(launch_fwd, inputs, weights, image, B, in_dim, activation, output_activation,
                      nullptr, outputs, count, st);
 }
 
@@ -1730,7 +1368,7 @@ extern "C" int ngp_nerf_sigma_forward(const void* inputs, const void* weights, c
     hipStream_t st = ngp_stream(stream);
     const EpiNerfSigma epi{static_cast<ngp_half*>(h_out), sigma, static_cast<ngp_half*>(color_in), dirs,
                            density_scale};
-    NGP_MLP_DISPATCH(launch_fwd_nerf, inputs, weights, image, B, in_dim, count, epi,
+    MLP_DISPATCH(launch_fwd_nerf, inputs, weights, image, B, in_dim, count, epi,
                      (flags & NGP_FFMLP_PAIR_MAJOR) != 0, st);
 }
 
@@ -1770,19 +1408,13 @@ extern "C" int ngp_nerf_forward(const void* enc, const void* sigma_image, const 
  * workspaces (ngp_ffmlp_backward_workspace_bytes of each network) for
  * ngp_ffmlp_reduce, as NGP_FFMLP_DEFER_REDUCE. Input gradients equal the two
  * calls bit for bit; dW is summed in another order. */
-struct ListIn {  // the in-launch list's inputs (ngp_nerf_backward_live_list), or all null
-    const int32_t *cnt = nullptr, *rays = nullptr, *src = nullptr;
-    int32_t* total = nullptr;
-    uint32_t n = 0;
-};
-
 static int nerf_backward_impl(const void* g_color_out, const void* color_in, const void* color_image,
                               void* g_h, const void* enc, const void* sigma_image, void* g_enc, uint32_t B,
                               const int32_t* count, const int32_t* rows, uint32_t hidden_dim, uint32_t num_layers,
                               uint32_t hidden_dim_color, uint32_t num_layers_color, void* sigma_workspace,
                               size_t sigma_workspace_bytes, void* color_workspace, size_t color_workspace_bytes,
-                              uint32_t* timing, void* stream, const ListIn& list = ListIn{}) {
-    NGP_REQUIRE(!rows || count || list.cnt, NGP_ERR_ARG, "nerf_backward_live: a row list needs its count");
+                              uint32_t* timing, void* stream) {
+    NGP_REQUIRE(!rows || count, NGP_ERR_ARG, "nerf_backward_live: a row list needs its count");
     NGP_REQUIRE(hidden_dim == 64 && hidden_dim_color == 64, NGP_ERR_UNSUPPORTED,
                 "nerf_backward: 64-wide networks only on this build, got %u / %u", hidden_dim, hidden_dim_color);
     NGP_REQUIRE(num_layers >= 2 && num_layers <= 3 && num_layers_color >= 2 && num_layers_color <= 3,
@@ -1812,16 +1444,8 @@ static int nerf_backward_impl(const void* g_color_out, const void* color_in, con
     a.B = B;
     a.count = count;
     a.timing = timing;
-    a.halves = mlp_bwd_halves_enabled() ? 1u : 0u;
     a.rows = rows;
-    a.list_cnt = list.cnt;
-    a.list_rays = list.rays;
-    a.list_src = list.src;
-    a.list_total = list.total;
-    a.list_n = list.n;
     hipStream_t st = ngp_stream(stream);
-    if (list.cnt && mlp_bwd_pair_enabled())
-        return ngp_set_error(NGP_ERR_UNSUPPORTED, "nerf_backward_live_list: not with NGP_MLP_BWD_PAIR=1");
     const uint32_t key = (num_layers - 1) * 8 + (num_layers_color - 1);
     switch (key) {
         case 1 * 8 + 1: return launch_nerf_bwd<1, 1>(a, st);
@@ -1854,30 +1478,6 @@ extern "C" int ngp_nerf_backward_live(const void* g_color_out, const void* color
                               sigma_workspace_bytes, color_workspace, color_workspace_bytes, timing, stream);
 }
 
-extern "C" int ngp_nerf_backward_live_list(const void* g_color_out, const void* color_in, const void* color_image,
-                                           void* g_h, const void* enc, const void* sigma_image, void* g_enc,
-                                           uint32_t B, const int32_t* rays, uint32_t N, const int32_t* live_cnt,
-                                           const int32_t* ray_rows, int32_t* live_rows, int32_t* live_total,
-                                           uint32_t hidden_dim, uint32_t num_layers, uint32_t hidden_dim_color,
-                                           uint32_t num_layers_color, void* sigma_workspace,
-                                           size_t sigma_workspace_bytes, void* color_workspace,
-                                           size_t color_workspace_bytes, uint32_t* timing, void* stream) {
-    NGP_REQUIRE(rays && live_cnt && ray_rows && live_rows && live_total, NGP_ERR_ARG,
-                "nerf_backward_live_list: null rays / live_cnt / ray_rows / live_rows / live_total");
-    NGP_REQUIRE(N >= 1 && N <= kListMaxRays, NGP_ERR_UNSUPPORTED,
-                "nerf_backward_live_list: 1..%u rays per call, got %u (use ngp_nerf_composite_loss_live + "
-                "ngp_nerf_backward_live)", kListMaxRays, N);
-    ListIn list;
-    list.cnt = live_cnt;
-    list.rays = rays;
-    list.src = ray_rows;
-    list.total = live_total;
-    list.n = N;
-    return nerf_backward_impl(g_color_out, color_in, color_image, g_h, enc, sigma_image, g_enc, B, nullptr,
-                              live_rows, hidden_dim, num_layers, hidden_dim_color, num_layers_color, sigma_workspace,
-                              sigma_workspace_bytes, color_workspace, color_workspace_bytes, timing, stream, list);
-}
-
 extern "C" int ngp_nerf_density_forward(const void* inputs, const void* weights, const void* image, uint32_t B,
                                         uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers,
                                         float density_scale, const int32_t* indices, float* tmp_grid,
@@ -1887,7 +1487,7 @@ extern "C" int ngp_nerf_density_forward(const void* inputs, const void* weights,
     if (B == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
     const EpiDensity epi{tmp_grid, indices, density_scale};
-    NGP_MLP_DISPATCH(launch_fwd_density, inputs, weights, image, B, in_dim, epi, st);
+    MLP_DISPATCH(launch_fwd_density, inputs, weights, image, B, in_dim, epi, st);
 }
 
 extern "C" int ngp_ffmlp_inference(const void* inputs, const void* weights, uint32_t B,
@@ -1953,7 +1553,7 @@ extern "C" int ngp_ffmlp_backward(const void* grad, const void* inputs, const vo
                 "ffmlp_backward: workspace of %zu bytes required, got %zu", need, workspace_bytes);
     hipStream_t st = ngp_stream(stream);
     void* gi = calc_grad_inputs ? grad_inputs : nullptr;
-    NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, nullptr, B, in_dim, activation, gi, false, grad_weights,
+    MLP_DISPATCH(launch_bwd, grad, inputs, weights, nullptr, B, in_dim, activation, gi, false, grad_weights,
                      gw_dtype, false, workspace, nullptr, st);
 }
 
@@ -1979,7 +1579,7 @@ extern "C" int ngp_ffmlp_backward_rows(const void* grad, const void* inputs, con
     hipStream_t st = ngp_stream(stream);
     const bool geo = (flags & NGP_FFMLP_NERF_GEO) != 0, defer = (flags & NGP_FFMLP_DEFER_REDUCE) != 0;
     const bool pm = (flags & NGP_FFMLP_PAIR_MAJOR) != 0;
-    NGP_MLP_DISPATCH(launch_bwd, grad, inputs, weights, image, B, in_dim, activation, grad_inputs, geo,
+    MLP_DISPATCH(launch_bwd, grad, inputs, weights, image, B, in_dim, activation, grad_inputs, geo,
                      grad_weights, gw_dtype, defer, workspace, count, st, pm);
 }
 

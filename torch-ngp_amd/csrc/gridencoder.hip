@@ -106,17 +106,10 @@ NGP_DEV void load_entry_as(const E* __restrict__ p, typename Acc<T>::F out[C]) {
 struct InMap {
     float shift, scale;  // scale == 0: inputs are used as given
     const int32_t* count;
-    // double-buffered table (fused Adam): grid = *sel ? alt : grid
-    const void* alt = nullptr;
-    const int32_t* sel = nullptr;
     // backward over a row list (the step's live rows): row b is rows[b], b < *count
     const int32_t* rows = nullptr;
 };
 NGP_DEV uint32_t phys_row(const InMap& m, uint32_t b) { return m.rows ? (uint32_t)m.rows[b] : b; }
-template <typename E>
-NGP_DEV const E* select_table(const E* grid, const InMap& m) {
-    return m.sel && *m.sel ? static_cast<const E*>(m.alt) : grid;
-}
 NGP_DEV uint32_t rows_of(uint32_t B, const InMap& m) {
     if (!m.count) return B;
     const int32_t c = *m.count;
@@ -143,7 +136,6 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= rows_of(B, im)) return;
     const uint32_t level = blockIdx.y;
-    grid = select_table(grid, im);
 
     T* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C
                              : outputs + ((size_t)b * L + level) * C;
@@ -276,10 +268,7 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
 // 1-2M query points measured faster level-interleaved (r05ad: full update
 // 0.655-0.668 -> 0.600-0.609 ms, partial unchanged), hence the threshold.
 constexpr uint32_t kFwdLevelsPerBlock = 2;
-#ifndef NGP_FWD_GROUP_MAJOR_MIN  // same-box A/B builds only (tools/variants.sh)
-#define NGP_FWD_GROUP_MAJOR_MIN (1u << 22)
-#endif
-constexpr uint32_t kFwdGroupMajorMin = NGP_FWD_GROUP_MAJOR_MIN;
+constexpr uint32_t kFwdGroupMajorMin = (1u << 22);
 
 // Levels [lo, hi) of the L-level table (the fused step splits the forward
 // in two launches, each beside a part of the optimizer sweep); blk is the
@@ -310,7 +299,6 @@ NGP_DEV void grid_fwd_pair_block(uint32_t blk, const float* __restrict__ inputs,
     const uint32_t xbit = threadIdx.x & 1;
     const bool live = b < rows_of(B, im);
     if (__ballot(live) == 0) return;  // wave-uniform exit; pairs stay together below
-    grid = select_table(grid, im);
 
     // Every load below is unconditional (dead lanes read a valid clamped
     // address and discard the value): a load under a divergent branch made the
@@ -442,48 +430,6 @@ k_grid_fwd_tail(const float* __restrict__ inputs, const E* __restrict__ grid,
     blk -= (uint32_t)ft.jobs.n;
     grid_fwd_pair_block<T, E, D, C, KL>(blk, inputs, grid, offsets, outputs, B, L, lv, gridtype, align_corners,
                                         interp, out_layout, im, LevelRange{0u, L});
-}
-
-// The fused step's grid forward in two launches (ngp_grid_encode_forward_fused_adam):
-// the first carries the part of the previous step's Adam sweep over the
-// levels the second encodes (blocks [0, nadam): 256-thread Adam blocks, the
-// march launch's sweep, dispatched first so they stream beside the
-// gather-bound forward blocks), the second the deferred GradScaler / LambdaLR /
-// loss bookkeeping of that update (one block, after every Adam block of the
-// earlier launches has read the scaler state). A level's forward never reads
-// a value the same launch's Adam writes.
-struct FwdAdam {
-    ngp_head::TensorList tl;
-    ngp_head::AdamArgs aa;
-    ngp_step::StepState* st;   // null: no Adam blocks
-    uint32_t nadam;
-    ngp_step::StepState* end;  // null: no bookkeeping block
-    ngp_step::ScalerArgs sa;
-    const float* loss_ray;
-    uint32_t n_rays;
-};
-
-template <typename T, typename E, uint32_t D, uint32_t C, uint32_t KL>
-__global__ void __launch_bounds__(256, 7)  // <= 72 VGPRs: the forward blocks keep most of their occupancy
-k_grid_fwd_adam(const float* __restrict__ inputs, const E* __restrict__ grid,
-                const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
-                GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
-                int32_t out_layout, InMap im, LevelRange lr, FwdAdam fa) {
-    const uint32_t nadam = fa.st ? fa.nadam : 0u;
-    if (blockIdx.x < nadam) {
-        ngp_head::adam_sweep_pipe<1>(fa.tl, fa.st, fa.aa, blockIdx.x, nadam, threadIdx.x);
-        return;
-    }
-    uint32_t blk = blockIdx.x - nadam;
-    if (fa.end) {
-        if (blk == 0) {
-            if (fa.end->end_pending) ngp_step::step_end_block(fa.end, fa.sa, nullptr, nullptr, fa.loss_ray, fa.n_rays);
-            return;
-        }
-        --blk;
-    }
-    grid_fwd_pair_block<T, E, D, C, KL>(blk, inputs, grid, offsets, outputs, B, L, lv, gridtype, align_corners,
-                                        interp, out_layout, im, lr);
 }
 
 // ---- scatter-add of one corner's C channels (values already weighted) -----
@@ -641,7 +587,7 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 // Scattered atomics cost one memory-side request per (point, corner pair)
 // whatever is done, and the coarse levels' few entries turn them into hot
 // spots. Instead every level's corner contributions are sorted into bins of
-// 2^kBinShift table entries (NGP_BIN_SHIFT, default 2^12 = 4096):
+// 2^kBinShift table entries (12, default 2^12 = 4096):
 //   k_grid_bwd_bin   one workgroup = kBinPts (512) consecutive samples of one
 //                    level; the grid is (level, block), levels interleaved.
 //                    Consecutive samples walk along a ray, so on coarse
@@ -669,41 +615,20 @@ k_grid_bwd(const T* __restrict__ grad, const float* __restrict__ inputs,
 // from launch to launch. Levels with more than kMaxBinsPerLevelBig bins (or
 // past the plan's kMaxTotalBins) use k_grid_bwd.
 // The NGP_* macros exist only for same-box A/B builds (tools/variants.sh).
-#ifndef NGP_BIN_SHIFT
-#define NGP_BIN_SHIFT 12
-#endif
-#ifndef NGP_SEG_ITEMS
-#define NGP_SEG_ITEMS 16384
-#endif
-#ifndef NGP_MERGE_MAX_RES
-#define NGP_MERGE_MAX_RES 128
-#endif
-#ifndef NGP_ACC_BATCH
-#define NGP_ACC_BATCH 8
-#endif
-#ifndef NGP_JOINT_MERGE
-#define NGP_JOINT_MERGE 1
-#endif
-#ifndef NGP_SPARSE_Q
-#define NGP_SPARSE_Q 4
-#endif
-#ifndef NGP_MATCH_MAX_BINS
-#define NGP_MATCH_MAX_BINS 64
-#endif
-constexpr uint32_t kBinShift = NGP_BIN_SHIFT;
+constexpr uint32_t kBinShift = 12;
 constexpr uint32_t kBinEntries = 1u << kBinShift;
 constexpr uint32_t kMaxBinsPerLevel = 256;       // the bin kernel's small instantiation
 constexpr uint32_t kMaxBinsPerLevelBig = 1024;   // ... and the large one (2^22-entry levels)
 // the accumulate keeps two words per bin in LDS beside its 64 KiB image
 constexpr uint32_t kMaxTotalBins = 11776;
-constexpr uint32_t kSegItems = NGP_SEG_ITEMS;
+constexpr uint32_t kSegItems = 16384;
 // entries within a bin are packed in 16 bits while staged (| bin << 16)
-static_assert(kBinShift >= 9 && kBinShift <= 16, "NGP_BIN_SHIFT must be in [9, 16]");
-static_assert(kSegItems > 0, "NGP_SEG_ITEMS must be positive");
+static_assert(kBinShift >= 9 && kBinShift <= 16, "12 must be in [9, 16]");
+static_assert(kSegItems > 0, "16384 must be positive");
 // Levels up to this resolution merge runs of equal corners in-wave: on the
 // Lego step the merge cuts their items 3.5-16x (tools/grid_bwd_micro.py);
 // finer levels gain less than the scan costs.
-constexpr uint32_t kMergeMaxRes = NGP_MERGE_MAX_RES;
+constexpr uint32_t kMergeMaxRes = 128;
 
 struct BinPlan {
     uint32_t nlev;                   // levels [0, nlev) are binned
@@ -899,21 +824,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         live[idx] = valid;
         vv[idx][0] = w * g0;
         vv[idx][1] = w * g1;
-#if !NGP_JOINT_MERGE
-        if (merge) {
-            const uint32_t kprev = ngp_dpp::prev_lane(k);
-            const bool same = valid && lane > 0 && kprev == k;
-            const uint64_t sm = __ballot(same);
-            if (sm) {
-                // runs of equal keys: segmented DPP scan, the run's last lane keeps the sum
-                ngp_dpp::seg_scan2(vv[idx][0], vv[idx][1], !same);
-                const bool next_same = lane < 63 && ((sm >> (lane + 1)) & 1ull);
-                live[idx] = valid && !next_same;
-            }
-        }
-#endif
     }
-#if NGP_JOINT_MERGE
     if (merge) {
         // Consecutive samples in one cell share all 2^D corners: one run
         // structure (cell equality with the previous lane) and one segmented
@@ -937,7 +848,6 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
             for (uint32_t idx = 0; idx < NC; idx++) live[idx] = valid && !next_same;
         }
     }
-#endif
 #pragma unroll
     for (uint32_t idx = 0; idx < NC; idx++) val[idx] = ngp_half2{(ngp_half)vv[idx][0], (ngp_half)vv[idx][1]};
     // Rank within the bin. When every live item of the wave (all corners) is
@@ -956,7 +866,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // matched bin's run at once; each item then adds its match's base (one
     // lane permute). Items left over (and every item of a many-bin level)
     // take the per-corner path.
-    constexpr uint32_t kMatchIters = 8, kMatchMaxBins = NGP_MATCH_MAX_BINS;
+    constexpr uint32_t kMatchIters = 8, kMatchMaxBins = 64;
     static_assert(kMatchIters <= 64, "one lane per match");
     BSTAMP(6);
     uint64_t pend[NC];
@@ -1122,27 +1032,10 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
 // (inf / NaN: fp16 overflow under the loss scale) cannot be carried by the
 // integers, so it marks the unit and the unit stores a NaN into its bin's
 // first entry, which is what GradScaler's inf check looks for.
-// Fused Adam (ngp_adam_table, world 1): with `st` set, every unit that owns
-// its slice of the zeroed grad updates the whole slice with Adam from its
-// exact sums -- rounded to the fp16 grad torch would hold, unscaled: the
-// arithmetic of the optimizer sweep (ngp_step::adam_update) -- reading the
-// current p / m / v buffers and writing the other ones, and tags its bin in
-// `done` with iter + 1; the step's optimizer launch updates the untagged
-// slices. The slice's grads are never written.
-struct AccAdam {
-    float* p[2];
-    float* m[2];
-    float* v[2];
-    uint32_t* done;
-    const ngp_step::StepState* st;  // null: no fused Adam
-    float lr, beta1, beta2, eps;
-    int32_t iters;
-};
-
-constexpr uint32_t kAccThreads = 512, kAccBatch = NGP_ACC_BATCH, kRetireGroups = 16;
+constexpr uint32_t kAccThreads = 512, kAccBatch = 8, kRetireGroups = 16;
 // the accumulate's static LDS (the 64 KiB image and its small arrays), for the launch's occupancy choice
 constexpr size_t kAccStaticLds = 66 * 1024 + 1024;
-static_assert(kAccBatch > 0, "NGP_ACC_BATCH must be positive");
+static_assert(kAccBatch > 0, "8 must be positive");
 static_assert(kMaxLevels <= 64, "the accumulate finds a bin's level with one wave ballot");
 static_assert(kBinEntries % kAccThreads == 0, "each flush thread owns whole entries (G > 0)");
 // the int64 LDS image of one bin (+ the counts in dynamic LDS) fits a CU's 160 KB
@@ -1155,7 +1048,7 @@ __global__ void __launch_bounds__(kAccThreads, 4)  // 2 workgroups per CU: <= 12
 k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
                  const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
-                 bool external, AccAdam ad, unsigned long long* __restrict__ msums,
+                 bool external, unsigned long long* __restrict__ msums,
                  uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing,
                  int32_t* __restrict__ reset_counter, unsigned long long* __restrict__ spill,
                  uint32_t* __restrict__ spill_bad) {
@@ -1202,25 +1095,6 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         }
     }
     lds_barrier();
-    // fused Adam: the constants of this update (the state the next step head's
-    // optimizer reads: scale, Adam step, LR epoch, current buffer)
-    bool adam_on = false;
-    ngp_step::AdamConsts ac{};
-    const float2 *a_sp = nullptr, *a_sm = nullptr, *a_sv = nullptr;
-    float2 *a_dp = nullptr, *a_dm = nullptr, *a_dv = nullptr;
-    uint32_t tag = 0;
-    if (ad.st) {
-        ac = ngp_step::adam_consts(ad.st, ad.lr, ad.beta1, ad.beta2, ad.iters, 1.0f);
-        adam_on = !ac.inv_bad;  // 1/scale inf: the step is skipped (the optimizer launch flags it)
-        const int src = ad.st->cur & 1;
-        a_sp = reinterpret_cast<const float2*>(ad.p[src]);
-        a_sm = reinterpret_cast<const float2*>(ad.m[src]);
-        a_sv = reinterpret_cast<const float2*>(ad.v[src]);
-        a_dp = reinterpret_cast<float2*>(ad.p[src ^ 1]);
-        a_dm = reinterpret_cast<float2*>(ad.m[src ^ 1]);
-        a_dv = reinterpret_cast<float2*>(ad.v[src ^ 1]);
-        tag = (uint32_t)ad.st->iter + 1u;
-    }
     auto level_of = [&](uint32_t b) {  // last level whose first bin is <= b (binary lifting)
         uint32_t l = 0;
 #pragma unroll
@@ -1390,7 +1264,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // one entry store the same value) and, after a barrier, clears just
     // those entries -- no 4096-entry flush and no zeroing pass for the next
     // unit. The entries are kept in ent[] (the prefetch overwrites it[]).
-    constexpr uint32_t kSparseQ = NGP_SPARSE_Q, kSparseMax = kSparseQ * kAccThreads;
+    constexpr uint32_t kSparseQ = 4, kSparseMax = kSparseQ * kAccThreads;
     static_assert(kSparseQ <= kAccBatch, "a sparse unit is one item batch");
     bool need_zero = true;  // the image holds entries no flush cleared (initially: all of it)
     for (uint32_t k = 0; u < total; ++k) {
@@ -1405,8 +1279,6 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         }
         [[maybe_unused]] const uint32_t sb = 4 + 5 * min(nstamp, 11u);
         STAMP(sb, __builtin_amdgcn_s_memtime());
-        // fused Adam of the slice this unit owns (whole slice, see the flush)
-        const bool adam_unit = adam_on && (cur.flags & kFresh);
         const size_t ebase = (size_t)s_off[cur.level] + (size_t)cur.lbin * kBinEntries;
         STAMP(sb + 3, (cur.s1 - cur.s0) | ((uint64_t)(cur.flags & kOwner) << 32) | ((uint64_t)cur.level << 40));
         bool bad = false;
@@ -1464,52 +1336,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         const bool unit_bad = s_bad != 0;
         const float q24 = 1.0f / 16777216.0f;
         bool inf_out = false;  // a stored grad is inf/nan (GradScaler's check, when `nonfinite` is given)
-        if (adam_unit) {
-            // every entry of the slice (zero where no item landed): the fp16
-            // grad torch would hold, then Adam into the other buffer. A quarter
-            // of the lane's entries at a time, each quarter's p / m / v loads
-            // issued together (unconditional, clamped), so the accumulate keeps
-            // its register budget (2 workgroups of 8 waves per CU)
-            constexpr uint32_t GH = G / 4;
-#pragma unroll
-            for (uint32_t h = 0; h < G / GH; ++h) {
-                float2 ap[GH], am[GH], av[GH];
-                ulonglong2 xs[GH];
-#pragma unroll
-                for (uint32_t j = 0; j < GH; ++j) {
-                    const uint32_t e = (h * GH + j) * kAccThreads + t;
-                    const size_t i = ebase + (e < cur.ne ? e : 0u);
-                    ap[j] = a_sp[i];
-                    am[j] = a_sm[i];
-                    av[j] = a_sv[i];
-                    xs[j] = e < cur.ne ? acc_entry(e) : ulonglong2{0ull, 0ull};
-                }
-#pragma unroll
-                for (uint32_t j = 0; j < GH; ++j) {
-                    const uint32_t e = (h * GH + j) * kAccThreads + t;
-                    if (e >= cur.ne) continue;
-                    const int64_t x0 = (int64_t)xs[j].x, x1 = (int64_t)xs[j].y;
-                    const ngp_half2 n{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
-                    inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
-                    ngp_step::adam_update(ap[j].x, am[j].x, av[j].x, (float)n[0], ac, ad.beta1, ad.beta2, ad.eps);
-                    ngp_step::adam_update(ap[j].y, am[j].y, av[j].y, (float)n[1], ac, ad.beta1, ad.beta2, ad.eps);
-                    a_dp[ebase + e] = ap[j];
-                    a_dm[ebase + e] = am[j];
-                    a_dv[ebase + e] = av[j];
-                }
-            }
-            if (sparse) {  // few items: clear just their entries
-                lds_barrier();  // every lane's reads are done before any entry is cleared
-#pragma unroll
-                for (uint32_t q = 0; q < kSparseQ; ++q)
-                    if (ent[q] != 0xffffffffu) reinterpret_cast<ulonglong2*>(acc)[ent[q]] = ulonglong2{0ull, 0ull};
-                if (t == 0) s_bad = 0;
-                need_zero = false;
-            } else {
-                need_zero = true;
-            }
-            if (t == 0) ad.done[cur.gb] = tag;
-        } else if (sparse) {
+        if (sparse) {
             ulonglong2 xs[kSparseQ];
 #pragma unroll
             for (uint32_t q = 0; q < kSparseQ; ++q)
@@ -1557,7 +1384,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             // bin's int64 slot (integer adds: the total does not depend on the
             // units' order), then the last unit to arrive takes the totals
             // (clearing the slot for the next call) and finishes the bin as an
-            // owner would: the fp16 grads, or Adam
+            // owner would
             unsigned long long* sums = msums + (size_t)cur.slot * kBinEntries * C;
 #pragma unroll 1
             for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
@@ -1572,7 +1399,6 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             if (s_lastunit) {
                 __threadfence();
                 if (t == 0) marrive[cur.slot] = 0;
-                const bool adam_bin = adam_on;
 #pragma unroll 1
                 for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
                     const int64_t x0 = (int64_t)atomicExch(sums + 2 * e, 0ull);
@@ -1585,18 +1411,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                     }
                     const ngp_half2 n{(ngp_half)(o0 + (float)x0 * q24), (ngp_half)(o1 + (float)x1 * q24)};
                     inf_out |= !__builtin_isfinite((float)n[0]) || !__builtin_isfinite((float)n[1]);
-                    if (adam_bin) {
-                        float2 pp = a_sp[ebase + e], mm = a_sm[ebase + e], vv = a_sv[ebase + e];
-                        ngp_step::adam_update(pp.x, mm.x, vv.x, (float)n[0], ac, ad.beta1, ad.beta2, ad.eps);
-                        ngp_step::adam_update(pp.y, mm.y, vv.y, (float)n[1], ac, ad.beta1, ad.beta2, ad.eps);
-                        a_dp[ebase + e] = pp;
-                        a_dm[ebase + e] = mm;
-                        a_dv[ebase + e] = vv;
-                    } else if (x0 != 0 || x1 != 0) {
-                        cur.tbl[e] = n;
-                    }
+                    if (x0 != 0 || x1 != 0) cur.tbl[e] = n;
                 }
-                if (adam_bin && t == 0) ad.done[cur.gb] = tag;
             }
         } else if (!ZEROED && (cur.flags & kOwner)) {
             need_zero = true;
@@ -1617,7 +1433,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             }
         }
         // a NaN grad marks a bad unit for a caller without the flag (a flagged
-        // one, and every fused-Adam unit, which writes no grads, reports below)
+        // one reports below)
         if (unit_bad && !nonfinite && t == 0) cur.tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
         if (nonfinite && (__ballot(inf_out) != 0 || unit_bad) && (t & 63) == 0) atomicOr(nonfinite, 1);
         lds_barrier();  // the image is rezeroed by the next unit
@@ -1816,19 +1632,19 @@ int fwd_c(const float* inputs, const void* emb, const int32_t* offsets, void* ou
         const uint32_t kl = gm ? 1u : kFwdLevelsPerBlock;
         const uint32_t gpx = ((L + 7) / 8 + kl - 1) / kl;
         const dim3 gp(8 * gpx * ngp_div_up(B, 128));
-#define NGP_FWD_PAIR(CC)                                                                                     \
+#define FWD_PAIR_CASE(CC)                                                                                     \
     (gm ? k_grid_fwd_pair<T, E, D, CC, 1><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, \
                                                              interp, layout, im)                              \
         : k_grid_fwd_pair<T, E, D, CC><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac,     \
                                                           interp, layout, im))
         switch (C) {
-            case 1: NGP_FWD_PAIR(1); break;
-            case 2: NGP_FWD_PAIR(2); break;
-            case 4: NGP_FWD_PAIR(4); break;
-            case 8: NGP_FWD_PAIR(8); break;
+            case 1: FWD_PAIR_CASE(1); break;
+            case 2: FWD_PAIR_CASE(2); break;
+            case 4: FWD_PAIR_CASE(4); break;
+            case 8: FWD_PAIR_CASE(8); break;
             default: return ngp_set_error(NGP_ERR_UNSUPPORTED, "GridEncoding: C must be 1, 2, 4, or 8.");
         }
-#undef NGP_FWD_PAIR
+#undef FWD_PAIR_CASE
         return ngp_check_launch("grid_encode_forward");
     }
     switch (C) {
@@ -2027,73 +1843,6 @@ extern "C" int ngp_grid_encode_forward_fused(const float* xyz, float bound, cons
                                   align_corners != 0, interp, out_layout, ngp_stream(stream), im);
 }
 
-extern "C" int ngp_grid_encode_forward_fused_adam(const float* xyz, float bound, const void* embeddings,
-                                                  int32_t emb_dtype, const int32_t* offsets, void* outputs,
-                                                  uint32_t B, const int32_t* count, uint32_t D, uint32_t C,
-                                                  uint32_t L, float S, uint32_t H, uint32_t gridtype,
-                                                  int32_t align_corners, uint32_t interp, uint32_t level_lo,
-                                                  uint32_t level_hi, const ngp_adam_job* job, void* state,
-                                                  void* end_state, float growth_factor, float backoff_factor,
-                                                  int32_t growth_interval, int32_t scaler_enabled,
-                                                  const float* loss_ray, uint32_t n_rays, void* stream) {
-    if (int e = check_common(L, embeddings, offsets, outputs)) return e;
-    NGP_REQUIRE(xyz && bound > 0.0f, NGP_ERR_ARG, "grid_encode_forward_fused_adam: null xyz or bound <= 0");
-    NGP_REQUIRE(D == 3 && C == 2, NGP_ERR_UNSUPPORTED, "grid_encode_forward_fused_adam: D 3, C 2 only");
-    NGP_REQUIRE(level_lo < level_hi && level_hi <= L, NGP_ERR_ARG,
-                "grid_encode_forward_fused_adam: levels [%u, %u) of %u", level_lo, level_hi, L);
-    NGP_REQUIRE(emb_dtype == NGP_DTYPE_F32 || emb_dtype == NGP_DTYPE_F16, NGP_ERR_ARG,
-                "grid_encode_forward_fused_adam: emb_dtype %d (F32 or F16)", emb_dtype);
-    NGP_REQUIRE(!job || state, NGP_ERR_ARG, "grid_encode_forward_fused_adam: a job needs the state");
-    NGP_REQUIRE(!end_state || loss_ray, NGP_ERR_ARG, "grid_encode_forward_fused_adam: the bookkeeping needs loss_ray");
-    FwdAdam fa{};
-    if (job) {
-        NGP_REQUIRE(job->n_tensors >= 1 && job->n_tensors <= ngp_head::kMaxTensors, NGP_ERR_ARG,
-                    "grid_encode_forward_fused_adam: 1..%d tensors", ngp_head::kMaxTensors);
-        for (int q = 0; q < job->n_tensors; ++q) {
-            NGP_REQUIRE(((reinterpret_cast<uintptr_t>(job->params[q]) |
-                          reinterpret_cast<uintptr_t>(job->exp_avg[q]) |
-                          reinterpret_cast<uintptr_t>(job->exp_avg_sq[q])) & 15) == 0 &&
-                            (reinterpret_cast<uintptr_t>(job->grads[q]) & 7) == 0 &&
-                            (reinterpret_cast<uintptr_t>(job->half_params[q]) & 7) == 0,
-                        NGP_ERR_ARG, "grid_encode_forward_fused_adam: tensor %d misaligned", q);
-        }
-        fa.tl = ngp_head::make_list(job->n_tensors, job->params, job->grads, job->exp_avg, job->exp_avg_sq,
-                                    job->half_params, job->sizes);
-        fa.aa = ngp_head::AdamArgs{job->lr, job->beta1, job->beta2, job->eps, job->iters, job->zero_grads,
-                                   job->grad_mult, 1};
-        fa.st = static_cast<ngp_step::StepState*>(state);
-        // three 256-thread Adam blocks per CU, as the march launch's (NGP_FWD_ADAM_BLOCKS: per CU, A/B)
-        const char* nb = getenv("NGP_FWD_ADAM_BLOCKS");
-        const uint32_t per_cu = nb ? (uint32_t)atoi(nb) : 3u;
-        fa.nadam = (per_cu ? per_cu : 1u) * ngp_num_cus();
-    }
-    if (end_state) {
-        fa.end = static_cast<ngp_step::StepState*>(end_state);
-        fa.sa = ngp_step::ScalerArgs{growth_factor, backoff_factor, growth_interval, scaler_enabled,
-                                     n_rays ? 1.0f / (float)n_rays : 0.0f};
-        fa.loss_ray = loss_ray;
-        fa.n_rays = n_rays;
-    }
-    if (B == 0) return NGP_OK;
-    GridLevels lv;
-    make_levels(lv, L, S, H);
-    const InMap im{bound, 1.0f / (2.0f * bound), count};
-    const LevelRange lr{level_lo, level_hi};
-    const uint32_t nfwd = 8u * ((level_hi - level_lo + 7) / 8) * ngp_div_up(B, 128);
-    const dim3 grid(nfwd + (fa.st ? fa.nadam : 0u) + (fa.end ? 1u : 0u));
-    hipStream_t st = ngp_stream(stream);
-    const bool ac = align_corners != 0;
-    if (emb_dtype == NGP_DTYPE_F16)
-        k_grid_fwd_adam<ngp_half, ngp_half, 3, 2, 1><<<grid, 256, 0, st>>>(
-            xyz, static_cast<const ngp_half*>(embeddings), offsets, static_cast<ngp_half*>(outputs), B, L, lv, gridtype,
-            ac, interp, 0, im, lr, fa);
-    else
-        k_grid_fwd_adam<ngp_half, float, 3, 2, 1><<<grid, 256, 0, st>>>(
-            xyz, static_cast<const float*>(embeddings), offsets, static_cast<ngp_half*>(outputs), B, L, lv, gridtype,
-            ac, interp, 0, im, lr, fa);
-    return ngp_check_launch("grid_encode_forward_fused_adam");
-}
-
 extern "C" int ngp_grid_encode_forward_fused_tail(const float* xyz, float bound, const void* embeddings,
                                                   int32_t emb_dtype, const int32_t* offsets, void* outputs, uint32_t B,
                                                   const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
@@ -2132,42 +1881,18 @@ extern "C" int ngp_grid_encode_forward_fused_tail(const float* xyz, float bound,
     if (grid.x == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
     ngp_half* o = static_cast<ngp_half*>(outputs);
-#define NGP_FWD_TAIL(E_)                                                                                          \
+#define FWD_TAIL_LAUNCH(E_)                                                                                          \
     (gm ? k_grid_fwd_tail<ngp_half, E_, 3, 2, 1><<<grid, 256, 0, st>>>(xyz, static_cast<const E_*>(embeddings),   \
                                                                         offsets, o, B, L, lv, gridtype, ac, interp, \
                                                                         0, im, ft)                                  \
         : k_grid_fwd_tail<ngp_half, E_, 3, 2><<<grid, 256, 0, st>>>(xyz, static_cast<const E_*>(embeddings), offsets, \
                                                                      o, B, L, lv, gridtype, ac, interp, 0, im, ft))
     if (emb_dtype == NGP_DTYPE_F16)
-        NGP_FWD_TAIL(ngp_half);
+        FWD_TAIL_LAUNCH(ngp_half);
     else
-        NGP_FWD_TAIL(float);
-#undef NGP_FWD_TAIL
+        FWD_TAIL_LAUNCH(float);
+#undef FWD_TAIL_LAUNCH
     return ngp_check_launch("grid_encode_forward_fused_tail");
-}
-
-extern "C" int ngp_grid_encode_forward_fused_sel(const float* xyz, float bound, const void* table0,
-                                                 const void* table1, const int32_t* sel, int32_t emb_dtype,
-                                                 const int32_t* offsets, void* outputs, uint32_t B,
-                                                 const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S,
-                                                 uint32_t H, uint32_t gridtype, int32_t align_corners,
-                                                 uint32_t interp, int32_t out_layout, void* stream) {
-    if (int e = check_common(L, table0, offsets, outputs)) return e;
-    NGP_REQUIRE(xyz && bound > 0.0f && table1 && sel, NGP_ERR_ARG,
-                "grid_encode_forward_fused_sel: null xyz / second table / selector or bound <= 0");
-    if (B == 0) return NGP_OK;
-    GridLevels lv;
-    make_levels(lv, L, S, H);
-    InMap im{bound, 1.0f / (2.0f * bound), count};
-    im.alt = table1;
-    im.sel = sel;
-    NGP_REQUIRE(emb_dtype == NGP_DTYPE_F32 || emb_dtype == NGP_DTYPE_F16, NGP_ERR_ARG,
-                "grid_encode_forward_fused_sel: emb_dtype %d (F32 or F16)", emb_dtype);
-    if (emb_dtype == NGP_DTYPE_F16)
-        return fwd_t<ngp_half, ngp_half>(xyz, table0, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
-                                         align_corners != 0, interp, out_layout, ngp_stream(stream), im);
-    return fwd_t<ngp_half, float>(xyz, table0, offsets, outputs, B, D, C, L, lv, nullptr, gridtype,
-                                  align_corners != 0, interp, out_layout, ngp_stream(stream), im);
 }
 
 extern "C" size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, uint32_t C,
@@ -2201,7 +1926,7 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
                    uint32_t B, const int32_t* count, uint32_t D, uint32_t C, uint32_t L, float S, uint32_t H,
                    uint32_t gridtype, int32_t align_corners, uint32_t interp, const int32_t* offsets_host,
                    void* workspace, size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
-                   const AccAdam& ad, void* stream, const ngp_reduce::ReduceJobs* rj = nullptr,
+                   void* stream, const ngp_reduce::ReduceJobs* rj = nullptr,
                    uint32_t nred = 0, const BinLego* blp = nullptr, const int32_t* rows = nullptr) {
     if (int e = check_common(L, grad, offsets, grad_embeddings)) return e;
     const bool zeroed = (grad_layout & NGP_GRID_GRAD_ZEROED) != 0;
@@ -2263,11 +1988,11 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         int32_t* reset = bl.nlego ? bl.out.counter : nullptr;
         if (zeroed)
             k_grid_bin_accum<true><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
-                offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
+                offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
                 marrive, timing, reset, spill, spill_bad);
         else
             k_grid_bin_accum<false><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
-                offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, ad, msums,
+                offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
                 marrive, timing, reset, spill, spill_bad);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
@@ -2316,7 +2041,7 @@ extern "C" int ngp_grid_encode_backward_fused(const void* grad, const float* xyz
                                               int32_t* nonfinite, void* stream) {
     return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                           align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
-                          AccAdam{}, stream);
+                          stream);
 }
 
 extern "C" int ngp_grid_encode_backward_fused_reduce(const void* grad, const float* xyz, float bound,
@@ -2355,7 +2080,7 @@ extern "C" int ngp_grid_encode_backward_fused_reduce(const void* grad, const flo
                                                         num_layers, grad_weights, mlp_nonfinite, rj);
     return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                           align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
-                          AccAdam{}, stream, &rj, nred);
+                          stream, &rj, nred);
 }
 
 static int reduce_batch_impl(
@@ -2396,11 +2121,11 @@ static int reduce_batch_impl(
         if (int e = ngp_reduce::launch_slab_reduce(rj, nred, stream)) return e;
         return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                               align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout,
-                              nonfinite, AccAdam{}, stream, nullptr, 0, &bl, rows);
+                              nonfinite, stream, nullptr, 0, &bl, rows);
     }
     return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
                           align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
-                          AccAdam{}, stream, &rj, nred, &bl, rows);
+                          stream, &rj, nred, &bl, rows);
 }
 
 extern "C" int ngp_grid_encode_backward_fused_reduce_batch(
@@ -2428,69 +2153,6 @@ extern "C" int ngp_grid_encode_backward_fused_reduce_batch_live(
                              align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
                              n_nets, mlp_workspaces, mlp_Bs, in_dims, hidden_dims, num_layers, grad_weights,
                              mlp_nonfinite, job, stream, live_rows);
-}
-
-extern "C" int ngp_grid_encode_backward_fused_adam(const void* grad, const float* xyz, float bound,
-                                                   const int32_t* offsets, void* grad_embeddings, uint32_t B,
-                                                   const int32_t* count, uint32_t D, uint32_t C, uint32_t L,
-                                                   float S, uint32_t H, uint32_t gridtype, int32_t align_corners,
-                                                   uint32_t interp, const int32_t* offsets_host, void* workspace,
-                                                   size_t workspace_bytes, int32_t grad_layout, int32_t* nonfinite,
-                                                   const ngp_adam_table* at, void* state, void* stream) {
-    NGP_REQUIRE(at && state && nonfinite, NGP_ERR_ARG,
-                "grid_encode_backward_fused_adam: table, state and the nonfinite flag are required");
-    NGP_REQUIRE(grad_layout & NGP_GRID_GRAD_ZEROED, NGP_ERR_ARG,
-                "grid_encode_backward_fused_adam: the grad must be zeroed on entry (NGP_GRID_GRAD_ZEROED)");
-    NGP_REQUIRE(at->grad == grad_embeddings && C == 2 && at->channels == 2 && at->done, NGP_ERR_ARG,
-                "grid_encode_backward_fused_adam: table / grad / channels mismatch");
-    for (int k = 0; k < 2; ++k)
-        NGP_REQUIRE(at->params[k] && at->exp_avg[k] && at->exp_avg_sq[k] &&
-                        ((reinterpret_cast<uintptr_t>(at->params[k]) | reinterpret_cast<uintptr_t>(at->exp_avg[k]) |
-                          reinterpret_cast<uintptr_t>(at->exp_avg_sq[k])) & 7) == 0,
-                    NGP_ERR_ARG, "grid_encode_backward_fused_adam: buffer %d null or misaligned", k);
-    AccAdam ad{};
-    for (int k = 0; k < 2; ++k) {
-        ad.p[k] = at->params[k];
-        ad.m[k] = at->exp_avg[k];
-        ad.v[k] = at->exp_avg_sq[k];
-    }
-    ad.done = at->done;
-    ad.st = static_cast<const ngp_step::StepState*>(state);
-    ad.lr = at->lr;
-    ad.beta1 = at->beta1;
-    ad.beta2 = at->beta2;
-    ad.eps = at->eps;
-    ad.iters = at->iters;
-    return bwd_fused_impl(grad, xyz, bound, offsets, grad_embeddings, B, count, D, C, L, S, H, gridtype,
-                          align_corners, interp, offsets_host, workspace, workspace_bytes, grad_layout, nonfinite,
-                          ad, stream);
-}
-
-extern "C" int ngp_grid_table_slices(const int32_t* offsets_host, uint32_t B, uint32_t D, uint32_t C, uint32_t L,
-                                     float S, uint32_t H, int32_t align_corners, uint32_t* slices_host,
-                                     uint32_t max_slices) {
-    NGP_REQUIRE(offsets_host && slices_host && L >= 1 && L <= kMaxLevels, NGP_ERR_ARG,
-                "grid_table_slices: null offsets / output or L out of range");
-    GridLevels lv;
-    make_levels(lv, L, S, H);
-    BinPlan bp{};
-    if (C == 2 && D == 3) bp = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B);
-    uint32_t n = 0;
-    auto add = [&](uint32_t e0, uint32_t ne, uint32_t bin) {
-        if (n < max_slices) {
-            slices_host[3 * n] = e0;
-            slices_host[3 * n + 1] = ne;
-            slices_host[3 * n + 2] = bin;
-        }
-        ++n;
-    };
-    for (uint32_t l = 0; l < L; ++l) {
-        const uint32_t off0 = (uint32_t)offsets_host[l], hs = (uint32_t)offsets_host[l + 1] - off0;
-        for (uint32_t e = 0, k = 0; e < hs; e += kBinEntries, ++k)
-            add(off0 + e, std::min(kBinEntries, hs - e), l < bp.nlev ? bp.bin0[l] + k : 0xffffffffu);
-    }
-    NGP_REQUIRE(n <= max_slices, NGP_ERR_ARG, "grid_table_slices: %u slices, room for %u", n, max_slices);
-    return (int)n;
 }
 
 #ifdef NGP_STAMPS

@@ -187,10 +187,7 @@ NGP_DEV Chunk scan_chunk(const Raw& rw, uint32_t base, uint32_t num_steps, uint3
 // (and kept for the backward): the serial per-chunk round trips of a long ray
 // set the kernel's time (a ray of 256 samples took 4 dependent loads in the
 // forward and 3 more in the backward).
-#ifndef NGP_LOSS_PRE
-#define NGP_LOSS_PRE 4
-#endif
-constexpr uint32_t kLossPre = NGP_LOSS_PRE;
+constexpr uint32_t kLossPre = 4;
 
 __global__ void __launch_bounds__(kLossWaves * 64)
 k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ color_out,
@@ -465,11 +462,9 @@ k_nonfinite(TensorList tl, StepState* __restrict__ st) {
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&st->found_inf, 1);
 }
 
-// blocks [0, nsb): the double-buffered table's slices (db.on), then Adam's sweep
 __global__ void __launch_bounds__(kAdamThreads)
-k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa, DbTable db, uint32_t nsb) {
-    if (blockIdx.x < nsb) adam_slices(db, st, aa, blockIdx.x, nsb, threadIdx.x);
-    else adam_sweep(tl, st, aa, blockIdx.x - nsb, gridDim.x - nsb, threadIdx.x);
+k_adam_multi(TensorList tl, StepState* __restrict__ st, AdamArgs aa) {
+    adam_sweep(tl, st, aa, blockIdx.x, gridDim.x, threadIdx.x);
 }
 
 // ---- data-parallel GradScaler guard ----------------------------------------------
@@ -539,20 +534,16 @@ k_step_head(const float* __restrict__ poses, LegoScene sc, uint32_t N, StepState
 // the march emit launch (raymarching.hip EmitTail).
 __global__ void __launch_bounds__(kAdamThreads)
 k_adam_head(TensorList tl, StepState* __restrict__ st, AdamArgs aa, uint32_t nadam, const float* __restrict__ poses,
-            LegoScene sc, uint32_t N, LegoOut out, uint32_t nlego, uint4* __restrict__ clear, uint32_t clear16,
-            DbTable db, uint32_t nsb) {
+            LegoScene sc, uint32_t N, LegoOut out, uint32_t nlego, uint4* __restrict__ clear, uint32_t clear16) {
     // the batch and clear blocks come first: workgroups are dispatched in
     // index order, and behind Adam's thousands of blocks the sampler's
-    // dependent chain (draw -> pose -> rays -> target) ran in the launch's tail;
-    // then the double-buffered table's slices (db.on), then Adam's sweep
+    // dependent chain (draw -> pose -> rays -> target) ran in the launch's tail
     if (blockIdx.x < nlego) {
         lego_rays_block(blockIdx.x, nlego, poses, sc, N, st, out);
     } else if (blockIdx.x == nlego) {
         for (uint32_t i = threadIdx.x; i < clear16; i += blockDim.x) clear[i] = uint4{0u, 0u, 0u, 0u};
-    } else if (blockIdx.x < nlego + 1 + nsb) {
-        adam_slices(db, st, aa, blockIdx.x - nlego - 1, nsb, threadIdx.x);
     } else {
-        adam_sweep(tl, st, aa, blockIdx.x - nlego - 1 - nsb, nadam, threadIdx.x);
+        adam_sweep(tl, st, aa, blockIdx.x - nlego - 1, nadam, threadIdx.x);
     }
 }
 
@@ -571,41 +562,14 @@ uint32_t sweep_blocks(uint64_t total, uint32_t per_thread) {
     return b ? (uint32_t)b : 1u;
 }
 
-DbTable make_db(const ngp_adam_table* at) {
-    DbTable db{};
-    if (!at) return db;
-    for (int k = 0; k < 2; ++k) {
-        db.p[k] = at->params[k];
-        db.m[k] = at->exp_avg[k];
-        db.v[k] = at->exp_avg_sq[k];
-    }
-    db.g = static_cast<ngp_half*>(at->grad);
-    db.done = at->done;
-    db.slices = at->slices;
-    db.nslices = at->nslices;
-    db.C = at->channels;
-    db.on = true;
-    return db;
-}
-
 int optimizer_launch(int32_t n_tensors, float* const* params, void* const* grads, float* const* exp_avg,
                      float* const* exp_avg_sq, void* const* half_params, const uint64_t* sizes, float lr,
                      float beta1, float beta2, float eps, int32_t iters, int32_t zero_grads, float grad_mult,
                      float growth_factor, float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
                      uint32_t num_rays, const int32_t* counter, int32_t* step_counter, const float* loss_ray,
-                     void* state, void* stream, bool defer_end, const HeadLaunch* head = nullptr,
-                     const ngp_adam_table* at = nullptr) {
+                     void* state, void* stream, bool defer_end, const HeadLaunch* head = nullptr) {
     NGP_REQUIRE(n_tensors >= 1 && n_tensors <= kMaxTensors, NGP_ERR_ARG,
                 "fused_optimizer_step: 1..%d tensors", kMaxTensors);
-    if (at) {
-        NGP_REQUIRE(at->grad && at->done && at->slices && at->nslices > 0 && at->channels > 0, NGP_ERR_ARG,
-                    "fused_optimizer_step: incomplete double-buffered table");
-        for (int k = 0; k < 2; ++k)
-            NGP_REQUIRE(((reinterpret_cast<uintptr_t>(at->params[k]) | reinterpret_cast<uintptr_t>(at->exp_avg[k]) |
-                          reinterpret_cast<uintptr_t>(at->exp_avg_sq[k])) & 15) == 0 &&
-                            (reinterpret_cast<uintptr_t>(at->grad) & 7) == 0,
-                        NGP_ERR_ARG, "fused_optimizer_step: table buffer %d misaligned", k);
-    }
     for (int k = 0; k < n_tensors; ++k)
         NGP_REQUIRE(((reinterpret_cast<uintptr_t>(params[k]) | reinterpret_cast<uintptr_t>(exp_avg[k]) |
                       reinterpret_cast<uintptr_t>(exp_avg_sq[k])) & 15) == 0 &&
@@ -618,30 +582,17 @@ int optimizer_launch(int32_t n_tensors, float* const* params, void* const* grads
                     NGP_ERR_ARG, "fused_optimizer_step: half shadow %d misaligned", k);
     const TensorList tl = make_list(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes);
     const uint64_t total = tl.start[n_tensors];
-    const DbTable db = make_db(at);
-    if (scaler_enabled == NGP_SCALER_SCAN) {
-        // the sweep also checks the double-buffered table's grads (the slices
-        // the accumulate updated hold none: it flagged those itself)
-        k_nonfinite<<<sweep_blocks(total, 8), 256, 0, s>>>(tl, st);
-        if (at) {
-            void* g = at->grad;
-            const uint64_t n = at->size;
-            k_nonfinite<<<sweep_blocks(n, 8), 256, 0, s>>>(make_list(1, nullptr, &g, nullptr, nullptr, nullptr, &n),
-                                                           st);
-        }
-    }
+    if (scaler_enabled == NGP_SCALER_SCAN) k_nonfinite<<<sweep_blocks(total, 8), 256, 0, s>>>(tl, st);
     AdamArgs aa{lr, beta1, beta2, eps, iters, zero_grads, grad_mult, defer_end ? 1 : 0};
     const uint64_t nchunks = (total + kAdamChunk - 1) / kAdamChunk;
     const uint64_t adam_blocks = std::min<uint64_t>(nchunks, 16ull * ngp_num_cus());
     const uint32_t na = (uint32_t)(adam_blocks ? adam_blocks : 1);
-    const uint32_t nsb = at ? std::min<uint32_t>(at->nslices, 16u * ngp_num_cus()) : 0u;
     if (head) {
         const uint32_t nlego = ngp_div_up(head->N, 256);
-        k_adam_head<<<na + nlego + 1 + nsb, kAdamThreads, 0, s>>>(tl, st, aa, na, head->poses, head->sc, head->N,
-                                                                    head->out, nlego, head->clear, head->clear16,
-                                                                    db, nsb);
+        k_adam_head<<<na + nlego + 1, kAdamThreads, 0, s>>>(tl, st, aa, na, head->poses, head->sc, head->N,
+                                                              head->out, nlego, head->clear, head->clear16);
     } else {
-        k_adam_multi<<<na + nsb, kAdamThreads, 0, s>>>(tl, st, aa, db, nsb);
+        k_adam_multi<<<na, kAdamThreads, 0, s>>>(tl, st, aa);
     }
     if (!defer_end) {
         ScalerArgs sa{growth_factor, backoff_factor, growth_interval, scaler_enabled,
@@ -754,31 +705,6 @@ extern "C" int ngp_nerf_composite_loss_live(const float* sigma, const void* colo
     return ngp_check_launch("nerf_composite_loss_live");
 }
 
-extern "C" int ngp_nerf_composite_loss_ray_lists(const float* sigma, const void* color_out, const void* h_sigma,
-                                                 const float* deltas, const int32_t* rays, uint32_t M, uint32_t N,
-                                                 float T_thresh, float density_scale, const float* gt,
-                                                 uint32_t gt_channels, const float* bg, void* state,
-                                                 void* grad_color_out, void* grad_h_sigma, float* out_image,
-                                                 float* out_ws, float* loss_ray, int32_t* ray_rows,
-                                                 int32_t* live_cnt, void* stream) {
-    NGP_REQUIRE(loss_ray, NGP_ERR_ARG, "composite_loss_ray_lists: loss_ray [N] buffer required");
-    NGP_REQUIRE(gt_channels == 3 || gt_channels == 4, NGP_ERR_ARG,
-                "composite_loss_ray_lists: gt must be RGB or RGBA");
-    NGP_REQUIRE(ray_rows && live_cnt, NGP_ERR_ARG, "composite_loss_ray_lists: null ray_rows [M] / live_cnt [N]");
-    if (N == 0) return NGP_OK;
-    LossArgs la;
-    la.T_thresh = T_thresh;
-    la.density_scale = density_scale;
-    la.inv_n = 1.0f / (float)N;
-    la.inv_c = 1.0f / 3.0f;
-    la.gt_channels = gt_channels;
-    k_composite_loss<<<ngp_div_up(N, kLossWaves), kLossWaves * 64, 0, ngp_stream(stream)>>>(
-        sigma, (const ngp_half*)color_out, (const ngp_half*)h_sigma, deltas, rays, M, N, gt, bg, la,
-        static_cast<StepState*>(state), (ngp_half*)grad_color_out, (ngp_half*)grad_h_sigma, out_image,
-        out_ws, loss_ray, ray_rows, live_cnt);
-    return ngp_check_launch("nerf_composite_loss_ray_lists");
-}
-
 extern "C" int ngp_fused_optimizer_step(int32_t n_tensors, float* const* params, void* const* grads,
                                         float* const* exp_avg, float* const* exp_avg_sq,
                                         void* const* half_params, const uint64_t* sizes, float lr,
@@ -857,115 +783,6 @@ extern "C" int ngp_fused_optimizer_update_head(
     return optimizer_launch(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes, lr, beta1, beta2,
                             eps, iters, zero_grads, grad_mult, 2.0f, 0.5f, 2000, scaler_enabled, 0, nullptr,
                             nullptr, nullptr, state, stream, true, &hl);
-}
-
-extern "C" int ngp_fused_optimizer_step_db(int32_t n_tensors, float* const* params, void* const* grads,
-                                           float* const* exp_avg, float* const* exp_avg_sq, void* const* half_params,
-                                           const uint64_t* sizes, float lr, float beta1, float beta2, float eps,
-                                           int32_t iters, int32_t zero_grads, float grad_mult, float growth_factor,
-                                           float backoff_factor, int32_t growth_interval, int32_t scaler_enabled,
-                                           uint32_t num_rays, const int32_t* counter, int32_t* step_counter,
-                                           const float* loss_ray, void* state, const ngp_adam_table* at,
-                                           void* stream) {
-    NGP_REQUIRE(at, NGP_ERR_ARG, "fused_optimizer_step_db: null table");
-    return optimizer_launch(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes, lr, beta1, beta2,
-                            eps, iters, zero_grads, grad_mult, growth_factor, backoff_factor, growth_interval,
-                            scaler_enabled, num_rays, counter, step_counter, loss_ray, state, stream, false, nullptr,
-                            at);
-}
-
-extern "C" int ngp_fused_optimizer_update_db(int32_t n_tensors, float* const* params, void* const* grads,
-                                             float* const* exp_avg, float* const* exp_avg_sq,
-                                             void* const* half_params, const uint64_t* sizes, float lr,
-                                             float beta1, float beta2, float eps, int32_t iters, int32_t zero_grads,
-                                             float grad_mult, int32_t scaler_enabled, void* state,
-                                             const ngp_adam_table* at, void* stream) {
-    NGP_REQUIRE(at, NGP_ERR_ARG, "fused_optimizer_update_db: null table");
-    return optimizer_launch(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes, lr, beta1, beta2,
-                            eps, iters, zero_grads, grad_mult, 0.0f, 0.0f, 0, scaler_enabled, 0, nullptr, nullptr,
-                            nullptr, state, stream, true, nullptr, at);
-}
-
-extern "C" int ngp_fused_optimizer_update_head_db(
-    int32_t n_tensors, float* const* params, void* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
-    void* const* half_params, const uint64_t* sizes, float lr, float beta1, float beta2, float eps, int32_t iters,
-    int32_t zero_grads, float grad_mult, int32_t scaler_enabled, void* state, const float* poses, uint32_t n_poses,
-    const float* intrinsics4, uint32_t H, uint32_t W, uint32_t N, const float* boxes, int32_t nboxes,
-    const float* aabb6, float min_near, uint32_t seed, float* rays_o, float* rays_d, float* rgba, float* bg,
-    float* nears, float* fars, float* noises, int32_t* counter, int32_t* step_counter, void* clear,
-    uint32_t clear_bytes, const ngp_adam_table* at, void* stream) {
-    NGP_REQUIRE(state && at, NGP_ERR_ARG, "fused_optimizer_update_head_db: null state or table");
-    NGP_REQUIRE(nboxes >= 0 && nboxes <= kMaxBoxes, NGP_ERR_ARG, "step_head: at most %d boxes", kMaxBoxes);
-    NGP_REQUIRE(n_poses > 0 && H > 0 && W > 0 && N > 0, NGP_ERR_ARG, "step_head: empty pose set, image or batch");
-    NGP_REQUIRE(clear_bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(clear) & 15) == 0, NGP_ERR_ARG,
-                "step_head: clear must be 16-byte aligned, a multiple of 16 bytes");
-    HeadLaunch hl{};
-    hl.poses = poses;
-    hl.sc = make_scene(n_poses, intrinsics4, H, W, boxes, nboxes, aabb6, min_near, seed);
-    hl.N = N;
-    hl.out = LegoOut{rays_o, rays_d, rgba, bg, nears, fars, noises, counter, step_counter};
-    hl.clear = static_cast<uint4*>(clear);
-    hl.clear16 = clear ? clear_bytes / 16 : 0u;
-    return optimizer_launch(n_tensors, params, grads, exp_avg, exp_avg_sq, half_params, sizes, lr, beta1, beta2,
-                            eps, iters, zero_grads, grad_mult, 2.0f, 0.5f, 2000, scaler_enabled, 0, nullptr,
-                            nullptr, nullptr, state, stream, true, &hl, at);
-}
-
-extern "C" int32_t* ngp_fused_table_select(void* state) {
-    StepState* st = static_cast<StepState*>(state);
-    return st ? &st->cur : nullptr;
-}
-
-namespace {
-__global__ void __launch_bounds__(256)
-k_table_to_half(const float* __restrict__ a, const float* __restrict__ b, const StepState* __restrict__ st,
-                ngp_half* __restrict__ out, uint64_t n4) {
-    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-    const float4* src = reinterpret_cast<const float4*>((st->cur & 1) ? b : a);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
-        const float4 v = src[i];
-        reinterpret_cast<half4*>(out)[i] = half4{(ngp_half)v.x, (ngp_half)v.y, (ngp_half)v.z, (ngp_half)v.w};
-    }
-}
-
-// buffer 1 -> buffer 0 (params, moments) when 1 is current; then cur = 0
-__global__ void __launch_bounds__(256)
-k_table_normalize(float* __restrict__ p0, float* __restrict__ m0, float* __restrict__ v0,
-                  const float* __restrict__ p1, const float* __restrict__ m1, const float* __restrict__ v1,
-                  const StepState* __restrict__ st, uint64_t n4) {
-    if ((st->cur & 1) == 0) return;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
-        reinterpret_cast<float4*>(p0)[i] = reinterpret_cast<const float4*>(p1)[i];
-        reinterpret_cast<float4*>(m0)[i] = reinterpret_cast<const float4*>(m1)[i];
-        reinterpret_cast<float4*>(v0)[i] = reinterpret_cast<const float4*>(v1)[i];
-    }
-}
-
-__global__ void k_table_cur_reset(StepState* __restrict__ st) {
-    if (threadIdx.x == 0) st->cur = 0;
-}
-}  // namespace
-
-extern "C" int ngp_fused_table_to_half(const ngp_adam_table* at, const void* state, void* out, uint64_t n,
-                                       void* stream) {
-    NGP_REQUIRE(at && state && out && n % 4 == 0 && n <= at->size, NGP_ERR_ARG,
-                "fused_table_to_half: null pointer, n not a multiple of 4, or past the table");
-    if (n == 0) return NGP_OK;
-    k_table_to_half<<<sweep_blocks(n, 4), 256, 0, ngp_stream(stream)>>>(
-        at->params[0], at->params[1], static_cast<const StepState*>(state), static_cast<ngp_half*>(out), n / 4);
-    return ngp_check_launch("fused_table_to_half");
-}
-
-extern "C" int ngp_fused_table_normalize(const ngp_adam_table* at, void* state, uint64_t n, void* stream) {
-    NGP_REQUIRE(at && state && n % 4 == 0 && n <= at->size, NGP_ERR_ARG,
-                "fused_table_normalize: null pointer, n not a multiple of 4, or past the table");
-    hipStream_t s = ngp_stream(stream);
-    StepState* st = static_cast<StepState*>(state);
-    if (n) k_table_normalize<<<sweep_blocks(n, 4), 256, 0, s>>>(at->params[0], at->exp_avg[0], at->exp_avg_sq[0],
-                                                                at->params[1], at->exp_avg[1], at->exp_avg_sq[1],
-                                                                st, n / 4);
-    k_table_cur_reset<<<1, 64, 0, s>>>(st);
-    return ngp_check_launch("fused_table_normalize");
 }
 
 extern "C" int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, void* state,

@@ -8,12 +8,6 @@
 
 #include <cfloat>
 
-#ifndef NGP_ADAM_NT
-#define NGP_ADAM_NT 0
-#endif
-#ifndef NGP_ADAM_ALT
-#define NGP_ADAM_ALT 0
-#endif
 
 namespace ngp_head {
 
@@ -348,30 +342,20 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
         const int k = find_tensor(tl, c0);
         return find_tensor(tl, c1 - 1) == k && c1 - tl.start[k] <= tl.size[k] ? k : -1;
     };
-    // NGP_ADAM_NT (same-box A/B builds): 1 = the moments and grads streamed
-    // nontemporal (read once per step), 2 = the parameters too
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    auto ld_f4 = [](const float* q, bool nt) {
-        if (!nt) return *reinterpret_cast<const float4*>(q);
-        const f4v x = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(q));
-        return float4{x[0], x[1], x[2], x[3]};
-    };
-    auto st_f4 = [](float* q, float4 x, bool nt) {
-        if (nt) __builtin_nontemporal_store(f4v{x.x, x.y, x.z, x.w}, reinterpret_cast<f4v*>(q));
-        else *reinterpret_cast<float4*>(q) = x;
-    };
-    constexpr bool kNtMV = NGP_ADAM_NT >= 1, kNtP = NGP_ADAM_NT >= 2;
+    // (the default cache policy: streamed nontemporal, the sweep measured 25 %
+    // slower, DESIGN.md "Measured and dropped")
+    auto ld_f4 = [](const float* q) { return *reinterpret_cast<const float4*>(q); };
+    auto st_f4 = [](float* q, float4 x) { *reinterpret_cast<float4*>(q) = x; };
     auto load = [&](uint64_t c, int k, Buf& b) {  // unconditional: past the end reads the chunk's first group
         const uint64_t c0 = c * kChunk, c1 = min(c0 + kChunk, total), first = c0 - tl.start[k];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t off = first + tid * 4 + u * (kChunk / U);
             const uint64_t lo = off + tl.start[k] < c1 ? off : first;
-            b.p[u] = ld_f4(tl.p[k] + lo, kNtP);
-            b.m[u] = ld_f4(tl.m[k] + lo, kNtMV);
-            b.v[u] = ld_f4(tl.v[k] + lo, kNtMV);
-            b.g[u] = kNtMV ? __builtin_nontemporal_load(reinterpret_cast<const half4*>(tl.g[k] + lo))
-                           : *reinterpret_cast<const half4*>(tl.g[k] + lo);
+            b.p[u] = ld_f4(tl.p[k] + lo);
+            b.m[u] = ld_f4(tl.m[k] + lo);
+            b.v[u] = ld_f4(tl.v[k] + lo);
+            b.g[u] = *reinterpret_cast<const half4*>(tl.g[k] + lo);
         }
     };
     auto apply = [&](uint64_t c, int k, Buf& b) {
@@ -385,17 +369,14 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
                 ngp_step::adam_update(b.p[u].y, b.m[u].y, b.v[u].y, (float)b.g[u][1], ac, aa.beta1, aa.beta2, aa.eps);
                 ngp_step::adam_update(b.p[u].z, b.m[u].z, b.v[u].z, (float)b.g[u][2], ac, aa.beta1, aa.beta2, aa.eps);
                 ngp_step::adam_update(b.p[u].w, b.m[u].w, b.v[u].w, (float)b.g[u][3], ac, aa.beta1, aa.beta2, aa.eps);
-                st_f4(tl.p[k] + off, b.p[u], kNtP);
-                st_f4(tl.m[k] + off, b.m[u], kNtMV);
-                st_f4(tl.v[k] + off, b.v[u], kNtMV);
+                st_f4(tl.p[k] + off, b.p[u]);
+                st_f4(tl.m[k] + off, b.m[u]);
+                st_f4(tl.v[k] + off, b.v[u]);
                 if (tl.ph[k])
                     *reinterpret_cast<half4*>(tl.ph[k] + off) =
                         half4{(ngp_half)b.p[u].x, (ngp_half)b.p[u].y, (ngp_half)b.p[u].z, (ngp_half)b.p[u].w};
             }
-            if (aa.zero_grads) {
-                if (kNtMV) __builtin_nontemporal_store(half4{0, 0, 0, 0}, reinterpret_cast<half4*>(tl.g[k] + off));
-                else *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
-            }
+            if (aa.zero_grads) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
         }
     };
     auto seam = [&](uint64_t c) {  // per element (the few chunks across a tensor boundary)
@@ -415,11 +396,7 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
             if (aa.zero_grads) tl.g[kk][off] = (ngp_half)0.0f;
         }
     };
-    // NGP_ADAM_ALT (same-box A/B builds): every other update sweeps the chunks
-    // in reverse, so it starts where the last one ended (the lines most
-    // recently written, likeliest still in the memory-side cache)
-    const bool rev = NGP_ADAM_ALT && (st->iter & 1);
-    auto at = [&](uint64_t i) { return rev ? nchunks - 1 - i : i; };
+    auto at = [](uint64_t i) { return i; };
     Buf a{}, b{};
     uint64_t c = blk;
     int ka = c < nchunks ? whole(at(c)) : -1;
@@ -433,55 +410,6 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
         a = b;
         ka = kb;
         c = cn;
-    }
-}
-
-// ---- the double-buffered hash table (fused Adam, ngp_adam_table) --------------
-struct DbTable {
-    float* p[2];
-    float* m[2];
-    float* v[2];
-    ngp_half* g;
-    const uint32_t* done;
-    const uint32_t* slices;  // (first entry, entries, bin) triplets
-    uint32_t nslices, C;
-    bool on;
-};
-
-// The table slices the grid backward's accumulate did not update (their bin's
-// done tag is not this update's): Adam from the fp16 grads into the other
-// buffer, grads cleared; one block per slice (<= 4096 entries x C). On a skip
-// only the grads are cleared. The first block marks the flip for step_end.
-NGP_DEV void adam_slices(const DbTable& db, StepState* __restrict__ st, const AdamArgs& aa, uint32_t blk,
-                         uint32_t nblk, uint32_t tid) {
-    const ngp_step::AdamConsts ac = ngp_step::adam_consts(st, aa.base_lr, aa.beta1, aa.beta2, aa.iters,
-                                                          aa.grad_mult);
-    const bool skip = st->found_inf != 0 || ac.inv_bad;
-    const int src = st->cur & 1;
-    const uint32_t tag = (uint32_t)st->iter + 1u;
-    if (blk == 0 && tid == 0) st->flip_pending = 1;  // read by step_end only (a later launch or block)
-    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-    for (uint32_t s = blk; s < db.nslices; s += nblk) {
-        const uint32_t e0 = db.slices[3 * s], ne = db.slices[3 * s + 1], bin = db.slices[3 * s + 2];
-        if (bin != 0xffffffffu && db.done[bin] == tag) continue;  // updated by the accumulate
-        const size_t q0 = (size_t)e0 * db.C, nq = (size_t)ne * db.C;  // multiples of 8 (offsets are)
-        for (size_t i = (size_t)tid * 4; i < nq; i += (size_t)blockDim.x * 4) {
-            half4* gp = reinterpret_cast<half4*>(db.g + q0 + i);
-            if (!skip) {
-                float4 p = *reinterpret_cast<const float4*>(db.p[src] + q0 + i);
-                float4 m = *reinterpret_cast<const float4*>(db.m[src] + q0 + i);
-                float4 v = *reinterpret_cast<const float4*>(db.v[src] + q0 + i);
-                const half4 g = *gp;
-                ngp_step::adam_update(p.x, m.x, v.x, (float)g[0], ac, aa.beta1, aa.beta2, aa.eps);
-                ngp_step::adam_update(p.y, m.y, v.y, (float)g[1], ac, aa.beta1, aa.beta2, aa.eps);
-                ngp_step::adam_update(p.z, m.z, v.z, (float)g[2], ac, aa.beta1, aa.beta2, aa.eps);
-                ngp_step::adam_update(p.w, m.w, v.w, (float)g[3], ac, aa.beta1, aa.beta2, aa.eps);
-                *reinterpret_cast<float4*>(db.p[src ^ 1] + q0 + i) = p;
-                *reinterpret_cast<float4*>(db.m[src ^ 1] + q0 + i) = m;
-                *reinterpret_cast<float4*>(db.v[src ^ 1] + q0 + i) = v;
-            }
-            *gp = half4{0, 0, 0, 0};
-        }
     }
 }
 

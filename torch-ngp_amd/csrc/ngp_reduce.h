@@ -6,14 +6,6 @@
 #pragma once
 #include "ngp_common.h"
 
-#ifndef NGP_NT_SLAB  // same-box A/B builds only: nontemporal slab stores / loads
-#define NGP_NT_SLAB 0
-#endif
-#if NGP_NT_SLAB
-#define NGP_SLAB_LOAD(p) __builtin_nontemporal_load(p)
-#else
-#define NGP_SLAB_LOAD(p) (*(p))
-#endif
 
 namespace ngp_reduce {
 
@@ -62,12 +54,12 @@ NGP_DEV void slab_reduce_block(const ReduceJobs& jobs, uint32_t blk, float (*par
         if (p < n) {
             uint32_t r = ph;
             for (; r + 3 * kReducePhases < rows; r += 4 * kReducePhases) {
-                s0 += NGP_SLAB_LOAD(slab + (size_t)r * n + p);
-                s1 += NGP_SLAB_LOAD(slab + (size_t)(r + kReducePhases) * n + p);
-                s2 += NGP_SLAB_LOAD(slab + (size_t)(r + 2 * kReducePhases) * n + p);
-                s3 += NGP_SLAB_LOAD(slab + (size_t)(r + 3 * kReducePhases) * n + p);
+                s0 += *(slab + (size_t)r * n + p);
+                s1 += *(slab + (size_t)(r + kReducePhases) * n + p);
+                s2 += *(slab + (size_t)(r + 2 * kReducePhases) * n + p);
+                s3 += *(slab + (size_t)(r + 3 * kReducePhases) * n + p);
             }
-            for (; r < rows; r += kReducePhases) s0 += NGP_SLAB_LOAD(slab + (size_t)r * n + p);
+            for (; r < rows; r += kReducePhases) s0 += *(slab + (size_t)r * n + p);
         }
         part[ph][lane] = (s0 + s1) + (s2 + s3);
     }

@@ -21,15 +21,12 @@ struct StepState {
     int32_t lego_done;     // k_lego_rays' finished-block count (last block bumps draw)
     int32_t local_inf;     // data parallel: this rank's own grads held an inf/nan (k_guard_*)
     int32_t end_pending;   // an optimizer update whose GradScaler/LR bookkeeping is deferred to k_step_head
-    int32_t cur;           // double-buffered table (fused Adam): which of the two p/m/v buffers is current
-    int32_t flip_pending;  // the pending update wrote the other buffer: step_end makes it current unless skipped
-    int32_t pad3;
+    int32_t reserved[3];
 };
 
 
 // ---- Adam (torch.optim.Adam, weight_decay 0) on an unscaled fp16 grad -------
-// Shared by the optimizer sweeps (ngp_head.h) and the grid backward's fused
-// Adam (gridencoder.hip), so both compute bit-identical updates.
+// Shared by the optimizer sweeps (ngp_head.h).
 struct AdamConsts {
     float inv_scale;     // 1 / GradScaler scale (x grad_mult)
     float step_size;     // lr_t / bias_correction1
@@ -96,10 +93,6 @@ NGP_DEV void step_end_block(StepState* __restrict__ st, const ScalerArgs& sa, co
         }
     }
     if (!inf) st->adam_step += 1;
-    // fused Adam (double-buffered table): the update went to the other buffer,
-    // which becomes current; a skipped step keeps the current one untouched
-    if (st->flip_pending && !inf) st->cur ^= 1;
-    st->flip_pending = 0;
     st->epoch += 1;
     if (step_counter) {
         const int slot = st->iter % 16;

@@ -323,10 +323,7 @@ constexpr size_t kMarchLdsBytes = 156 * 1024;
 // workgroups per ray group in k_march_emit: 8 left half the SIMDs idle on a
 // 4096-ray batch (16 groups); 32 (same box, profiles/r04w_emit_split_ab.txt):
 // the march + emit tick 33.6 -> 30.8 us
-#ifndef NGP_EMIT_SPLIT  // same-box A/B builds
-#define NGP_EMIT_SPLIT 32
-#endif
-constexpr uint32_t kEmitSplit = NGP_EMIT_SPLIT;
+constexpr uint32_t kEmitSplit = 32;
 constexpr uint32_t kInf = 0xffffffffu;
 
 struct OccLayout {
@@ -708,17 +705,9 @@ struct MarchAdam {
     ngp_step::StepState* st;  // null: no Adam in this launch
     uint4* clear;             // also zeroed (the grid backward's bin cursors), or null
     uint32_t clear16;
+    bool emit_launch;         // the samples emitted by a launch of their own (NGP_ADAM_JOB_EMIT_LAUNCH)
 };
-#ifndef NGP_MARCH_ADAM_WAVES  // march waves of a march + Adam workgroup (same-box A/B builds)
-#define NGP_MARCH_ADAM_WAVES 4
-#endif
-constexpr uint32_t kMarchAdamWaves = NGP_MARCH_ADAM_WAVES;
-#ifndef NGP_MARCH_ADAM_PIPE  // the Adam waves' sweep: software-pipelined (1) or plain (0)
-#define NGP_MARCH_ADAM_PIPE 1
-#endif
-#ifndef NGP_MARCH_ADAM_U     // 16-byte groups per stream, thread and chunk
-#define NGP_MARCH_ADAM_U 2
-#endif
+constexpr uint32_t kMarchAdamWaves = 4;
 
 // The emit inside the march + Adam launch (world 1; ngp_march_rays_train_prebuilt_adam):
 // the march waves finish long before the Adam waves, so they also emit the
@@ -773,13 +762,8 @@ k_march_train(const float* __restrict__ rays_o, const float* __restrict__ rays_d
         constexpr uint32_t kVirt = (kSegWaves - MW) / 4;  // 256-thread virtual blocks per workgroup
         if (blockIdx.x == 0 && wave == MW)
             for (uint32_t i = threadIdx.x & 63u; i < ma.clear16; i += 64) ma.clear[i] = uint4{0u, 0u, 0u, 0u};
-#if NGP_MARCH_ADAM_PIPE
-        ngp_head::adam_sweep_pipe<NGP_MARCH_ADAM_U>(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4,
+        ngp_head::adam_sweep_pipe<2>(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4,
                                                     gridDim.x * kVirt, threadIdx.x & 255u);
-#else
-        ngp_head::adam_sweep<NGP_MARCH_ADAM_U>(ma.tl, ma.st, ma.aa, blockIdx.x * kVirt + (wave - MW) / 4,
-                                               gridDim.x * kVirt, threadIdx.x & 255u);
-#endif
         return;
     }
     const OccLds occ_lds{sum, pre, reinterpret_cast<const uint8_t*>(pre + L.ngroups)};
@@ -899,7 +883,7 @@ static_assert((kSegWaves - kMarchAdamWaves) % 4 == 0, "Adam waves form 256-threa
 // instead of in a latency-bound launch of their own.
 struct EmitTail {
     ngp_step::StepState* st;  // null: no tail row
-    bool end;                 // run the bookkeeping (false: a later launch does, NGP_ADAM_JOB_END_LATER)
+    bool end;                 // run the bookkeeping
     ngp_step::ScalerArgs sa;
     const float* loss_ray;
     uint32_t n_rays, groups;  // groups: emit ray groups (gridDim.x may be wider)
@@ -1438,12 +1422,9 @@ extern "C" size_t ngp_march_rays_train_error_offset(uint32_t N, uint32_t max_ste
            (occ_image_bytes(L) + occ_scratch_bytes(L) + 255) / 256 * 256 + 4;
 }
 
-// The march + Adam launch emits the samples itself (MarchEmit) unless
-// NGP_MARCH_EMIT_INLINE=0 or a ray block would exceed kEmitMaxBlockRays.
-static bool march_emit_inline() {
-    const char* e = getenv("NGP_MARCH_EMIT_INLINE");
-    return !(e && e[0] == '0');
-}
+// The march + Adam launch emits the samples itself (MarchEmit) unless the job
+// asks for the emit launch (NGP_ADAM_JOB_EMIT_LAUNCH) or a ray block would
+// exceed kEmitMaxBlockRays.
 
 static int march_train_impl(const float* rays_o, const float* rays_d, const uint8_t* grid,
                              float bound, float dt_gamma, uint32_t max_steps, uint32_t N, uint32_t C,
@@ -1478,7 +1459,7 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
     MarchEmit me{};
     if (ma && ma->st) {  // every CU gets a workgroup: the Adam waves sweep 1/gridDim of the parameters each
         const uint32_t rb = ngp_div_up(N, kMaxMarchBlocks);
-        if (rb <= kEmitMaxBlockRays && march_emit_inline()) {
+        if (rb <= kEmitMaxBlockRays && !ma->emit_launch) {
             uint8_t* sync = img + (occ_image_bytes(L) + occ_scratch_bytes(L) + 255) / 256 * 256;
             me = MarchEmit{reinterpret_cast<uint32_t*>(sync), reinterpret_cast<uint32_t*>(sync) + 1,
                            reinterpret_cast<unsigned long long*>(sync + 256), counter, xyzs, dirs, deltas, M, rb};
@@ -1594,7 +1575,7 @@ extern "C" int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const flo
     }
     EmitTail tail{};
     tail.st = static_cast<ngp_step::StepState*>(state);
-    tail.end = (job->flags & NGP_ADAM_JOB_END_LATER) == 0;
+    tail.end = true;
     tail.sa = ngp_step::ScalerArgs{growth_factor, backoff_factor, growth_interval, scaler_enabled,
                                    N ? 1.0f / (float)N : 0.0f};
     tail.loss_ray = loss_ray;
@@ -1613,6 +1594,7 @@ extern "C" int ngp_march_rays_train_prebuilt_adam(const float* rays_o, const flo
                 "march_rays_train_prebuilt_adam: clear must be 16-byte aligned, a multiple of 16 bytes");
     ma.clear = static_cast<uint4*>(job->clear);
     ma.clear16 = job->clear ? job->clear_bytes / 16 : 0u;
+    ma.emit_launch = (job->flags & NGP_ADAM_JOB_EMIT_LAUNCH) != 0;
     // NGP_ADAM_JOB_TAIL_LATER: the bookkeeping and the packs ride in the next
     // launch (ngp_grid_encode_forward_fused_tail)
     const bool later = (job->flags & NGP_ADAM_JOB_TAIL_LATER) != 0;

@@ -23,7 +23,7 @@ sample -> march -> network], so one graph holds a whole step. Data parallel
 fp16 forward copy, overlapped with [sample -> march] -> [network] -> guard +
 averaging reduce-scatter of the gradient, captured as one graph over RCCL
 (the all-gather on RCCL's stream beside sample + march); with gloo or
-NGP_DP_GRAPH=0 the collectives sit between three graphs. The arithmetic is the reference's, in the
+options dp_graph=False the collectives sit between three graphs. The arithmetic is the reference's, in the
 reference's order; only the last step's update stays pending until
 `flush()` (the read-outs below flush first). Running that optimizer on a side
 stream beside sample + march was measured and lost: Adam and the marcher's
@@ -31,7 +31,6 @@ scan/emit are both memory-bound and slowed each other more than they
 overlapped (profiles/r01u_overlap_trace.txt).
 """
 import ctypes
-import os
 import sys
 
 import numpy as np
@@ -56,29 +55,48 @@ def _vp_array(ptrs):
     return (ctypes.c_void_p * len(ptrs))(*ptrs)
 
 
+# The step's structure. Every option defaults to the measured-fastest form
+# (DESIGN.md section 1); the alternatives remain because a configuration needs
+# them (the data-parallel step, shapes the one-launch kernels do not cover) or
+# as the reference forms the equivalence tests compare against, selected per
+# trainer with `options=`:
+#   table16       world 1: keep an fp16 copy of the table for the grid forward
+#                 (default: the forward reads the fp32 table, rounding on load)
+#   split_head    world 1: the step head (Adam + batch) as its own launch
+#   split_reduce  the MLP dW slab reduce in its own launch
+#   split_fwd     the sigma and colour MLP forwards as two launches
+#   split_bwd     the two MLP backwards as two launches
+#   march_adam    world 1: the pending Adam rides in the march launch
+#   tail_in_fwd   the bookkeeping + MLP packs ride in the grid forward's launch
+#   emit_inline   the march launch emits its samples itself (no emit launch)
+#   draw_ahead    the next batch is drawn in the grid backward's bin launch
+#   live_rows     the backwards walk the rows with a nonzero gradient only
+#   dp_graph      data parallel over RCCL: the whole step is one graph
+#   density_sort  partial density updates query their cells in brick order
+DEFAULT_OPTIONS = dict(table16=False, split_head=False, split_reduce=False, split_fwd=False, split_bwd=False,
+                       march_adam=True, tail_in_fwd=True, emit_inline=True, draw_ahead=True, live_rows=True,
+                       dp_graph=True, density_sort=True)
+
+
 class FusedTrainer:
     def __init__(self, model, dataset, M, lr=1e-2, iters=30000, max_steps=1024, T_thresh=1e-4,
                  dt_gamma=0.0, seed=0, betas=(0.9, 0.99), eps=1e-15, init_scale=65536.0,
-                 growth_interval=2000, distributed=False, fused_adam=None, grid_timing=None):
+                 growth_interval=2000, distributed=False, grid_timing=False, options=None):
         """distributed: ray-sharded data parallelism over the initialised
         torch.distributed group: each rank draws its own rays; the flat fp16
         gradient is averaged with one RCCL reduce-scatter, each rank's Adam
         updates its 1/world shard and the fp16 forward copy is all-gathered
         (ZeRO-1; see `_reduce`).
-        fused_adam (world 1; default off, NGP_FUSED_ADAM=1 turns it on): the
-        grid backward's accumulate applies Adam to the table slices it owns,
-        into a second buffer of the table's p / m / v (ngp_adam_table), and
-        the table grads of those slices are never written; the step's
-        optimizer launch updates the rest. Bit-identical parameters either way
-        (tests/test_gpu_fused.py); off, every table grad is materialised in
-        `grads[0]`, which the parity tests inspect. Measured slower on the
-        Lego step (DESIGN.md "Measured and dropped": the accumulate becomes
-        bandwidth-bound on the moved Adam stream, 14.5 -> 62 us, while the
-        head's Adam fell 50.6 -> 17 us).
         grid_timing: the binned grid backward times itself on the chip's
         constant clock (`grid_timing()`, the bench's roofline clock); off by
-        default (NGP_GRID_TIMING=1 turns it on), since it adds ring stores to
-        the backward's launches."""
+        default, since it adds ring stores to the backward's launches.
+        options: DEFAULT_OPTIONS overrides (the step's structure)."""
+        opts = dict(DEFAULT_OPTIONS)
+        for k, v in (options or {}).items():
+            if k not in opts:
+                raise ValueError(f"FusedTrainer: unknown option {k!r} (known: {sorted(opts)})")
+            opts[k] = bool(v)
+        self.options = opts
         assert model.cuda_ray, "the fused step marches the density bitfield (cuda_ray=True)"
         enc = model.encoder
         assert enc.level_dim == 2 and enc.num_levels * enc.level_dim == 32 and enc.input_dim == 3
@@ -172,8 +190,6 @@ class FusedTrainer:
         self._grid_timing_at = int(nat.lib().ngp_grid_encode_backward_fused_timing_offset(
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
             int(enc.align_corners), self._offsets_host))
-        if grid_timing is None:
-            grid_timing = os.environ.get("NGP_GRID_TIMING", "0") == "1"
         if not grid_timing:
             self._grid_timing_at = 0
         if self._grid_timing_at:
@@ -210,18 +226,18 @@ class FusedTrainer:
         # half as it loads it (the same values autocast's cast gives), so Adam
         # does not write an fp16 copy of the table (2 of its 28 B / parameter).
         # Data parallel: the fp16 copy is what the all-gather moves.
-        self.table32 = not self.dp and os.environ.get("NGP_FUSED_TABLE16") != "1"
-        self._merge_head = not self.dp and os.environ.get("NGP_FUSED_SPLIT_HEAD") != "1"
-        # the MLP dW reduce in the grid backward's bin launch (NGP_FUSED_SPLIT_REDUCE=1: its own launch)
-        self._split_reduce = os.environ.get("NGP_FUSED_SPLIT_REDUCE") == "1"
+        self.table32 = not self.dp and not opts["table16"]
+        self._merge_head = not self.dp and not opts["split_head"]
+        # the MLP dW reduce in the grid backward's bin launch (split_reduce: its own launch)
+        self._split_reduce = opts["split_reduce"]
         # one launch for the sigma + colour forwards where ngp_nerf_forward covers
-        # the shapes (NGP_FUSED_SPLIT_FWD=1 keeps two launches, for A/B and tests)
+        # the shapes (split_fwd keeps two launches)
         sn_, cn_ = self.sig_net, self.col_net
-        self._one_fwd = (os.environ.get("NGP_FUSED_SPLIT_FWD") != "1" and sn_.hidden_dim == 64
+        self._one_fwd = (not opts["split_fwd"] and sn_.hidden_dim == 64
                          and cn_.hidden_dim == 64 and sn_.input_dim == 32 and cn_.input_dim == 32
                          and 2 <= sn_.num_layers <= 3 and 2 <= cn_.num_layers <= 4)
-        # ... and for both backwards (ngp_nerf_backward; NGP_FUSED_SPLIT_BWD=1: two launches)
-        self._one_bwd = (os.environ.get("NGP_FUSED_SPLIT_BWD") != "1" and sn_.hidden_dim == 64
+        # ... and for both backwards (ngp_nerf_backward; split_bwd: two launches)
+        self._one_bwd = (not opts["split_bwd"] and sn_.hidden_dim == 64
                          and cn_.hidden_dim == 64 and sn_.input_dim == 32 and cn_.input_dim == 32
                          and 2 <= sn_.num_layers <= 3 and 2 <= cn_.num_layers <= 3)
         sec = plan.sections(self.table32)  # the table, then the two MLPs
@@ -234,11 +250,6 @@ class FusedTrainer:
             sizes=(ctypes.c_uint64 * len(sec))(*[n for _, n, _ in sec]),
             n=len(sec))
         self._nccl = self.dp and dist.get_backend() == "nccl"
-        if fused_adam is None:
-            fused_adam = os.environ.get("NGP_FUSED_ADAM", "0") == "1"
-        self.fused_adam = bool(fused_adam) and not self.dp and self.table32
-        if self.fused_adam:
-            self._setup_fused_adam(sec)
         # GradScaler's inf check is made by the kernels that write the grads
         # (grid backward, MLP dW reduce) into this flag: the optimizer's found-inf
         # flag (world 1) or the data-parallel guard's per-rank flag
@@ -246,9 +257,8 @@ class FusedTrainer:
         # World 1: the pending Adam rides in the march launch (its workgroups'
         # Adam waves stream the parameters while the march waves probe the
         # occupancy image); the step head then only draws the batch.
-        # NGP_MARCH_ADAM=0: Adam in the head launch, before the march.
-        self._march_adam = (self._merge_head and not self.fused_adam
-                            and os.environ.get("NGP_MARCH_ADAM", "1") != "0")
+        # march_adam=False: Adam in the head launch, before the march.
+        self._march_adam = self._merge_head and opts["march_adam"]
         if self._march_adam:
             o, job = self._opt, nat.AdamJob()
             job.n_tensors = o["n"]
@@ -258,52 +268,26 @@ class FusedTrainer:
             job.lr, job.beta1, job.beta2, job.eps = self.lr, self.betas[0], self.betas[1], self.eps
             job.iters, job.zero_grads, job.grad_mult = self.iters, 1, 1.0
             self._job = job
-        # ... and (NGP_ADAM_UNDER_FWD=1) the table levels past NGP_ADAM_SPLIT_LEVEL
-        # are swept instead by Adam blocks of the grid forward's first launch
-        # (levels [0, 8)), and the forward of levels [8, L) plus the deferred
-        # bookkeeping run in a second launch: the march launch's sweep is
-        # shorter and the rest of Adam streams beside the gather-bound forward
-        # (DESIGN.md "Adam under the grid forward"). Same arithmetic per value.
-        self._fwd_split = None
-        L = enc.num_levels
-        split = int(os.environ.get("NGP_ADAM_SPLIT_LEVEL", "10"))
-        if (self._march_adam and os.environ.get("NGP_ADAM_UNDER_FWD", "0") == "1" and L == 16
-                and 8 <= split < L and self.table32):
-            x = int(enc.offsets[split].item()) * enc.level_dim  # first table value of level `split`
-            nt = self._starts[1]
-            job, o = self._job, self._opt
-            # the march launch's job: table values [0, x) and the MLP section; its
-            # emit launch leaves the bookkeeping to the forward's second launch
-            job.sizes[0] = x
-            job.flags = nat.ADAM_JOB_END_LATER
-            j2 = nat.AdamJob()
-            j2.n_tensors = 1
-            j2.params[0], j2.grads[0] = o["params"][0] + 4 * x, o["grads"][0] + 2 * x
-            j2.exp_avg[0], j2.exp_avg_sq[0], j2.half_params[0] = o["m"][0] + 4 * x, o["v"][0] + 4 * x, None
-            j2.sizes[0] = nt - x
-            j2.lr, j2.beta1, j2.beta2, j2.eps = self.lr, self.betas[0], self.betas[1], self.eps
-            j2.iters, j2.zero_grads, j2.grad_mult = self.iters, 1, 1.0
-            self._fwd_split = (8, j2)
         # ... and (with the Adam sweep whole in the march launch) the march
         # launch emits its samples itself and leaves the bookkeeping + MLP packs
-        # row to the grid forward's launch: no emit launch (NGP_TAIL_IN_FWD=0:
-        # the tail row in the emit launch; NGP_MARCH_EMIT_INLINE=0: the emit launch)
-        self._tail_in_fwd = (self._march_adam and self._fwd_split is None
-                             and os.environ.get("NGP_TAIL_IN_FWD", "1") != "0")
+        # row to the grid forward's launch: no emit launch (tail_in_fwd=False:
+        # the tail row in the emit launch; emit_inline=False: the emit launch)
+        self._tail_in_fwd = self._march_adam and opts["tail_in_fwd"]
         if self._tail_in_fwd:
             self._job.flags |= nat.ADAM_JOB_TAIL_LATER
+        if self._march_adam and not opts["emit_inline"]:
+            self._job.flags |= nat.ADAM_JOB_EMIT_LAUNCH
         # ... and the next batch is drawn while this step's grid backward runs
         # (a column of the bin launch; the batch buffers are dead once the
         # composite has read its targets), so the step starts with the march:
         # no head launch. The march + Adam launch clears the bin cursors.
-        # NGP_DRAW_AHEAD=0: the head launch draws the batch.
+        # draw_ahead=False: the head launch draws the batch.
         # Data parallel too (round 5): the bin launch draws the next batch, the
         # step clears the bin cursors itself, and the deferred bookkeeping and the
         # MLP packs ride in the grid forward's launch (_dp_tail): no head launch
         # and no pack launch per step.
-        self._draw_ahead = ((self._march_adam or self.dp) and not self._split_reduce
-                            and os.environ.get("NGP_DRAW_AHEAD", "1") != "0")
-        self._dp_tail = self.dp and os.environ.get("NGP_TAIL_IN_FWD", "1") != "0"
+        self._draw_ahead = (self._march_adam or self.dp) and not self._split_reduce and opts["draw_ahead"]
+        self._dp_tail = self.dp and opts["tail_in_fwd"]
         self._ahead = False  # the batch buffers hold the next step's batch
         self._pre_ahead = None  # data parallel: the batch state the "pre" graph was captured in
         if self._draw_ahead and self._march_adam:
@@ -319,19 +303,13 @@ class FusedTrainer:
             bj.nears, bj.fars, bj.noises = nat.ptr(self.nears), nat.ptr(self.fars), nat.ptr(self.noises)
             bj.counter, bj.step_counter = nat.ptr(self.counter), nat.ptr(m_.step_counter)
             self._batch_job = bj
-        # the backwards over the live rows only (NGP_LIVE_ROWS, default on): rows whose
+        # the backwards over the live rows only (live_rows, default on): rows whose
         # gradient the composite left zero in every component (behind a ray's
         # early termination, or underflowed to zero in fp16) are skipped by the
         # MLP and grid backwards, as instant-ngp compacts its samples before
         # the backward; needs the one-launch MLP backward and the draw-ahead
         # bin launch (where the list is consumed)
-        self._live = (os.environ.get("NGP_LIVE_ROWS", "1") != "0" and self._one_bwd and self._draw_ahead
-                      and not self.fused_adam and not self._split_reduce)
-        # the list joined inside the MLP backward's launch (NGP_LIVE_LIST=1;
-        # default: its own k_live_compact launch after the composite, which
-        # measured faster: profiles/r05p_live_rows_ab.txt, r05y)
-        self._live_list = (self._live and os.environ.get("NGP_LIVE_LIST", "0") == "1" and N <= 4096
-                           and os.environ.get("NGP_MLP_BWD_PAIR") != "1")
+        self._live = opts["live_rows"] and self._one_bwd and self._draw_ahead and not self._split_reduce
         if self._live:
             i32 = torch.int32
             self._live_bufs = dict(ray_rows=z(M, dtype=i32), cnt=z(N, dtype=i32), rows=z(M, dtype=i32),
@@ -339,69 +317,17 @@ class FusedTrainer:
         self.graph = None
         self.graph_multi, self._multi = None, 1  # capture(multi=S): S step bodies in one graph
         # data parallel over RCCL: the whole step is captured, collectives included
-        # (NGP_DP_GRAPH=0: three graphs with the collectives between them)
-        self._dp_graph = self.dp and os.environ.get("NGP_DP_GRAPH", "1") != "0"
+        # (dp_graph=False: three graphs with the collectives between them)
+        self._dp_graph = self.dp and opts["dp_graph"]
         self._dp_whole = None
         self._fresh = None  # world 1: graph of the first step after a flush (capture)
         self.eager_steps = 0  # world 1: steps run as eager launches (not graph replays)
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
-        # partial updates query their random cells in brick order (NGP_DENSITY_SORT=0: draw order)
-        self._dens_sorted = os.environ.get("NGP_DENSITY_SORT", "1") != "0"
+        # partial updates query their random cells in brick order (density_sort=False: draw order)
+        self._dens_sorted = opts["density_sort"]
         self._pending = False  # gradients of the last forward/backward not yet applied
-
-    def _setup_fused_adam(self, sec):
-        """The double-buffered table (ngp_adam_table): buffer 0 is the table
-        part of flat_param / exp_avg / exp_avg_sq (what the model's Parameter
-        and the checkpoints see after flush()), buffer 1 a second copy; the
-        optimizer's own tensor list keeps only the MLPs."""
-        nt = self._starts[1]  # table values, 8-aligned
-        n_tab = self.params[0].numel()
-        dev = self.dev
-        self._nt = nt
-        self.table_b = torch.zeros(nt, device=dev)
-        self.exp_avg_b, self.exp_avg_sq_b = torch.zeros(nt, device=dev), torch.zeros(nt, device=dev)
-        e = self.enc
-        cap = int(self.params[0].shape[0]) // 4096 + 2 * e.num_levels + 8
-        host = (ctypes.c_uint32 * (3 * cap))()
-        n = nat.lib().ngp_grid_table_slices(self._offsets_host, self.M, e.input_dim, e.level_dim, e.num_levels,
-                                            self.S, e.base_resolution, int(e.align_corners), host, cap)
-        if n < 0:
-            nat.check(n, "grid_table_slices")
-        sl = np.frombuffer(host, dtype=np.uint32)[:3 * n].reshape(n, 3).copy()
-        assert int(sl[-1, 0] + sl[-1, 1]) * e.level_dim == n_tab and int(sl[0, 0]) == 0
-        self.slices = torch.from_numpy(sl.view(np.int32)).to(dev)
-        bins = sl[:, 2][sl[:, 2] != 0xFFFFFFFF]
-        self.bin_done = torch.zeros(int(bins.max()) + 1 if bins.size else 1, dtype=torch.int32, device=dev)
-        at = nat.AdamTable()
-        at.params[0], at.params[1] = nat.ptr(self.flat_param), nat.ptr(self.table_b)
-        at.exp_avg[0], at.exp_avg[1] = nat.ptr(self.exp_avg), nat.ptr(self.exp_avg_b)
-        at.exp_avg_sq[0], at.exp_avg_sq[1] = nat.ptr(self.exp_avg_sq), nat.ptr(self.exp_avg_sq_b)
-        at.grad, at.size = nat.ptr(self.flat_grad), n_tab
-        at.done, at.slices, at.nslices, at.channels = nat.ptr(self.bin_done), nat.ptr(self.slices), n, e.level_dim
-        at.lr, at.beta1, at.beta2, at.eps, at.iters = self.lr, self.betas[0], self.betas[1], self.eps, self.iters
-        self._at = at
-        # the optimizer launches update the MLP section; the table goes through `at`
-        mlp = [t for t in sec if t[0] != 0]
-        self._opt = dict(
-            params=_vp_array([nat.ptr(self.flat_param) + 4 * a for a, _, _ in mlp]),
-            grads=_vp_array([nat.ptr(self.grad_shard) + 2 * a for a, _, _ in mlp]),
-            m=_vp_array([nat.ptr(self.exp_avg) + 4 * a for a, _, _ in mlp]),
-            v=_vp_array([nat.ptr(self.exp_avg_sq) + 4 * a for a, _, _ in mlp]),
-            half=_vp_array([nat.ptr(self.flat_half) + 2 * a for a, _, _ in mlp]),
-            sizes=(ctypes.c_uint64 * len(mlp))(*[k for _, k, _ in mlp]),
-            n=len(mlp))
-        self._table_sel = nat.lib().ngp_fused_table_select(nat.ptr(self.state))
-
-    def _normalize_table(self):
-        """Make buffer 0 of the double-buffered table current (device side: a
-        copy when buffer 1 is, then cur = 0), so the Parameter views, the
-        moments and every host read-out see the current table."""
-        if self.fused_adam:
-            nat.check(nat.lib().ngp_fused_table_normalize(ctypes.byref(self._at), nat.ptr(self.state),
-                                                          self.params[0].numel(), nat.stream_of(self.state)),
-                      "fused_table_normalize")
 
     def sync_half(self):
         """Refresh the fp16 forward copies after the fp32 parameters were
@@ -661,7 +587,7 @@ class FusedTrainer:
         if not self._pending:
             self.step()
         per, counts = {}, []
-        self.body_live_counts = []  # the live rows of those steps (NGP_LIVE_ROWS)
+        self.body_live_counts = []  # the live rows of those steps (live_rows)
         for _ in range(k):
             torch.cuda.synchronize()
             torch.cuda._sleep(4_000_000)
@@ -683,8 +609,8 @@ class FusedTrainer:
         sample -> march -> network forward/backward. With an update pending,
         Adam and the batch draw share one launch and the deferred scaler
         bookkeeping + MLP packs ride in the march's emit launch (12 launches
-        instead of 13; NGP_FUSED_SPLIT_HEAD=1 keeps them apart). By default
-        (NGP_MARCH_ADAM) Adam runs inside the march launch instead, beside the
+        instead of 13; options split_head keeps them apart). By default
+        (march_adam) Adam runs inside the march launch instead, beside the
         march waves, and the head launch only draws the batch."""
         if pending and self._march_adam:
             if not self._ahead:
@@ -716,11 +642,7 @@ class FusedTrainer:
                 float(m.min_near), self.seed, P(self.rays_o), P(self.rays_d), P(self.rgba), P(self.bg),
                 P(self.nears), P(self.fars), P(self.noises), P(self.counter), P(m.step_counter),
                 P(self.grid_ws) if self._grid_counter_bytes else None, self._grid_counter_bytes)
-        if self.fused_adam:
-            nat.check(lib.ngp_fused_optimizer_update_head_db(*args, ctypes.byref(self._at), s),
-                      "fused_optimizer_update_head_db")
-        else:
-            nat.check(lib.ngp_fused_optimizer_update_head(*args, s), "fused_optimizer_update_head")
+        nat.check(lib.ngp_fused_optimizer_update_head(*args, s), "fused_optimizer_update_head")
         self._tick("optimizer")
 
     # ---- data parallel (world > 1): ZeRO-1 --------------------------------
@@ -839,20 +761,7 @@ class FusedTrainer:
         grid_args = (e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id,
                      int(e.align_corners), e.interp_id, s)
         table, tdt = (self.params[0], _F32) if self.table32 else (self.w_half[0], _F16)
-        if adam_split and self._fwd_split is not None:
-            # levels [0, f) beside the rest of the previous step's Adam, then
-            # levels [f, L) with the update's deferred bookkeeping
-            f, j2 = self._fwd_split
-            fa = (P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets), P(self.enc_out), M, cnt,
-                  *grid_args[:-1])
-            chk(lib.ngp_grid_encode_forward_fused_adam(*fa, 0, f, ctypes.byref(j2), P(self.state), None, 2.0, 0.5,
-                                                       self.growth_interval, 1, P(self.loss_ray), N, s),
-                "grid_encode_forward_fused_adam")
-            self._tick("grid_encode_forward+adam")
-            chk(lib.ngp_grid_encode_forward_fused_adam(*fa, f, e.num_levels, None, None, P(self.state), 2.0, 0.5,
-                                                       self.growth_interval, 1, P(self.loss_ray), N, s),
-                "grid_encode_forward_fused_end")
-        elif self.dp and self._dp_tail:
+        if self.dp and self._dp_tail:
             # + the deferred bookkeeping of the shard update (when the head did
             # not run it: batch drawn ahead) and the MLP packs of the gathered weights
             chk(lib.ngp_grid_encode_forward_fused_tail(P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets),
@@ -868,10 +777,6 @@ class FusedTrainer:
                                                        0.5, self.growth_interval, 1, P(self.loss_ray), N, 2, pk["w"],
                                                        pk["ins"], pk["hid"], pk["nl"], pk["img"], s),
                 "grid_encode_forward_fused_tail")
-        elif self.fused_adam:  # the current one of the double-buffered table
-            chk(lib.ngp_grid_encode_forward_fused_sel(P(self.xyzs), float(m.bound), P(table), P(self.table_b),
-                                                      self._table_sel, tdt, P(e.offsets), P(self.enc_out), M, cnt,
-                                                      *grid_args[:-1], 0, s), "grid_encode_fused_sel")
         else:
             chk(lib.ngp_grid_encode_forward_fused(P(self.xyzs), float(m.bound), P(table), tdt, P(e.offsets),
                                                   P(self.enc_out), M, cnt, *grid_args[:-1], 0, s),
@@ -898,15 +803,7 @@ class FusedTrainer:
         # the live rows (a nonzero gradient) listed by the composite: both
         # backwards then run over them only (the other rows' products are zeros)
         live = self._live and draw
-        if live and self._live_list:
-            lv = self._live_bufs
-            chk(lib.ngp_nerf_composite_loss_ray_lists(P(self.sigma), P(self.color_out), P(self.h_sigma),
-                                                      P(self.deltas), P(self.rays), M, N, self.T_thresh,
-                                                      float(m.density_scale), P(self.rgba), 4, P(self.bg),
-                                                      P(self.state), P(self.g_color_out), P(self.g_h), None, None,
-                                                      P(self.loss_ray), P(lv["ray_rows"]), P(lv["cnt"]), s),
-                "composite_loss_ray_lists")
-        elif live:
+        if live:
             lv = self._live_bufs
             chk(lib.ngp_nerf_composite_loss_live(P(self.sigma), P(self.color_out), P(self.h_sigma), P(self.deltas),
                                                  P(self.rays), M, N, self.T_thresh, float(m.density_scale),
@@ -922,15 +819,7 @@ class FusedTrainer:
         self._tick("composite_loss")
         if self._one_bwd:  # both networks' backward in one launch (ngp_nerf_backward)
             timing = P(self.grid_ws) + self._grid_timing_at if self._grid_timing_at else None
-            if live and self._live_list:
-                chk(lib.ngp_nerf_backward_live_list(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
-                                                    P(self.enc_out), P(img[0]), P(self.g_enc), M, P(self.rays), N,
-                                                    P(lv["cnt"]), P(lv["ray_rows"]), P(lv["rows"]), P(lv["total"]),
-                                                    sn.hidden_dim, sn.num_layers, cn.hidden_dim, cn.num_layers,
-                                                    P(self.mlp_ws[0]), self.mlp_ws[0].numel(), P(self.mlp_ws[1]),
-                                                    self.mlp_ws[1].numel(), timing, s),
-                    "nerf_backward_live_list")
-            elif live:
+            if live:
                 chk(lib.ngp_nerf_backward_live(P(self.g_color_out), P(self.color_in), P(img[1]), P(self.g_h),
                                                P(self.enc_out), P(img[0]), P(self.g_enc), M, P(lv["rows"]),
                                                P(lv["total"]), sn.hidden_dim, sn.num_layers, cn.hidden_dim,
@@ -970,15 +859,11 @@ class FusedTrainer:
         bargs = (P(self.g_enc), P(self.xyzs), float(m.bound), P(e.offsets), P(self.grads[0]), M, cnt,
                  *grid_args[:-1], self._offsets_host, P(self.grid_ws), self.grid_ws.numel(), self._grid_flags,
                  self._inf_flag)
-        if self.fused_adam or self._split_reduce:
+        if self._split_reduce:
             chk(lib.ngp_ffmlp_reduce(2, pk["ws"], pk["B"], pk["ins"], pk["hid"], pk["nl"], pk["gw"], _F16,
                                      self._inf_flag, s), "ffmlp_reduce")
             self._tick("ffmlp_reduce")
-            if self.fused_adam:
-                chk(lib.ngp_grid_encode_backward_fused_adam(*bargs, ctypes.byref(self._at), P(self.state), s),
-                    "grid_backward_fused_adam")
-            else:
-                chk(lib.ngp_grid_encode_backward_fused(*bargs, s), "grid_backward_fused")
+            chk(lib.ngp_grid_encode_backward_fused(*bargs, s), "grid_backward_fused")
         elif draw and self._live:
             # over the live rows (the MLP backward wrote g_enc for those only)
             lv = self._live_bufs
@@ -1024,15 +909,7 @@ class FusedTrainer:
         # inside a step (world 1) the found-inf flag was set by the backward's kernels;
         # otherwise (flush, direct calls, the averaged shard) the grads are swept
         mode = _PRECHECKED if defer and not self.dp else _SCAN
-        if self.fused_adam:
-            at = ctypes.byref(self._at)
-            if defer:
-                chk(lib.ngp_fused_optimizer_update_db(*args, mode, P(self.state), at, s), "fused_optimizer_update_db")
-            else:
-                chk(lib.ngp_fused_optimizer_step_db(*args, 2.0, 0.5, self.growth_interval, mode, N, cnt, None,
-                                                    P(self.loss_ray), P(self.state), at, s),
-                    "fused_optimizer_step_db")
-        elif defer:
+        if defer:
             chk(lib.ngp_fused_optimizer_update(*args, mode, P(self.state), s), "fused_optimizer_update")
         else:
             chk(lib.ngp_fused_optimizer_step(*args, 2.0, 0.5, self.growth_interval, mode, N, cnt, None,
@@ -1078,7 +955,7 @@ class FusedTrainer:
                 self._body(self._pending)
                 self.eager_steps += 1
         elif self._dp_whole is not None and self._pending and self._ahead == self._pre_ahead:
-            self._dp_whole.replay()  # the whole step, collectives included (NGP_DP_GRAPH)
+            self._dp_whole.replay()  # the whole step, collectives included (dp_graph)
         else:
             g = self.graph if self._pending else None
             work = None
@@ -1134,13 +1011,12 @@ class FusedTrainer:
             self._gather_half(wait=True)
             self._gather_masters()
             self._pending = False
-        self._normalize_table()
 
     def capture(self, warmup=2, ring=0, multi=1):
         """hipGraph(s) of the step body. World 1: one graph (optimizer of the
         previous gradients, sample, march, network). Data parallel over RCCL:
         the whole step, collectives included (_dp_body); with gloo or
-        NGP_DP_GRAPH=0, three graphs (optimizer | sample + march | network)
+        options dp_graph=False, three graphs (optimizer | sample + march | network)
         with the collectives between them. ring=R (world 1): R further copies of the body graph
         with an event-record node after each launch; step() then replays
         them in turn (instead of the plain graph) and `ring_times` reads the
@@ -1248,7 +1124,7 @@ class FusedTrainer:
 
     def live_fraction(self):
         """Live rows (a nonzero gradient) over samples in the last step the
-        backwards ran over the live rows only (NGP_LIVE_ROWS), else None."""
+        backwards ran over the live rows only (live_rows), else None."""
         if not self._live:
             return None
         torch.cuda.synchronize()
@@ -1326,7 +1202,7 @@ class FusedTrainer:
                  "mean_count": self.mean_count, "mean_density": self.mean_density,
                  "model": m.state_dict(),
                  # draw: batches drawn; ahead: the last of them is the next step's (drawn during
-                 # the last backward, NGP_DRAW_AHEAD), which a restored trainer draws again
+                 # the last backward, draw_ahead), which a restored trainer draws again
                  "fused": {"draw": int(si[self._S_DRAW]), "ahead": int(self._ahead)}}
         if full:
             m1, m2 = self._moments()
@@ -1371,8 +1247,6 @@ class FusedTrainer:
             return
         si = self.state.view(torch.int32)
         si[self._S_ITER] = int(state.get("global_step", 0))
-        if self.fused_adam:  # the accumulate's tags are iteration numbers: none may match the restored ones
-            self.bin_done.zero_()
         self._ahead = False
         if "fused" in state:
             draw = int(state["fused"]["draw"])
