@@ -7,6 +7,8 @@ an optimizer step (the same contract RCCL provides on the 8x MI355X node)."""
 import os
 import socket
 
+import numpy as np
+
 import pytest
 import torch
 import torch.distributed as dist
@@ -90,10 +92,15 @@ def test_two_rank_gradient_average_matches_full_batch():
 # ---- the fused engine's ZeRO-1 sharding (nerf/zero1.py) over gloo ----------------
 # The fused step's collectives on the flat buffers of its ShardPlan: guard
 # poison at the head of every rank's chunk, averaging reduce-scatter into the
-# owner's shard, an update of the shard's optimizer sections only, all-gather
-# of the updated values. The result must equal one process updating the whole
-# flat buffer with the mean gradient; a rank's poisoned gradient must reach
-# every owner's shard.
+# owner's shard, the fused optimizer's arithmetic on the shard's sections only
+# (GradScaler's inf check of the shard, unscale, torch.optim.Adam with
+# betas (0.9, 0.99), eps 1e-15, LambdaLR 0.1 ** (epoch / iters);
+# csrc/ngp_step.h adam_consts / adam_update / step_end_block, restated below
+# in float32 with the kernels' operation order), all-gather of the updated
+# values. The result must equal one process running torch.optim.Adam over the
+# whole flat buffer with the mean gradient; a rank's poisoned gradient must
+# reach every owner's shard, so every rank skips the step and backs the scale
+# off together.
 _SIZES = [2 * 40013, 7168, 11264]  # a small table + the NeRF sigma / colour MLPs
 
 
@@ -105,11 +112,46 @@ def _flat_grad(plan, rank):
     return flat
 
 
-def _update(p, g, sections, lo):
-    """A stand-in elementwise optimizer over [lo + a, lo + a + n) sections."""
-    for a, n, _ in sections:
-        s = slice(lo + a, lo + a + n)
-        p[s] -= 0.1 * g[a:a + n].float() + 0.01 * p[s]
+_LR, _B1, _B2, _EPS, _ITERS = 1e-2, 0.9, 0.99, 1e-15, 30000
+
+
+class _ShardAdam:
+    """The fused optimizer on one rank's shard (csrc/ngp_step.h): the state's
+    GradScaler scale / growth tracker / Adam step / LR epoch, the shard's
+    moments, the inf check over the averaged fp16 shard (NGP_SCALER_SCAN)."""
+
+    def __init__(self, n, scale=65536.0):
+        self.m, self.v = torch.zeros(n), torch.zeros(n)
+        self.scale, self.tracker, self.step, self.epoch = scale, 0, 0, 0
+
+    def update(self, p, g16, sections, lo):
+        import math
+        inf = not bool(torch.isfinite(g16.float()).all())
+        f32 = torch.float32
+        inv_scale = torch.tensor(1.0 / self.scale, dtype=torch.float64).to(f32)  # (float)(1.0 / (double)scale)
+        step = self.step + 1
+        lr = _LR * 0.1 ** min(self.epoch / _ITERS, 1.0)
+        step_size = torch.tensor(lr / (1.0 - _B1 ** step), dtype=torch.float64).to(f32)
+        inv_bc2 = 1.0 / torch.tensor(math.sqrt(1.0 - _B2 ** step), dtype=torch.float64).to(f32)
+        b1, b2, eps = (torch.tensor(x, dtype=f32) for x in (_B1, _B2, _EPS))
+        if not inf:
+            for a, n, _ in sections:
+                s = slice(lo + a, lo + a + n)
+                gk = g16[a:a + n].float() * inv_scale
+                m, v = self.m[a:a + n], self.v[a:a + n]
+                m += (1.0 - b1) * (gk - m)
+                v.mul_(b2).add_((1.0 - b2) * gk * gk)
+                denom = torch.sqrt(v) * inv_bc2 + eps
+                p[s] -= step_size * (m / denom)
+        # GradScaler.update (growth_interval 2000 is not reached here), LR epoch, Adam step
+        if inf:
+            self.scale *= 0.5
+            self.tracker = 0
+        else:
+            self.tracker += 1
+            self.step += 1
+        self.epoch += 1
+        return inf
 
 
 def _zero1_worker(rank, world, port, q):
@@ -121,18 +163,26 @@ def _zero1_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     plan = ShardPlan(_SIZES, world, rank)
     params = torch.linspace(-1, 1, plan.total)
-    flat = _flat_grad(plan, rank)
+    opt = _ShardAdam(plan.chunk)
     shard = torch.empty(plan.chunk, dtype=torch.float16)
-    dist.reduce_scatter_tensor(shard, flat, op=dist.ReduceOp.AVG)
-    _update(params, shard, plan.sections(split_first=False), plan.lo)
-    full = torch.empty(plan.total)
-    dist.all_gather_into_tensor(full, params[plan.lo:plan.hi].contiguous())
+    fulls = []
+    for it in range(3):  # three averaged updates of this rank's shard, gathered after each
+        flat = _flat_grad(plan, rank + 10 * it)
+        dist.reduce_scatter_tensor(shard, flat, op=dist.ReduceOp.AVG)
+        assert not opt.update(params, shard, plan.sections(split_first=False), plan.lo)
+        full = torch.empty(plan.total)
+        dist.all_gather_into_tensor(full, params[plan.lo:plan.hi].contiguous())
+        params = full.clone()
+        fulls.append(full.numpy())
     # guard: rank 1's gradient overflowed; it poisons the head of every chunk
     bad = _flat_grad(plan, rank)
     if rank == 1:
         bad[torch.arange(world) * plan.chunk] = float("nan")
     dist.reduce_scatter_tensor(shard, bad, op=dist.ReduceOp.AVG)
-    q.put((rank, full.numpy(), bool(torch.isnan(shard[0]).item()), plan.lo, plan.hi, plan.chunk))
+    before = params.clone()
+    skipped = opt.update(params, shard, plan.sections(split_first=False), plan.lo)
+    q.put((rank, fulls, bool(torch.isnan(shard[0]).item()), plan.lo, plan.hi, plan.chunk, skipped,
+           bool(torch.equal(before, params)), opt.scale, opt.step))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -173,11 +223,22 @@ def test_zero1_reduce_scatter_update_all_gather_two_ranks():
         p.join(timeout=60)
         assert p.exitcode == 0
     plan = ShardPlan(_SIZES, 2, 0)
-    # one process: the mean gradient (fp16 average, as the reduction's output) over the whole buffer
-    mean = ((_flat_grad(plan, 0).float() + _flat_grad(plan, 1).float()) / 2).half()
-    ref = torch.linspace(-1, 1, plan.total)
-    _update(ref, mean, [(0, plan.total, True)], 0)
-    for rank, full, poisoned, lo, hi, chunk in out:
+    # one process: torch.optim.Adam (+ LambdaLR) over the whole flat buffer with
+    # the mean gradient (the fp16 average the reduction outputs), unscaled
+    ref = torch.nn.Parameter(torch.linspace(-1, 1, plan.total))
+    adam = torch.optim.Adam([ref], lr=_LR, betas=(_B1, _B2), eps=_EPS)
+    sched = torch.optim.lr_scheduler.LambdaLR(adam, lambda it: 0.1 ** min(it / _ITERS, 1))
+    refs = []
+    for it in range(3):
+        mean = ((_flat_grad(plan, 10 * it).float() + _flat_grad(plan, 1 + 10 * it).float()) / 2).half()
+        ref.grad = mean.float() * (1.0 / 65536.0)  # GradScaler: the scaled fp16 grad x (1 / scale)
+        adam.step()
+        sched.step()
+        refs.append(ref.detach().clone())
+    for rank, fulls, poisoned, lo, hi, chunk, skipped, unchanged, scale, steps in out:
         assert (lo, hi) == (rank * chunk, (rank + 1) * chunk)
-        assert torch.allclose(torch.from_numpy(full), ref, rtol=0, atol=2e-3)
+        for full, want in zip(fulls, refs):  # fused arithmetic vs torch's Adam: fp32 rounding of the same formula
+            torch.testing.assert_close(torch.from_numpy(full), want, rtol=1e-6, atol=1e-7)
         assert poisoned  # the overflow on rank 1 reached rank 0's shard too
+        assert skipped and unchanged and scale == 32768.0 and steps == 3  # every rank skipped and backed off
+    assert np.array_equal(out[0][1][-1], out[1][1][-1])  # both ranks hold the same gathered parameters
