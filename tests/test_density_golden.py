@@ -14,8 +14,10 @@ CPU: the fixture is self-consistent with the oracle's packbits / morton
 GPU: this build's reference-API `update_extra_state` and
 `mark_untrained_grid` (nerf/renderer.py, csrc/density_grid.hip) replay the
 same draws on the same analytic field: the -1 mask and the bitfield bit for
-bit, the grid within fp32 exp rounding (1e-6 rel), mean_density within 1e-6,
-mean_count / local_step exact. The fused update's own stages (brick-sorted
+bit (but for cells within the grid tolerance of the threshold), the grid
+within RTOL (the analytic field's exp of an argument up to ~10 evaluated in
+fp32 on the device and on the host: a few ulps of the argument), mean_density
+within RTOL, mean_count / local_step exact. The fused update's own stages (brick-sorted
 query points, the EMA + packbits launch) are checked against the same
 updates.
 """
@@ -29,6 +31,17 @@ import oracle
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = [("b2", 2, 10.0), ("b1", 1, 0.5)]
+RTOL = 2e-5
+
+
+def _bits_match(got, want, grid, thresh):
+    """Bitfields equal, except for cells whose density lies within RTOL of the
+    threshold (the two fields may round to either side there)."""
+    gb = np.unpackbits(got, bitorder="little")
+    wb = np.unpackbits(want, bitorder="little")
+    g = grid.reshape(-1)
+    near = np.abs(g - thresh) <= RTOL * max(abs(thresh), 1e-30)
+    return bool(np.all((gb == wb) | near))
 
 
 def _fixture():
@@ -122,10 +135,10 @@ def test_reference_api_density_pipeline_matches_reference(cuda, monkeypatch, tag
         torch.cuda.synchronize()
         g, ref = m.density_grid.cpu().numpy(), f[f"{tag}_u{u}_grid"]
         assert np.array_equal(g < 0, ref < 0)
-        np.testing.assert_allclose(g, ref, rtol=1e-6, atol=1e-30)
+        np.testing.assert_allclose(g, ref, rtol=RTOL, atol=1e-30)
         md = float(f[f"{tag}_u{u}_mean_density"])
-        assert abs(m.mean_density - md) <= 1e-6 * md
-        assert np.array_equal(m.density_bitfield.cpu().numpy(), f[f"{tag}_u{u}_bitfield"]), u
+        assert abs(m.mean_density - md) <= RTOL * md
+        assert _bits_match(m.density_bitfield.cpu().numpy(), f[f"{tag}_u{u}_bitfield"], ref, min(md, thresh)), u
         assert m.mean_count == int(f[f"{tag}_u{u}_mean_count"]) and m.local_step == 0
 
 
@@ -182,8 +195,8 @@ def test_fused_density_stages_match_reference(cuda, tag, bound, thresh):
                   "ema_pack")
         torch.cuda.synchronize()
         ref = f[f"{tag}_u{u}_grid"]
-        np.testing.assert_allclose(grid.cpu().numpy(), ref, rtol=1e-6, atol=1e-30)
+        np.testing.assert_allclose(grid.cpu().numpy(), ref, rtol=RTOL, atol=1e-30)
         md = float(np.float32(stats.item() / grid.numel()))
-        assert abs(md - float(f[f"{tag}_u{u}_mean_density"])) <= 1e-6 * md
-        assert np.array_equal(bits.cpu().numpy(), f[f"{tag}_u{u}_bitfield"]), u
+        assert abs(md - float(f[f"{tag}_u{u}_mean_density"])) <= RTOL * md
+        assert _bits_match(bits.cpu().numpy(), f[f"{tag}_u{u}_bitfield"], ref, min(md, thresh)), u
         assert float(tmp.max()) == -1.0  # the EMA launch resets the scratch grid

@@ -1,8 +1,10 @@
-"""Phase clocks of the grid accumulate kernel (diagnostic build with
--DNGP_STAMPS, built by this script's caller into torch-ngp_amd/dbg/):
-runs fused steps, then one grid backward, and summarises the per-workgroup
-s_memtime stamps (step 1 / retire / per unit: zero, adds, flush).
-    NGP_HIP_LIB=torch-ngp_amd/dbg/libngp_hip_stamps.so python tools/accum_stamps.py"""
+"""Phase clocks of the grid backward (bin + accumulate kernels) in the
+trained regime (diagnostic build with -DNGP_STAMPS:
+SRCS="gridencoder ffmlp" bash tools/variants.sh stamps "-DNGP_STAMPS"):
+runs [steps] fused steps of the bench's Lego workload, then one more, and
+summarises the per-workgroup s_memtime stamps (step 1 / retire / per unit:
+zero, adds, flush; bin phases).
+    NGP_HIP_LIB=torch-ngp_amd/variants/stamps/libngp_hip.so python tools/accum_stamps.py [steps]"""
 import ctypes
 import json
 import os
@@ -19,25 +21,28 @@ from nerf.network_ff import NeRFNetwork  # noqa: E402
 from nerf.provider import SyntheticLego, lego_bitfield  # noqa: E402
 
 dev = torch.device("cuda:0")
-torch.manual_seed(0)
-model = NeRFNetwork(bound=1, cuda_ray=True).to(dev)
-model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
-ft = FusedTrainer(model, SyntheticLego(dev, num_rays=4096), M=101762)
+import bench  # noqa: E402
+_argv, sys.argv = sys.argv, sys.argv[:1]
+_args = bench.parse()
+sys.argv = _argv
+STEPS = int(_argv[1]) if len(_argv) > 1 else 300  # the trained regime (live rows) by default
+model, data, *_ = bench.make_workload("lego", dev, 1, 4096)
+ft, _ = bench.make_trainer(_args, model, data, 1, dev, 0.0, grid_timing=False)
 stamps = torch.zeros(4096 * 64, dtype=torch.int64, device=dev)
 lib = nat.lib()
 assert lib.ngp_debug_stamps(ctypes.c_void_p(nat.ptr(stamps))) == 0
-# k_mlp_bwd: (NH - 1) * 2048 + wave rows of 16 (ffmlp.hip MSTAMP), then the
-# one-launch forward's rows (FSTAMP); set before any step
-ms = torch.zeros(2 * 2048 * 16 + 4096 * 16, dtype=torch.int64, device=dev)
+# k_mlp_bwd / k_nerf_bwd: (NH - 1) * 2048 + wave rows of 16 (ffmlp.hip MSTAMP); set before any step
+ms = torch.zeros(3 * 2048 * 16 + 4096 * 16, dtype=torch.int64, device=dev)
 if hasattr(lib, "ngp_debug_mlp_stamps"):
     assert lib.ngp_debug_mlp_stamps(ctypes.c_void_p(nat.ptr(ms))) == 0
-for _ in range(12):
+for _ in range(STEPS):
     ft.step()
 torch.cuda.synchronize()
 stamps.zero_()  # one more step on a clean buffer: no stale stamps of workgroups that exited early
 ms.zero_()
 ft.step()
 torch.cuda.synchronize()
+print(json.dumps({"steps": STEPS, "samples": ft.sample_count(), "live_frac": ft.live_fraction()}))
 st = stamps[:32768].view(-1, 64).cpu().numpy().astype(np.int64)  # accumulate: 2 workgroups per CU
 nwg = int((st[:, 0] > 0).sum())
 st = st[:nwg]
