@@ -92,6 +92,22 @@ NGP_DEV void copy_frags(half8* __restrict__ lds, const half8* __restrict__ image
     }
 }
 
+// An image copied by `nthr` threads of the workgroup (tid in [0, nthr)), four
+// loads of a thread in flight per round: the NeRF backward's idle waves copy
+// the sigma image during the colour pass.
+template <int FRAGS>
+NGP_DEV void copy_frags_part(half8* __restrict__ lds, const half8* __restrict__ image, uint32_t tid, uint32_t nthr) {
+    constexpr uint32_t TOTAL = FRAGS * 64;
+    for (uint32_t i0 = tid; i0 < TOTAL; i0 += 4 * nthr) {
+        half8 v[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) v[k] = image[min(i0 + k * nthr, TOTAL - 1)];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (i0 + k * nthr < TOTAL) lds[i0 + k * nthr] = v[k];
+    }
+}
+
 // Two images copied with every load of both issued before the first LDS
 // store: one round trip instead of two (the NeRF backward's prologue).
 template <int F1, int F2, int THREADS>
@@ -816,28 +832,36 @@ constexpr uint32_t kNoHalf = 0xffffffffu;
 struct NoHalf {
     NGP_DEV uint32_t operator()() const { return kNoHalf; }
 };
+struct NoIdle {
+    NGP_DEV void operator()() const {}
+};
 
 template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI, typename MAP, typename PRE,
-          typename HALF = NoHalf>
+          typename HALF = NoHalf, typename IDLE = NoIdle>
 NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tiles, float* __restrict__ img_base,
                        const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs, XL xl, GI gi_out,
                        bool want_gi, float* __restrict__ slab, uint32_t nparams, uint32_t B, uint32_t in_dim,
-                       FA act, MAP map, PRE pre, HALF half = HALF{}) {
+                       FA act, MAP map, PRE pre, HALF half = HALF{}, IDLE idle = IDLE{}) {
     using N = Net<W, IN_KS, NH>;
     constexpr int LAST = N::NMAT - 1;
     MSTAMP(0);
     const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
     uint32_t chunk = map(0u);
+    // a wave whose only work is a half chunk (the live-row regime's common
+    // case) requests the half's rows here instead, beside the prologue
+    const uint32_t hrow = half();
+    const bool half_first = chunk >= nchunks && hrow != kNoHalf;  // wave-uniform
+    const uint32_t first_row = half_first ? hrow : chunk * 16 * kNB;
     half8 xn[kNB][IN_KS], dn[kNB][1];
-    xl.template operator()<IN_KS>(inputs, in_dim, chunk * 16 * kNB, B, xn);
-    load_rows<1>(grad, kOut, chunk * 16 * kNB, B, dn, xl.map);  // output activation ignored (ffmlp.cu:783)
+    xl.template operator()<IN_KS>(inputs, in_dim, first_row, B, xn);
+    load_rows<1>(grad, kOut, first_row, B, dn, xl.map);  // output activation ignored (ffmlp.cu:783)
     pre();
     MSTAMP(1);
     [[maybe_unused]] uint32_t nst = 0;
 
     ngp_half* dT = tiles + (size_t)wave * 2 * kTileRows * kTileLd;
     ngp_half* hT = dT + (size_t)kTileRows * kTileLd;
-    const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
 
     f32x4 dw_last[1][N::MTW], dw_hid[NH][N::MTW][N::MTW], dw_first[N::MTW][N::IN_MT];
     zero_tiles(dw_last);
@@ -909,11 +933,16 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
     }
     // the wave's half chunk: 16 samples in rows 0..15 of the transposing
     // tiles, rows 16..31 zero (the dW products' K runs over all 32 rows)
-    const uint32_t hrow = half();
     if (hrow != kNoHalf) {
         half8 x1[1][IN_KS], d1[1][1];
-        xl.template operator()<IN_KS>(inputs, in_dim, hrow, B, x1);
-        load_rows<1>(grad, kOut, hrow, B, d1, xl.map);
+        if (half_first) {  // requested at the start
+#pragma unroll
+            for (int s2 = 0; s2 < IN_KS; ++s2) x1[0][s2] = xn[0][s2];
+            d1[0][0] = dn[0][0];
+        } else {
+            xl.template operator()<IN_KS>(inputs, in_dim, hrow, B, x1);
+            load_rows<1>(grad, kOut, hrow, B, d1, xl.map);
+        }
         asm volatile("" ::: "memory");  // after the last chunk's transposed reads
         const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint32_t lane = threadIdx.x & 63;
@@ -944,6 +973,7 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
     };
     __shared__ uint32_t s_took[kBwdWaves];  // each wave writes its own slot before the barrier below
     if ((threadIdx.x & 63) == 0) s_took[wave] = nst != 0 || hrow != kNoHalf ? 1u : 0u;
+    if (nst == 0 && hrow == kNoHalf) idle();  // a wave without rows (wave-uniform)
     // fragments and tiles are dead from here on; a full barrier: the waves'
     // input-gradient stores are complete for the workgroup (the NeRF
     // backward's sigma pass reads the colour pass's), the later ones order LDS only
@@ -964,26 +994,36 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
     const f32x4* i0 = reinterpret_cast<const f32x4*>(img_base);
     const f32x4* i1 = i0 + NT * 64;
     float* slab_row = slab + (size_t)blockIdx.x * nparams;
-    for (int tt = (int)wave; tt < NT; tt += kBwdWaves) {
-        int local, mi;
-        uint32_t in_w, out_w, off;
+    // all of the wave's image reads first (one LDS wait), then its stores back
+    // to back; each tile's geometry from compile-time divisors
+    constexpr int TPW = (NT + kBwdWaves - 1) / kBwdWaves;
+    f32x4 sv[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int tt = min((int)wave + q * kBwdWaves, NT - 1);
+        sv[q] = i0[tt * 64 + lane] + i1[tt * 64 + lane];
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int tt = (int)wave + q * kBwdWaves;
+        if (tt >= NT) break;
+        uint32_t m, k, in_w, out_w, off;
         if (tt < T_FIRST) {
-            local = tt; mi = N::IN_MT; in_w = in_dim; out_w = W; off = 0;
+            m = (uint32_t)tt / N::IN_MT; k = (uint32_t)tt % N::IN_MT; in_w = in_dim; out_w = W; off = 0;
         } else if (tt < T_FIRST + NH * T_HID) {
-            const int q = (tt - T_FIRST) / T_HID;
-            local = tt - T_FIRST - q * T_HID; mi = N::MTW; in_w = W; out_w = W;
-            off = fwd_desc<W, IN_KS, NH>(q + 1, in_dim).off;
+            const uint32_t h = (uint32_t)(tt - T_FIRST) / T_HID, local = (uint32_t)(tt - T_FIRST) - h * T_HID;
+            m = local / N::MTW; k = local % N::MTW; in_w = W; out_w = W;
+            off = fwd_desc<W, IN_KS, NH>((int)h + 1, in_dim).off;
         } else {
-            local = tt - T_FIRST - NH * T_HID; mi = N::MTW; in_w = W; out_w = kOut;
+            const uint32_t local = (uint32_t)(tt - T_FIRST - NH * T_HID);
+            m = local / N::MTW; k = local % N::MTW; in_w = W; out_w = kOut;
             off = fwd_desc<W, IN_KS, NH>(LAST, in_dim).off;
         }
-        const uint32_t m = (uint32_t)(local / mi), k = (uint32_t)(local % mi);
-        const f32x4 a = i0[tt * 64 + lane], b = i1[tt * 64 + lane];
         const uint32_t i = 16 * k + c;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t o = 16 * m + 4 * g + r;
-            if (o < out_w && i < in_w) slab_row[off + o * in_w + i] = a[r] + b[r];
+            if (o < out_w && i < in_w) slab_row[off + o * in_w + i] = sv[q][r];
         }
     }
     MSTAMP(14);
@@ -1080,6 +1120,11 @@ k_nerf_bwd(NerfBwdArgs a) {
     auto half_of = [=](uint32_t slot) {
         return [=]() { return nf < n && slot < 2 * r ? (b + (nf + slot / 2) * G) * 16 * kNB + 16 * (slot & 1) : kNoHalf; };
     };
+    // With 1 or 3 chunks the colour pass leaves the last waves without rows
+    // (waves 2-3: two halves; wave 3: three whole chunks): they copy the sigma
+    // image meanwhile, off the colour pass's critical path
+    const bool idle_copy = n == 1 || n == 3;
+    const uint32_t idle0 = n == 1 ? 2u : 3u;
     // live rows: the workgroups past the slab rows the reduce reads have no
     // chunk and skip both passes (ngp_reduce::live_slab_rows)
     if (!a.rows || b < ngp_reduce::live_slab_rows((int32_t)B, G)) {
@@ -1089,9 +1134,14 @@ k_nerf_bwd(NerfBwdArgs a) {
                           true, a.slab_color, a.np_color, B, 32u, ActReLU{}, map_of(w),
                           [&]() {
                               copy_frags<LC::FRAGS, kBwdThreads>(lds, a.color_image);
-                              copy_frags<LS::FRAGS, kBwdThreads>(sfr, a.sigma_image);
+                              if (!idle_copy) copy_frags<LS::FRAGS, kBwdThreads>(sfr, a.sigma_image);
                               __syncthreads();
-                          }, half_of(w));
+                          }, half_of(w),
+                          [&]() {  // the colour pass's idle waves copy the sigma image (done by the fold's barrier)
+                              if (idle_copy)
+                                  copy_frags_part<LS::FRAGS>(sfr, a.sigma_image, threadIdx.x - idle0 * 64,
+                                                             (kBwdWaves - idle0) * 64);
+                          });
     // the colour pass's geo grads (global stores of every wave) are complete
     // (the fold's first barrier) and its fold images read before the sigma
     // pass loads g_h and reuses LDS: an LDS-only barrier, so the colour slab
