@@ -96,6 +96,10 @@ def parse():
                     help="collective backend for N > 1: nccl (= RCCL, the measured path) or gloo "
                          "(host-staged; a rehearsal of the data-parallel step with every rank on the "
                          "visible GPUs, e.g. 2 ranks on a 1-GPU box)")
+    ap.add_argument("--exchange", choices=["zero1", "sparse"], default="zero1",
+                    help="data-parallel gradient exchange for N > 1: zero1 (reduce-scatter + sharded Adam + "
+                         "all-gather, whole step in one graph) or sparse (every rank runs the world-1 step and "
+                         "the full Adam; touched-entry lists all-gathered, DESIGN.md section 7)")
     return ap.parse_args()
 
 
@@ -177,7 +181,8 @@ def main():
     torch.cuda.set_device(dev)
     # what the collective layer itself reports (the ranks RCCL / gloo joined)
     comm = {"backend": dist.get_backend() if world > 1 else None,
-            "world_size": dist.get_world_size() if world > 1 else 1}
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "exchange": args.exchange if world > 1 else None}
     assert comm["world_size"] == args.gpus
     torch.manual_seed(1234 + rank)
     np.random.seed(rank)
@@ -199,6 +204,7 @@ def main():
         # the backwards walk only these rows (the rest carry a zero gradient)
         result["live_rows_frac"] = round(ft.live_fraction(), 4)
     if world == 1 and args.engine == "fused":
+        result["touched"] = touched_pairs(ft)
         ft.flush()
         if args.render:
             result["render"] = render_probe(args, model, data, dev)
@@ -257,9 +263,24 @@ def run_leg(args, name, dev):
                                                  counts if getattr(ft, "_live", False) else None)}
     if ft.live_fraction() is not None:
         out["live_rows_frac"] = round(ft.live_fraction(), 4)
+    out["touched"] = touched_pairs(ft)
     del ft, model
     torch.cuda.empty_cache()
     return out
+
+
+def touched_pairs(ft, steps=4):
+    """Nonzero fp16 channel pairs of a step's flat gradient (table + MLPs):
+    what one rank lists per step in the replicated step's touched-entry
+    exchange (8 bytes each), against the dense buffer."""
+    n = []
+    for _ in range(steps):
+        ft.step()  # the step's gradient stays in flat_grad until the next step's Adam
+        torch.cuda.synchronize()
+        n.append(int(((ft.flat_grad.view(torch.int32) & 0x7fff7fff) != 0).sum()))
+    pairs = float(np.mean(n))
+    return {"pairs_per_step": round(pairs, 1), "list_bytes": int(8 * pairs), "flat_pairs": int(ft.total // 2),
+            "dense_fp16_bytes": int(2 * ft.total), "frac": round(pairs / (ft.total // 2), 4)}
 
 
 def render_probe(args, model, data, dev, images=5, pose=7):
@@ -351,6 +372,20 @@ def dp_path_probe(args, model, data, dev, headline):
         e3, g3, _ = timed_run(args, ft3, 1, dev, steps, 5, 300, 1)
         three = {"ms_per_step": round(e3 / steps * 1e3, 4), "graphs": bool(g3)}
         del ft3, m3
+        # the replicated step (sparse_exchange, DESIGN.md section 7 option B): the
+        # world-1 step graph, then the touched-entry exchange (list, header
+        # all-gather + read-back, list all-gather, sum) after every step
+        m4, d4, _, _, _, _, _ = make_workload(args.workload, dev, 1, args.num_rays)
+        ft4, _ = make_trainer(args, m4, d4, 1, dev, dtg, distributed=True, options=dict(sparse_exchange=True))
+        assert ft4.xchg
+        e4, g4, _ = timed_run(args, ft4, 1, dev, steps, 5, 300, 1)
+        xc = ft4._xchg
+        sparse = {"ms_per_step": round(e4 / steps * 1e3, 4), "graphs": bool(g4),
+                  "whole_step_graph": ft4.graph is not None, "list_cap": xc.cap,
+                  "longest_list": int(xc.stats[1]), "list_bytes_per_rank": xc.bytes_per_step()[0],
+                  "pairs_total": int(xc.pairs), "overflows": xc.overflows,
+                  "per_rank_bytes_8_ranks": {"send": xc.bytes_per_step()[0], "receive": 7 * xc.bytes_per_step()[0]}}
+        del ft4, m4
         grad_bytes = 2 * ft.total  # the flat fp16 gradient = the fp16 forward copy
         truck_bytes = 2 * _flat_total(22)
         W = 8
@@ -359,7 +394,7 @@ def dp_path_probe(args, model, data, dev, headline):
         out = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "graphs": used_graph,
                "whole_step_graph": whole_captured, "graph_steps": graph_steps,
                "ms_per_step": round(ms, 4), "rays_per_s": round(args.num_rays / (ms * 1e-3), 1),
-               "three_graphs": three,
+               "three_graphs": three, "sparse_exchange": sparse,
                "phases_ms": {k: round(v, 5) for k, v in phases.items()},
                "flat_grad_bytes": int(grad_bytes),
                "per_rank_bytes_8_ranks": {
@@ -611,6 +646,11 @@ def timed_run(args, ft, world, dev, steps, warmup, settle, graph_steps):
     for i in range(0, settle, 64):
         ft.run(min(64, settle - i))
         torch.cuda.synchronize()
+    if ft.xchg:
+        # the replicated step's touched-entry lists sized for the steady regime
+        # (2 x the longest list of the settle steps; graphs captured again)
+        ft.fit_exchange(2.0)
+        ft.run(max(2, graph_steps))
     torch.cuda.synchronize()
     # ---------------- timed region ----------------
     if world > 1:
@@ -628,6 +668,8 @@ def timed_run(args, ft, world, dev, steps, warmup, settle, graph_steps):
     err = ft.device_errors()
     if err:
         raise RuntimeError(f"march emit wait timed out during the run (error word {err:#x})")
+    if ft.exchange_overflows:  # a skipped update is work not done: not a result either
+        raise RuntimeError(f"{ft.exchange_overflows} steps skipped on a gradient-exchange list overflow")
     grid_clock = ft.grid_timing(last=steps)  # the timed region's grid backwards (<= 256 of them)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -688,10 +730,8 @@ def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload, live=None):
     traffic, src = pmc_traffic(dom, workload)
     out.update(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                traffic=traffic, traffic_source=src, algorithmic_bytes_per_launch=int(b))
-    if dom in ("march_rays_train+adam", "grid_encode_forward+adam"):
-        ab = b - {"march_rays_train+adam": 48 * rays + 32 * S}.get(dom, 0)
-        if dom == "grid_encode_forward+adam":
-            ab = 28 * int(ft._fwd_split[1].sizes[0])
+    if dom == "march_rays_train+adam":
+        ab = b - (48 * rays + 32 * S)
         out["adam_bytes"] = int(ab)
         out["adam_bytes_frac"] = round(ab / b, 4)
     out["per_launch_ms"] = {k: round(v, 5) for k, v in kernel_ms.items()}
@@ -701,7 +741,8 @@ def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload, live=None):
 
 
 def run_fused(args, model, data, bits, world, dev):
-    ft, mean_count = make_trainer(args, model, data, world, dev, args.dt_gamma)
+    opts = dict(sparse_exchange=True) if args.exchange == "sparse" else None
+    ft, mean_count = make_trainer(args, model, data, world, dev, args.dt_gamma, options=opts)
     elapsed, used_graph, grid_clock = timed_run(args, ft, world, dev, args.steps, args.warmup, args.settle_steps,
                                                 args.graph_steps)
     ms_per_step = elapsed / args.steps * 1e3

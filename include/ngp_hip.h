@@ -639,6 +639,32 @@ int ngp_grad_guard(void* grad_half, uint64_t n, uint64_t chunk, int32_t world, v
 /* (n == 0: no scan; the per-rank flag ngp_fused_inf_flag(state, 1) was set by
  * the kernels that wrote the gradient.) */
 
+/* Touched-entry gradient exchange of the replicated data-parallel step
+ * (nerf/exchange.py; DESIGN.md §7 option B). Replaces the reference's DDP
+ * gradient all-reduce (nerf/utils.py:325-327) for the fused engine: each rank
+ * lists its nonzero fp16 channel pairs, the lists (fixed size, so the step
+ * captures whole) are all-gathered, and every rank sums all of them exactly
+ * (int64, 2^-24 fixed point) into the same flat gradient, then runs the full
+ * Adam (world 1's step).
+ *   list: grad_half[n_values] (16-byte aligned, n_values % 8 == 0) -> send,
+ *     ngp_grad_exchange_words(n_values, cap) int64 words: header (int32
+ *     count, int32 flags: bit 0 a non-finite value or *inf_flag (nullable)
+ *     set; the header must be zero before the call), a table of
+ *     bins(n_values) words ((count << 32) | start) and up to cap items
+ *     ((half2 bits << 32) | pair index). The gradient is not changed.
+ *   reduce: recv = world lists back to back -> grad_half = fp16(sum / world)
+ *     over every value (dense); any rank's flag -> *inf_flag |= 1; a list over
+ *     cap -> *inf_flag |= 2 (the update is skipped without a scale back-off)
+ *     and grad_half zeroed; stats[0] += 1 per overflowed exchange, stats[1] =
+ *     max(stats[1], the largest count); send (nullable): this rank's list,
+ *     whose header is cleared for the next list call. */
+uint32_t ngp_grad_exchange_bins(uint64_t n_values);
+uint64_t ngp_grad_exchange_words(uint64_t n_values, uint32_t cap);
+int ngp_grad_exchange_list(const void* grad_half, uint64_t n_values, const int32_t* inf_flag, void* send,
+                           uint32_t cap, void* stream);
+int ngp_grad_exchange_reduce(const void* recv, int32_t world, uint32_t cap, void* grad_half, uint64_t n_values,
+                             int32_t* inf_flag, int32_t* stats, void* send, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Density-grid update (replaces the torch glue of NeRFRenderer.             */
 /* update_extra_state, nerf/renderer.py:498-598, and its packbits call,      */

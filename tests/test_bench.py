@@ -81,17 +81,19 @@ def test_fox_leg_occupancy_is_not_degenerate():
 
 
 @pytest.mark.gpu
-def test_bench_gpus2_gloo_runs_two_ranks():
+@pytest.mark.parametrize("exchange", ["zero1", "sparse"])
+def test_bench_gpus2_gloo_runs_two_ranks(exchange):
     """`bench.py --gpus 2 --backend gloo` on the one-GPU box: both ranks run the
-    data-parallel step and rank 0 reports n_gpus 2 and the 2 ranks gloo joined."""
+    data-parallel step (ZeRO-1, or the replicated step with the touched-entry
+    exchange) and rank 0 reports n_gpus 2 and the 2 ranks gloo joined."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
                         "--steps", "3", "--warmup", "2", "--kernel-steps", "1", "--no-cpu", "--no-graph",
-                        "--settle-steps", "2"],
+                        "--settle-steps", "2", "--exchange", exchange],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
-    assert out["config"]["collective"] == {"backend": "gloo", "world_size": 2}
+    assert out["config"]["collective"] == {"backend": "gloo", "world_size": 2, "exchange": exchange}
     assert out["value"] > 0 and out["config"]["global_batch_rays"] == 2 * out["config"]["num_rays_per_gpu"]

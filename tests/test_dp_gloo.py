@@ -242,3 +242,145 @@ def test_zero1_reduce_scatter_update_all_gather_two_ranks():
         assert poisoned  # the overflow on rank 1 reached rank 0's shard too
         assert skipped and unchanged and scale == 32768.0 and steps == 3  # every rank skipped and backed off
     assert np.array_equal(out[0][1][-1], out[1][1][-1])  # both ranks hold the same gathered parameters
+
+
+# ---- the replicated step's touched-entry exchange (nerf/exchange.py) over gloo ----
+# SparseExchange's host side (the fixed-size list buffers, their all-gather,
+# the kernels' arguments) with its two kernels (csrc/exchange.hip) restated on
+# the CPU: every rank must end with the exact mean of all ranks' fp16
+# gradients rounded once to fp16, the same bits on every rank; a non-finite
+# value on one rank raises every rank's GradScaler flag; a list longer than
+# the capacity makes every rank skip (flag bit 1, zero gradient).
+_BIN = 4096  # pairs per bin (csrc/exchange.hip kBinPairs)
+
+
+def _exchange_grads(rank, n, step):
+    rng = np.random.default_rng(100 * step + rank)
+    g = np.zeros(n, np.float16)
+    k = int(rng.integers(n // 20, n // 4))  # ragged: every rank lists a different number of pairs
+    idx = rng.choice(n, k, replace=False)
+    g[idx] = (rng.standard_normal(k) * 10.0 ** rng.integers(-8, 4, k)).astype(np.float16)
+    g[:8] = np.float16(1.5 + rank)  # pairs every rank touches
+    return g
+
+
+def _exchange_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "torch-ngp_amd")]
+    import nerf.exchange as xm
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class _Lib:  # the buffer-size arithmetic of csrc/exchange.hip
+        @staticmethod
+        def ngp_grad_exchange_bins(n):
+            return (n // 2 + _BIN - 1) // _BIN
+
+        @staticmethod
+        def ngp_grad_exchange_words(n, cap):
+            return 2 + _Lib.ngp_grad_exchange_bins(n) + cap
+
+    xm.nat.lib = lambda: _Lib
+
+    class CpuExchange(xm.SparseExchange):
+        """The kernels restated in numpy; a bin's items in index order, the
+        bins' segments placed in a rank-dependent order (the device reserves
+        them with atomics)."""
+
+        def list(self):
+            w = self.grad.view(torch.int32).numpy().view(np.uint32)
+            bad = ((w & 0x7c00) == 0x7c00) | ((w & 0x7c000000) == 0x7c000000)
+            ok = ((w & 0x7fff7fff) != 0) & ~bad
+            send = self.send.numpy().view(np.uint64)
+            assert send[0] == 0  # cleared by the last reduce (or a new buffer)
+            send[:] = 0
+            hdr = send[:2].view(np.int32)
+            hdr[1] = int(bad.any() or int(self.inf_flag[0]) != 0)
+            nb, pos = self.n_bins, 0
+            for b in np.random.default_rng(rank).permutation(nb):
+                idx = np.nonzero(ok[b * _BIN:(b + 1) * _BIN])[0] + b * _BIN
+                send[2 + b] = (np.uint64(idx.size) << np.uint64(32)) | np.uint64(pos)
+                for j, p in enumerate(idx):
+                    if pos + j < self.cap:
+                        send[2 + nb + pos + j] = (np.uint64(w[p]) << np.uint64(32)) | np.uint64(p)
+                pos += idx.size
+            hdr[0] = pos
+
+        def reduce(self):
+            recv = self.recv.numpy().view(np.uint64).reshape(self.world, self.words)
+            hdr = recv[:, :2].copy().view(np.int32).reshape(self.world, 4)
+            self.send[0] = 0  # the next list starts from a zero header
+            over = bool((hdr[:, 0] > self.cap).any())
+            if (hdr[:, 1] & 1).any() or over:
+                self.inf_flag[0] |= (1 if (hdr[:, 1] & 1).any() else 0) | (2 if over else 0)
+            self.stats[0] += int(over)
+            self.stats[1] = max(int(self.stats[1]), int(hdr[:, 0].max()))
+            acc = np.zeros(self.n, np.int64)
+            if not over:
+                nb = self.n_bins
+                for r in range(self.world):
+                    for b in range(nb):
+                        t = recv[r, 2 + b]
+                        start, cnt = int(t & np.uint64(0xffffffff)), int(t >> np.uint64(32))
+                        it = recv[r, 2 + nb + start:2 + nb + start + cnt]
+                        pair = (it & np.uint64(0xffffffff)).astype(np.int64)
+                        h = (it >> np.uint64(32)).astype(np.uint32).view(np.float16).reshape(-1, 2)
+                        for c in range(2):
+                            np.add.at(acc, 2 * pair + c, (h[:, c].astype(np.float64) * 2.0 ** 24).astype(np.int64))
+            self.grad.copy_(torch.from_numpy((acc.astype(np.float64) * 2.0 ** -24 / self.world).astype(np.float16)))
+
+    n = 8 * 4096 + 64  # 5 bins, the last one ragged
+    flat = torch.zeros(n, dtype=torch.float16)
+    inf = torch.zeros(1, dtype=torch.int32)
+    xc = CpuExchange(flat, inf, world, nccl=False, cap=n // 2)
+    outs = []
+    for step in range(2):
+        flat.copy_(torch.from_numpy(_exchange_grads(rank, n, step)))
+        xc()
+        outs.append((flat.numpy().copy(), int(inf[0]), int(xc.stats[1])))
+    # rank 1 overflows: every rank's flag goes up, nothing non-finite reaches the mean
+    g = _exchange_grads(rank, n, 2)
+    if rank == 1:
+        g[100] = np.float16(np.inf)
+    flat.copy_(torch.from_numpy(g))
+    xc()
+    outs.append((flat.numpy().copy(), int(inf[0]), int(xc.stats[1])))
+    # a list over the capacity: every rank skips (bit 1), zero gradient, counted
+    inf.zero_()
+    xc.resize(16)
+    flat.copy_(torch.from_numpy(_exchange_grads(rank, n, 0)))
+    xc()
+    outs.append((flat.numpy().copy(), int(inf[0]), xc.overflows))
+    q.put((rank, outs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sparse_exchange_exact_mean_on_every_rank(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 8 * 4096 + 64
+    peak = 0
+    for step in range(3):
+        gs = [_exchange_grads(r, n, step) for r in range(world)]
+        if step == 2:
+            gs[1][100] = 0  # the non-finite value is dropped from the sum
+        want = (np.sum([g.astype(np.float64) for g in gs], axis=0) / world).astype(np.float16)
+        peak = max([peak] + [int(np.count_nonzero(g.view(np.uint32) & 0x7fff7fff)) for g in gs])
+        for r in range(world):
+            got, inf, seen = out[r][step]
+            assert np.array_equal(got.view(np.uint16), want.view(np.uint16)), (step, r)
+            assert inf == (1 if step == 2 else 0) and seen == peak
+    for r in range(world):
+        got, inf, overflows = out[r][3]
+        assert inf == 2 and overflows == 1 and not got.any()

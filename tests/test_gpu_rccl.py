@@ -11,7 +11,10 @@ identity, so the run must equal the single-process (non data-parallel) step
 bit for bit: parameters, Adam moments, GradScaler state, density grid and
 bitfield (reference hook: nerf/utils.py:325-327, the DDP wrap this replaces).
 This is the code path the driver's 8-GPU bench runs; here it executes RCCL on
-the one GPU of the box.
+the one GPU of the box. The replicated step (options sparse_exchange: the
+world-1 step on every rank, the gradients averaged by the touched-entry
+exchange of nerf/exchange.py) must equal it too: at world 1 the exchange's
+exact fixed-point mean of one rank's list is that rank's gradient.
 """
 import os
 import socket
@@ -32,7 +35,7 @@ def _free_port():
     return p
 
 
-def _trainer(dev, distributed, whole_graph=True):
+def _trainer(dev, distributed, mode="whole_step_graph"):
     from nerf.fused import FusedTrainer
     from nerf.network_ff import NeRFNetwork
     from nerf.provider import SyntheticLego, lego_bitfield
@@ -41,8 +44,8 @@ def _trainer(dev, distributed, whole_graph=True):
     with torch.no_grad():
         model.encoder.embeddings.normal_(0, 0.05)
     model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
-    return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, distributed=distributed,
-                        options=dict(dp_graph=whole_graph))
+    opts = dict(sparse_exchange=True) if mode == "sparse_exchange" else dict(dp_graph=mode == "whole_step_graph")
+    return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, distributed=distributed, options=opts)
 
 
 def _snap(ft):
@@ -73,11 +76,11 @@ def _run_steps(ft):
                 v=m2[:ft._starts[-1] + ft.params[-1].numel()].cpu().numpy(),
                 steps=ft.optimizer_steps, scale=ft.scale, loss=ft.last_loss,
                 grid=ft.model.density_grid.cpu().numpy(), bits=ft.model.density_bitfield.cpu().numpy(),
-                mean_density=ft.mean_density, dp=ft.dp, nccl=ft._nccl,
+                mean_density=ft.mean_density, dp=ft.dp, xchg=ft.xchg, nccl=ft._nccl,
                 whole=getattr(ft, "_dp_whole", None) is not None)
 
 
-def _worker(port, q, whole_graph=False):
+def _worker(port, q, mode):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "torch-ngp_amd")]
@@ -89,7 +92,7 @@ def _worker(port, q, whole_graph=False):
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
         backend = dist.get_backend()
         # the whole step, collectives included, in one graph (the default), or three graphs
-        dp = _run_steps(_trainer(dev, True, whole_graph))
+        dp = _run_steps(_trainer(dev, True, mode))
         single = _run_steps(_trainer(dev, False))
         dist.barrier()
         dist.destroy_process_group()
@@ -99,18 +102,22 @@ def _worker(port, q, whole_graph=False):
         q.put(("error", repr(e), traceback.format_exc(), None))
 
 
-@pytest.mark.parametrize("whole_graph", [False, True], ids=["three_graphs", "whole_step_graph"])
-def test_rccl_world1_data_parallel_step_equals_single_process(parity_report, whole_graph):
+@pytest.mark.parametrize("mode", ["three_graphs", "whole_step_graph", "sparse_exchange"])
+def test_rccl_world1_data_parallel_step_equals_single_process(parity_report, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_worker, args=(_free_port(), q, whole_graph))
+    p = ctx.Process(target=_worker, args=(_free_port(), q, mode))
     p.start()
     status, backend, dp, single = q.get(timeout=300)
     p.join(timeout=60)
     assert status == "ok", (backend, dp)
     assert p.exitcode == 0
-    assert backend == "nccl" and dp["dp"] and dp["nccl"] and not single["dp"]
-    assert dp["whole"] == whole_graph  # the graph phase replayed the whole-step graph
+    assert backend == "nccl" and dp["nccl"] and not single["dp"] and not single["xchg"]
+    if mode == "sparse_exchange":
+        assert dp["xchg"] and not dp["dp"]
+    else:
+        assert dp["dp"] and not dp["xchg"]
+        assert dp["whole"] == (mode == "whole_step_graph")  # the graph phase replayed the whole-step graph
     assert dp["steps"] == single["steps"] >= 8 and dp["scale"] == single["scale"]
     assert np.isfinite(dp["loss"]) and dp["loss"] == single["loss"]
     for ph in dp["phases"]:  # first phase where the runs part, and by how much
@@ -127,6 +134,6 @@ def test_rccl_world1_data_parallel_step_equals_single_process(parity_report, who
                               np.argwhere(ne)[:4].tolist())
     assert np.array_equal(dp["m"].view(np.uint32), single["m"].view(np.uint32))
     assert np.array_equal(dp["v"].view(np.uint32), single["v"].view(np.uint32))
-    parity_report(f"RCCL world 1 ZeRO-1 step ({'one graph per step' if whole_graph else 'three graphs'}): "
+    parity_report(f"RCCL world 1 data-parallel step ({mode}): "
                   f"{dp['steps']} optimizer steps, params / moments / density grid bit-identical to the "
                   f"single-process step, loss {dp['loss']:.6f}")

@@ -149,6 +149,10 @@ SIGNATURES = {
                                        c_vp, c_vp, c_vp],
     "ngp_density_grid_draw": [c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_sz, c_vp],
     "ngp_grid_encode_backward_fused_timing_offset": [c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32, c_vp],
+    "ngp_grad_exchange_bins": [ctypes.c_uint64],
+    "ngp_grad_exchange_words": [ctypes.c_uint64, c_u32],
+    "ngp_grad_exchange_list": [c_vp, ctypes.c_uint64, c_vp, c_vp, c_u32, c_vp],
+    "ngp_grad_exchange_reduce": [c_vp, c_i32, c_u32, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp],
     "ngp_grid_encode_backward_fused_reduce": [c_vp, c_vp, c_f32, c_vp, c_vp, c_u32, c_vp, c_u32, c_u32, c_u32,
                                               c_f32, c_u32, c_u32, c_i32, c_u32, c_vp, c_vp, c_sz, c_i32, c_vp,
                                               c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
@@ -168,6 +172,8 @@ _RESTYPES = {
     "ngp_ffmlp_image_bytes": c_sz,
     "ngp_density_grid_draw_workspace_bytes": c_sz,
     "ngp_density_grid_sort_workspace_bytes": c_sz,
+    "ngp_grad_exchange_bins": c_u32,
+    "ngp_grad_exchange_words": ctypes.c_uint64,
 }
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}

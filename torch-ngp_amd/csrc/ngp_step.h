@@ -13,7 +13,7 @@ struct StepState {
     float last_loss;       // mean loss of the last finished step
     float pad;
     int32_t growth_tracker;
-    int32_t found_inf;
+    int32_t found_inf;     // bit 0 inf/nan in the grads, bit 1 gradient exchange overflow (update skipped)
     int32_t adam_step;     // optimizer steps taken (skipped steps excluded)
     int32_t epoch;         // LambdaLR epoch (every step)
     int32_t iter;          // finished steps (k_step_end)
@@ -82,17 +82,21 @@ NGP_DEV void step_end_block(StepState* __restrict__ st, const ScalerArgs& sa, co
     }
     if (threadIdx.x != 0) return;
     if (loss_ray) st->loss_sum = part[0];
-    const bool inf = st->found_inf != 0;
+    // found_inf bit 0: an inf/nan (GradScaler backs off); bit 1: the replicated
+    // step's gradient exchange overflowed its lists (the update is skipped on
+    // every rank, the scale is left alone; csrc/exchange.hip)
+    const bool skip = st->found_inf != 0;
+    const bool inf = (st->found_inf & 1) != 0;
     if (sa.enabled) {
         if (inf) {
             st->scale *= sa.backoff_factor;
             st->growth_tracker = 0;
-        } else if (++st->growth_tracker == sa.growth_interval) {
+        } else if (!skip && ++st->growth_tracker == sa.growth_interval) {
             st->scale *= sa.growth_factor;
             st->growth_tracker = 0;
         }
     }
-    if (!inf) st->adam_step += 1;
+    if (!skip) st->adam_step += 1;
     st->epoch += 1;
     if (step_counter) {
         const int slot = st->iter % 16;

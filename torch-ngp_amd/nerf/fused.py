@@ -40,6 +40,7 @@ import torch.distributed as dist
 import _ngp_native as nat
 
 from .provider import LEGO_BOXES, LEGO_COLORS
+from .exchange import SparseExchange
 from .zero1 import ShardPlan
 
 _F16 = nat.DTYPE_CODE[torch.float16]
@@ -73,9 +74,12 @@ def _vp_array(ptrs):
 #   live_rows     the backwards walk the rows with a nonzero gradient only
 #   dp_graph      data parallel over RCCL: the whole step is one graph
 #   density_sort  partial density updates query their cells in brick order
+#   sparse_exchange  data parallel: every rank runs the world-1 step with the
+#                 full Adam, the gradients meet in a touched-entry exchange
+#                 (nerf/exchange.py) instead of the ZeRO-1 collectives
 DEFAULT_OPTIONS = dict(table16=False, split_head=False, split_reduce=False, split_fwd=False, split_bwd=False,
                        march_adam=True, tail_in_fwd=True, emit_inline=True, draw_ahead=True, live_rows=True,
-                       dp_graph=True, density_sort=True)
+                       dp_graph=True, density_sort=True, sparse_exchange=False)
 
 
 class FusedTrainer:
@@ -111,9 +115,12 @@ class FusedTrainer:
         self.growth_interval, self.seed = int(growth_interval), int(seed)
         self.density_seed = int(seed)  # the density-grid draws are the same on every rank
         # dp: the data-parallel (ZeRO-1) step with its collectives, also at
-        # world size 1 (a one-rank group runs the same RCCL calls)
-        self.dp = bool(distributed and dist.is_initialized())
-        self.world = dist.get_world_size() if self.dp else 1
+        # world size 1 (a one-rank group runs the same RCCL calls);
+        # sparse_exchange: the world-1 step on every rank + the exchange (xchg)
+        self._dist = bool(distributed and dist.is_initialized())
+        self.xchg = self._dist and opts["sparse_exchange"]
+        self.dp = self._dist and not self.xchg
+        self.world = dist.get_world_size() if self._dist else 1
         if self.world > 1:
             self.seed += 7919 * dist.get_rank()
         self.enc = enc
@@ -149,9 +156,10 @@ class FusedTrainer:
         # collective each
         self.params = [enc.embeddings, self.sig_net.weights, self.col_net.weights]
         sizes = [p.numel() for p in self.params]
-        self.rank = dist.get_rank() if self.dp else 0
-        # ZeRO-1 layout (nerf/zero1.py): 8-aligned tensors, a 64-aligned chunk per rank
-        self.plan = plan = ShardPlan(sizes, self.world, self.rank)
+        self.rank = dist.get_rank() if self._dist else 0
+        # ZeRO-1 layout (nerf/zero1.py): 8-aligned tensors, a 64-aligned chunk
+        # per rank (sparse_exchange: every rank owns everything)
+        self.plan = plan = ShardPlan(sizes, 1, 0) if self.xchg else ShardPlan(sizes, self.world, self.rank)
         starts = plan.starts + [plan.used]
         self.chunk = chunk = plan.chunk
         self.total = total = plan.total
@@ -249,11 +257,14 @@ class FusedTrainer:
             half=_vp_array([nat.ptr(self.flat_half) + 2 * (self.lo + a) if hv else None for a, _, hv in sec]),
             sizes=(ctypes.c_uint64 * len(sec))(*[n for _, n, _ in sec]),
             n=len(sec))
-        self._nccl = self.dp and dist.get_backend() == "nccl"
+        self._nccl = self._dist and dist.get_backend() == "nccl"
         # GradScaler's inf check is made by the kernels that write the grads
         # (grid backward, MLP dW reduce) into this flag: the optimizer's found-inf
         # flag (world 1) or the data-parallel guard's per-rank flag
         self._inf_flag = nat.lib().ngp_fused_inf_flag(nat.ptr(self.state), int(self.dp))
+        # sparse_exchange: the averaged gradient of every rank's batch replaces
+        # this rank's after each backward (the optimizer reads the flag above)
+        self._xchg = SparseExchange(self.flat_grad, self._inf_flag, self.world, self._nccl) if self.xchg else None
         # World 1: the pending Adam rides in the march launch (its workgroups'
         # Adam waves stream the parameters while the march waves probe the
         # occupancy image); the step head then only draws the batch.
@@ -407,7 +418,7 @@ class FusedTrainer:
         nat.check(lib.ngp_nerf_density_forward(P_(d["enc"]), P_(self.w_half[1]), None, n, sn.input_dim, sn.hidden_dim,
                                                sn.num_layers, float(m.density_scale), P_(d["idx"]) + 4 * lo,
                                                P_(d["tmp"]), s), "nerf_density_forward")
-        if self.dp:
+        if self._dist:
             if self._nccl:
                 dist.all_reduce(d["tmp"], op=dist.ReduceOp.MAX)
             else:
@@ -632,6 +643,15 @@ class FusedTrainer:
                 self._sample()
             self._march()
         self._network(draw=self._draw_ahead, adam_split=pending and self._march_adam)
+
+    def _xbody(self, pending, graph=False):
+        """The world-1 body, and with sparse_exchange the gradient exchange
+        after it (RCCL: in the same graph; gloo stages through the host, so a
+        graph holds the body only and step() runs the exchange after it)."""
+        self._body(pending)
+        if self._xchg is not None and (self._nccl or not graph):
+            self._xchg()
+            self._tick("grad_exchange")
 
     def _optimizer_head(self):
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
@@ -944,6 +964,8 @@ class FusedTrainer:
         """One training iteration (the optimizer half lags by one step, see
         the module docstring)."""
         if not self.dp:
+            # gloo: the graphs hold the body only, the exchange runs here
+            host_x = self._xchg is not None and not self._nccl
             if self._ring and self._pending:  # timing ring: graphs with event nodes
                 self._ring[self._ring_i % len(self._ring)][0].replay()
                 self._ring_i += 1
@@ -952,8 +974,11 @@ class FusedTrainer:
             elif self._fresh is not None and not self._pending and self._ahead:
                 self._fresh.replay()  # captured with the batch drawn ahead; leaves it drawn ahead
             else:
-                self._body(self._pending)
+                self._xbody(self._pending)
                 self.eager_steps += 1
+                host_x = False
+            if host_x:
+                self._xchg()
         elif self._dp_whole is not None and self._pending and self._ahead == self._pre_ahead:
             self._dp_whole.replay()  # the whole step, collectives included (dp_graph)
         else:
@@ -1034,7 +1059,7 @@ class FusedTrainer:
                     self._events, self._capturing = [], True
                     with torch.cuda.graph(g):
                         self._tick("start")
-                        self._body(True)
+                        self._xbody(True, graph=True)
                     self._ring.append((g, self._events))
             except Exception:
                 self._ring = []
@@ -1046,7 +1071,7 @@ class FusedTrainer:
             self._ring, self._ring_i = [], 0  # step() would replay an older timing ring first
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
-                self._body(True)
+                self._xbody(True, graph=True)
             # ... and the body of the first step after a flush (no update
             # pending, the batch drawn ahead by the last backward): so a
             # training loop's flush points (density updates, read-outs) cost no
@@ -1055,14 +1080,14 @@ class FusedTrainer:
             if self._draw_ahead and self._ahead:
                 gf = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gf):
-                    self._body(False)
+                    self._xbody(False, graph=True)
                 self._fresh = gf
             self.graph_multi, self._multi = None, 1
-            if multi > 1:
+            if multi > 1 and (self._xchg is None or self._nccl):
                 gm = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gm):
                     for _ in range(multi):
-                        self._body(True)
+                        self._xbody(True, graph=True)
                 self.graph_multi, self._multi = gm, multi
         elif self._dp_graph and self._nccl:
             # the whole data-parallel step in one graph, the collectives on
@@ -1161,6 +1186,29 @@ class FusedTrainer:
         if clear and v:
             w.zero_()
         return v
+
+    def fit_exchange(self, margin=2.0):
+        """sparse_exchange: size the touched-entry lists to margin x the
+        longest list since the last fit (nerf/exchange.py), for the steady
+        regime of training (the default lists hold every pair and cannot
+        overflow); graphs captured before are captured again. Call it at the
+        same step on every rank. Returns the lists' capacity."""
+        if self._xchg is None:
+            return None
+        cap = self._xchg.fit(margin)
+        if self.graph is not None or self._ring:
+            ring, multi = len(self._ring), self._multi
+            self.capture(warmup=0, multi=multi)
+            if ring:  # (the plain capture drops the timing ring)
+                self.capture(warmup=0, ring=ring)
+        return cap
+
+    @property
+    def exchange_overflows(self):
+        """sparse_exchange: steps whose update every rank skipped because some
+        rank's touched-entry list was longer than the lists' capacity (0 when
+        every step applied its update; a host read). None otherwise."""
+        return self._xchg.overflows if self._xchg is not None else None
 
     # ------------------------------------------------------ checkpoints
     # StepState as int32 words: 0 scale (f32), 4 growth tracker, 6 Adam steps,
