@@ -700,10 +700,18 @@ int ngp_density_grid_points_sorted(const int32_t* coords, const float* noise, ui
 int ngp_nerf_density_forward(const void* inputs, const void* weights, const void* image, uint32_t B,
                              uint32_t in_dim, uint32_t hidden_dim, uint32_t num_layers, float density_scale,
                              const int32_t* indices, float* tmp_grid, void* stream);
+/* The same densities stored per row, sigma[b] (no index, no atomic): the full
+ * update's Morton-ordered queries (row = cell) and the brick-ordered partial
+ * queries (then ngp_density_grid_run_max). 32 inputs, image required. */
+int ngp_nerf_density_forward_rows(const void* inputs, const void* image, uint32_t B, uint32_t hidden_dim,
+                                  uint32_t num_layers, float density_scale, float* sigma, void* stream);
 /* EMA (renderer.py:582-583: where grid >= 0 and tmp >= 0, grid = max(grid *
  * decay, tmp)), tmp reset to -1, stats[0] = sum(clamp(grid, 0)) as a double
  * (mean_density = float(stats[0] / (C H^3)), :584), and the bitfield at
- * min(mean_density, density_thresh) (:589-590), all on the device. */
+ * min(mean_density, density_thresh) (:589-590), all on the device. stats:
+ * NGP_DENSITY_STATS_LEN doubles (the sum, then per-block partial sums added
+ * in a fixed order: no atomics, no clear). */
+#define NGP_DENSITY_STATS_LEN 1025
 int ngp_density_grid_ema_pack(float* grid, float* tmp_grid, uint32_t C, uint32_t H, float decay,
                               double density_thresh, double* stats, uint8_t* bitfield, void* stream);
 /* Device-side draws of an update (no host sync, graph-capturable): partial=0:
@@ -716,6 +724,34 @@ size_t ngp_density_grid_draw_workspace_bytes(uint32_t C, uint32_t H);
 int ngp_density_grid_draw(const float* grid, uint32_t C, uint32_t H, uint32_t partial, uint32_t seed,
                           uint32_t update, int32_t* coords, float* noise, void* ws, size_t ws_bytes,
                           void* stream);
+/* A partial update's draws for the fused trainer, generated in Morton order:
+ * per cascade N = H^3/4 uniform cells and N cells out of the occupied list
+ * (grid > 0), i.i.d. with replacement as the reference draws them
+ * (renderer.py:548-558), made as uniform order statistics (prefix sums of N+1
+ * exponentials from the counter RNG, exact 2^-32 fixed point), so each half's
+ * cells come out sorted by Morton code with no sort; the points [lo, hi) of
+ * the C * 2N draws (cascade-major, uniform half first) are written to xyzs /
+ * indices [0, hi - lo) with k_density_points' arithmetic. H a power of two.
+ * draw_ws: ngp_density_grid_draw_workspace_bytes; ostat_ws:
+ * ngp_density_grid_ostat_workspace_bytes. */
+size_t ngp_density_grid_ostat_workspace_bytes(uint32_t C, uint32_t H);
+int ngp_density_grid_draw_sorted(const float* grid, uint32_t C, uint32_t H, uint32_t seed, uint32_t update,
+                                 float bound, uint32_t lo, uint32_t hi, void* draw_ws, size_t draw_ws_bytes,
+                                 void* ostat_ws, size_t ostat_ws_bytes, float* xyzs, int32_t* indices, void* stream);
+/* tmp_grid from the densities sigma[0, hi - lo) of ngp_density_grid_draw_sorted's
+ * points [lo, hi): a cell's draws are adjacent within a half, so each run's
+ * max is stored by its first point (uniform halves), then folded in with
+ * max (occupied halves, a second launch): no global atomics. tmp_grid holds
+ * -1 where nothing was drawn (as the EMA leaves it). */
+int ngp_density_grid_run_max(const float* sigma, const int32_t* indices, uint32_t C, uint32_t H, uint32_t lo,
+                             uint32_t hi, float* tmp_grid, void* stream);
+/* mean_count after an update (renderer.py:593-595: int(mean of the last
+ * min(16, local_step) batches' sample counts)) on the device: *out = floor(sum
+ * / total) over the fused trainer's step-counter ring (int32 [16][2], slot =
+ * batch % 16; *draw = batches drawn; ahead: the newest batch is in the ring,
+ * else in counter[0]). */
+int ngp_density_mean_count(const int32_t* step_counter, const int32_t* draw, const int32_t* counter,
+                           uint32_t total, uint32_t ahead, int64_t* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -158,7 +158,7 @@ def test_fused_density_stages_match_reference(cuda, tag, bound, thresh):
     grid = torch.from_numpy(f[f"{tag}_marked"]).to(cuda).contiguous()
     bits = torch.zeros(C * H3 // 8, dtype=torch.uint8, device=cuda)
     tmp = torch.full((C, H3), -1.0, device=cuda)
-    stats = torch.zeros(1, dtype=torch.float64, device=cuda)
+    stats = torch.zeros(nat.DENSITY_STATS_LEN, dtype=torch.float64, device=cuda)
     s = nat.stream_of(grid)
     cen = torch.tensor([0.15, -0.1, 0.05], device=cuda) * bound
     for u in range(4):
@@ -196,7 +196,7 @@ def test_fused_density_stages_match_reference(cuda, tag, bound, thresh):
         torch.cuda.synchronize()
         ref = f[f"{tag}_u{u}_grid"]
         np.testing.assert_allclose(grid.cpu().numpy(), ref, rtol=RTOL, atol=1e-30)
-        md = float(np.float32(stats.item() / grid.numel()))
+        md = float(np.float32(stats[0].item() / grid.numel()))
         assert abs(md - float(f[f"{tag}_u{u}_mean_density"])) <= RTOL * md
         assert _bits_match(bits.cpu().numpy(), f[f"{tag}_u{u}_bitfield"], ref, min(md, thresh)), u
         assert float(tmp.max()) == -1.0  # the EMA launch resets the scratch grid

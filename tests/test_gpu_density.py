@@ -219,6 +219,45 @@ def _draws(seed, update, P, ppc, H, grid=None):
     return coords, noise
 
 
+def _exp_fixed(r):
+    """csrc/density_grid.hip exp_fixed: -ln(u) of u = ((r >> 8) + 1) / 2^24 in
+    2^-32 fixed point, the same IEEE double operations in the same order."""
+    v = (np.asarray(r, np.uint32) >> np.uint32(8)).astype(np.uint64) + np.uint64(1)
+    e = np.array([int(x).bit_length() - 1 for x in v.ravel()], np.int64).reshape(v.shape)
+    m = v.astype(np.float64) / np.exp2(e.astype(np.float64))
+    s = (m - 1.0) / (m + 1.0)
+    s2 = s * s
+    q = np.full_like(s, 1.0 / 15.0)
+    for c in (1.0 / 13.0, 1.0 / 11.0, 1.0 / 9.0, 1.0 / 7.0, 1.0 / 5.0, 1.0 / 3.0, 1.0):
+        q = q * s2 + c
+    lnm = 2.0 * s * q
+    E = (24 - e).astype(np.float64) * 0.6931471805599453 - lnm
+    return np.where(E > 0, (np.maximum(E, 0) * 4294967296.0).astype(np.uint64), np.uint64(0))
+
+
+def _draws_ostat(seed, update, C, H, grid):
+    """ngp_density_grid_draw_sorted's draws (cells per point, uniform half then
+    occupied half per cascade) restated in numpy: uniform order statistics
+    S_k / S_N from the prefix sums of N + 1 fixed-point exponentials."""
+    seed = np.uint32(seed ^ DENSITY_RNG_DOMAIN)
+    H3, N = H ** 3, H ** 3 // 4
+    j = np.arange(N + 1, dtype=np.uint32)
+    cells = []
+    for cas in range(C):
+        occ = np.nonzero(grid[cas] > 0)[0].astype(np.int64)
+        for half in range(2):
+            E = _exp_fixed(_rng_u32(seed, update, j, 16 + 2 * cas + half))
+            S = np.cumsum(E, dtype=np.uint64)
+            t = S[:N].astype(np.float64) / np.float64(S[N])
+            if half and occ.size:
+                cells.append(occ[np.minimum(np.floor(t * occ.size), occ.size - 1).astype(np.int64)])
+            else:
+                cells.append(np.minimum(np.floor(t * H3), H3 - 1).astype(np.int64))
+    cells = np.concatenate(cells)
+    _, noise = _draws(int(seed ^ np.uint32(DENSITY_RNG_DOMAIN)), update, C * 2 * N, 2 * N, H)
+    return oracle.morton3D_invert(cells.astype(np.int32)).astype(np.int32), noise, cells
+
+
 @torch.no_grad()
 def _torch_update_from(m, coords, noise, ppc, decay=0.95):
     """The reference update (:524-590) from given cells and noise (torch ops on
@@ -243,13 +282,17 @@ def _torch_update_from(m, coords, noise, ppc, decay=0.95):
                                               m.density_bitfield)
 
 
-@pytest.mark.parametrize("bound", [1, 2])
-def test_fused_update_density_matches_restatement(cuda, bound):
+@pytest.mark.parametrize("bound,ordered", [(1, True), (2, True), (1, False)], ids=["b1", "b2", "b1_draw_order"])
+def test_fused_update_density_matches_restatement(cuda, bound, ordered):
+    """Full updates (every cell, Morton-ordered queries) and partial ones: the
+    Morton-ordered order-statistics draws (density_sort, default) or the
+    counter-RNG draws in draw order, restated in numpy, through the
+    reference's update on the model's autograd density path."""
     from nerf.fused import FusedTrainer
     from nerf.provider import SyntheticLego
     a = _model(cuda, bound=bound)
     b = copy.deepcopy(a)
-    ft = FusedTrainer(a, SyntheticLego(cuda, num_rays=256), M=20000, seed=5)
+    ft = FusedTrainer(a, SyntheticLego(cuda, num_rays=256), M=20000, seed=5, options=dict(density_sort=ordered))
     H, C = a.grid_size, a.cascade
     allc = torch.stack(torch.meshgrid(*[torch.arange(H, dtype=torch.int32, device=cuda)] * 3, indexing="ij"),
                        -1).reshape(-1, 3).repeat(C, 1)
@@ -260,11 +303,16 @@ def test_fused_update_density_matches_restatement(cuda, bound):
         pre = b.density_grid.cpu().numpy()
         ft.update_density()
         ppc = H ** 3 // 2 if partial else H ** 3
-        coords, noise = _draws(5, a.iter_density - 1, C * ppc, ppc, H, pre if partial else None)
         d = ft._dens
-        np.testing.assert_array_equal(d["noise"][:C * ppc].cpu().numpy(), noise)
-        if partial:
-            np.testing.assert_array_equal(d["coords"][:C * ppc].cpu().numpy(), coords)
+        if partial and ordered:
+            coords, noise, cells = _draws_ostat(5, a.iter_density - 1, C, H, pre)
+            idx = (np.repeat(np.arange(C), ppc) * H ** 3 + cells).astype(np.int32)
+            np.testing.assert_array_equal(d["idx"][:C * ppc].cpu().numpy(), idx)  # the draws, bit for bit
+        else:
+            coords, noise = _draws(5, a.iter_density - 1, C * ppc, ppc, H, pre if partial else None)
+            np.testing.assert_array_equal(d["noise"][:C * ppc].cpu().numpy(), noise)
+            if partial:
+                np.testing.assert_array_equal(d["coords"][:C * ppc].cpu().numpy(), coords)
         with torch.autocast("cuda", dtype=torch.float16):
             _torch_update_from(b, torch.from_numpy(coords).to(cuda) if partial else allc,
                                torch.from_numpy(noise).to(cuda), ppc)
@@ -318,22 +366,71 @@ def test_sorted_points_are_a_permutation_in_brick_order(cuda, C, H):
         assert np.all(np.diff(bucket) >= 0)
 
 
-def test_fused_partial_update_sorted_equals_draw_order(cuda):
-    """A partial update with the brick-ordered query (default) leaves the same
-    density grid, mean and bitfield as the draw-order query, bit for bit."""
+@pytest.mark.parametrize("C,H", [(1, 32), (2, 16)])
+def test_ordered_draws_slices_and_statistics(cuda, C, H):
+    """ngp_density_grid_draw_sorted: two slices [0, s) + [s, P) (the
+    data-parallel split) give the numpy restatement's points bit for bit
+    (xyz and index); each half's cells are in Morton order; the occupied half
+    draws only occupied cells; over many updates the uniform half's cells are
+    uniform (chi-square over 64 Morton blocks)."""
+    import _ngp_native as nat
+    from scipy import stats
+    lib, P_ = nat.lib(), nat.ptr
+    H3, N = H ** 3, H ** 3 // 4
+    P = C * 2 * N
+    g = torch.Generator(device="cpu").manual_seed(C * 10 + H)
+    grid = (torch.rand(C, H3, generator=g) - 0.7).to(cuda)  # ~30 % occupied
+    dws = torch.zeros(int(lib.ngp_density_grid_draw_workspace_bytes(C, H)), dtype=torch.uint8, device=cuda)
+    ows = torch.zeros(int(lib.ngp_density_grid_ostat_workspace_bytes(C, H)), dtype=torch.uint8, device=cuda)
+    xyz, idx = torch.zeros(P, 3, device=cuda), torch.zeros(P, dtype=torch.int32, device=cuda)
+    s = nat.stream_of(xyz)
+    split = P // 3 + 5
+    counts = np.zeros(64)
+    for upd in range(8):
+        for lo, hi in ((0, split), (split, P)):
+            nat.check(lib.ngp_density_grid_draw_sorted(P_(grid), C, H, 9, upd, 1.0, lo, hi, P_(dws), dws.numel(),
+                                                       P_(ows), ows.numel(), P_(xyz) + 12 * lo, P_(idx) + 4 * lo, s),
+                      "draw_sorted")
+        torch.cuda.synchronize()
+        got = idx.cpu().numpy()
+        coords, noise, cells = _draws_ostat(9, upd, C, H, grid.cpu().numpy())
+        np.testing.assert_array_equal(got, (np.repeat(np.arange(C), 2 * N) * H3 + cells).astype(np.int32))
+        if upd == 0:
+            want, wi = torch.zeros(P, 3, device=cuda), torch.zeros(P, dtype=torch.int32, device=cuda)
+            tc, tn = torch.from_numpy(coords).to(cuda), torch.from_numpy(noise).to(cuda)  # (held: the pointers outlive P_)
+            nat.check(lib.ngp_density_grid_points(P_(tc), P_(tn), P, 2 * N, C, H, 1.0, P_(want), P_(wi), s), "points")
+            torch.cuda.synchronize()
+            assert torch.equal(xyz, want)  # k_density_points' arithmetic, bit for bit
+        for cas in range(C):
+            u, o = cells[cas * 2 * N:cas * 2 * N + N], cells[cas * 2 * N + N:(cas + 1) * 2 * N]
+            assert np.all(np.diff(u) >= 0) and np.all(np.diff(o) >= 0)
+            assert np.all(grid[cas].cpu().numpy()[o] > 0)
+            counts += np.bincount(u * 64 // H3, minlength=64)
+    assert stats.chisquare(counts).pvalue > 1e-3
+
+
+def test_fused_mean_count_kernel_matches_the_ring(cuda):
+    """ngp_density_mean_count (the update's mean_count bookkeeping in one
+    launch) equals int(mean) of the last `total` batches' counts gathered from
+    the step-counter ring with torch ops (FusedTrainer._recent_counts), with
+    the next batch drawn ahead and not, for every total in 1..16."""
     from nerf.fused import FusedTrainer
     from nerf.provider import SyntheticLego
     a = _model(cuda, bound=1)
-    b = copy.deepcopy(a)
-    fa = FusedTrainer(a, SyntheticLego(cuda, num_rays=256), M=20000, seed=5)
-    fb = FusedTrainer(b, SyntheticLego(cuda, num_rays=256), M=20000, seed=5)
-    fb._dens_sorted = False
-    for it in range(4):
-        if it == 2:
-            a.iter_density = b.iter_density = 16
-        fa.update_density()
-        fb.update_density()
+    ft = FusedTrainer(a, SyntheticLego(cuda, num_rays=256), M=20000, seed=3)
+    ft._dens = dict(mean_count=torch.zeros(1, dtype=torch.int64, device=cuda))
+    seen = set()
+    for it in range(20):
+        ft.step()
         torch.cuda.synchronize()
-        assert torch.equal(a.density_grid, b.density_grid)
-        assert fa.mean_density == fb.mean_density
-        assert torch.equal(a.density_bitfield, b.density_bitfield)
+        for total in range(1, 17):
+            want = int(ft._recent_counts(total).sum().item()) // total
+            assert int(ft._recent_count_mean(total).item()) == want, (it, total, ft._ahead)
+        seen.add(ft._ahead)
+    ft.flush()
+    ft._sample()  # a batch drawn by the head: not ahead
+    torch.cuda.synchronize()
+    for total in range(1, 17):
+        assert int(ft._recent_count_mean(total).item()) == int(ft._recent_counts(total).sum().item()) // total
+    seen.add(ft._ahead)
+    assert seen == {True, False}

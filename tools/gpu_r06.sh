@@ -11,7 +11,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_grid_fused.py tests/test_de
     tests/test_gpu_e2e_oracle.py -v --timeout 120 --timeout-method thread > $O/first.log 2>&1
 rc=$?; echo "first: rc $rc $(tail -1 $O/first.log)"
 [ $rc -gt 1 ] && exit $rc
-timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "gpu: rc $rc $(tail -1 $O/pytest_gpu.log)"
 [ $rc -gt 1 ] && exit $rc
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1

@@ -148,6 +148,12 @@ SIGNATURES = {
     "ngp_density_grid_points_sorted": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_u32, c_vp, c_sz,
                                        c_vp, c_vp, c_vp],
     "ngp_density_grid_draw": [c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_sz, c_vp],
+    "ngp_density_mean_count": [c_vp, c_vp, c_vp, c_u32, c_u32, c_vp, c_vp],
+    "ngp_nerf_density_forward_rows": [c_vp, c_vp, c_u32, c_u32, c_u32, c_f32, c_vp, c_vp],
+    "ngp_density_grid_run_max": [c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp],
+    "ngp_density_grid_ostat_workspace_bytes": [c_u32, c_u32],
+    "ngp_density_grid_draw_sorted": [c_vp, c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_u32, c_vp, c_sz, c_vp, c_sz,
+                                     c_vp, c_vp, c_vp],
     "ngp_grid_encode_backward_fused_timing_offset": [c_u32, c_u32, c_u32, c_u32, c_f32, c_u32, c_i32, c_vp],
     "ngp_grad_exchange_bins": [ctypes.c_uint64],
     "ngp_grad_exchange_words": [ctypes.c_uint64, c_u32],
@@ -172,11 +178,13 @@ _RESTYPES = {
     "ngp_ffmlp_image_bytes": c_sz,
     "ngp_density_grid_draw_workspace_bytes": c_sz,
     "ngp_density_grid_sort_workspace_bytes": c_sz,
+    "ngp_density_grid_ostat_workspace_bytes": c_sz,
     "ngp_grad_exchange_bins": c_u32,
     "ngp_grad_exchange_words": ctypes.c_uint64,
 }
 
 DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.float64: 2}
+DENSITY_STATS_LEN = 1025  # include/ngp_hip.h NGP_DENSITY_STATS_LEN (doubles of ngp_density_grid_ema_pack's stats)
 
 
 class AdamJob(ctypes.Structure):

@@ -137,9 +137,12 @@ NGP_DEV float torch_maximum(float a, float b) {  // torch.maximum: NaN propagate
 
 constexpr uint32_t kEmaThreads = 256;
 
+// per-block partial sums (fixed order, no atomics) that k_density_pack adds up
+constexpr uint32_t kEmaMaxBlocks = 1024;
+
 __global__ void __launch_bounds__(kEmaThreads)
 k_density_ema(float* __restrict__ grid, float* __restrict__ tmp, uint32_t n, float decay,
-              double* __restrict__ sum) {
+              double* __restrict__ partial) {
     __shared__ double wsum[kEmaThreads / 64];
     double acc = 0.0;
     for (uint32_t i = blockIdx.x * kEmaThreads + threadIdx.x; i < n; i += gridDim.x * kEmaThreads) {
@@ -160,7 +163,7 @@ k_density_ema(float* __restrict__ grid, float* __restrict__ tmp, uint32_t n, flo
         double b = 0.0;
 #pragma unroll
         for (uint32_t w = 0; w < kEmaThreads / 64; ++w) b += wsum[w];
-        atomicAdd(sum, b);
+        partial[blockIdx.x] = b;
     }
 }
 
@@ -168,11 +171,23 @@ k_density_ema(float* __restrict__ grid, float* __restrict__ tmp, uint32_t n, flo
 // torch.mean(...).item() of the fp32 grid (a float32 value), compared with
 // the Python float density_thresh in double; the winner is cast to float.
 __global__ void __launch_bounds__(256)
-k_density_pack(const float* __restrict__ grid, uint32_t nbytes, uint32_t n, const double* __restrict__ sum,
-               double density_thresh, uint8_t* __restrict__ bitfield) {
+k_density_pack(const float* __restrict__ grid, uint32_t nbytes, uint32_t n, const double* __restrict__ partial,
+               uint32_t nparts, double density_thresh, uint8_t* __restrict__ bitfield, double* __restrict__ stats) {
+    // every block adds the EMA's partial sums up in the same order
+    __shared__ double s_sum[256];
+    double acc = 0.0;
+    for (uint32_t i = threadIdx.x; i < nparts; i += 256) acc += partial[i];
+    s_sum[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) s_sum[threadIdx.x] += s_sum[threadIdx.x + o];
+        __syncthreads();
+    }
+    const double sum = s_sum[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) stats[0] = sum;
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nbytes) return;
-    const double mean = (double)(float)(*sum / (double)n);
+    const double mean = (double)(float)(sum / (double)n);
     const float thresh = (float)(mean < density_thresh ? mean : density_thresh);
     const float4* g = reinterpret_cast<const float4*>(grid + (size_t)b * 8);
     const float4 a = g[0], c = g[1];
@@ -273,30 +288,40 @@ constexpr uint32_t kDensityRngDomain = 0xd3a5b1c7u;
 // partial mode per cascade N = ppc / 2 uniform cells, then N cells drawn from
 // the occupied list (uniform cells again where the cascade has none, as the
 // reference's occ[randint(0, 0)] cannot), each with its noise.
+struct PartialDraw {
+    uint32_t ppc, H, seed, update;  // seed: already XORed with kDensityRngDomain
+    const uint32_t* occ;            // occupied cells of each cascade, cell order
+    const uint32_t* total;          // their counts
+};
+
+// The cell of partial-update point p (a pure function of the counter RNG and
+// the occupied list, so the sorted query regenerates it instead of storing it)
+NGP_DEV void partial_cell(const PartialDraw& d, uint32_t p, uint32_t c[3]) {
+    const uint32_t cas = p / d.ppc, k = p - cas * d.ppc, half = d.ppc / 2;
+    const uint32_t n_occ = d.total[cas];
+    if (k >= half && n_occ > 0) {
+        const uint32_t cell = d.occ[(size_t)cas * d.H * d.H * d.H + rng_u32(d.seed, d.update, p, 7) % n_occ];
+        c[0] = compact_bits(cell);
+        c[1] = compact_bits(cell >> 1);
+        c[2] = compact_bits(cell >> 2);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c[j] = rng_u32(d.seed, d.update, p, 8 + j) % d.H;
+    }
+}
+
 __global__ void __launch_bounds__(256)
-k_density_draw(uint32_t P, uint32_t ppc, uint32_t H, uint32_t seed, uint32_t update,
-               const uint32_t* __restrict__ occ, const uint32_t* __restrict__ total,
-               int32_t* __restrict__ coords, float* __restrict__ noise) {
+k_density_draw(uint32_t P, PartialDraw d, bool partial, int32_t* __restrict__ coords, float* __restrict__ noise) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
-    if (occ) {
-        const uint32_t cas = p / ppc, k = p - cas * ppc, half = ppc / 2;
-        const uint32_t n_occ = total[cas];
+    if (partial) {
         uint32_t c[3];
-        if (k >= half && n_occ > 0) {
-            const uint32_t cell = occ[(size_t)cas * H * H * H + rng_u32(seed, update, p, 7) % n_occ];
-            c[0] = compact_bits(cell);
-            c[1] = compact_bits(cell >> 1);
-            c[2] = compact_bits(cell >> 2);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) c[j] = rng_u32(seed, update, p, 8 + j) % H;
-        }
+        partial_cell(d, p, c);
 #pragma unroll
         for (int j = 0; j < 3; ++j) coords[(size_t)p * 3 + j] = (int32_t)c[j];
     }
 #pragma unroll
-    for (int j = 0; j < 3; ++j) noise[(size_t)p * 3 + j] = rng_unit(seed, update, p, 1 + j);
+    for (int j = 0; j < 3; ++j) noise[(size_t)p * 3 + j] = rng_unit(d.seed, d.update, p, 1 + j);
 }
 
 // ---- partial-update points in brick order ----------------------------------------
@@ -422,16 +447,206 @@ k_density_sort_scatter(const int32_t* __restrict__ coords, const float* __restri
 
 // shift and buckets per cascade: bricks of >= 2^9 cells, at most
 // kSortMaxBuckets buckets over the cascades
-static SortPlan sort_plan(uint32_t C, uint32_t H, uint32_t ppc, uint32_t lo, uint32_t n) {
+static SortPlan sort_plan(uint32_t C, uint32_t H, uint32_t ppc, uint32_t lo, uint32_t n, uint32_t min_shift = 9) {
     uint32_t bits = 0;
     while ((1u << bits) < H) ++bits;
     const uint32_t mbits = 3 * bits;  // Morton codes of the cube are < 2^mbits
-    uint32_t shift = std::min<uint32_t>(9, mbits);
+    uint32_t shift = std::min<uint32_t>(min_shift, mbits);
     while (shift < mbits && (size_t)C << (mbits - shift) > kSortMaxBuckets) ++shift;
     return SortPlan{lo, n, ppc, H, shift, 1u << (mbits - shift)};
 }
 
+// ---- partial-update draws generated in Morton order (the fused trainer) ---------
+// A partial update draws, per cascade, N = H^3/4 uniform cells and N cells
+// out of the occupied list, i.i.d. with replacement (renderer.py:548-558).
+// tmp_grid is a max over the points, so only the multiset of draws matters,
+// and the same multiset comes out sorted when each half's draws are made as
+// uniform order statistics: U_(k) = S_k / S_N with S_k the prefix sums of N+1
+// i.i.d. exponentials (Renyi). The uniform half's cell is then the Morton code
+// floor(U_(k) H^3) and the occupied half's the occupied cell floor(U_(k) n_occ)
+// (the list is in Morton order), so both halves come out in Morton order: the
+// query's waves read neighbouring cells, as the full update's do, with no sort.
+// Reproducible bit for bit (tests restate it in numpy): the exponentials come
+// from the counter RNG through a fixed double-precision log (no libm) and are
+// summed in 2^-32 fixed point (exact, any order); t and the cells in double.
+constexpr uint32_t kOstatThreads = 256, kOstatPer = 4, kOstatChunk = kOstatThreads * kOstatPer;
+constexpr uint32_t kOstatStream = 16;  // RNG streams 16 + 2 cascade + half (the draws' own: 1..10)
+
+// -ln(u), u = (r >> 8 + 1) / 2^24, as 2^-32 fixed point: ln(v) of the integer
+// v = 2^e m (m in [1, 2)) by the atanh series of s = (m - 1) / (m + 1), Horner
+// in s^2, every operation a plain IEEE double one (-ffp-contract=off)
+NGP_DEV uint64_t exp_fixed(uint32_t r) {
+    const uint32_t v = (r >> 8) + 1u;                 // [1, 2^24]
+    const int e = 31 - __clz(v);
+    const double m = (double)v / (double)(1u << e);  // exact
+    const double s = (m - 1.0) / (m + 1.0);
+    const double s2 = s * s;
+    double q = 1.0 / 15.0;
+    q = q * s2 + 1.0 / 13.0;
+    q = q * s2 + 1.0 / 11.0;
+    q = q * s2 + 1.0 / 9.0;
+    q = q * s2 + 1.0 / 7.0;
+    q = q * s2 + 1.0 / 5.0;
+    q = q * s2 + 1.0 / 3.0;
+    q = q * s2 + 1.0;
+    const double lnm = 2.0 * s * q;
+    const double E = (double)(24 - e) * 0.6931471805599453 - lnm;  // -ln(v / 2^24) >= 0
+    return E > 0.0 ? (uint64_t)(E * 4294967296.0) : 0ull;
+}
+
+struct Ostat {
+    uint32_t C, H, N, seed, update;  // N = draws per half; seed already XORed with the domain
+    const uint32_t* occ;
+    const uint32_t* total;
+};
+
+// exponential j of segment g = 2 cascade + half (j in [0, N])
+NGP_DEV uint64_t ostat_exp(const Ostat& o, uint32_t g, uint32_t j) {
+    return exp_fixed(rng_u32(o.seed, o.update, j, kOstatStream + g));
+}
+
+// Each block sums one chunk of a segment's N + 1 exponentials.
+__global__ void __launch_bounds__(kOstatThreads)
+k_ostat_sums(Ostat o, uint32_t chunks, unsigned long long* __restrict__ sums) {
+    const uint32_t g = blockIdx.x / chunks, ch = blockIdx.x - g * chunks;
+    unsigned long long acc = 0;
+    for (uint32_t i = 0; i < kOstatPer; ++i) {
+        const uint32_t j = ch * kOstatChunk + i * kOstatThreads + threadIdx.x;
+        if (j <= o.N) acc += ostat_exp(o, g, j);
+    }
+#pragma unroll
+    for (uint32_t off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    __shared__ unsigned long long w[kOstatThreads / 64];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) sums[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
+}
+
+// Each block: its chunk's prefix sums (the earlier chunks' sums + a block scan,
+// exact integers), then its points k < N of the segment that fall in
+// [lo, hi): cell, k_density_points' xyz arithmetic, index; in point order.
+__global__ void __launch_bounds__(kOstatThreads)
+k_ostat_points(Ostat o, uint32_t chunks, const unsigned long long* __restrict__ sums, uint32_t lo, uint32_t hi,
+               CascadeScales cs, float* __restrict__ xyzs, int32_t* __restrict__ indices) {
+    const uint32_t g = blockIdx.x / chunks, ch = blockIdx.x - g * chunks;
+    const uint32_t cas = g >> 1, half = g & 1, ppc = 2 * o.N;
+    const uint32_t p0 = cas * ppc + half * o.N;  // the segment's first point
+    const uint32_t k0 = ch * kOstatChunk;
+    if (p0 + k0 >= hi || p0 + min(k0 + kOstatChunk, o.N) <= lo) return;  // no point of the slice
+    __shared__ unsigned long long s_w[kOstatThreads / 64];
+    __shared__ unsigned long long s_base, s_tot;
+    if (threadIdx.x < 64) {  // the earlier chunks' sums and the segment's total, wave 0
+        unsigned long long b = 0, t = 0;
+        for (uint32_t c = threadIdx.x; c < chunks; c += 64) {
+            const unsigned long long v = sums[g * chunks + c];
+            b += c < ch ? v : 0ull;
+            t += v;
+        }
+#pragma unroll
+        for (uint32_t off = 32; off > 0; off >>= 1) {
+            b += __shfl_down(b, off, 64);
+            t += __shfl_down(t, off, 64);
+        }
+        if (threadIdx.x == 0) s_base = b, s_tot = t;
+    }
+    // thread t takes kOstatPer consecutive exponentials: j = k0 + t * kOstatPer + i
+    uint64_t e[kOstatPer];
+    unsigned long long mine = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kOstatPer; ++i) {
+        const uint32_t j = k0 + threadIdx.x * kOstatPer + i;
+        e[i] = j <= o.N ? ostat_exp(o, g, j) : 0ull;
+        mine += e[i];
+    }
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned long long incl = mine;
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const unsigned long long u = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += u;
+    }
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    unsigned long long run = s_base + incl - mine;
+    for (uint32_t w = 0; w < wv; ++w) run += s_w[w];
+    const double tot = (double)s_tot;
+    const uint32_t H3 = o.H * o.H * o.H, n_occ = half ? o.total[cas] : 0u;
+    const float inv = 1.0f / (float)(o.H - 1);
+    const float sc = cs.s[cas], hg = cs.hgs[cas];
+#pragma unroll
+    for (uint32_t i = 0; i < kOstatPer; ++i) {
+        run += e[i];  // S_k, k = j: the (k+1)-th smallest of N uniforms is S_k / S_N
+        const uint32_t k = k0 + threadIdx.x * kOstatPer + i, p = p0 + k;
+        if (k >= o.N || p < lo || p >= hi) continue;
+        const double t = (double)run / tot;
+        uint32_t cell;
+        if (half && n_occ > 0) {
+            const uint32_t q = (uint32_t)fmin(floor(t * (double)n_occ), (double)(n_occ - 1));
+            cell = o.occ[(size_t)cas * H3 + q];
+        } else {
+            cell = (uint32_t)fmin(floor(t * (double)H3), (double)(H3 - 1));
+        }
+        const uint32_t c[3] = {compact_bits(cell), compact_bits(cell >> 1), compact_bits(cell >> 2)};
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {  // k_density_points' arithmetic
+            float x = 2.0f * (float)c[jj];
+            x = x * inv;
+            x = x - 1.0f;
+            x = x * sc;
+            float jt = rng_unit(o.seed, o.update, p, 1 + jj) * 2.0f;
+            jt = jt - 1.0f;
+            jt = jt * hg;
+            xyzs[(size_t)(p - lo) * 3 + jj] = x + jt;
+        }
+        indices[p - lo] = (int32_t)(cas * H3 + cell);
+    }
+}
+
+// The densities of the Morton-ordered points [lo, hi) -> tmp_grid, no global
+// atomics: the draws of one cell are adjacent within a half, so the first point
+// of each run takes the run's max; the uniform halves store it, the occupied
+// halves (a second launch) fold it into what the first left.
+__global__ void __launch_bounds__(256)
+k_density_run_max(const float* __restrict__ sigma, const int32_t* __restrict__ indices, uint32_t lo, uint32_t hi,
+                  uint32_t N, uint32_t half, float* __restrict__ tmp) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x, p = lo + i;
+    if (p >= hi || (p / N & 1u) != half) return;
+    const uint32_t seg_end = min(hi, (p / N + 1) * N);
+    const int32_t c = indices[i];
+    if (p > lo && p % N != 0 && indices[i - 1] == c) return;  // not the run's first point
+    float m = sigma[i];
+    for (uint32_t q = p + 1; q < seg_end && indices[q - lo] == c; ++q) m = fmaxf(m, sigma[q - lo]);
+    tmp[c] = half ? fmaxf(tmp[c], m) : m;
+}
+
+// The reference's bookkeeping after an update (renderer.py:593-595):
+// mean_count = int(mean of the sample counts of the last `total` batches), from
+// the fused trainer's step-counter ring (slot = batch % 16, written when the
+// next batch is drawn) and the newest batch's counter. One thread.
+__global__ void k_density_mean_count(const int32_t* __restrict__ step_counter, const int32_t* __restrict__ draw,
+                                     const int32_t* __restrict__ counter, uint32_t total, uint32_t ahead,
+                                     int64_t* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const int32_t d = *draw;
+    int64_t sum = 0;
+    if (ahead) {  // the next batch is drawn: the newest count is in the ring too
+        for (uint32_t k = 0; k < total; ++k) sum += step_counter[((d - 2 - (int32_t)k) & 15) * 2];
+    } else {
+        for (uint32_t k = 1; k < total; ++k) sum += step_counter[((d - 1 - (int32_t)k) & 15) * 2];
+        sum += counter[0];
+    }
+    *out = sum / (int64_t)total;  // counts are >= 0: floor division
+}
+
 }  // namespace
+
+extern "C" int ngp_density_mean_count(const int32_t* step_counter, const int32_t* draw, const int32_t* counter,
+                                      uint32_t total, uint32_t ahead, int64_t* out, void* stream) {
+    NGP_REQUIRE(step_counter && draw && counter && out, NGP_ERR_ARG, "density_mean_count: null pointer");
+    NGP_REQUIRE(total >= 1 && total <= 16, NGP_ERR_ARG, "density_mean_count: total %u not in [1, 16]", total);
+    k_density_mean_count<<<1, 64, 0, ngp_stream(stream)>>>(step_counter, draw, counter, total, ahead, out);
+    return ngp_check_launch("density_mean_count");
+}
 
 extern "C" size_t ngp_density_grid_sort_workspace_bytes(uint32_t C, uint32_t H) {
     const SortPlan sp = sort_plan(C, H, 1, 0, 1);
@@ -488,12 +703,61 @@ extern "C" int ngp_density_grid_ema_pack(float* grid, float* tmp_grid, uint32_t 
     NGP_REQUIRE(H % 2 == 0 && C >= 1, NGP_ERR_ARG, "density_grid_ema_pack: grid size %u must be even", H);
     const uint32_t n = C * H * H * H;
     hipStream_t st = ngp_stream(stream);
-    if (hipMemsetAsync(stats, 0, sizeof(double), st) != hipSuccess)
-        return ngp_set_error(NGP_ERR_HIP, "density_grid_ema_pack: stats clear failed");
-    const uint32_t blocks = std::min<uint32_t>(ngp_div_up(n, kEmaThreads), 4 * ngp_num_cus());
-    k_density_ema<<<blocks, kEmaThreads, 0, st>>>(grid, tmp_grid, n, decay, stats);
-    k_density_pack<<<ngp_div_up(n / 8, 256), 256, 0, st>>>(grid, n / 8, n, stats, density_thresh, bitfield);
+    // stats: [0] the sum, [1..] the EMA blocks' partial sums
+    const uint32_t blocks = std::min<uint32_t>(ngp_div_up(n, kEmaThreads), kEmaMaxBlocks);
+    k_density_ema<<<blocks, kEmaThreads, 0, st>>>(grid, tmp_grid, n, decay, stats + 1);
+    k_density_pack<<<ngp_div_up(n / 8, 256), 256, 0, st>>>(grid, n / 8, n, stats + 1, blocks, density_thresh,
+                                                           bitfield, stats);
     return ngp_check_launch("density_grid_ema_pack");
+}
+
+extern "C" size_t ngp_density_grid_ostat_workspace_bytes(uint32_t C, uint32_t H) {
+    const uint32_t N = H * H * H / 4, chunks = (N + 1 + kOstatChunk - 1) / kOstatChunk;
+    return (size_t)2 * C * chunks * sizeof(unsigned long long);
+}
+
+extern "C" int ngp_density_grid_draw_sorted(const float* grid, uint32_t C, uint32_t H, uint32_t seed, uint32_t update,
+                                            float bound, uint32_t lo, uint32_t hi, void* draw_ws, size_t draw_ws_bytes,
+                                            void* ostat_ws, size_t ostat_ws_bytes, float* xyzs, int32_t* indices,
+                                            void* stream) {
+    NGP_REQUIRE(grid && draw_ws && ostat_ws && xyzs && indices, NGP_ERR_ARG, "density_grid_draw_sorted: null pointer");
+    NGP_REQUIRE(C >= 1 && C <= kMaxCascades && H >= 2 && H <= 1024 && (H & (H - 1)) == 0 && H % 2 == 0, NGP_ERR_ARG,
+                "density_grid_draw_sorted: cascade %u / grid size %u (a power of two) out of range", C, H);
+    const uint32_t H3 = H * H * H, N = H3 / 4, P = C * 2 * N;
+    NGP_REQUIRE(lo <= hi && hi <= P, NGP_ERR_ARG, "density_grid_draw_sorted: [%u, %u) outside the %u draws", lo, hi,
+                P);
+    NGP_REQUIRE(draw_ws_bytes >= ngp_density_grid_draw_workspace_bytes(C, H) &&
+                    ostat_ws_bytes >= ngp_density_grid_ostat_workspace_bytes(C, H),
+                NGP_ERR_ARG, "density_grid_draw_sorted: workspace too small");
+    hipStream_t st = ngp_stream(stream);
+    const uint32_t nblk = ngp_div_up(H3, kOccBlock);
+    uint32_t* bcount = static_cast<uint32_t*>(draw_ws);
+    uint32_t* total = bcount + (size_t)C * nblk;
+    uint32_t* occ = reinterpret_cast<uint32_t*>(static_cast<char*>(draw_ws) +
+                                                ((C * nblk + C) * sizeof(uint32_t) + 255) / 256 * 256);
+    k_density_occ_count<<<dim3(nblk, C), kOccBlock, 0, st>>>(grid, H3, bcount);
+    k_density_occ_scan<<<C, 1024, 0, st>>>(bcount, nblk, total);
+    k_density_occ_write<<<dim3(nblk, C), kOccBlock, 0, st>>>(grid, H3, bcount, occ);
+    if (hi == lo) return ngp_check_launch("density_grid_draw_sorted");
+    const Ostat o{C, H, N, seed ^ kDensityRngDomain, update, occ, total};
+    const uint32_t chunks = ngp_div_up(N + 1, kOstatChunk);
+    unsigned long long* sums = static_cast<unsigned long long*>(ostat_ws);
+    k_ostat_sums<<<2 * C * chunks, kOstatThreads, 0, st>>>(o, chunks, sums);
+    k_ostat_points<<<2 * C * chunks, kOstatThreads, 0, st>>>(o, chunks, sums, lo, hi, cascade_scales(C, H, bound),
+                                                             xyzs, indices);
+    return ngp_check_launch("density_grid_draw_sorted");
+}
+
+extern "C" int ngp_density_grid_run_max(const float* sigma, const int32_t* indices, uint32_t C, uint32_t H,
+                                        uint32_t lo, uint32_t hi, float* tmp_grid, void* stream) {
+    NGP_REQUIRE(sigma && indices && tmp_grid, NGP_ERR_ARG, "density_grid_run_max: null pointer");
+    const uint32_t N = H * H * H / 4;
+    NGP_REQUIRE(N > 0 && lo <= hi && hi <= C * 2 * N, NGP_ERR_ARG, "density_grid_run_max: bad range");
+    if (hi == lo) return NGP_OK;
+    hipStream_t st = ngp_stream(stream);
+    for (uint32_t half = 0; half < 2; ++half)
+        k_density_run_max<<<ngp_div_up(hi - lo, 256), 256, 0, st>>>(sigma, indices, lo, hi, N, half, tmp_grid);
+    return ngp_check_launch("density_grid_run_max");
 }
 
 extern "C" size_t ngp_density_grid_draw_workspace_bytes(uint32_t C, uint32_t H) {
@@ -520,6 +784,7 @@ extern "C" int ngp_density_grid_draw(const float* grid, uint32_t C, uint32_t H, 
         k_density_occ_scan<<<C, 1024, 0, st>>>(bcount, nblk, total);
         k_density_occ_write<<<dim3(nblk, C), kOccBlock, 0, st>>>(grid, H3, bcount, occ);
     }
-    k_density_draw<<<ngp_div_up(P, 256), 256, 0, st>>>(P, ppc, H, seed ^ kDensityRngDomain, update, occ, total, coords, noise);
+    const PartialDraw d{ppc, H, seed ^ kDensityRngDomain, update, occ, total};
+    k_density_draw<<<ngp_div_up(P, 256), 256, 0, st>>>(P, d, partial != 0, coords, noise);
     return ngp_check_launch("density_grid_draw");
 }

@@ -477,8 +477,21 @@ struct EpiDensity {
     float* tmp_grid;
     const int32_t* index;
     float density_scale;
+    float* sigma_out;  // non-null: the density of row r stored at sigma_out[r] (no index, no atomic)
     template <typename FO>
     NGP_DEV void operator()(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act) const {
+        int32_t ix[kNB];
+        load_index(row0, B, ix);
+        run(row0, B, o, out_act, ix);
+    }
+    // the chunk's cell indices (lane group 0: row c of each column block)
+    NGP_DEV void load_index(uint32_t row0, uint32_t B, int32_t (&ix)[kNB]) const {
+        const int c = threadIdx.x & 15;
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) ix[nb] = sigma_out ? 0 : index[clamp_row(row0 + nb * 16 + c, B)];
+    }
+    template <typename FO>
+    NGP_DEV void run(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act, const int32_t (&ix)[kNB]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
         if (g != 0) return;  // column 0 (the log density) lives in lane group 0, register 0
 #pragma unroll
@@ -486,7 +499,10 @@ struct EpiDensity {
             const uint32_t row = row0 + nb * 16 + c;
             if (row >= B) continue;
             const float s = expf((float)(ngp_half)out_act.fwd(o[nb][0][0])) * density_scale;
-            atomicMax(reinterpret_cast<int*>(tmp_grid) + index[row], __float_as_int(s));
+            if (sigma_out)
+                sigma_out[row] = s;
+            else
+                atomicMax(reinterpret_cast<int*>(tmp_grid) + ix[nb], __float_as_int(s));
         }
     }
 };
@@ -530,6 +546,54 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
     }
 }
 
+
+// The density query's sigma network (update_extra_state, renderer.py:533-538)
+// on the pair-major encodings of the grid forward, from the prepacked image:
+// each wave requests its next chunk's encodings and cell indices before it
+// computes the current one, so the 1-2M-point batch streams at HBM rate
+// instead of one round trip per chunk. Same values as k_mlp_fwd<EpiDensity>.
+template <int W, int NH>
+__global__ void __launch_bounds__(kThreads)
+k_density_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img, uint32_t B, EpiDensity epi) {
+    using N = Net<W, 1, NH>;
+    const InPairMajor xl{B};
+    extern __shared__ half8 lds[];
+    const ActReLU act;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t nchunks = ngp_div_up(B, 16 * kNB), stride = gridDim.x * kWaves;
+    uint32_t chunk = blockIdx.x * kWaves + wave;
+    half8 xn[kNB][1];
+    int32_t in_[kNB];
+    xl.template operator()<1>(enc, 32u, chunk * 16 * kNB, B, xn);
+    epi.load_index(chunk * 16 * kNB, B, in_);
+    copy_frags<N::FWD_FRAGS, kThreads>(lds, img);
+    __syncthreads();
+    for (; chunk < nchunks; chunk += stride) {
+        const uint32_t row0 = chunk * 16 * kNB;
+        half8 x[kNB][1];
+        int32_t ix[kNB];
+#pragma unroll
+        for (int nb = 0; nb < kNB; ++nb) {
+            x[nb][0] = xn[nb][0];
+            ix[nb] = in_[nb];
+        }
+        // the next chunk's inputs (clamped rows: no branch), in flight during this one
+        xl.template operator()<1>(enc, 32u, row0 + stride * 16 * kNB, B, xn);
+        epi.load_index(row0 + stride * 16 * kNB, B, in_);
+        f32x4 acc[kNB][N::MTW];
+        half8 h[kNB][N::KSW];
+        dense<N::MTW, 1>(lds, fwd_desc<W, 1, NH>(0, 32u).frag0, x, acc);
+        pack_act<N::MTW, N::KSW>(acc, act, h);
+#pragma unroll
+        for (int q = 1; q <= NH; ++q) {
+            dense<N::MTW, N::KSW>(lds, fwd_desc<W, 1, NH>(q, 32u).frag0, h, acc);
+            pack_act<N::MTW, N::KSW>(acc, act, h);
+        }
+        f32x4 o[kNB][1];
+        dense<1, N::KSW>(lds, fwd_desc<W, 1, NH>(NH + 1, 32u).frag0, h, o);
+        epi.run(row0, B, o, ActNone{}, ix);
+    }
+}
 
 // The NeRF forward in one launch (network_ff.py:51-74): per 32-sample chunk
 // the sigma network on the pair-major encodings, its epilogue (h, sigma,
@@ -1240,6 +1304,15 @@ int launch_fwd_nerf(const void* in, const void* w, const void* image, uint32_t B
 template <int W, int IN_KS, int NH>
 int launch_fwd_density(const void* in, const void* w, const void* image, uint32_t B, uint32_t in_dim,
                        const EpiDensity& epi, hipStream_t st) {
+    if (IN_KS == 1 && image) {  // the streaming kernel (prepacked image, 32 inputs)
+        using N = Net<W, 1, NH>;
+        const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
+        uint32_t blocks = ngp_div_up(nchunks, kWaves);
+        if (blocks > 2048) blocks = 2048;
+        hipLaunchKernelGGL((k_density_fwd<W, NH>), dim3(blocks), dim3(kThreads), (size_t)N::FWD_FRAGS * 64 * 16, st,
+                           (const ngp_half*)in, (const half8*)image, B, epi);
+        return ngp_check_launch("nerf_density_forward");
+    }
     return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActReLU{}, ActNone{}, nullptr, nullptr, epi, st,
                                       InPairMajor{B});
 }
@@ -1536,7 +1609,19 @@ extern "C" int ngp_nerf_density_forward(const void* inputs, const void* weights,
     NGP_REQUIRE(indices && tmp_grid, NGP_ERR_ARG, "nerf_density_forward: null indices / tmp_grid");
     if (B == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
-    const EpiDensity epi{tmp_grid, indices, density_scale};
+    const EpiDensity epi{tmp_grid, indices, density_scale, nullptr};
+    MLP_DISPATCH(launch_fwd_density, inputs, weights, image, B, in_dim, epi, st);
+}
+
+extern "C" int ngp_nerf_density_forward_rows(const void* inputs, const void* image, uint32_t B, uint32_t hidden_dim,
+                                             uint32_t num_layers, float density_scale, float* sigma, void* stream) {
+    const uint32_t in_dim = 32;
+    if (int e = check_shape(B, in_dim, kOut, hidden_dim, num_layers)) return e;
+    NGP_REQUIRE(image && sigma, NGP_ERR_ARG, "nerf_density_forward_rows: null image / sigma");
+    if (B == 0) return NGP_OK;
+    hipStream_t st = ngp_stream(stream);
+    const EpiDensity epi{nullptr, nullptr, density_scale, sigma};
+    const void* weights = nullptr;
     MLP_DISPATCH(launch_fwd_density, inputs, weights, image, B, in_dim, epi, st);
 }
 

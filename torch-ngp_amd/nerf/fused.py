@@ -73,7 +73,8 @@ def _vp_array(ptrs):
 #   draw_ahead    the next batch is drawn in the grid backward's bin launch
 #   live_rows     the backwards walk the rows with a nonzero gradient only
 #   dp_graph      data parallel over RCCL: the whole step is one graph
-#   density_sort  partial density updates query their cells in brick order
+#   density_sort  partial density updates draw their cells as order statistics, in
+#                 Morton order (False: the counter-RNG draws in draw order)
 #   sparse_exchange  data parallel: every rank runs the world-1 step with the
 #                 full Adam, the gradients meet in a touched-entry exchange
 #                 (nerf/exchange.py) instead of the ZeRO-1 collectives
@@ -336,7 +337,8 @@ class FusedTrainer:
         self._ring, self._ring_i = [], 0  # timing graphs (capture(ring=R))
         self._events, self._capturing = None, False
         self._dens = None  # density-grid update buffers (update_density)
-        # partial updates query their random cells in brick order (density_sort=False: draw order)
+        # partial updates draw their random cells in Morton order (density_sort=False: the
+        # counter-RNG draws in draw order, as ngp_density_grid_draw makes them)
         self._dens_sorted = opts["density_sort"]
         self._pending = False  # gradients of the last forward/backward not yet applied
 
@@ -381,28 +383,31 @@ class FusedTrainer:
                 idx=torch.zeros(C * H3, dtype=torch.int32, device=dev),
                 enc=torch.zeros(self.enc.num_levels, C * H3 // self.world + 1, 2, dtype=torch.float16, device=dev),
                 tmp=torch.full((C, H3), -1.0, device=dev),
-                stats=torch.zeros(1, dtype=torch.float64, device=dev),
+                stats=torch.zeros(nat.DENSITY_STATS_LEN, dtype=torch.float64, device=dev),
                 ws=torch.zeros(max(wsb, 256), dtype=torch.uint8, device=dev),
-                sort_ws=torch.zeros(max(int(lib.ngp_density_grid_sort_workspace_bytes(C, H)), 256),
-                                    dtype=torch.uint8, device=dev),
-                table=torch.zeros_like(self.params[0], dtype=torch.float16) if self.table32 else None)
+                ostat_ws=torch.zeros(max(int(lib.ngp_density_grid_ostat_workspace_bytes(C, H)), 256),
+                                     dtype=torch.uint8, device=dev),
+                table=torch.zeros_like(self.params[0], dtype=torch.float16) if self.table32 else None,
+                mean_count=torch.zeros(1, dtype=torch.int64, device=dev),
+                sigma=torch.zeros(C * H3 // 2 // self.world + 1, device=dev))
         partial = int(m.iter_density >= 16)
         ppc = 2 * (H3 // 4) if partial else H3
         P = C * ppc
-        nat.check(lib.ngp_density_grid_draw(P_(m.density_grid), C, H, partial, self.density_seed, m.iter_density,
-                                            P_(d["coords"]), P_(d["noise"]), P_(d["ws"]), d["ws"].numel(), s),
-                  "density_grid_draw")
         lo, hi = self.rank * P // self.world, (self.rank + 1) * P // self.world
-        e, n = self.enc, hi - lo
-        if partial and self._dens_sorted:
-            # this rank's slice of the draws in brick order (same max per cell),
-            # at the head of xyzs / idx
-            nat.check(lib.ngp_density_grid_points_sorted(P_(d["coords"]), P_(d["noise"]), P, ppc, C, H,
-                                                         float(m.bound), lo, hi, P_(d["sort_ws"]),
-                                                         d["sort_ws"].numel(), P_(d["xyzs"]), P_(d["idx"]), s),
-                      "density_grid_points_sorted")
+        lo0, e, n = lo, self.enc, hi - lo
+        sorted_ = bool(partial and self._dens_sorted and H & (H - 1) == 0)
+        if sorted_:
+            # this rank's slice of the draws, generated in Morton order (the
+            # same i.i.d. draws as order statistics), at the head of xyzs / idx
+            nat.check(lib.ngp_density_grid_draw_sorted(P_(m.density_grid), C, H, self.density_seed, m.iter_density,
+                                                       float(m.bound), lo, hi, P_(d["ws"]), d["ws"].numel(),
+                                                       P_(d["ostat_ws"]), d["ostat_ws"].numel(), P_(d["xyzs"]),
+                                                       P_(d["idx"]), s), "density_grid_draw_sorted")
             lo = 0
         else:
+            nat.check(lib.ngp_density_grid_draw(P_(m.density_grid), C, H, partial, self.density_seed,
+                                                m.iter_density, P_(d["coords"]), P_(d["noise"]), P_(d["ws"]),
+                                                d["ws"].numel(), s), "density_grid_draw")
             nat.check(lib.ngp_density_grid_points(P_(d["coords"]) if partial else None, P_(d["noise"]), P, ppc, C,
                                                   H, float(m.bound), P_(d["xyzs"]), P_(d["idx"]), s),
                       "density_grid_points")
@@ -414,10 +419,23 @@ class FusedTrainer:
             P_(d["xyzs"]) + 12 * lo, float(m.bound), P_(table), _F16, P_(e.offsets), P_(d["enc"]), n, None,
             e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id, int(e.align_corners),
             e.interp_id, 0, s), "grid_encode_fused")
-        sn = self.sig_net
-        nat.check(lib.ngp_nerf_density_forward(P_(d["enc"]), P_(self.w_half[1]), None, n, sn.input_dim, sn.hidden_dim,
-                                               sn.num_layers, float(m.density_scale), P_(d["idx"]) + 4 * lo,
-                                               P_(d["tmp"]), s), "nerf_density_forward")
+        sn, pk = self.sig_net, self._pk
+        # the fragment images of the weights the flush above left (the next
+        # step packs them again from the same weights)
+        nat.check(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
+        dens = (P_(d["enc"]), P_(self.mlp_img[0]), n, sn.hidden_dim, sn.num_layers, float(m.density_scale))
+        if sorted_:
+            # densities per point, then each run of one cell's draws -> its max (no global atomics)
+            nat.check(lib.ngp_nerf_density_forward_rows(*dens, P_(d["sigma"]), s), "nerf_density_forward_rows")
+            nat.check(lib.ngp_density_grid_run_max(P_(d["sigma"]), P_(d["idx"]), C, H, lo0, hi, P_(d["tmp"]), s),
+                      "density_grid_run_max")
+        elif not partial and H & (H - 1) == 0:
+            # the full update's point p is cell p (Morton order): densities straight into tmp_grid
+            nat.check(lib.ngp_nerf_density_forward_rows(*dens, P_(d["tmp"]) + 4 * lo, s), "nerf_density_forward_rows")
+        else:
+            nat.check(lib.ngp_nerf_density_forward(P_(d["enc"]), P_(self.w_half[1]), P_(self.mlp_img[0]), n,
+                                                   sn.input_dim, sn.hidden_dim, sn.num_layers, float(m.density_scale),
+                                                   P_(d["idx"]) + 4 * lo, P_(d["tmp"]), s), "nerf_density_forward")
         if self._dist:
             if self._nccl:
                 dist.all_reduce(d["tmp"], op=dist.ReduceOp.MAX)
@@ -442,19 +460,20 @@ class FusedTrainer:
 
     def _recent_count_mean(self, total):
         """int(mean) of the sample counts of the last `total` batches, as a
-        device scalar (no host sync). At the upstream cadence (16 steps per
-        update, the next batch drawn ahead) those are exactly the 16
-        step_counter slots: one sum instead of the gather's eight small ops."""
-        if total == 16 and self._ahead:
-            return torch.div(self.model.step_counter[:, 0].sum(dtype=torch.int64), 16, rounding_mode="floor")
-        return torch.div(self._recent_counts(total).sum(), total, rounding_mode="floor")
+        device scalar (no host sync): one launch (ngp_density_mean_count)
+        instead of the gather's small torch ops."""
+        out = self._dens["mean_count"]
+        nat.check(nat.lib().ngp_density_mean_count(
+            nat.ptr(self.model.step_counter), nat.ptr(self.state) + 4 * self._S_DRAW, nat.ptr(self.counter), total,
+            int(self._ahead), nat.ptr(out), nat.stream_of(out)), "density_mean_count")
+        return out
 
     @property
     def mean_density(self):
         """model.mean_density, after the last update_density's value
         (torch.mean(...).item(), :584) has been read back from the device."""
         if getattr(self, "_mean_density_pending", False):
-            self.model.mean_density = float(np.float32(self._dens["stats"].item() / self.model.density_grid.numel()))
+            self.model.mean_density = float(np.float32(self._dens["stats"][0].item() / self.model.density_grid.numel()))
             self._mean_density_pending = False
         return float(self.model.mean_density)
 

@@ -327,13 +327,13 @@ class NeRFRenderer(nn.Module):
         step = H ** 3
         for a in range(0, P, step):
             self._query_density(xyzs[a:a + step], indices[a:a + step], tmp)
-        stats = torch.empty(1, dtype=torch.float64, device=dev)
+        stats = torch.empty(nat.DENSITY_STATS_LEN, dtype=torch.float64, device=dev)
         nat.check(nat.lib().ngp_density_grid_ema_pack(nat.ptr(self.density_grid), nat.ptr(tmp), C, H,
                                                       float(decay), float(self.density_thresh), nat.ptr(stats),
                                                       nat.ptr(self.density_bitfield), st),
                   "density_grid_ema_pack")
         # mean_density: torch.mean(...).item() of the fp32 grid, :584
-        self.mean_density = float(np.float32(stats.item() / self.density_grid.numel()))
+        self.mean_density = float(np.float32(stats[0].item() / self.density_grid.numel()))
         self.iter_density += 1
         total_step = min(16, self.local_step)
         if total_step > 0:
