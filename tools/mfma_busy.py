@@ -17,7 +17,7 @@ def main():
         for f in glob.glob(d + "/*/run_counter_collection.csv"):
             for r in csv.DictReader(open(f)):
                 name = r["Kernel_Name"]
-                key = next((k for k in ("k_nerf_bwd_pair", "k_nerf_bwd", "k_nerf_fwd", "k_mlp_fwd", "k_mlp_bwd")
+                key = next((k for k in ("k_nerf_bwd", "k_nerf_fwd", "k_density_fwd", "k_mlp_fwd", "k_mlp_bwd")
                             if k in name), None)
                 if key is None:
                     continue

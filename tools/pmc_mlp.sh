@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R"
-KRE='k_mlp|k_nerf_fwd|k_nerf_bwd|k_grid_bwd_bin|k_grid_bin_accum|k_grid_fwd|k_adam'
+KRE='k_mlp|k_nerf_fwd|k_nerf_bwd|k_density_fwd|k_grid_bwd_bin|k_grid_bin_accum|k_grid_fwd|k_adam'
 i=0
 for PMC in "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_BUSY_CU_CYCLES" "SQ_WAVE_CYCLES SQ_WAVES"; do
   i=$((i+1))
