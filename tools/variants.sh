@@ -15,7 +15,7 @@ while [ $# -ge 2 ]; do
     out=$R/torch-ngp_amd/variants/$name
     mkdir -p "$out"
     objs=""
-    for o in ngp_lib gridencoder raymarching shencoder ffmlp adam nerf_fused density_grid freqencoder; do
+    for o in ngp_lib gridencoder raymarching shencoder ffmlp adam nerf_fused density_grid freqencoder exchange; do
         if [[ " $SRCS " == *" $o "* ]]; then
             /opt/rocm/bin/hipcc $FLAGS $defs -c "$R/torch-ngp_amd/csrc/$o.hip" -o "$out/$o.o"
             objs="$objs $out/$o.o"

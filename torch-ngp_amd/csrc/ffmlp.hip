@@ -900,7 +900,7 @@ struct NoIdle {
     NGP_DEV void operator()() const {}
 };
 
-template <int W, int IN_KS, int NH, typename FA, typename XL, typename GI, typename MAP, typename PRE,
+template <int W, int IN_KS, int NH, bool GI_SYNC, typename FA, typename XL, typename GI, typename MAP, typename PRE,
           typename HALF = NoHalf, typename IDLE = NoIdle>
 NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tiles, float* __restrict__ img_base,
                        const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs, XL xl, GI gi_out,
@@ -1038,10 +1038,15 @@ NGP_DEV void bwd_phase(const half8* __restrict__ fr, ngp_half* __restrict__ tile
     __shared__ uint32_t s_took[kBwdWaves];  // each wave writes its own slot before the barrier below
     if ((threadIdx.x & 63) == 0) s_took[wave] = nst != 0 || hrow != kNoHalf ? 1u : 0u;
     if (nst == 0 && hrow == kNoHalf) idle();  // a wave without rows (wave-uniform)
-    // fragments and tiles are dead from here on; a full barrier: the waves'
-    // input-gradient stores are complete for the workgroup (the NeRF
-    // backward's sigma pass reads the colour pass's), the later ones order LDS only
-    __syncthreads();
+    // fragments and tiles are dead from here on. GI_SYNC (the NeRF backward's
+    // colour pass, whose input gradients the sigma pass reads): a full barrier,
+    // the waves' input-gradient stores complete for the workgroup; otherwise
+    // (nothing in the workgroup reads them) an LDS-only one, so the fold does
+    // not wait for the stores to land. The later barriers order LDS only.
+    if constexpr (GI_SYNC)
+        __syncthreads();
+    else
+        lds_barrier();
     if (wave < 2) fold(std::true_type{});
     lds_barrier();
 #pragma unroll 1
@@ -1108,7 +1113,7 @@ k_mlp_bwd(const ngp_half* __restrict__ grad, const ngp_half* __restrict__ inputs
     extern __shared__ half8 lds[];
     ngp_half* tiles = reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + L::frag_bytes);
     const uint32_t stride = gridDim.x * kBwdWaves, c0 = blockIdx.x * kBwdWaves + (threadIdx.x >> 6);
-    bwd_phase<W, IN_KS, NH>(lds, tiles, reinterpret_cast<float*>(lds), grad, inputs, xl, gi_out, want_gi, slab,
+    bwd_phase<W, IN_KS, NH, false>(lds, tiles, reinterpret_cast<float*>(lds), grad, inputs, xl, gi_out, want_gi, slab,
                             nparams, B, in_dim, act, [=](uint32_t k) { return c0 + k * stride; },
                             [&]() {
                                 copy_frags<L::FRAGS, kBwdThreads>(lds, image);
@@ -1192,7 +1197,7 @@ k_nerf_bwd(NerfBwdArgs a) {
     // live rows: the workgroups past the slab rows the reduce reads have no
     // chunk and skip both passes (ngp_reduce::live_slab_rows)
     if (!a.rows || b < ngp_reduce::live_slab_rows((int32_t)B, G)) {
-    bwd_phase<64, 1, NHC>(lds, reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes),
+    bwd_phase<64, 1, NHC, true>(lds, reinterpret_cast<ngp_half*>(reinterpret_cast<char*>(lds) + LC::frag_bytes),
                           reinterpret_cast<float*>(lds), a.g_color_out, a.color_in, InRowMajor{a.rows},
                           GiNerfGeo{a.g_h, a.rows},
                           true, a.slab_color, a.np_color, B, 32u, ActReLU{}, map_of(w),
@@ -1211,7 +1216,7 @@ k_nerf_bwd(NerfBwdArgs a) {
     // pass loads g_h and reuses LDS: an LDS-only barrier, so the colour slab
     // row's stores need not land first
     lds_barrier();
-    bwd_phase<64, 1, NHS>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
+    bwd_phase<64, 1, NHS, false>(sfr, reinterpret_cast<ngp_half*>(lds), reinterpret_cast<float*>(lds), a.g_h, a.enc,
                           InPairMajor{a.B, a.rows}, GiPairMajor{a.g_enc, a.B, a.rows}, true, a.slab_sigma, a.np_sigma,
                           B, 32u, ActReLU{}, map_of(kBwdWaves - 1 - w), []() {}, half_of(kBwdWaves - 1 - w));
     }
