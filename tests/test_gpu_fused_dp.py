@@ -45,6 +45,9 @@ def _worker(rank, world, port, q):
         model.encoder.embeddings.normal_(0, 0.05)
     model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
     ft = FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, distributed=world > 1)
+    if world > 1:  # the data-parallel defaults this test covers: draw-ahead, the tail in
+        # the grid forward's launch, the live-row backwards (gloo: the three-graph form)
+        assert ft.dp and ft._draw_ahead and ft._dp_tail and ft._live and not ft._nccl
     for _ in range(3):
         ft.step()
     ft.capture(warmup=1)
