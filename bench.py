@@ -575,25 +575,33 @@ def run_autograd(args, model, data, bits, world, dev):
     return result
 
 
-def adam_bytes(ft):
+def adam_bytes(ft, groups=None):
     """Algorithmic HBM bytes of one Adam sweep of this rank (SURVEY §8(d) and
     DESIGN.md §4): per parameter p, m, v read + write (24 B) and the fp16 grad
     read + clear (4 B); + 2 B for an fp16 forward copy where one is written (the
-    MLPs; the table too when it is kept, data parallel)."""
+    MLPs; the table too when it is kept, data parallel). groups (world 1, from
+    FusedTrainer.adam_groups): the sweep stores nothing for a table group it
+    leaves unchanged (moments and gradient zero: 16 B / parameter, the reads)
+    and does not clear a gradient group that is zero (26 B), so those bytes
+    are not counted."""
     n_tab = int(ft.params[0].numel())
     n_mlp = int(sum(p.numel() for p in ft.params[1:]))
     if ft.dp:
         return int(30 * ft.chunk)
-    return int((28 if ft.table32 else 30) * n_tab + 30 * n_mlp)
+    if groups is None or not ft.table32:
+        return int((28 if ft.table32 else 30) * n_tab + 30 * n_mlp)
+    idle, zero_g, total = groups
+    rest = n_tab - 4 * (idle + zero_g)
+    return int(16 * 4 * idle + 26 * 4 * zero_g + 28 * rest + 30 * n_mlp)
 
 
-def launch_bytes(ft, samples, rays, live=None):
+def launch_bytes(ft, samples, rays, live=None, groups=None):
     """SURVEY §8(d) per-unit bytes of each launch of the world-1 step body
     (timed_body_steps names): None for the MFMA-bound MLP launches. The grid
     backward's 1,100 B are per LIVE sample when the backwards walk only the
     rows with a nonzero gradient (options live_rows; `live` = their count)."""
     march = 48 * rays + 32 * samples
-    out = {"march_rays_train+adam": adam_bytes(ft) + march, "march_rays_train": march,
+    out = {"march_rays_train+adam": adam_bytes(ft, groups) + march, "march_rays_train": march,
            "step_head": None, "grid_encode_forward": 588 * samples, "grid_encode_backward": 1100 * (samples if live is None else live),
            "composite_loss": (32 + 52) * rays + (24 + 40) * samples, "ffmlp_forward": None, "ffmlp_backward": None}
     return out
@@ -706,14 +714,14 @@ def grid_roofline(grid_clock, steps, workload, all_samples=None):
     return out
 
 
-def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload, live=None):
+def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload, live=None, groups=None):
     """The step's longest launch (over all launches of the body, timed with
     HIP events between the launches of eager body steps on the launch stream,
     the sample counts of those same steps): its algorithmic bytes (SURVEY
     §8(d)) over its mean duration. World 1 that is the march launch carrying
     the previous step's Adam; `adam_bytes_frac` is Adam's share of its bytes."""
     S = float(np.mean(counts))
-    nbytes = launch_bytes(ft, S, rays, live)
+    nbytes = launch_bytes(ft, S, rays, live, groups)
     dom = max(kernel_ms, key=lambda k: kernel_ms[k])
     out = {"kernel": dom, "timing": "eager_body_events", "launches_timed": len(per_step[dom]),
            "avg_launch_ms": round(kernel_ms[dom], 5),
@@ -734,6 +742,8 @@ def launch_roofline(ft, kernel_ms, per_step, counts, rays, workload, live=None):
         ab = b - (48 * rays + 32 * S)
         out["adam_bytes"] = int(ab)
         out["adam_bytes_frac"] = round(ab / b, 4)
+        if groups is not None:  # the table's 4-parameter groups Adam leaves / does not clear
+            out["adam_table_groups"] = {"unchanged": groups[0], "grad_zero": groups[1], "total": groups[2]}
     out["per_launch_ms"] = {k: round(v, 5) for k, v in kernel_ms.items()}
     out["per_launch_frac"] = {k: round(nbytes[k] / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                               for k, v in kernel_ms.items() if nbytes.get(k)}
@@ -752,8 +762,10 @@ def run_fused(args, model, data, bits, world, dev):
     loss = ft.last_loss
 
     # ---------------- per-launch device time (roofline) ----------------
+    groups = None
     if world == 1:
         kernel_ms, per_step, counts = ft.timed_body_steps(args.kernel_steps)
+        groups = ft.adam_groups()  # the pending update's (the last timed body step's gradient)
     else:
         ft.flush()
         kernel_ms, per_step, counts = ft.timed_steps(args.kernel_steps, with_counts=True)
@@ -765,7 +777,7 @@ def run_fused(args, model, data, bits, world, dev):
     grid = grid_roofline(grid_clock, args.steps, args.workload,
                          samples_per_step if getattr(ft, "_live", False) else None)
     if world == 1:
-        roofline = launch_roofline(ft, kernel_ms, per_step, counts, args.num_rays, args.workload, live)
+        roofline = launch_roofline(ft, kernel_ms, per_step, counts, args.num_rays, args.workload, live, groups)
     else:  # the data-parallel step's phases include collectives: the grid backward names the roofline
         roofline = grid
     mlp_ms = sum(v for k, v in kernel_ms.items() if k.startswith("ffmlp"))

@@ -44,6 +44,11 @@ def test_algorithmic_bytes_of_the_step_launches():
     assert b["composite_loss"] == 84 * 4096 + 64 * 80000 and b["ffmlp_backward"] is None
     dp = types.SimpleNamespace(params=ft.params, table32=False, dp=True, chunk=1532288)
     assert bench.adam_bytes(dp) == 30 * 1532288
+    # the table groups the sweep leaves unchanged (reads only, 16 B) or does not clear (26 B)
+    idle, zg = 1000000, 2000000
+    assert bench.adam_bytes(ft, (idle, zg, 12239728 // 4)) == (16 * 4 * idle + 26 * 4 * zg
+                                                               + 28 * (12239728 - 4 * (idle + zg)) + 30 * 18432)
+    assert bench.adam_bytes(ft, (0, 0, 12239728 // 4)) == bench.adam_bytes(ft)
 
 
 def test_flat_buffer_sizes_of_configs_4_and_5():

@@ -135,6 +135,72 @@ def test_fused_optimizer_matches_torch_adam_and_scaler(cuda):
     assert torch.equal(ft.w_half[2], ft.params[2].detach().half())
 
 
+def test_fused_optimizer_leaves_untouched_groups_and_clears_the_grad(cuda):
+    """The sweep stores nothing for a 4-value group Adam leaves unchanged
+    (moments +0 and gradient +-0 give m' = v' = +0 and p' = p exactly) and
+    clears only the gradient groups with a bit set (-0 included): after one
+    update the untouched groups keep their p / m / v bits, the other groups
+    move as torch's Adam moves them, and the whole gradient is +0."""
+    _, _, _, ft = _setup(cuda)
+    n = ft.params[0].numel() // 4 * 4
+    grp = torch.arange(n, device=cuda) // 4
+    kind = grp % 4  # 0: untouched, 1: gradient only, 2: moments only, 3: untouched with -0 grads
+    gen = torch.Generator(device=cuda).manual_seed(7)
+    g = torch.randn(n, device=cuda, generator=gen) * 0.01
+    g = torch.where(kind == 1, g, torch.zeros_like(g)).half()
+    g[kind == 3] = -0.0
+    ft.grads[0].view(-1)[:n] = g
+    m0 = torch.where(kind == 2, torch.randn(n, device=cuda, generator=gen) * 1e-3, torch.zeros(n, device=cuda))
+    v0 = torch.where(kind == 2, torch.rand(n, device=cuda, generator=gen) * 1e-6, torch.zeros(n, device=cuda))
+    ft.exp_avg[:n] = m0
+    ft.exp_avg_sq[:n] = v0
+    p0 = ft.flat_param[:n].clone()
+    scale = ft.scale
+    ft._optimizer()
+    torch.cuda.synchronize()
+    p1, m1, v1 = ft.flat_param[:n], ft.exp_avg[:n], ft.exp_avg_sq[:n]
+    idle = (kind == 0) | (kind == 3)
+    for a, b in ((p1, p0), (m1, m0), (v1, v0)):
+        assert torch.equal(a[idle].view(torch.int32), b[idle].view(torch.int32))
+    assert int((ft.flat_grad.view(torch.int16) != 0).sum()) == 0  # every bit cleared, -0 too
+    # the moved groups against torch.optim.Adam (+ GradScaler's unscale) from the same state
+    q = torch.nn.Parameter(p0.clone())
+    q.grad = g.float() / scale
+    opt = torch.optim.Adam([q], lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+    opt.state[q] = {"step": torch.tensor(0.0), "exp_avg": m0.clone(), "exp_avg_sq": v0.clone()}
+    opt.step()
+    moved = ~idle
+    assert not torch.equal(p1[moved], p0[moved])
+    # (atol: a tiny v makes some updates ~0.1, p - update then cancels to ~1e-3)
+    assert torch.allclose(p1[moved], q.detach()[moved], rtol=1e-5, atol=1e-6)
+    assert torch.allclose(m1[moved], opt.state[q]["exp_avg"][moved], rtol=1e-5, atol=1e-12)
+    assert torch.allclose(v1[moved], opt.state[q]["exp_avg_sq"][moved], rtol=1e-5, atol=1e-15)
+
+
+def test_march_launch_adam_equals_plain_sweep(cuda):
+    """Adam inside the march launch (the default: the software-pipelined sweep
+    beside the march waves) against the plain sweep of a flush, on the same
+    pending gradient of a fresh table (most groups still untouched, whose
+    stores both sweeps drop): parameters and moments bit for bit, after
+    several steps so the moments are a mix of touched and untouched."""
+    _, _, _, a = _setup(cuda)
+    _, _, _, b = _setup(cuda)
+    for t in (a, b):
+        for _ in range(4):
+            t.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.flat_grad.view(torch.int16), b.flat_grad.view(torch.int16))
+    a.step()   # applies the pending update in its march launch (and runs one more forward/backward)
+    b.flush()  # applies it with the plain sweep
+    torch.cuda.synchronize()
+    assert a._march_adam
+    for x, y in zip(a.params, b.params):
+        assert torch.equal(x.detach(), y.detach())
+    assert torch.equal(a.exp_avg, b.exp_avg) and torch.equal(a.exp_avg_sq, b.exp_avg_sq)
+    idle = ((a.exp_avg == 0) & (a.exp_avg_sq == 0)).float().mean()
+    assert 0.05 < float(idle) < 1.0  # untouched table entries took part
+
+
 def test_fused_optimizer_skips_on_inf(cuda):
     model, ref, data, ft = _setup(cuda)
     before = [p.detach().clone() for p in ft.params]

@@ -231,6 +231,34 @@ struct AdamArgs {
 // index space, chunk c to block c mod gridDim; every thread keeps U 16-byte
 // groups of each stream in flight. A chunk inside one tensor (all but the few
 // at the seams) takes its pointers from scalar loads.
+// The grads are cleared where they are nonzero only (bits, so a -0 too): most
+// of a step's gradient is zero already (the backward writes the entries its
+// samples touch), and a 32-byte sector nobody stores to is never written
+// back. NGP_ADAM_ZERO_ALL (A/B builds only) stores every group.
+typedef _Float16 adam_half4 __attribute__((ext_vector_type(4)));
+NGP_DEV bool grad_set(adam_half4 g) {
+#ifdef NGP_ADAM_ZERO_ALL
+    (void)g;
+    return true;
+#else
+    const uint2 w = __builtin_bit_cast(uint2, g);
+    return (w.x | w.y) != 0u;
+#endif
+}
+// A group Adam leaves exactly as it is: m = v = +0 (never touched; they
+// cannot become -0) and g = +-0 give m' = v' = +0 and p' = p - step * 0 = p,
+// so its stores are dropped (on a hash grid most entries of the fine levels
+// stay untouched). NGP_ADAM_STORE_ALL (A/B builds only) stores every group.
+NGP_DEV bool adam_idle(const float4& m, const float4& v, adam_half4 g) {
+#ifdef NGP_ADAM_STORE_ALL
+    (void)m; (void)v; (void)g;
+    return false;
+#else
+    const uint2 w = __builtin_bit_cast(uint2, g);
+    return ((w.x | w.y) & 0x7fff7fffu) == 0u && m.x == 0.0f && m.y == 0.0f && m.z == 0.0f && m.w == 0.0f &&
+           v.x == 0.0f && v.y == 0.0f && v.z == 0.0f && v.w == 0.0f;
+#endif
+}
 constexpr uint32_t kAdamThreads = 256, kAdamChunk = kAdamThreads * 8;
 // U: 16-byte groups of each stream per thread and chunk (chunk = 1024 U
 // elements). The standalone sweep keeps 2 in flight; the sweep inside the
@@ -278,7 +306,7 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
             for (int u = 0; u < U; ++u) {
                 if (!in[u]) continue;
                 const uint64_t off = base + u * (kChunk / U);
-                if (!skip) {
+                if (!skip && !adam_idle(mv[u], vv[u], gh[u])) {
                     adam1(pv[u].x, mv[u].x, vv[u].x, (float)gh[u][0]);
                     adam1(pv[u].y, mv[u].y, vv[u].y, (float)gh[u][1]);
                     adam1(pv[u].z, mv[u].z, vv[u].z, (float)gh[u][2]);
@@ -290,7 +318,7 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
                         *reinterpret_cast<half4*>(tl.ph[k] + off) =
                             half4{(ngp_half)pv[u].x, (ngp_half)pv[u].y, (ngp_half)pv[u].z, (ngp_half)pv[u].w};
                 }
-                if (aa.zero_grads) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
+                if (aa.zero_grads && grad_set(gh[u])) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
             }
             continue;
         }
@@ -364,7 +392,7 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
         for (int u = 0; u < U; ++u) {
             const uint64_t off = first + tid * 4 + u * (kChunk / U);
             if (off + tl.start[k] >= c1) continue;
-            if (!skip) {
+            if (!skip && !adam_idle(b.m[u], b.v[u], b.g[u])) {
                 ngp_step::adam_update(b.p[u].x, b.m[u].x, b.v[u].x, (float)b.g[u][0], ac, aa.beta1, aa.beta2, aa.eps);
                 ngp_step::adam_update(b.p[u].y, b.m[u].y, b.v[u].y, (float)b.g[u][1], ac, aa.beta1, aa.beta2, aa.eps);
                 ngp_step::adam_update(b.p[u].z, b.m[u].z, b.v[u].z, (float)b.g[u][2], ac, aa.beta1, aa.beta2, aa.eps);
@@ -376,7 +404,7 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
                     *reinterpret_cast<half4*>(tl.ph[k] + off) =
                         half4{(ngp_half)b.p[u].x, (ngp_half)b.p[u].y, (ngp_half)b.p[u].z, (ngp_half)b.p[u].w};
             }
-            if (aa.zero_grads) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
+            if (aa.zero_grads && grad_set(b.g[u])) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
         }
     };
     auto seam = [&](uint64_t c) {  // per element (the few chunks across a tensor boundary)

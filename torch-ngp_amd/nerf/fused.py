@@ -1206,6 +1206,23 @@ class FusedTrainer:
             w.zero_()
         return v
 
+    def adam_groups(self):
+        """World 1, an update pending: the table's 4-parameter groups the
+        pending Adam leaves unchanged (moments and gradient zero: it stores
+        nothing for them), the other groups whose gradient is zero (it does
+        not clear them), and all groups (ngp_head.h adam_idle / grad_set).
+        None when no update is pending or the parameters are sharded."""
+        if self.dp or not self._pending:
+            return None
+        torch.cuda.synchronize()
+        n4 = self.params[0].numel() // 4
+        m = self.exp_avg[:4 * n4].view(-1, 4)
+        v = self.exp_avg_sq[:4 * n4].view(-1, 4)
+        g = self.flat_grad[:4 * n4].view(torch.int16).view(-1, 4)
+        idle = (m == 0).all(1) & (v == 0).all(1) & ((g & 0x7fff) == 0).all(1)
+        zero_g = (g == 0).all(1) & ~idle
+        return int(idle.sum()), int(zero_g.sum()), int(n4)
+
     def fit_exchange(self, margin=2.0):
         """sparse_exchange: size the touched-entry lists to margin x the
         longest list since the last fit (nerf/exchange.py), for the steady
