@@ -672,7 +672,7 @@ def test_step_overflow_skips_via_kernel_flags(cuda):
     before = [p.detach().clone() for p in ft.params]
     ft.step()   # grads overflow
     ft.step()   # applies the pending update (kernel-flag mode): skipped
-    ft.flush()  # the second step's update (sweep mode): skipped as well
+    ft.flush()  # the second step's update (its kernels' flag, as in a step): skipped as well
     torch.cuda.synchronize()
     assert ft.optimizer_steps == 0
     assert ft.scale == 2.0 ** 38

@@ -932,10 +932,12 @@ class FusedTrainer:
             self._ahead = False
         self._tick("grid_encode_backward")
 
-    def _optimizer(self, defer=False):
+    def _optimizer(self, defer=False, prechecked=False):
         """GradScaler inf check + Adam (unscaled fp16 grads, LambdaLR) + scaler
         update. defer: the scaler / LR / loss bookkeeping is left to the next
-        step head (_sample), which runs right after it in a step."""
+        step head (_sample), which runs right after it in a step. prechecked
+        (world 1): the grads are a step's, whose kernels set the found-inf
+        flag, so no sweep over them checks it again."""
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         o, chk, N, cnt = self._opt, nat.check, self.N, P(self.counter)
         # world 1 zeroes the grads here; data parallel: the shard is the reduce-scatter's
@@ -945,9 +947,9 @@ class FusedTrainer:
             self.flat_grad.zero_()
         args = (o["n"], o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
                 self.betas[1], self.eps, self.iters, int(not self.dp), 1.0)
-        # inside a step (world 1) the found-inf flag was set by the backward's kernels;
-        # otherwise (flush, direct calls, the averaged shard) the grads are swept
-        mode = _PRECHECKED if defer and not self.dp else _SCAN
+        # inside a step or a flush (world 1) the found-inf flag was set by the
+        # backward's kernels; otherwise (direct calls, the averaged shard) the grads are swept
+        mode = _PRECHECKED if (defer or prechecked) and not self.dp else _SCAN
         if defer:
             chk(lib.ngp_fused_optimizer_update(*args, mode, P(self.state), s), "fused_optimizer_update")
         else:
@@ -1051,7 +1053,9 @@ class FusedTrainer:
         parameters, or evaluating); data parallel: every rank then holds the
         full fp32 masters and fp16 forward copies."""
         if self._pending:
-            self._optimizer()
+            # the pending grads are the last step's: its kernels (and the
+            # exchange's reduce) set the found-inf flag
+            self._optimizer(prechecked=True)
             self._gather_half(wait=True)
             self._gather_masters()
             self._pending = False
