@@ -28,6 +28,7 @@ def main():
         for name, attrs in (("base", base), ("variant", variant)):
             for k, v in attrs.items():
                 setattr(ft, k, v)
+            ft.capture(warmup=0, multi=args.graph_steps)  # the graphs again, in this form
             c = bench.density_cadence(ft, bits, args)
             print(r, name, c["ms_per_step"], c["parts_ms_per_cycle_synced"], flush=True)
 
