@@ -177,6 +177,32 @@ def test_fused_optimizer_leaves_untouched_groups_and_clears_the_grad(cuda):
     assert torch.allclose(v1[moved], opt.state[q]["exp_avg_sq"][moved], rtol=1e-5, atol=1e-15)
 
 
+def test_adam_groups_count_what_the_sweep_skips(cuda):
+    """FusedTrainer.adam_groups (the bench's algorithmic-byte accounting for the
+    sweep's skipped stores) against a direct count over the pending update's
+    state, and the bytes it leads to between the all-read (16 B) and the
+    all-written (28 B) bounds per table value."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    _, _, _, ft = _setup(cuda)
+    assert ft.adam_groups() is None  # no update pending
+    for _ in range(4):
+        ft.step()
+    idle, zero_g, total = ft.adam_groups()
+    n = ft.params[0].numel() // 4 * 4
+    m, v = ft.exp_avg[:n].view(-1, 4), ft.exp_avg_sq[:n].view(-1, 4)
+    g = ft.flat_grad[:n].float().view(-1, 4)
+    gb = ft.flat_grad[:n].view(torch.int16).view(-1, 4)
+    want_idle = ((m == 0).all(1) & (v == 0).all(1) & (g == 0).all(1))
+    assert idle == int(want_idle.sum()) and total == n // 4 and 0 < idle < total
+    assert zero_g == int(((gb == 0).all(1) & ~want_idle).sum())
+    n_tab = ft.params[0].numel()
+    ab = bench.adam_bytes(ft, (idle, zero_g, total)) - bench.adam_bytes(ft) + 28 * n_tab
+    assert 16 * n_tab < ab < 28 * n_tab
+
+
 def test_march_launch_adam_equals_plain_sweep(cuda):
     """Adam inside the march launch (the default: the software-pipelined sweep
     beside the march waves) against the plain sweep of a flush, on the same
