@@ -186,6 +186,36 @@ def test_grid_forward_fused_bit_exact(cuda, table, layout):
     assert np.all(got[n:] == 7.0)  # rows past the sample count untouched
 
 
+@pytest.mark.parametrize("count", [None, 250001])
+def test_grid_forward_large_batch_lends_chunks_bit_exact(cuda, count):
+    """A density-query-sized batch (>= 2^18 points): the XCDs holding two hashed
+    levels lend a share of their point chunks to the XCDs with a dense level
+    (gridencoder.hip kFwdBorrowPct); every (point, level) is still encoded
+    once, bit-exact vs the oracle, for the full batch and for a sample count
+    that ends mid-chunk (the lent chunks are the last live ones)."""
+    nat = _lib()
+    B, L, H, scale, bound = 300000, 16, 16, LEGO_SCALE, 1.0
+    offs = oracle.grid_offsets(3, L, 2, H, scale, 19)
+    rng = np.random.default_rng(8)
+    emb = (rng.standard_normal((int(offs[-1]), 2)) * 0.1).astype(np.float32)
+    w = _world(B, bound, seed=8)
+    n = B if count is None else count
+    S = float(np.float32(np.log2(scale)))
+    out = torch.full((B, L * 2), 7.0, dtype=torch.float16, device=cuda)
+    wt, et, ot = (torch.from_numpy(a).to(cuda) for a in (w, emb, offs))
+    et = et.half()
+    cnt = torch.tensor([n], dtype=torch.int32, device=cuda) if count is not None else None
+    nat.check(nat.lib().ngp_grid_encode_forward_fused(nat.ptr(wt), bound, nat.ptr(et), nat.DTYPE_CODE[et.dtype],
+                                                      nat.ptr(ot), nat.ptr(out), B,
+                                                      nat.ptr(cnt) if cnt is not None else None, 3, 2, L, S, H,
+                                                      0, 0, 0, 1, nat.stream_of(out)), "grid_forward_fused")
+    torch.cuda.synchronize()
+    ref, _ = oracle.grid_encode_forward(_normalise(w[:n], bound), emb.astype(np.float16), offs, scale, H)
+    got = out.cpu().numpy()
+    assert np.array_equal(got[:n].view(np.uint16), ref.view(np.uint16))
+    assert np.all(got[n:] == 7.0)
+
+
 @pytest.mark.parametrize("log2T,zeroed", [(19, False), (19, True), (22, True), (23, False)])
 def test_grid_backward_fused_flags_nonfinite(cuda, log2T, zeroed):
     """The nonfinite flag is GradScaler's inf check made by the kernels that

@@ -269,6 +269,25 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
 // 0.655-0.668 -> 0.600-0.609 ms, partial unchanged), hence the threshold.
 constexpr uint32_t kFwdLevelsPerBlock = 2;
 constexpr uint32_t kFwdGroupMajorMin = (1u << 22);
+// XCD balance of the level-interleaved forward for large batches (the
+// density queries; 16 levels: one level pair per XCD): the XCDs whose pair is
+// two hashed levels (with a 2^19 table: 5, 6, 7) lend this share of their live
+// point chunks to the five XCDs with a dense level. Same values (the same
+// per-point work, on another XCD). Same-box A/B (profiles/r06_fwd_borrow_ab.txt):
+// density update full 0.576 -> 0.531 ms, partial 0.401 -> 0.374 ms at 15 %
+// (25 %: 0.547 / 0.374); the step's ~80K-point forward is not XCD-bound and
+// lost 1-2 % with it, hence the threshold.
+#ifndef NGP_FWD_BORROW
+#define NGP_FWD_BORROW 15
+#endif
+constexpr uint32_t kFwdBorrowPct = NGP_FWD_BORROW;
+constexpr uint32_t kFwdBorrowMin = 1u << 18;  // points (the grid's B) from which the chunks are lent
+constexpr uint32_t kFwdBorrowDense = 5;       // the dense levels the host sizes the grid for
+__host__ __device__ static inline uint32_t fwd_borrow_pct(uint32_t B) { return B >= kFwdBorrowMin ? kFwdBorrowPct : 0u; }
+__host__ __device__ static inline uint32_t fwd_borrow_extra(uint32_t B) {  // blocks per XCD beyond the chunks
+    const uint32_t ng = (B + 127) / 128 * fwd_borrow_pct(B) / 100;
+    return ((8 - kFwdBorrowDense) * ng + kFwdBorrowDense - 1) / kFwdBorrowDense;
+}
 
 // Levels [lo, hi) of the L-level table (the fused step splits the forward
 // in two launches, each beside a part of the optimizer sweep); blk is the
@@ -290,8 +309,33 @@ NGP_DEV void grid_fwd_pair_block(uint32_t blk, const float* __restrict__ inputs,
     const uint32_t gpx = (lpx + KL - 1) / KL;               // level groups per XCD
     const uint32_t k = blk >> 3;
     const uint32_t nch = (B + 127) / 128;                   // point chunks (grid sized on B)
-    const uint32_t grp = kGroupMajor ? k / nch : k % gpx, chunk = kGroupMajor ? k % nch : k / gpx;
-    const uint32_t level0 = lr.lo + (blk & 7) + 8 * KL * grp;  // this block: level0, level0 + 8, ...
+    uint32_t grp = kGroupMajor ? k / nch : k % gpx, chunk = kGroupMajor ? k % nch : k / gpx;
+    uint32_t xcd = blk & 7;
+    if constexpr (!kGroupMajor && kFwdBorrowPct > 0) {
+        if (lr.lo == 0 && lr.hi == 16 && L == 16 && fwd_borrow_pct(B) > 0) {
+            // dense levels among 0..7 (a hashed level's table is the finest level's size)
+            const uint32_t hmax = (uint32_t)(offsets[16] - offsets[15]);
+            uint32_t nd = 0;
+#pragma unroll
+            for (uint32_t l = 0; l < 8; ++l) nd += (uint32_t)(offsets[l + 1] - offsets[l]) < hmax ? 1u : 0u;
+            if (nd == kFwdBorrowDense) {
+                const uint32_t live = (rows_of(B, im) + 127) / 128;  // chunks with points
+                const uint32_t ng = live * fwd_borrow_pct(B) / 100, nh = 8 - nd;
+                grp = 0;
+                if (xcd >= nd) {  // a pair of hashed levels: its last ng live chunks are lent
+                    chunk = k < live - ng ? k : nch;
+                } else if (k < live) {
+                    chunk = k;
+                } else {  // borrowed: i-th lent chunk, dealt over the dense XCDs
+                    const uint32_t i = (k - live) * nd + xcd;
+                    chunk = i < nh * ng ? live - ng + i / nh : nch;
+                    xcd = i < nh * ng ? nd + i % nh : xcd;
+                }
+                if (chunk >= nch) return;
+            }
+        }
+    }
+    const uint32_t level0 = lr.lo + xcd + 8 * KL * grp;  // this block: level0, level0 + 8, ...
     if (level0 >= lr.hi) return;
     const uint32_t Lfull = L;  // the [B, L, C] layout's row width
     L = lr.hi;                 // the loops below stop at the range's end
@@ -1631,7 +1675,7 @@ int fwd_c(const float* inputs, const void* emb, const int32_t* offsets, void* ou
         const bool gm = B >= kFwdGroupMajorMin;
         const uint32_t kl = gm ? 1u : kFwdLevelsPerBlock;
         const uint32_t gpx = ((L + 7) / 8 + kl - 1) / kl;
-        const dim3 gp(8 * gpx * ngp_div_up(B, 128));
+        const dim3 gp(8 * (gpx * ngp_div_up(B, 128) + (!gm && L == 16 ? fwd_borrow_extra(B) : 0u)));
 #define FWD_PAIR_CASE(CC)                                                                                     \
     (gm ? k_grid_fwd_pair<T, E, D, CC, 1><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, \
                                                              interp, layout, im)                              \
@@ -1876,7 +1920,9 @@ extern "C" int ngp_grid_encode_forward_fused_tail(const float* xyz, float bound,
     const bool ac = align_corners != 0;
     const bool gm = B >= kFwdGroupMajorMin;
     const uint32_t kl = gm ? 1u : kFwdLevelsPerBlock;
-    const uint32_t nfwd = B ? 8u * (((L + 7) / 8 + kl - 1) / kl) * ngp_div_up(B, 128) : 0u;
+    const uint32_t nfwd = B ? 8u * ((((L + 7) / 8 + kl - 1) / kl) * ngp_div_up(B, 128) +
+                                    (!gm && L == 16 ? fwd_borrow_extra(B) : 0u))
+                            : 0u;
     const dim3 grid(nfwd + (ft.end ? 1u : 0u) + (uint32_t)ft.jobs.n);
     if (grid.x == 0) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
