@@ -565,6 +565,7 @@ int ngp_nerf_composite_loss_live(const float* sigma, const void* color_out, cons
  * check as a sweep over the grads; on, with the check already made by the
  * kernels that wrote the grads into the state's flag (ngp_fused_inf_flag). */
 #define NGP_SCALER_OFF 0
+#define NGP_ADAM_SHADOW_ALL 2
 #define NGP_SCALER_SCAN 1
 #define NGP_SCALER_PRECHECKED 2
 /* The state's GradScaler flag (local == 0: the found-inf flag the optimizer
@@ -573,7 +574,9 @@ int ngp_nerf_composite_loss_live(const float* sigma, const void* color_out, cons
 int32_t* ngp_fused_inf_flag(void* state, int32_t local);
 /* Adam (+ GradScaler inf check/unscale/update, LambdaLR 0.1^(epoch/iters))
  * over n_tensors fp32 params with fp16 grads; half_params[k] (nullable) is
- * refreshed with half(p) after the update; grads are zeroed when zero_grads;
+ * refreshed with half(p) where the update changed p (every value with
+ * zero_grads | NGP_ADAM_SHADOW_ALL: a shadow written only now and then);
+ * grads are zeroed when zero_grads & 1;
  * grads are multiplied by grad_mult as well as unscaled (data-parallel mean).
  * step_counter (nullable; pass null when ngp_lego_rays records it) gets
  * counter[0..1] at slot iter % 16. */
@@ -740,9 +743,9 @@ int ngp_density_grid_draw_sorted(const float* grid, uint32_t C, uint32_t H, uint
                                  void* ostat_ws, size_t ostat_ws_bytes, float* xyzs, int32_t* indices, void* stream);
 /* tmp_grid from the densities sigma[0, hi - lo) of ngp_density_grid_draw_sorted's
  * points [lo, hi): a cell's draws are adjacent within a half, so each run's
- * max is stored by its first point (uniform halves), then folded in with
- * max (occupied halves, a second launch): no global atomics. tmp_grid holds
- * -1 where nothing was drawn (as the EMA leaves it). */
+ * max is folded in by its first point with one integer atomic max (exact, in
+ * any order). tmp_grid holds -1 where nothing was drawn (as the EMA leaves
+ * it); densities are >= 0. */
 int ngp_density_grid_run_max(const float* sigma, const int32_t* indices, uint32_t C, uint32_t H, uint32_t lo,
                              uint32_t hi, float* tmp_grid, void* stream);
 /* mean_count after an update (renderer.py:593-595: int(mean of the last

@@ -602,21 +602,25 @@ k_ostat_points(Ostat o, uint32_t chunks, const unsigned long long* __restrict__ 
     }
 }
 
-// The densities of the Morton-ordered points [lo, hi) -> tmp_grid, no global
-// atomics: the draws of one cell are adjacent within a half, so the first point
-// of each run takes the run's max; the uniform halves store it, the occupied
-// halves (a second launch) fold it into what the first left.
+// The densities of the Morton-ordered points [lo, hi) -> tmp_grid: the draws
+// of one cell are adjacent within a half, so the first point of each run takes
+// the run's max and folds it in with one integer atomic max (a cell's runs in
+// the uniform and the occupied half meet there; the two halves as two launches
+// with a plain store and a read-modify-write were one launch more).
 __global__ void __launch_bounds__(256)
 k_density_run_max(const float* __restrict__ sigma, const int32_t* __restrict__ indices, uint32_t lo, uint32_t hi,
-                  uint32_t N, uint32_t half, float* __restrict__ tmp) {
+                  uint32_t N, float* __restrict__ tmp) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x, p = lo + i;
-    if (p >= hi || (p / N & 1u) != half) return;
+    if (p >= hi) return;
     const uint32_t seg_end = min(hi, (p / N + 1) * N);
     const int32_t c = indices[i];
     if (p > lo && p % N != 0 && indices[i - 1] == c) return;  // not the run's first point
     float m = sigma[i];
     for (uint32_t q = p + 1; q < seg_end && indices[q - lo] == c; ++q) m = fmaxf(m, sigma[q - lo]);
-    tmp[c] = half ? fmaxf(tmp[c], m) : m;
+    // a cell can have a run in each half: the max as an integer max of the
+    // float bits (sigma >= 0 and tmp's -1 order as their bits do as signed
+    // integers), exact in any order, in one launch for both halves
+    atomicMax(reinterpret_cast<int*>(tmp) + c, __float_as_int(m));
 }
 
 // The reference's bookkeeping after an update (renderer.py:593-595):
@@ -755,8 +759,7 @@ extern "C" int ngp_density_grid_run_max(const float* sigma, const int32_t* indic
     NGP_REQUIRE(N > 0 && lo <= hi && hi <= C * 2 * N, NGP_ERR_ARG, "density_grid_run_max: bad range");
     if (hi == lo) return NGP_OK;
     hipStream_t st = ngp_stream(stream);
-    for (uint32_t half = 0; half < 2; ++half)
-        k_density_run_max<<<ngp_div_up(hi - lo, 256), 256, 0, st>>>(sigma, indices, lo, hi, N, half, tmp_grid);
+    k_density_run_max<<<ngp_div_up(hi - lo, 256), 256, 0, st>>>(sigma, indices, lo, hi, N, tmp_grid);
     return ngp_check_launch("density_grid_run_max");
 }
 

@@ -275,6 +275,10 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
         if (aa.defer_end) st->end_pending = 1;  // read by k_step_head only
     }
     typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+    // zero_grads bit 1 (NGP_ADAM_SHADOW_ALL): every fp16 shadow value is
+    // written, updated or not (a shadow kept only now and then, the density
+    // query's table copy); otherwise the groups left unchanged keep theirs
+    const bool shadow_all = (aa.zero_grads & 2) != 0;
     auto adam1 = [&](float& p, float& m, float& v, float gh) {
         ngp_step::adam_update(p, m, v, gh, ac, aa.beta1, aa.beta2, aa.eps);
     };
@@ -306,7 +310,8 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
             for (int u = 0; u < U; ++u) {
                 if (!in[u]) continue;
                 const uint64_t off = base + u * (kChunk / U);
-                if (!skip && !adam_idle(mv[u], vv[u], gh[u])) {
+                const bool upd = !skip && !adam_idle(mv[u], vv[u], gh[u]);
+                if (upd) {
                     adam1(pv[u].x, mv[u].x, vv[u].x, (float)gh[u][0]);
                     adam1(pv[u].y, mv[u].y, vv[u].y, (float)gh[u][1]);
                     adam1(pv[u].z, mv[u].z, vv[u].z, (float)gh[u][2]);
@@ -314,10 +319,10 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
                     *reinterpret_cast<float4*>(tl.p[k] + off) = pv[u];
                     *reinterpret_cast<float4*>(tl.m[k] + off) = mv[u];
                     *reinterpret_cast<float4*>(tl.v[k] + off) = vv[u];
-                    if (tl.ph[k])
-                        *reinterpret_cast<half4*>(tl.ph[k] + off) =
-                            half4{(ngp_half)pv[u].x, (ngp_half)pv[u].y, (ngp_half)pv[u].z, (ngp_half)pv[u].w};
                 }
+                if (tl.ph[k] && (upd || shadow_all))
+                    *reinterpret_cast<half4*>(tl.ph[k] + off) =
+                        half4{(ngp_half)pv[u].x, (ngp_half)pv[u].y, (ngp_half)pv[u].z, (ngp_half)pv[u].w};
                 if (aa.zero_grads && grad_set(gh[u])) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
             }
             continue;
@@ -327,14 +332,15 @@ NGP_DEV void adam_sweep(const TensorList& tl, StepState* __restrict__ st, const 
             const int kk = find_tensor(tl, i);
             const uint64_t off = i - tl.start[kk];
             if (off >= tl.size[kk]) continue;  // alignment padding between tensors
+            float p = tl.p[kk][off];
             if (!skip) {
-                float p = tl.p[kk][off], m = tl.m[kk][off], v = tl.v[kk][off];
+                float m = tl.m[kk][off], v = tl.v[kk][off];
                 adam1(p, m, v, (float)tl.g[kk][off]);
                 tl.p[kk][off] = p;
                 tl.m[kk][off] = m;
                 tl.v[kk][off] = v;
-                if (tl.ph[kk]) tl.ph[kk][off] = (ngp_half)p;
             }
+            if (tl.ph[kk] && (!skip || shadow_all)) tl.ph[kk][off] = (ngp_half)p;
             if (aa.zero_grads) tl.g[kk][off] = (ngp_half)0.0f;
         }
     }

@@ -50,6 +50,7 @@ _DEFER, _GEO, _PAIR = 1, 2, 4  # NGP_FFMLP_DEFER_REDUCE, NGP_FFMLP_NERF_GEO, NGP
 _SCAN, _PRECHECKED = 1, 2  # NGP_SCALER_SCAN, NGP_SCALER_PRECHECKED
 _ZEROED, _EXTERNAL = 0x10, 0x20  # NGP_GRID_GRAD_ZEROED, NGP_GRID_CURSORS_EXTERNAL (grad layout 0: [L,M,2])
 _TIMING = 0x40  # NGP_GRID_TIMING
+_SHADOW_ALL = 2  # NGP_ADAM_SHADOW_ALL (zero_grads bit 1)
 
 
 def _vp_array(ptrs):
@@ -368,7 +369,6 @@ class FusedTrainer:
         seed does not depend on the rank), queries its 1/world of them, and a
         MAX all-reduce of the scratch grid gives every rank the same grid and
         bitfield. mean_density stays on the device (`mean_density`)."""
-        self.flush()  # the pending optimizer update first: the query reads the parameters
         m, lib, P_ = self.model, nat.lib(), nat.ptr
         H, C = m.grid_size, m.cascade
         H3 = H ** 3
@@ -390,6 +390,10 @@ class FusedTrainer:
                 table=torch.zeros_like(self.params[0], dtype=torch.float16) if self.table32 else None,
                 mean_count=torch.zeros(1, dtype=torch.int64, device=dev),
                 sigma=torch.zeros(C * H3 // 2 // self.world + 1, device=dev))
+        # the pending optimizer update first (the query reads the parameters);
+        # its sweep writes the query's fp16 table copy as well
+        fresh_table = d["table"] is not None and self._pending and not self.dp
+        self.flush(table_half=d["table"] if fresh_table else None)
         partial = int(m.iter_density >= 16)
         ppc = 2 * (H3 // 4) if partial else H3
         P = C * ppc
@@ -411,7 +415,7 @@ class FusedTrainer:
             nat.check(lib.ngp_density_grid_points(P_(d["coords"]) if partial else None, P_(d["noise"]), P, ppc, C,
                                                   H, float(m.bound), P_(d["xyzs"]), P_(d["idx"]), s),
                       "density_grid_points")
-        if d["table"] is not None:  # world 1 keeps no fp16 table copy: make one for the query
+        if d["table"] is not None and not fresh_table:  # world 1 keeps no fp16 table copy: make one for the query
             d["table"].copy_(self.params[0].detach())
         table = d["table"] if d["table"] is not None else self.w_half[0]
         # the encodings are [L][n][2] (pair-major, row stride n) at the buffer's head
@@ -932,12 +936,14 @@ class FusedTrainer:
             self._ahead = False
         self._tick("grid_encode_backward")
 
-    def _optimizer(self, defer=False, prechecked=False):
+    def _optimizer(self, defer=False, prechecked=False, table_half=None):
         """GradScaler inf check + Adam (unscaled fp16 grads, LambdaLR) + scaler
         update. defer: the scaler / LR / loss bookkeeping is left to the next
         step head (_sample), which runs right after it in a step. prechecked
         (world 1): the grads are a step's, whose kernels set the found-inf
-        flag, so no sweep over them checks it again."""
+        flag, so no sweep over them checks it again. table_half (world 1, fp32
+        table): an fp16 buffer the sweep fills with half(table) as well, every
+        value (NGP_ADAM_SHADOW_ALL; the density query's copy)."""
         lib, P, s = nat.lib(), nat.ptr, nat.stream_of(self.rays_o)
         o, chk, N, cnt = self._opt, nat.check, self.N, P(self.counter)
         # world 1 zeroes the grads here; data parallel: the shard is the reduce-scatter's
@@ -945,8 +951,13 @@ class FusedTrainer:
         # for the next backward in the same graph
         if self.dp:
             self.flat_grad.zero_()
-        args = (o["n"], o["params"], o["grads"], o["m"], o["v"], o["half"], o["sizes"], self.lr, self.betas[0],
-                self.betas[1], self.eps, self.iters, int(not self.dp), 1.0)
+        half, zg = o["half"], int(not self.dp)
+        if table_half is not None:  # the table section first (plan.sections), world 1 only
+            assert not self.dp and self.table32 and self.lo == 0
+            half = _vp_array([nat.ptr(table_half)] + [o["half"][q] for q in range(1, o["n"])])
+            zg |= _SHADOW_ALL
+        args = (o["n"], o["params"], o["grads"], o["m"], o["v"], half, o["sizes"], self.lr, self.betas[0],
+                self.betas[1], self.eps, self.iters, zg, 1.0)
         # inside a step or a flush (world 1) the found-inf flag was set by the
         # backward's kernels; otherwise (direct calls, the averaged shard) the grads are swept
         mode = _PRECHECKED if (defer or prechecked) and not self.dp else _SCAN
@@ -1048,14 +1059,14 @@ class FusedTrainer:
         for _ in range(k):
             self.step()
 
-    def flush(self):
+    def flush(self, table_half=None):
         """Apply the pending optimizer step (before reading or saving the
         parameters, or evaluating); data parallel: every rank then holds the
         full fp32 masters and fp16 forward copies."""
         if self._pending:
             # the pending grads are the last step's: its kernels (and the
             # exchange's reduce) set the found-inf flag
-            self._optimizer(prechecked=True)
+            self._optimizer(prechecked=True, table_half=table_half)
             self._gather_half(wait=True)
             self._gather_masters()
             self._pending = False
