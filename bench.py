@@ -373,18 +373,29 @@ def dp_path_probe(args, model, data, dev, headline):
         three = {"ms_per_step": round(e3 / steps * 1e3, 4), "graphs": bool(g3)}
         del ft3, m3
         # the replicated step (sparse_exchange, DESIGN.md section 7 option B): the
-        # world-1 step graph, then the touched-entry exchange (list, header
-        # all-gather + read-back, list all-gather, sum) after every step
+        # world-1 step graph with the touched-entry exchange captured after its
+        # backward (list kernel, one fixed-size all-gather, reduce kernel; no
+        # host read-back)
         m4, d4, _, _, _, _, _ = make_workload(args.workload, dev, 1, args.num_rays)
         ft4, _ = make_trainer(args, m4, d4, 1, dev, dtg, distributed=True, options=dict(sparse_exchange=True))
         assert ft4.xchg
         e4, g4, _ = timed_run(args, ft4, 1, dev, steps, 5, 300, 1)
         xc = ft4._xchg
+        timed_longest = int(xc.stats[1])  # the timed steps' longest list (statistics restarted by the fit)
+        mean_list = touched_pairs(ft4)["pairs_per_step"]
+        fit_peak = getattr(ft4, "xchg_fit_peak", None)
         sparse = {"ms_per_step": round(e4 / steps * 1e3, 4), "graphs": bool(g4),
                   "whole_step_graph": ft4.graph is not None, "list_cap": xc.cap,
-                  "longest_list": int(xc.stats[1]), "list_bytes_per_rank": xc.bytes_per_step()[0],
+                  "fit": "2 x the longest list of the trailing settle block (statistics restarted before it)",
+                  "fit_window_longest_list": fit_peak, "longest_list": timed_longest,
+                  "mean_list": mean_list,
+                  "longest_over_mean": round(timed_longest / mean_list, 3) if mean_list else None,
+                  "cap_over_longest": round(xc.cap / max(timed_longest, 1), 3),
+                  "list_bytes_per_rank": xc.bytes_per_step()[0],
                   "pairs_total": int(xc.pairs), "overflows": xc.overflows,
-                  "per_rank_bytes_8_ranks": {"send": xc.bytes_per_step()[0], "receive": 7 * xc.bytes_per_step()[0]}}
+                  "per_rank_bytes_8_ranks": {"send": xc.bytes_per_step()[0], "receive": 7 * xc.bytes_per_step()[0],
+                                             "zero1_reduce_scatter_plus_all_gather":
+                                                 int(2 * 2 * ft4.total * 7 / 8)}}
         del ft4, m4
         grad_bytes = 2 * ft.total  # the flat fp16 gradient = the fp16 forward copy
         truck_bytes = 2 * _flat_total(22)
@@ -652,11 +663,17 @@ def timed_run(args, ft, world, dev, steps, warmup, settle, graph_steps):
     # fixed number of untimed steps (same on every rank: they hold
     # collectives) runs before the timed region.
     for i in range(0, settle, 64):
+        if ft.xchg and i > 0 and i + 64 >= settle:
+            # the lists are fitted on a trailing window: the statistics restart
+            # before the last settle block, so the early-training peak (12x
+            # the steady longest list in round 5) does not size them
+            ft._xchg.reset_stats()
         ft.run(min(64, settle - i))
         torch.cuda.synchronize()
     if ft.xchg:
         # the replicated step's touched-entry lists sized for the steady regime
-        # (2 x the longest list of the settle steps; graphs captured again)
+        # (2 x the longest list of the trailing settle block; graphs captured again)
+        ft.xchg_fit_peak = int(ft._xchg.stats[1])
         ft.fit_exchange(2.0)
         ft.run(max(2, graph_steps))
     torch.cuda.synchronize()

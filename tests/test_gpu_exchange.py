@@ -124,6 +124,49 @@ def test_exchange_kernels_exact_mean(parity_report, world):
                   f"numpy's exact fp64 mean rounded once to fp16")
 
 
+def _tie_grads(rng, n, world):
+    """Per-rank fp16 gradients whose exact mean is an fp16 rounding tie at
+    every value (a mean formed with the inexact reciprocal of
+    2^24 * world rounds twice and may leave a tie on the wrong side). Value j:
+    tie m = x + ulp(x)/2 for a random normal x; ranks 1.. take random fp16
+    values, rank 0 the remainder world * m - rest when that is an fp16 value
+    (rejection sampling over candidates)."""
+    out = np.zeros((world, n), dtype=np.float16)
+    filled = np.zeros(n, dtype=bool)
+    while not filled.all():
+        k = int((~filled).sum())
+        x = (rng.uniform(0.25, 64.0, 8 * k) * rng.choice([-1.0, 1.0], 8 * k)).astype(np.float16)
+        xd = x.astype(np.float64)
+        ulp = np.abs(np.nextafter(x, np.float16(np.inf) * np.sign(x)).astype(np.float64) - xd)
+        m = xd + np.sign(xd) * ulp / 2
+        rest = (rng.uniform(-4.0, 4.0, (world - 1, 8 * k)) * (rng.random((world - 1, 8 * k)) < 0.7)).astype(np.float16)
+        r0 = world * m - rest.astype(np.float64).sum(0)
+        ok = (np.abs(r0) < 60000) & (r0.astype(np.float16).astype(np.float64) == r0)
+        idx = np.nonzero(~filled)[0][:int(ok.sum())]
+        sel = np.nonzero(ok)[0][:idx.size]
+        out[0, idx] = r0[sel].astype(np.float16)
+        out[1:, idx] = rest[:, sel]
+        filled[idx] = True
+    return list(out)
+
+
+@pytest.mark.parametrize("world", [3, 5, 6, 7])
+def test_exchange_mean_rounds_ties_once(parity_report, world):
+    nat = _lib()
+    dev = torch.device("cuda:0")
+    n = 8 * 1024
+    gs = _tie_grads(np.random.default_rng(100 + world), n, world)
+    exact = np.sum([g.astype(np.float64) for g in gs], axis=0) / world  # every value is an fp16 tie
+    assert (exact.astype(np.float16).astype(np.float64) != exact).all()
+    sends = [_list(nat, g, dev) for g in gs]
+    out, inf, _ = _reduce(nat, sends, n, dev, n // 2)
+    want = exact.astype(np.float16)  # numpy: one correctly rounded conversion (ties to even)
+    ne = out.view(np.uint16) != want.view(np.uint16)
+    assert not ne.any(), (int(ne.sum()), np.argwhere(ne)[:4].ravel().tolist())
+    parity_report(f"grad exchange kernels, world {world}: {n} means that are fp16 ties, each rounded once "
+                  f"(ties to even), bit-identical to numpy")
+
+
 def test_exchange_nonfinite_raises_every_rank_flag():
     nat = _lib()
     dev = torch.device("cuda:0")

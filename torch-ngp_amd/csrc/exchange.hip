@@ -20,14 +20,19 @@
 // A rank with more nonzero pairs than cap lists only cap of them; every rank
 // sees that in the gathered headers, and every rank skips the update (the
 // GradScaler flag's bit 1: no scale back-off) instead of applying a partial
-// sum; the host grows cap (nerf/exchange.py).
+// sum; the host sees that in the exchange's statistics and grows cap at its
+// next check (SparseExchange.check, run from FusedTrainer.flush).
 //
 // Reduction. One workgroup per bin sums every rank's items of the bin into
 // an LDS image of int64 values in 2^-24 fixed point (fp16 values are
 // multiples of 2^-24 and at most 65504: exact, so the order the LDS atomics
 // land in does not matter), then writes the whole bin of the gradient densely
-// as fp16(sum / world): every rank rounds the same exact mean once, and the
-// ranks' parameters stay bit-identical with no parameter collective.
+// as fp16(sum / world): the integer sum (< 2^49) and 2^24 * world are exact
+// doubles, so the double quotient is the correctly rounded mean; it is exact
+// whenever the mean is an fp16 tie, and otherwise lies too far from any fp16
+// tie for the double rounding to cross one (world < 2^10), so fp16() of it
+// rounds the exact mean once. Every rank computes the same bits, and the ranks'
+// parameters stay bit-identical with no parameter collective.
 #include "ngp_common.h"
 
 namespace {
@@ -162,14 +167,14 @@ k_xchg_reduce(const int64_t* __restrict__ recv, uint32_t world, uint64_t stride,
     __syncthreads();
     // the bin's values, 8 per thread per round (16-B stores); an overflowed
     // exchange leaves zeros (the update is skipped on every rank)
-    const double inv = 1.0 / (kFixed * (double)world);
+    const double den = kFixed * (double)world;  // exact; divided, not multiplied by an inexact reciprocal
     const uint64_t v0 = (uint64_t)bin * 2 * kBinPairs;
     typedef _Float16 half8 __attribute__((ext_vector_type(8)));
     for (uint32_t c = threadIdx.x; c < 2 * kBinPairs / 8; c += kThreads) {
         if (v0 + 8 * c >= n_values) break;  // n_values % 8 == 0
         half8 o;
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) o[k] = (ngp_half)((double)(long long)acc[8 * c + k] * inv);
+        for (uint32_t k = 0; k < 8; ++k) o[k] = (ngp_half)((double)(long long)acc[8 * c + k] / den);
         *reinterpret_cast<half8*>(grad + v0 + 8 * c) = o;
     }
 }
@@ -203,7 +208,7 @@ extern "C" int ngp_grad_exchange_reduce(const void* recv, int32_t world, uint32_
                                         uint64_t n_values, int32_t* inf_flag, int32_t* stats, void* send,
                                         void* stream) {
     NGP_REQUIRE(recv && grad_half && inf_flag && stats, NGP_ERR_ARG, "grad_exchange_reduce: null pointer");
-    NGP_REQUIRE(world >= 1, NGP_ERR_ARG, "grad_exchange_reduce: world >= 1");
+    NGP_REQUIRE(world >= 1 && world < 1024, NGP_ERR_ARG, "grad_exchange_reduce: 1 <= world < 1024 (the mean's single rounding)");
     NGP_REQUIRE(n_values % 8 == 0 && n_values / 2 < 0xffffffffull, NGP_ERR_ARG,
                 "grad_exchange_reduce: n_values % 8 == 0 and n_values / 2 < 2^32");
     NGP_REQUIRE((reinterpret_cast<uintptr_t>(grad_half) & 15) == 0, NGP_ERR_ARG,

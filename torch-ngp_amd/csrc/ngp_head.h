@@ -364,6 +364,10 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
         if (ac.inv_bad) st->found_inf = 1;
         if (aa.defer_end) st->end_pending = 1;
     }
+    // NGP_ADAM_SHADOW_ALL as in adam_sweep: every fp16 shadow value written,
+    // updated or not (the flag meant the same in both sweeps only
+    // while no caller passed it here)
+    const bool shadow_all = (aa.zero_grads & 2) != 0;
     const uint64_t total = tl.start[tl.n];
     const uint64_t nchunks = (total + kChunk - 1) / kChunk;
     struct Buf {
@@ -398,7 +402,8 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
         for (int u = 0; u < U; ++u) {
             const uint64_t off = first + tid * 4 + u * (kChunk / U);
             if (off + tl.start[k] >= c1) continue;
-            if (!skip && !adam_idle(b.m[u], b.v[u], b.g[u])) {
+            const bool upd = !skip && !adam_idle(b.m[u], b.v[u], b.g[u]);
+            if (upd) {
                 ngp_step::adam_update(b.p[u].x, b.m[u].x, b.v[u].x, (float)b.g[u][0], ac, aa.beta1, aa.beta2, aa.eps);
                 ngp_step::adam_update(b.p[u].y, b.m[u].y, b.v[u].y, (float)b.g[u][1], ac, aa.beta1, aa.beta2, aa.eps);
                 ngp_step::adam_update(b.p[u].z, b.m[u].z, b.v[u].z, (float)b.g[u][2], ac, aa.beta1, aa.beta2, aa.eps);
@@ -406,10 +411,10 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
                 st_f4(tl.p[k] + off, b.p[u]);
                 st_f4(tl.m[k] + off, b.m[u]);
                 st_f4(tl.v[k] + off, b.v[u]);
-                if (tl.ph[k])
-                    *reinterpret_cast<half4*>(tl.ph[k] + off) =
-                        half4{(ngp_half)b.p[u].x, (ngp_half)b.p[u].y, (ngp_half)b.p[u].z, (ngp_half)b.p[u].w};
             }
+            if (tl.ph[k] && (upd || shadow_all))
+                *reinterpret_cast<half4*>(tl.ph[k] + off) =
+                    half4{(ngp_half)b.p[u].x, (ngp_half)b.p[u].y, (ngp_half)b.p[u].z, (ngp_half)b.p[u].w};
             if (aa.zero_grads && grad_set(b.g[u])) *reinterpret_cast<half4*>(tl.g[k] + off) = half4{0, 0, 0, 0};
         }
     };
@@ -419,14 +424,15 @@ NGP_DEV void adam_sweep_pipe(const TensorList& tl, StepState* __restrict__ st, c
             const int kk = find_tensor(tl, i);
             const uint64_t off = i - tl.start[kk];
             if (off >= tl.size[kk]) continue;
+            float p = tl.p[kk][off];
             if (!skip) {
-                float p = tl.p[kk][off], m = tl.m[kk][off], v = tl.v[kk][off];
+                float m = tl.m[kk][off], v = tl.v[kk][off];
                 ngp_step::adam_update(p, m, v, (float)tl.g[kk][off], ac, aa.beta1, aa.beta2, aa.eps);
                 tl.p[kk][off] = p;
                 tl.m[kk][off] = m;
                 tl.v[kk][off] = v;
-                if (tl.ph[kk]) tl.ph[kk][off] = (ngp_half)p;
             }
+            if (tl.ph[kk] && (!skip || shadow_all)) tl.ph[kk][off] = (ngp_half)p;
             if (aa.zero_grads) tl.g[kk][off] = (ngp_half)0.0f;
         }
     };

@@ -26,13 +26,18 @@ to a margin over the longest list of the steps since the last fit, once
 training is in its steady regime. A list longer than that is seen by every
 rank in the gathered headers: every rank then skips the update (without a
 scale back-off) and counts it in `overflows`, which the bench requires to be
-0 over its timed region.
+0 over its timed region. `check` (run by FusedTrainer.flush, i.e. at every
+density update, checkpoint and read-out) reads that count: after a new
+overflow it warns and grows the lists to twice the longest list seen (and at
+least twice their capacity), and the trainer captures its graphs again.
 
 Per step a rank sends its list buffer (8 bytes per item of capacity) and
 receives the other ranks'; the dense ZeRO-1 step (nerf/zero1.py) moves
 2 x (world - 1) / world of the flat fp16 buffer instead (byte counts in
 DESIGN.md §7).
 """
+import warnings
+
 import torch
 import torch.distributed as dist
 
@@ -54,6 +59,8 @@ class SparseExchange:
         self.n_bins = int(nat.lib().ngp_grad_exchange_bins(self.n))
         # device: [overflowed exchanges, the largest list seen]
         self.stats = torch.zeros(2, dtype=torch.int32, device=flat_grad.device)
+        self.seen_overflows = 0  # overflows `check` has already answered
+        self.grown = 0           # resizes `check` made
         self.resize(cap if cap is not None else self.pairs)
 
     def resize(self, cap):
@@ -76,7 +83,33 @@ class SparseExchange:
         if peak > 0:
             self.resize(int(peak * margin) + 1024)
         self.stats.zero_()
+        self.seen_overflows = 0
         return self.cap
+
+    def reset_stats(self):
+        """Restart the statistics (the longest list, the overflow count), so a
+        later `fit` sizes the lists on the steps after this call only."""
+        self.stats.zero_()
+        self.seen_overflows = 0
+
+    def check(self):
+        """After an overflow since the last check (a host read of the device
+        statistics, the same on every rank: they come from the gathered
+        headers), warn and grow the lists to 2 x the longest list seen and at
+        least 2 x the old capacity. Returns True when it resized (graphs that
+        hold the old buffers must be captured again)."""
+        over, peak = (int(v) for v in self.stats.tolist())
+        if over <= self.seen_overflows:
+            return False
+        self.seen_overflows = over
+        if self.cap >= self.pairs:
+            return False
+        old = self.cap
+        self.resize(max(2 * peak + 1024, 2 * old))
+        self.grown += 1
+        warnings.warn(f"SparseExchange: {over} update(s) skipped since the lists overflowed (longest list {peak} > "
+                      f"capacity {old}); lists grown to {self.cap} items", RuntimeWarning, stacklevel=3)
+        return True
 
     @property
     def overflows(self):

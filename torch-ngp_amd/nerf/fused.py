@@ -1070,6 +1070,10 @@ class FusedTrainer:
             self._gather_half(wait=True)
             self._gather_masters()
             self._pending = False
+        # sparse_exchange: lists that overflowed since the last flush are grown
+        # (a skipped update is never silent)
+        if self._xchg is not None and self._xchg.check():
+            self._recapture()
 
     def capture(self, warmup=2, ring=0, multi=1):
         """hipGraph(s) of the step body. World 1: one graph (optimizer of the
@@ -1103,6 +1107,9 @@ class FusedTrainer:
             return
         if not self.dp:
             self._ring, self._ring_i = [], 0  # step() would replay an older timing ring first
+            if self._xchg is not None and self._nccl:
+                self._capture_replicated(multi)
+                return
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._xbody(True, graph=True)
@@ -1173,6 +1180,45 @@ class FusedTrainer:
             self.graph = graphs
         # capture recorded the launches without running them: the pending
         # update is still pending and the next step() replays it first
+
+    def _capture_replicated(self, multi):
+        """sparse_exchange over RCCL: the world-1 body graphs with the
+        exchange's all-gather inside them. Every rank takes the same form
+        (ADVICE r05): a capture that fails on one rank would leave it eager
+        while the others replay graphs, and their collective sequences would
+        differ. Capture records without running, so no collective has run."""
+        self.graph = self._fresh = self.graph_multi = None
+        self._multi = 1
+        ahead = self._ahead
+        err = None
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._xbody(True, graph=True)
+            gf = None
+            if self._draw_ahead and self._ahead:
+                gf = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gf):
+                    self._xbody(False, graph=True)
+            gm = None
+            if multi > 1:
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm):
+                    for _ in range(multi):
+                        self._xbody(True, graph=True)
+        except RuntimeError as e:  # a stack that cannot capture the collective
+            err = e
+        torch.cuda.synchronize()
+        ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=self.dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            print(f"FusedTrainer: replicated-step capture failed on {'this' if err is not None else 'another'} rank "
+                  f"({err!r:.200}); eager steps on every rank", file=sys.stderr)
+            self._ahead = ahead  # the batch state before the recording
+            return
+        self.graph, self._fresh = g, gf
+        if gm is not None:
+            self.graph_multi, self._multi = gm, multi
 
     # ----------------------------------------------------------- read-outs
     def _state_f(self):
@@ -1247,12 +1293,16 @@ class FusedTrainer:
         if self._xchg is None:
             return None
         cap = self._xchg.fit(margin)
+        self._recapture()
+        return cap
+
+    def _recapture(self):
+        """Capture the graphs again (they hold the exchange's old buffers)."""
         if self.graph is not None or self._ring:
             ring, multi = len(self._ring), self._multi
             self.capture(warmup=0, multi=multi)
             if ring:  # (the plain capture drops the timing ring)
                 self.capture(warmup=0, ring=ring)
-        return cap
 
     @property
     def exchange_overflows(self):
