@@ -54,7 +54,7 @@ def _normalise(w, bound):
 
 
 def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, reps=1, layout=1, flag=None,
-         zeroed=False):
+         zeroed=False, external=False):
     B = w.shape[0]
     S = float(np.float32(np.log2(scale)))
     offs_host = np.ascontiguousarray(offs, dtype=np.int32)
@@ -67,12 +67,18 @@ def _bwd(nat, dev, g16, w, offs, L, H, scale, bound, count=None, table=None, rep
     if layout == 0:  # [L, B, C]
         gt = gt.view(B, L, 2).permute(1, 0, 2).contiguous()
     cnt = torch.tensor([count], dtype=torch.int32, device=dev) if count is not None else None
+    # NGP_GRID_CURSORS_EXTERNAL (0x20): the caller clears the bin cursors, as
+    # the fused step does; with a zeroed grad the hashed levels' bins then go
+    # one per wave (gridencoder.hip wave_bin) instead of the workgroup image
+    cbytes = int(nat.lib().ngp_grid_encode_backward_fused_counter_bytes(B, 3, 2, L, S, H, 0, hp))
     for _ in range(reps):
         nat.check(nat.lib().ngp_grid_encode_backward_fused(
             nat.ptr(gt), nat.ptr(wt), float(bound), nat.ptr(ot), nat.ptr(table), B,
             nat.ptr(cnt) if cnt is not None else None, 3, 2, L, S, H, 0, 0, 0, hp,
-            nat.ptr(ws), ws.numel(), layout | (0x10 if zeroed else 0), nat.ptr(flag) if flag is not None else None,
-            nat.stream_of(table)), "grid_backward_fused")
+            nat.ptr(ws), ws.numel(), layout | (0x10 if zeroed else 0) | (0x20 if external else 0),
+            nat.ptr(flag) if flag is not None else None, nat.stream_of(table)), "grid_backward_fused")
+        if external:
+            ws[:cbytes].zero_()
     torch.cuda.synchronize()
     # the workspace's counters are left zeroed for the next call
     assert int(ws[:256].sum()) == 0
@@ -117,6 +123,33 @@ def test_grid_backward_fused_vs_oracle(cuda, case):
     x = _normalise(w, bound)
     ref = oracle.grid_encode_backward(g16, x, offs, 2, scale, H)
     _check_levels(got, ref, offs, layout)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[4] <= 22] + [(40000, 12, 16, 1.5, 19, "spill")],
+                         ids=lambda c: f"B{c[0]}L{c[1]}T{c[4]}{c[5]}")
+def test_grid_backward_wave_bins_equal_image_path(cuda, parity_report, case):
+    """The hashed levels' bins summed one per wave (cursors cleared by the
+    caller, grad zeroed: the fused step's configuration) against the same
+    bins through the workgroup image (the cursors left to the kernel):
+    bit-identical table grads, including bins that spilled past their
+    capacity (the 0.03-wide cube) and 2^22-entry levels; and two wave-path
+    calls give the same bits. (2^23-entry levels are past the binned prefix:
+    their fp16 atomics add in arrival order, so that case is not compared.)"""
+    nat = _lib()
+    B, L, H, scale, log2T, layout = case
+    bound = 1.0 if layout != "rays" else 2.0
+    offs = oracle.grid_offsets(3, L, 2, H, scale, log2T)
+    conc = {"concentrated": 0.25, "spill": 0.03}.get(layout, 0.0)
+    w = _world(B, bound, seed=B + L, concentrated=conc, ordered=layout == "rays")
+    g16 = (np.random.default_rng(5).standard_normal((B, L * 2)) * 0.5).astype(np.float16)
+    img = _bwd(nat, cuda, g16, w, offs, L, H, scale, bound, zeroed=True)
+    wave = _bwd(nat, cuda, g16, w, offs, L, H, scale, bound, zeroed=True, external=True)
+    again = _bwd(nat, cuda, g16, w, offs, L, H, scale, bound, zeroed=True, external=True)
+    ne = img.view(np.uint32) != wave.view(np.uint32)
+    assert not ne.any(), (int(ne.sum()), np.argwhere(ne.any(1))[:4].ravel().tolist())
+    assert np.array_equal(wave.view(np.uint32), again.view(np.uint32))
+    parity_report(f"grid backward wave bins {layout} B{B} L{L} T2^{log2T}: {int((wave != 0).any(1).sum())} "
+                  f"entries, bit-identical to the workgroup image path")
 
 
 def test_grid_backward_fused_bin_overflow(cuda):
@@ -216,13 +249,14 @@ def test_grid_forward_large_batch_lends_chunks_bit_exact(cuda, count):
     assert np.all(got[n:] == 7.0)
 
 
-@pytest.mark.parametrize("log2T,zeroed", [(19, False), (19, True), (22, True), (23, False)])
-def test_grid_backward_fused_flags_nonfinite(cuda, log2T, zeroed):
+@pytest.mark.parametrize("log2T,zeroed,external", [(19, False, False), (19, True, False), (22, True, False),
+                                                    (23, False, False), (19, True, True), (22, True, True)])
+def test_grid_backward_fused_flags_nonfinite(cuda, log2T, zeroed, external):
     """The nonfinite flag is GradScaler's inf check made by the kernels that
     write the grads: an inf output grad, or finite terms whose fp16 sum
     overflows, must set it, on the binned levels (read-modify-write, fresh
     per-entry and per-item flushes) and (T = 2^23: levels past the binned
-    prefix) the scanned ones."""
+    prefix) the scanned ones; external: the hashed levels' wave bins."""
     nat = _lib()
     B, L, H, scale = 20000, 16, 16, LEGO_SCALE
     offs = oracle.grid_offsets(3, L, 2, H, scale, log2T)
@@ -232,9 +266,9 @@ def test_grid_backward_fused_flags_nonfinite(cuda, log2T, zeroed):
         g = g16.copy()
         g[B // 2, 2 * lvl] = np.float16(np.inf)
         flag = torch.zeros(1, dtype=torch.int32, device=cuda)
-        _bwd(nat, cuda, g, w, offs, L, H, scale, 1.0, flag=flag, zeroed=zeroed)
+        _bwd(nat, cuda, g, w, offs, L, H, scale, 1.0, flag=flag, zeroed=zeroed, external=external)
         assert int(flag.item()) == 1, ("inf grad", lvl)
     big = np.full((B, L * 2), 60000.0, np.float16)  # finite terms, their fp16 sums overflow
     flag = torch.zeros(1, dtype=torch.int32, device=cuda)
-    _bwd(nat, cuda, big, w, offs, L, H, scale, 1.0, flag=flag, zeroed=zeroed)
+    _bwd(nat, cuda, big, w, offs, L, H, scale, 1.0, flag=flag, zeroed=zeroed, external=external)
     assert int(flag.item()) == 1, "sum overflow"

@@ -15,7 +15,7 @@ for v in "$@"; do
 done
 for i in 1 2; do
     for v in base "$@"; do
-        NGP_HIP_LIB=$(lib $v) timeout -k 10 200 python -u bench.py --no-cpu --no-legs --no-dp-path --no-render --steps 200 --warmup 20 \
+        NGP_HIP_LIB=$(lib $v) timeout -k 10 200 python -u bench.py --no-cpu --no-legs --no-dp-path --no-render --steps 200 --warmup 20 ${BENCH_ARGS:-} \
             > $O/$v$i.json 2> $O/$v$i.err
         python -c "import json; d=json.load(open('$O/$v$i.json')); print('$v', $i, d['value'], d['ms_per_step'], {k: round(v * 1000, 1) for k, v in d['kernels_ms'].items()}, d.get('density_update_ms'))"
     done

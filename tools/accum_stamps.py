@@ -46,6 +46,37 @@ print(json.dumps({"steps": STEPS, "samples": ft.sample_count(), "live_frac": ft.
 st = stamps[:32768].view(-1, 64).cpu().numpy().astype(np.int64)  # accumulate: 2 workgroups per CU
 nwg = int((st[:, 0] > 0).sum())
 st = st[:nwg]
+wr = st[:, 10] > 0  # wave-bin workgroups (gridencoder.hip wave_bin): their own phase clocks
+st_all, wr_all = st.copy(), wr.copy()
+ws = stamps[131072:131072 + 4096 * 4].view(-1, 4).cpu().numpy().astype(np.int64)
+ws = ws[ws[:, 1] > 0]
+if len(ws):
+    n, lvw, dur = ws[:, 0] & 0xffffffff, (ws[:, 0] >> 32) & 0xff, ws[:, 2] - ws[:, 1]
+    order = np.argsort(dur)[::-1][:12]
+    print(json.dumps({"wave_bins": {"bins": int(len(ws)), "dur_pct": [int(x) for x in np.percentile(dur, [10, 50, 90, 99, 100])],
+                                    "n_pct": [int(x) for x in np.percentile(n, [10, 50, 90, 100])],
+                                    "spilled": int(((ws[:, 0] >> 40) & 1).sum()),
+                                    "slowest": [[int(dur[i]), int(n[i]), int(lvw[i]), int(ws[i, 3])] for i in order],
+                                    "corr_n_dur": float(np.corrcoef(n, dur)[0, 1])}}))
+if wr.any():
+    w = st[wr]
+    t0w = st[:, 0].min()
+    print(json.dumps({"wave_role": {
+        "workgroups": int(wr.sum()),
+        "entry_med": int(np.median(w[:, 0] - t0w)), "entry_max": int(np.max(w[:, 0] - t0w)),
+        "lds_zero_med": int(np.median(w[:, 10] - w[:, 0])),
+        "count_load_med": int(np.median(w[w[:, 11] > 0, 11] - w[w[:, 11] > 0, 10])) if (w[:, 11] > 0).any() else None,
+        "bitmap_med": int(np.median(w[w[:, 12] > 0, 12] - w[w[:, 12] > 0, 11])) if (w[:, 12] > 0).any() else None,
+        "passes_med": int(np.median(w[w[:, 13] > 0, 13] - w[w[:, 13] > 0, 12])) if (w[:, 13] > 0).any() else None,
+        "wave0_total_med": int(np.median(w[:, 14] - w[:, 0])), "wave0_total_max": int(np.max(w[:, 14] - w[:, 0])),
+        "end_med_rel": int(np.median(w[:, 14] - t0w)), "end_max_rel": int(np.max(w[:, 14] - t0w))}}))
+    if (~wr).any():
+        im = st[~wr]
+        print(json.dumps({"image_role": {"workgroups": int((~wr).sum()),
+                                         "entry_med": int(np.median(im[:, 0] - t0w)),
+                                         "prologue_med": int(np.median(im[:, 1] - im[:, 0]))}}))
+    st = st[~wr] if (~wr).any() else st
+    nwg = len(st)
 t0 = st[:, 0].min()
 res = {"workgroups": nwg, "kernel_cycles": int(max(st[i, 4 + 5 * (int(st[i, 3]) - 1) + 2] if st[i, 3] else st[i, 2]
                                                     for i in range(nwg)) - t0)}
@@ -84,7 +115,8 @@ print(json.dumps(res, indent=1))
 # counter init, after corners + ranks, after reservation + scan, after
 # staging, end
 b = stamps[32768:32768 + 16 * 4096].view(-1, 16).cpu().numpy().astype(np.int64)
-gx = (ft.M + 511) // 512  # bin-kernel workgroups per level (kBinPts samples each)
+BP = int(os.environ.get("BIN_PTS", "512"))
+gx = (ft.M + BP - 1) // BP  # bin-kernel workgroups per level (kBinPts samples each)
 blevel = np.arange(len(b)) // gx
 bidx = np.arange(len(b))[b[:, 0] > 0]  # linear workgroup id: XCD = id % 8 (each XCD has its own clock)
 blevel = blevel[b[:, 0] > 0]  # workgroups past the sample count leave before stamping
@@ -99,6 +131,20 @@ print(json.dumps({"bin_workgroups": int(len(b)),
                   "bin_phase_p90": [int(x) for x in np.percentile(d, 90, axis=0)],
                   "bin_phases": (["loads", "corners+merge", "rank"] if d.shape[1] == 6 else ["corners+rank"])
                   + ["reserve+scan", "stage", "write-out"]}))
+# chip-wide 100 MHz realtime clock: the bin workgroups' [start, end] (slots
+# 8, 9) and the accumulate workgroups' (60, 61), relative to the first bin start
+if (b[:, 8] > 0).all() and (st_all[:, 60] > 0).all():
+    r0 = b[:, 8].min()
+    tl = {"bin_start_us": [round((x - r0) / 100, 2) for x in np.percentile(b[:, 8], [0, 50, 100])],
+          "bin_end_us": [round((x - r0) / 100, 2) for x in np.percentile(b[:, 9], [0, 50, 90, 100])],
+          "bin_wg_dur_us": [round(x / 100, 2) for x in np.percentile(b[:, 9] - b[:, 8], [10, 50, 90, 100])],
+          "acc_start_us": [round((x - r0) / 100, 2) for x in np.percentile(st_all[:, 60], [0, 50, 100])],
+          "acc_end_us": [round((x - r0) / 100, 2) for x in np.percentile(st_all[:, 61], [0, 50, 90, 100])]}
+    if wr.any():
+        for nm, sel in (("wave", wr_all), ("image", ~wr_all)):
+            if sel.any():
+                tl[nm + "_end_us"] = [round((x - r0) / 100, 2) for x in np.percentile(st_all[sel, 61], [0, 50, 90, 100])]
+    print(json.dumps({"timeline": tl}))
 per = {}
 for lv in np.unique(blevel):
     per[int(lv)] = [int(x) for x in np.median(d[blevel == lv], axis=0)]
@@ -123,6 +169,8 @@ if hasattr(lib, "ngp_debug_mlp_stamps"):
                     break
                 chunk_t.append(r[k] - prev)
                 prev = r[k]
+        if not chunk_t:
+            continue
         out[name] = {"waves": int(len(w)), "frag_copy_med": int(np.median(w[:, 1] - w[:, 0])),
                      "chunk_med": int(np.median(chunk_t)), "chunk_p90": int(np.percentile(chunk_t, 90)),
                      "chunks_per_wave_max": int(max(np.count_nonzero(r[2:12]) for r in w)),

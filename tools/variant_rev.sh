@@ -12,7 +12,7 @@ out=$R/torch-ngp_amd/variants/$NAME
 mkdir -p "$out"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function"
 objs=""
-for o in ngp_lib gridencoder raymarching shencoder ffmlp adam nerf_fused density_grid freqencoder; do
+for o in ngp_lib gridencoder raymarching shencoder ffmlp adam nerf_fused density_grid freqencoder exchange; do
     if [[ " $* " == *" $o "* ]]; then
         git -C "$R" show "$REV:torch-ngp_amd/csrc/$o.hip" > "$C/.rev_$o.hip"
         /opt/rocm/bin/hipcc $FLAGS -c "$C/.rev_$o.hip" -o "$out/$o.o"

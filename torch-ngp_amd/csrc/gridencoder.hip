@@ -671,8 +671,14 @@ static_assert(kBinShift >= 9 && kBinShift <= 16, "12 must be in [9, 16]");
 static_assert(kSegItems > 0, "16384 must be positive");
 // Levels up to this resolution merge runs of equal corners in-wave: on the
 // Lego step the merge cuts their items 3.5-16x (tools/grid_bwd_micro.py);
-// finer levels gain less than the scan costs.
-constexpr uint32_t kMergeMaxRes = 128;
+// finer levels gain less than the scan costs. Round 7: 128 -> 256. The live
+// rows are runs of consecutive samples at the surface, which share corners up
+// to res ~300: unmerged, levels 7-8's bins held ~4 items per distinct entry
+// (per-wave stamps, r07h); same box +3.5 % (r07i: m256 vs base).
+#ifndef NGP_MERGE_MAX_RES
+#define NGP_MERGE_MAX_RES 256
+#endif
+constexpr uint32_t kMergeMaxRes = NGP_MERGE_MAX_RES;
 
 struct BinPlan {
     uint32_t nlev;                   // levels [0, nlev) are binned
@@ -689,6 +695,8 @@ struct BinPlan {
     uint32_t mslot0[kMaxLevels];     // first slot of the level's bins, or kNoSlot
     uint32_t nmslots;
     uint32_t spill_entries;          // table entries of the binned levels (the spill image's size)
+    uint32_t img_bins;               // bins of the leading dense levels (z-slab bins); the rest are hashed
+    uint32_t off[kMaxLevels + 1];    // the levels' first table entries (offsets), levels [0, nlev]
 };
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
@@ -710,7 +718,23 @@ NGP_DEV uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-constexpr uint32_t kBinPts = 512;  // samples (threads) per bin-kernel workgroup
+#ifndef NGP_BIN_PTS
+#define NGP_BIN_PTS 512
+#endif
+constexpr uint32_t kBinPts = NGP_BIN_PTS;  // samples (threads) per bin-kernel workgroup
+#ifndef NGP_BIN_WAVES
+#define NGP_BIN_WAVES 6
+#endif
+constexpr uint32_t kBinWavesPerSimd = NGP_BIN_WAVES;  // the bin kernel's occupancy bound (8: <= 64 VGPRs, spills)
+#ifndef NGP_SPLIT_BITS
+#define NGP_SPLIT_BITS 6
+#endif
+constexpr uint32_t kSplitBits = NGP_SPLIT_BITS;  // levels of <= 2^kSplitBits bins rank by wave multisplit
+static_assert(kBinPts % 64 == 0 && kBinPts >= 128 && kBinPts <= 1024, "whole waves, 2..16 per workgroup");
+#ifndef NGP_BIN_YCAP
+#define NGP_BIN_YCAP 0xffffffffu
+#endif
+constexpr uint32_t kBinYCap = NGP_BIN_YCAP;  // point blocks per level in the grid (each workgroup loops)
 // NGP_GRID_TIMING ring (u32 words): [0] calls, heads {start, samples,
 // accumulate workgroups, -} from word 64, per-workgroup ends from kTimingEnds
 constexpr uint32_t kTimingHeads = 64, kTimingEnds = kTimingHeads + 4 * NGP_GRID_TIMING_RING;
@@ -727,10 +751,13 @@ __device__ unsigned long long* g_stamps;
 // cannot order workgroups against each other)
 #define BRSTAMP(slot) do { if (g_stamps && threadIdx.x == 0) g_stamps[32768 + (size_t)stamp_id * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define RSTAMP(slot) STAMP(slot, __builtin_amdgcn_s_memrealtime())
+// per wave (lane 0) of the accumulate's wave bins: [n | level << 32 | spilled << 40, start, end]
+#define WSTAMP(slot, v) do { if (g_stamps && (threadIdx.x & 63) == 0) g_stamps[131072 + (size_t)(blockIdx.x * (kAccThreads / 64) + (threadIdx.x >> 6)) * 4 + (slot)] = (v); } while (0)
 // after the wave's outstanding loads have arrived
 #define BSTAMPW(slot) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); BSTAMP(slot); } while (0)
 #else
 #define BSTAMPW(slot) do { } while (0)
+#define WSTAMP(slot, v) do { } while (0)
 #define BRSTAMP(slot) do { } while (0)
 #define RSTAMP(slot) do { } while (0)
 #define STAMP(slot, v) do { } while (0)
@@ -749,7 +776,7 @@ struct BinLego {
 };
 
 template <uint32_t D, uint32_t NBMAX>
-__global__ void __launch_bounds__(kBinPts, 8)  // 4 workgroups per CU: <= 64 VGPRs
+__global__ void __launch_bounds__(kBinPts, kBinWavesPerSimd * 256 / kBinPts)  // kBinWavesPerSimd waves per SIMD
 k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
                const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
                uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
@@ -796,10 +823,14 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // first and alone when the grid was level-major: 9-16 us per workgroup
     // against 6-8 us on the fine levels) shares the CUs with the fine levels'
     // latency-bound work
-    const uint32_t level = blockIdx.x, chunk = blockIdx.y;
-    [[maybe_unused]] const uint32_t stamp_id = level * gridDim.y + chunk;
+    // A workgroup takes point blocks blockIdx.y, blockIdx.y + gridDim.y, ...:
+    // the host may cap the grid's height below the row capacity (most of a
+    // capacity-sized grid exits at once in the live-row regime)
+    const uint32_t level = blockIdx.x;
     const uint32_t rows = rows_of(B, im);
-    if (chunk * kBinPts >= rows) return;
+    for (uint32_t chunk = blockIdx.y; chunk * kBinPts < rows; chunk += gridDim.y) {
+    if (chunk != blockIdx.y) __syncthreads();  // the last block's write-out has read the LDS
+    [[maybe_unused]] const uint32_t stamp_id = level * gridDim.y + chunk;
     const uint32_t nb = bp.nbins[level];
     const bool merge = (bp.merge_mask >> level) & 1u;
     const int lane = (int)(threadIdx.x & 63);
@@ -894,80 +925,55 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     }
 #pragma unroll
     for (uint32_t idx = 0; idx < NC; idx++) val[idx] = ngp_half2{(ngp_half)vv[idx][0], (ngp_half)vv[idx][1]};
-    // Rank within the bin. When every live item of the wave (all corners) is
-    // in one bin -- the dense levels' z-slab bins, where all the workgroup's
-    // waves hit the same counter -- the wave takes its whole run with ONE LDS
-    // atomic (same-address LDS atomics serialize: 8 per wave were ~half of
-    // those levels' bin time, tools/accum_stamps.py); otherwise per corner:
-    // one atomic per wave when the wave's items of that corner share a bin,
-    // else one per item.
-    // On levels with few bins (dense levels: z-slab bins) a wave's items fall
-    // in a handful of bins: up to kMatchIters distinct bins over all corners
-    // are matched first (per-item atomics there were 2-3 counters hit by every
-    // lane, serialized: corners + rank 15-29 K cycles on levels 0-4 against
-    // 8 K on the hashed ones, tools/accum_stamps.py). Lane i keeps match i's
-    // bin and item count, and ONE LDS atomic instruction reserves every
-    // matched bin's run at once; each item then adds its match's base (one
-    // lane permute). Items left over (and every item of a many-bin level)
-    // take the per-corner path.
-    constexpr uint32_t kMatchIters = 8, kMatchMaxBins = 64;
-    static_assert(kMatchIters <= 64, "one lane per match");
+    // Rank within the bin (the item's slot in the workgroup's run of its bin).
+    // On levels of at most 2^kSplitBits bins (round 7) the ranks come from a
+    // wave multisplit: per corner, the lanes whose items share my bin
+    // are found with one ballot per bin bit (no LDS), the lowest of them
+    // reserves the group's run with one LDS atomic (one instruction for all
+    // of the wave's groups, distinct addresses) and a lane permute hands the
+    // base to the others. The match loop this replaced (up to 8 rounds of 8
+    // ballots and read-lanes, then per-item atomics on the few counters every
+    // lane hits) was the bin launch's critical path in the live-row regime:
+    // 12-16 K cycles on the dense levels against ~3-4 K elsewhere (phase
+    // clocks, r07c). Other levels: one LDS atomic per wave when the corner's
+    // items share one bin, else one per item.
     BSTAMP(6);
-    uint64_t pend[NC];
-    uint32_t mit[NC];  // the item's match, or kMatchIters (none)
+    const uint32_t nbits = nb > 1 ? 32u - (uint32_t)__builtin_clz(nb - 1u) : 0u;
 #pragma unroll
-    for (uint32_t idx = 0; idx < NC; idx++) {
-        pend[idx] = __ballot(live[idx]);
-        rank[idx] = 0;
-        mit[idx] = kMatchIters;
-    }
-    uint32_t nmatch = 0, m_bin = 0, m_total = 0;
-    for (; nb <= kMatchMaxBins && nmatch < kMatchIters; ++nmatch) {
-        uint32_t bf = 0xffffffffu;
-#pragma unroll
-        for (uint32_t idx = 0; idx < NC; idx++)
-            if (bf == 0xffffffffu && pend[idx])
-                bf = __builtin_amdgcn_readlane(key[idx], __ffsll((unsigned long long)pend[idx]) - 1) >> kBinShift;
-        if (bf == 0xffffffffu) break;
-        uint32_t run = 0;
+    for (uint32_t idx = 0; idx < NC; idx++) rank[idx] = 0;
+    if (nbits <= kSplitBits) {
 #pragma unroll
         for (uint32_t idx = 0; idx < NC; idx++) {
-            const uint64_t m = __ballot(live[idx] && (key[idx] >> kBinShift) == bf);
-            if ((m >> lane) & 1ull) {
-                rank[idx] = run + lanes_below(m);
-                mit[idx] = nmatch;
+            const uint32_t bin = key[idx] >> kBinShift;  // garbage for a dead item: it is not in any ballot
+            uint64_t m = __ballot(live[idx]);
+            for (uint32_t bt = 0; bt < nbits; ++bt) {
+                const bool bit = ((bin >> bt) & 1u) != 0;
+                const uint64_t bb = __ballot(live[idx] && bit);
+                m &= bit ? bb : ~bb;
             }
-            run += (uint32_t)__popcll(m);
-            pend[idx] &= ~m;
+            // m (live lanes): the lanes whose item of this corner is in my bin
+            const int leader = m ? __ffsll((unsigned long long)m) - 1 : lane;
+            uint32_t base = 0;
+            if (live[idx] && lane == leader) base = atomicAdd(&cnt[bin], (uint32_t)__popcll(m));
+            base = (uint32_t)__shfl((int)base, leader, 64);
+            if (live[idx]) rank[idx] = base + lanes_below(m);
         }
-        if ((uint32_t)lane == nmatch) {
-            m_bin = bf;
-            m_total = run;
-        }
-    }
-    if (nmatch) {
-        uint32_t base = 0;
-        if ((uint32_t)lane < nmatch) base = atomicAdd(&cnt[m_bin], m_total);
+    } else {
 #pragma unroll
         for (uint32_t idx = 0; idx < NC; idx++) {
-            const uint32_t bm = __shfl(base, (int)(mit[idx] & 63u), 64);
-            if (mit[idx] < kMatchIters) rank[idx] += bm;
-        }
-    }
-#pragma unroll
-    for (uint32_t idx = 0; idx < NC; idx++) {
-        const uint64_t lm = pend[idx];
-        if (!lm) continue;
-        const bool mine = (lm >> lane) & 1ull;
-        const uint32_t bin = key[idx] >> kBinShift;
-        const int first = __ffsll((unsigned long long)lm) - 1;
-        const uint32_t bf = __builtin_amdgcn_readlane(bin, first);
-        if (__ballot(mine && bin != bf) == 0) {
-            uint32_t r0 = 0;
-            if (lane == first) r0 = atomicAdd(&cnt[bf], (uint32_t)__popcll(lm));
-            if (mine) rank[idx] = __builtin_amdgcn_readlane(r0, first) + lanes_below(lm);
-        } else if (mine) {
-            rank[idx] = atomicAdd(&cnt[bin], 1u);
+            const uint64_t lm = __ballot(live[idx]);
+            if (!lm) continue;
+            const bool mine = (lm >> lane) & 1ull;
+            const uint32_t bin = key[idx] >> kBinShift;
+            const int first = __ffsll((unsigned long long)lm) - 1;
+            const uint32_t bf = __builtin_amdgcn_readlane(bin, first);
+            if (__ballot(mine && bin != bf) == 0) {
+                uint32_t r0 = 0;
+                if (lane == first) r0 = atomicAdd(&cnt[bf], (uint32_t)__popcll(lm));
+                if (mine) rank[idx] = __builtin_amdgcn_readlane(r0, first) + lanes_below(lm);
+            } else if (mine) {
+                rank[idx] = atomicAdd(&cnt[bin], 1u);
+            }
         }
     }
     lds_barrier();
@@ -1059,6 +1065,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     }
     BSTAMP(4);
     BRSTAMP(9);
+    }
 }
 
 // Persistent accumulation: every workgroup reads all bins' counts, forms the
@@ -1084,6 +1091,237 @@ static_assert(kMaxLevels <= 64, "the accumulate finds a bin's level with one wav
 static_assert(kBinEntries % kAccThreads == 0, "each flush thread owns whole entries (G > 0)");
 // the int64 LDS image of one bin (+ the counts in dynamic LDS) fits a CU's 160 KB
 static_assert(kBinEntries * 2 * sizeof(unsigned long long) <= 128 * 1024, "bin image exceeds LDS");
+// Wave bins (round 7). In the live-row regime a hashed level's bin holds a few
+// dozen to a few hundred items (Lego: ~120 of 4096 entries), and the
+// workgroup image above spends most of its ~5.5 K cycles per unit zeroing,
+// draining and flushing behind workgroup barriers, after a prologue that reads
+// every bin's count (phase clocks, tools/accum_stamps.py). Here ONE WAVE owns
+// a bin and needs no barrier and no prologue: it reads its own bin's count,
+//   1. marks its items' entries in a 4096-bit LDS bitmap (ds_or),
+//   2. ranks the marked entries (popcounts + one wave scan): entry e of the
+//      bin gets a compact index among the bin's distinct entries,
+//   3. adds every item's exact int64 2^-24 counts at its compact index
+//      (ds_add_u64; integers, so the sum does not depend on the order),
+//   4. walks the marked bits and stores each distinct entry's fp16 once.
+// Same sums, same single rounding as the image path: the grads are bit-for-
+// bit those of the workgroup image. A wave holds kWaveAcc distinct entries at a
+// time; a bin with more runs steps 3-4 once per range of compact indices. LDS
+// ops of one wave complete in issue order, so the phases need only the wave's
+// own lgkmcnt waits. Used for the hashed levels of a cleared grad whose
+// cursors the caller clears (the fused step); the dense levels (z-slab bins,
+// thousands of items) keep the workgroup image.
+constexpr uint32_t kWaveWords = kBinEntries / 32;                      // bitmap words per bin
+constexpr uint32_t kWaveLdsUll = kBinEntries * 2 / (kAccThreads / 64);  // int64 words of LDS per wave
+constexpr uint32_t kWaveAcc = (kWaveLdsUll - kWaveWords) / 2;          // distinct entries per pass (448)
+#ifndef NGP_WAVE_Q
+#define NGP_WAVE_Q 8
+#endif
+constexpr uint32_t kWaveQ = NGP_WAVE_Q;  // items per lane in flight (a bin of <= 64 kWaveQ items: one load round)
+#ifndef NGP_WAVE_BINS
+#define NGP_WAVE_BINS 1
+#endif
+constexpr bool kWaveBins = NGP_WAVE_BINS != 0;  // (0: the image path for every bin, A/B builds)
+#ifndef NGP_ACC_IMAGE_WGS
+#define NGP_ACC_IMAGE_WGS 128
+#endif
+constexpr uint32_t kAccImageWgs = NGP_ACC_IMAGE_WGS;  // workgroups of the image path beside the wave bins
+static_assert(kWaveWords == 128, "two bitmap words per lane");
+
+NGP_DEV void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+NGP_DEV void wave_bin(uint32_t gb, uint32_t level, uint32_t lbin, uint32_t cap, uint32_t item0, uint32_t off0,
+                      uint32_t off1, const uint32_t* __restrict__ cursor,
+                      const BinItem* __restrict__ items, ngp_half* __restrict__ grad_grid,
+                      int32_t* __restrict__ nonfinite, unsigned long long* __restrict__ spill,
+                      uint32_t* __restrict__ spill_bad, uint32_t* bm, uint32_t* pre, unsigned long long* sums,
+                      uint32_t lane) {
+    constexpr uint32_t C = 2;
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(items + item0 + (size_t)lbin * cap);
+    // the first kWaveQ x 64 item slots are requested beside the count (slots
+    // past the count hold stale items and are masked below; clamped to the
+    // bin's capacity, so every address is the bin's own)
+    uint64_t it[kWaveQ];
+#pragma unroll
+    for (uint32_t q = 0; q < kWaveQ; ++q) it[q] = __builtin_nontemporal_load(src + min(q * 64 + lane, cap - 1u));
+    const uint32_t raw = cursor[gb];
+    STAMP(11, raw ? __builtin_amdgcn_s_memtime() : 0ull);
+    if (raw == 0) return;
+    WSTAMP(0, (unsigned long long)min(raw, cap) | ((unsigned long long)level << 32) | ((unsigned long long)(raw > cap) << 40));
+    WSTAMP(1, __builtin_amdgcn_s_memtime());
+    const uint32_t n = min(raw, cap);
+    const bool spilled = raw > cap;
+    const uint32_t e0 = lbin * kBinEntries;
+    const uint32_t ne = min(kBinEntries, off1 - off0 - e0);
+    const size_t ebase = (size_t)off0 + e0;
+    ngp_half2* tbl = reinterpret_cast<ngp_half2*>(grad_grid + ebase * C);
+    unsigned long long* sp = spill + 2 * ebase;
+    // a bin of at most 64 kWaveQ items stays in registers; a larger one is
+    // read again in each step (L2-warm)
+    const bool one = n <= 64 * kWaveQ;
+    auto load = [&](uint32_t k0) {
+#pragma unroll
+        for (uint32_t q = 0; q < kWaveQ; ++q) {
+            const uint32_t k = k0 + q * 64 + lane;
+            it[q] = k < n ? __builtin_nontemporal_load(src + k) : ~0ull;
+        }
+    };
+    auto mask = [&]() {
+#pragma unroll
+        for (uint32_t q = 0; q < kWaveQ; ++q)
+            if (q * 64 + lane >= n) it[q] = ~0ull;
+    };
+    // 1. bitmap of the bin's entries
+    bool bad = false;
+    for (uint32_t k0 = 0; k0 < n; k0 += 64 * kWaveQ) {
+        if (k0) load(k0);
+        else mask();
+#pragma unroll
+        for (uint32_t q = 0; q < kWaveQ; ++q) {
+            if (it[q] == ~0ull) continue;
+            const uint32_t e = (uint32_t)it[q] & (kBinEntries - 1), v = (uint32_t)(it[q] >> 32);
+            bad |= ((v >> 10) & 31u) == 31u || ((v >> 26) & 31u) == 31u;
+            atomicOr(&bm[e >> 5], 1u << (e & 31));
+        }
+    }
+    if (spilled) {  // entries past the bin's capacity went to the spill image (rare)
+        for (uint32_t e = lane; e < ne; e += 64) {
+            const ulonglong2 x = reinterpret_cast<const ulonglong2*>(sp)[e];
+            if (x.x | x.y) atomicOr(&bm[e >> 5], 1u << (e & 31));
+        }
+        if (lane == 0 && spill_bad[gb]) {
+            bad = true;
+            spill_bad[gb] = 0u;
+        }
+    }
+    lds_wait();
+    STAMP(12, __builtin_amdgcn_s_memtime());
+    // 2. compact index of each marked entry: prefix of the popcounts
+    const uint32_t w0 = bm[2 * lane], w1 = bm[2 * lane + 1];
+    const uint32_t c0 = (uint32_t)__popc(w0), cnt = c0 + (uint32_t)__popc(w1);
+    const uint32_t incl = ngp_dpp::scan_incl_u32(cnt);
+    const uint32_t distinct = __builtin_amdgcn_readlane(incl, 63);
+    pre[2 * lane] = incl - cnt;
+    pre[2 * lane + 1] = incl - cnt + c0;
+    lds_wait();
+    auto cidx = [&](uint32_t e) {  // compact index of a marked entry
+        const uint32_t w = bm[e >> 5];
+        return pre[e >> 5] + (uint32_t)__popc(w & ((1u << (e & 31)) - 1u));
+    };
+    const bool unit_bad = __ballot(bad) != 0;
+    const float q24 = 1.0f / 16777216.0f;
+    bool inf_out = false;
+    auto out_of = [&](const ulonglong2& xs, bool& store) {
+        const int64_t x0 = (int64_t)xs.x, x1 = (int64_t)xs.y;
+        store = !unit_bad && (x0 != 0 || x1 != 0);
+        const ngp_half2 o{(ngp_half)((float)x0 * q24), (ngp_half)((float)x1 * q24)};
+        if (store) inf_out |= !__builtin_isfinite((float)o[0]) || !__builtin_isfinite((float)o[1]);
+        return o;
+    };
+    if (one && !spilled && distinct <= kWaveAcc) {
+        // the common case: every item in registers, one range of sums. Each
+        // item stores its entry's sum (items of one entry store the same
+        // value); all LDS reads before the stores, no store in a loop (the
+        // compiler waits for a store's data before reusing its registers)
+        uint32_t ci[kWaveQ];
+#pragma unroll
+        for (uint32_t q = 0; q < kWaveQ; ++q)
+            ci[q] = it[q] == ~0ull ? 0xffffffffu : cidx((uint32_t)it[q] & (kBinEntries - 1));
+#pragma unroll
+        for (uint32_t q = 0; q < kWaveQ; ++q) {
+            if (ci[q] == 0xffffffffu) continue;
+            const uint32_t v = (uint32_t)(it[q] >> 32);
+            atomicAdd(&sums[2 * ci[q]], (unsigned long long)half_fixed24(v & 0xffffu));
+            atomicAdd(&sums[2 * ci[q] + 1], (unsigned long long)half_fixed24(v >> 16));
+        }
+        lds_wait();
+        ulonglong2 xs[kWaveQ];
+#pragma unroll
+        for (uint32_t q = 0; q < kWaveQ; ++q)
+            xs[q] = ci[q] == 0xffffffffu ? ulonglong2{0ull, 0ull} : reinterpret_cast<const ulonglong2*>(sums)[ci[q]];
+        lds_wait();  // every read is done before any clear
+#pragma unroll
+        for (uint32_t q = 0; q < kWaveQ; ++q)
+            if (ci[q] != 0xffffffffu) reinterpret_cast<ulonglong2*>(sums)[ci[q]] = ulonglong2{0ull, 0ull};
+#pragma unroll
+        for (uint32_t q = 0; q < kWaveQ; ++q) {
+            bool store;
+            const ngp_half2 o = out_of(xs[q], store);
+            if (store) tbl[(uint32_t)it[q] & (kBinEntries - 1)] = o;
+        }
+    } else {
+        for (uint32_t r0 = 0; r0 < distinct; r0 += kWaveAcc) {
+            // 3. exact sums of this range's entries
+            for (uint32_t k0 = 0; k0 < n; k0 += 64 * kWaveQ) {
+                if (!one || r0 > 0) load(k0);
+#pragma unroll
+                for (uint32_t q = 0; q < kWaveQ; ++q) {
+                    if (it[q] == ~0ull) continue;
+                    const uint32_t e = (uint32_t)it[q] & (kBinEntries - 1), v = (uint32_t)(it[q] >> 32);
+                    const uint32_t i = cidx(e) - r0;
+                    if (i >= kWaveAcc) continue;
+                    atomicAdd(&sums[2 * i], (unsigned long long)half_fixed24(v & 0xffffu));
+                    atomicAdd(&sums[2 * i + 1], (unsigned long long)half_fixed24(v >> 16));
+                }
+            }
+            if (spilled) {
+                for (uint32_t e = lane; e < ne; e += 64) {
+                    const ulonglong2 x = reinterpret_cast<const ulonglong2*>(sp)[e];
+                    if (!(x.x | x.y)) continue;
+                    const uint32_t i = cidx(e) - r0;
+                    if (i >= kWaveAcc) continue;
+                    atomicAdd(&sums[2 * i], x.x);
+                    atomicAdd(&sums[2 * i + 1], x.y);
+                }
+            }
+            lds_wait();
+            // 4. each distinct entry of the range once: the lane owning its
+            // bitmap word reads the sums and stores the fp16 pair, kFlushB at
+            // a time (all reads of a batch before its stores)
+            constexpr uint32_t kFlushB = 8;
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                uint32_t w = h ? w1 : w0;
+                uint32_t rank = h ? pre[2 * lane] + c0 : pre[2 * lane];
+                while (w) {
+                    uint32_t ent[kFlushB];
+                    ulonglong2 xs[kFlushB];
+#pragma unroll
+                    for (uint32_t j = 0; j < kFlushB; ++j) {
+                        ent[j] = 0xffffffffu;
+                        xs[j] = ulonglong2{0ull, 0ull};
+                        if (!w) continue;
+                        const uint32_t bt = (uint32_t)__builtin_ctz(w);
+                        w &= w - 1u;
+                        const uint32_t i = rank++ - r0;
+                        if (i >= kWaveAcc) continue;
+                        ent[j] = (2 * lane + h) * 32 + bt;
+                        xs[j] = reinterpret_cast<const ulonglong2*>(sums)[i];
+                    }
+#pragma unroll
+                    for (uint32_t j = 0; j < kFlushB; ++j) {
+                        bool store;
+                        const ngp_half2 o = out_of(xs[j], store);
+                        if (store && ent[j] != 0xffffffffu) tbl[ent[j]] = o;
+                    }
+                }
+            }
+            lds_wait();  // every read of the range is done before any clear
+            for (uint32_t i = lane; i < min(kWaveAcc, distinct - r0); i += 64)
+                reinterpret_cast<ulonglong2*>(sums)[i] = ulonglong2{0ull, 0ull};
+        }
+    }
+    STAMP(13, __builtin_amdgcn_s_memtime());
+    if (spilled)  // folded: clear the bin's slice of the spill image for the next call
+        for (uint32_t e = lane; e < ne; e += 64) reinterpret_cast<ulonglong2*>(sp)[e] = ulonglong2{0ull, 0ull};
+    bm[2 * lane] = 0u;
+    bm[2 * lane + 1] = 0u;
+    lds_wait();
+    if (unit_bad && !nonfinite && lane == 0) tbl[0] = ngp_half2{(ngp_half)__builtin_nanf(""), (ngp_half)0.0f};
+    if (nonfinite && (__ballot(inf_out) != 0 || unit_bad) && lane == 0) atomicOr(nonfinite, 1);
+    WSTAMP(2, __builtin_amdgcn_s_memtime());
+    WSTAMP(3, distinct);
+}
+
 // ZEROED (the fused step: NGP_GRID_GRAD_ZEROED) drops the read-back of owned
 // slices (non-fresh owners occur only with a grad that was not zeroed) and the
 // registers it holds.
@@ -1095,7 +1333,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                  bool external, unsigned long long* __restrict__ msums,
                  uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing,
                  int32_t* __restrict__ reset_counter, unsigned long long* __restrict__ spill,
-                 uint32_t* __restrict__ spill_bad) {
+                 uint32_t* __restrict__ spill_bad, uint32_t wave_bins0, uint32_t nimg) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     // [entry][channel]; a channel-planar image (8-byte lane stride for the
     // 64-bit atomics instead of 16) measured the same
@@ -1104,7 +1342,11 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     __shared__ uint32_t wsum[NW];
     __shared__ uint32_t s_last, s_bad;
     extern __shared__ uint32_t dyn[];
-    const uint32_t nbins = bp.total_bins;
+    // bins [wave_bins0, total) go one per wave (wave_bin) to the workgroups
+    // from nimg on; the first nimg workgroups run the image path over the
+    // bins before wave_bins0 (wave_bins0 = total: every workgroup, every bin)
+    const uint32_t nbins = min(wave_bins0, bp.total_bins);
+    const bool wave_role = nbins < bp.total_bins && blockIdx.x >= nimg;
     STAMP(0, __builtin_amdgcn_s_memtime());
     RSTAMP(60);
     uint32_t* upre = dyn;              // [nbins + 1] first unit of each bin
@@ -1119,6 +1361,24 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // the sample counter of the batch whose backward this is, once every
     // kernel that reads it has finished (the bin launch drew the next batch)
     if (reset_counter && blockIdx.x == 0 && t < 2) reset_counter[t] = 0;
+    if (wave_role) {
+        // no plan copy and no barrier: a wave's level and plan entries are
+        // wave-uniform, read from the kernel arguments with scalar loads
+        unsigned long long* wl = acc + wv * kWaveLdsUll;  // this wave's 8 KB: bitmap, prefix, sums
+        for (uint32_t i = lane; i < kWaveLdsUll / 2; i += 64) reinterpret_cast<ulonglong2*>(wl)[i] = ulonglong2{0ull, 0ull};
+        STAMP(10, __builtin_amdgcn_s_memtime());
+        const uint32_t nw = (gridDim.x - nimg) * NW;
+        uint32_t lv = 0;
+        for (uint32_t gb = nbins + (blockIdx.x - nimg) * NW + wv; gb < bp.total_bins; gb += nw) {
+            gb = __builtin_amdgcn_readfirstlane(gb);
+            while (lv + 1 < nlev && gb >= bp.bin0[lv + 1]) ++lv;
+            wave_bin(gb, lv, gb - bp.bin0[lv], bp.cap[lv], bp.item0[lv], bp.off[lv], bp.off[lv + 1], cursor, items,
+                     grad_grid, nonfinite, spill, spill_bad, reinterpret_cast<uint32_t*>(wl),
+                     reinterpret_cast<uint32_t*>(wl) + kWaveWords, wl + kWaveWords, lane);
+        }
+        STAMP(14, __builtin_amdgcn_s_memtime());
+        __syncthreads();  // the workgroup's end below is its last wave's
+    } else {
     // the first group of this thread's bin counts (step 1 below) is loaded
     // before anything else: its round trip overlaps the plan's LDS copy
     constexpr uint32_t kStep1Loads = 4;
@@ -1127,17 +1387,21 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
     for (uint32_t j = 0; j < kStep1Loads; ++j) {
         const uint32_t b = t * per + j;
-        cv0[j] = j < per && b < nbins ? cursor[b] : 0u;
+        cv0[j] = !wave_role && j < per && b < nbins ? cursor[b] : 0u;
     }
     if (t <= nlev) {
-        s_bin0[t] = t < nlev ? bp.bin0[t] : nbins;
-        s_off[t] = (uint32_t)offsets[t];
+        s_bin0[t] = t < nlev ? bp.bin0[t] : bp.total_bins;
+        s_off[t] = bp.off[t];  // (the plan's host copy: no global load ahead of the first barrier)
         if (t < nlev) {
             s_cap[t] = bp.cap[t];
             s_item0[t] = bp.item0[t];
             s_mslot0[t] = bp.mslot0[t];
         }
     }
+    // the image starts zeroed (while the counts are in flight)
+    for (uint32_t i = t; i < kBinEntries * C / 2; i += kAccThreads)
+        reinterpret_cast<uint4*>(acc)[i] = uint4{0u, 0u, 0u, 0u};
+    if (t == 0) s_bad = 0;
     lds_barrier();
     auto level_of = [&](uint32_t b) {  // last level whose first bin is <= b (binary lifting)
         uint32_t l = 0;
@@ -1291,7 +1555,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // units run in bin order, so round 0's first workgroups hold the coarse
     // levels' long units (up to 4x the items of a fine-level unit); dealt
     // forward they also got a round-2 unit and finished last.
-    const uint32_t ngr = gridDim.x, full = total / ngr;
+    const uint32_t ngr = nbins < bp.total_bins ? nimg : gridDim.x, full = total / ngr;
     auto unit_at = [&](uint32_t k) {  // this workgroup's k-th unit, or total (none)
         const uint32_t uk = k < full ? k * ngr + blockIdx.x : full * ngr + (ngr - 1 - blockIdx.x);
         return k <= full && uk < total ? uk : total;
@@ -1310,7 +1574,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // unit. The entries are kept in ent[] (the prefetch overwrites it[]).
     constexpr uint32_t kSparseQ = 4, kSparseMax = kSparseQ * kAccThreads;
     static_assert(kSparseQ <= kAccBatch, "a sparse unit is one item batch");
-    bool need_zero = true;  // the image holds entries no flush cleared (initially: all of it)
+    bool need_zero = false;  // the image holds entries no flush cleared (zeroed at the start)
     for (uint32_t k = 0; u < total; ++k) {
         // (clearing each entry in the flush right after reading it, by the
         // same lane -- no zeroing pass -- gave wrong sums on the GPU; the
@@ -1487,6 +1751,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         cur = nxt;
         u = un;
     }
+    }  // image role
     RSTAMP(61);
     // launch timing (NGP_GRID_TIMING): every workgroup stores its end in the
     // call's ring entry (one vector store each, no atomics, so the timed
@@ -1524,6 +1789,7 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
         if (nb > kMaxBinsPerLevelBig || bins + nb > kMaxTotalBins) break;
         const double side = (double)(align_corners ? lv.res[l] : lv.res[l] + 1);
         const bool hashed = std::pow(side, (double)D) > (double)hs;
+        if (!hashed && bp.img_bins == bins) bp.img_bins = bins + nb;  // still in the dense prefix
         const uint64_t cap = hashed ? std::min<uint64_t>(items_all, 2 * ((items_all + nb - 1) / nb) + 2048)
                                     : items_all;
         bp.nbins[l] = nb;
@@ -1538,6 +1804,7 @@ static BinPlan make_bin_plan(const int32_t* offsets_host, uint32_t L, uint32_t D
         bp.nlev = l + 1;
     }
     if (slots >= 0xffffffffull) bp.nlev = 0;  // item offsets are 32-bit: fall back to atomics
+    for (uint32_t l = 0; l <= bp.nlev; ++l) bp.off[l] = (uint32_t)offsets_host[l];
     bp.total_bins = bins;
     bp.spill_entries = bp.nlev ? (uint32_t)offsets_host[bp.nlev] : 0u;
     return bp;
@@ -2016,7 +2283,7 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         // + one column of the next batch's sampler blocks (blp, fully binned plans only)
         const BinLego bl = blp && bp.nlev == L ? *blp : BinLego{};
         const dim3 grid(bp.nlev + (nred ? 1u : 0u) + (bl.nlego ? 1u : 0u),
-                        std::max(std::max(ngp_div_up(B, kBinPts), nred), bl.nlego));
+                        std::max(std::max(std::min(ngp_div_up(B, kBinPts), kBinYCap), nred), bl.nlego));
         uint32_t nbmax = 0;
         for (uint32_t l = 0; l < bp.nlev; ++l) nbmax = std::max(nbmax, bp.nbins[l]);
         if (nbmax <= kMaxBinsPerLevel)
@@ -2027,19 +2294,27 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
             k_grid_bwd_bin<3, kMaxBinsPerLevelBig><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
                 im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad);
+        // the hashed levels' bins one per wave (wave_bin) when the grad is
+        // cleared and the caller clears the cursors (the fused step): the
+        // image path then covers only the dense levels' bins, on the first
+        // kAccImageWgs workgroups
+        const bool waves = zeroed && external && kWaveBins && bp.img_bins < bp.total_bins;
+        const uint32_t img_bins = waves ? bp.img_bins : bp.total_bins;
         // two persistent workgroups per CU while both fit the CU's LDS (the
         // 64 KiB image + two words per bin), else one
-        const size_t dyn = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
+        const size_t dyn = (2 * (size_t)img_bins + 1) * sizeof(uint32_t);
         const uint32_t per_cu = 2 * (dyn + kAccStaticLds) <= 160 * 1024 ? 2u : 1u;
+        const uint32_t grid_acc = per_cu * ngp_num_cus();
+        const uint32_t nimg = waves ? (img_bins ? std::min(kAccImageWgs, grid_acc / 2) : 0u) : grid_acc;
         int32_t* reset = bl.nlego ? bl.out.counter : nullptr;
         if (zeroed)
-            k_grid_bin_accum<true><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
+            k_grid_bin_accum<true><<<grid_acc, kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
-                marrive, timing, reset, spill, spill_bad);
+                marrive, timing, reset, spill, spill_bad, img_bins, nimg);
         else
-            k_grid_bin_accum<false><<<per_cu * ngp_num_cus(), kAccThreads, dyn, st>>>(
+            k_grid_bin_accum<false><<<grid_acc, kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
-                marrive, timing, reset, spill, spill_bad);
+                marrive, timing, reset, spill, spill_bad, img_bins, nimg);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
