@@ -783,7 +783,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
                InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
                int32_t grad_layout, int32_t* __restrict__ nonfinite, ngp_reduce::ReduceJobs rj, uint32_t nred,
                uint32_t* __restrict__ timing, BinLego next_batch, unsigned long long* __restrict__ spill,
-               uint32_t* __restrict__ spill_bad) {
+               uint32_t* __restrict__ spill_bad, uint32_t* __restrict__ rows_out) {
     constexpr uint32_t NC = 1u << D, NW = kBinPts / 64;
     constexpr uint32_t BPT = (NBMAX + kBinPts - 1) / kBinPts;  // bins per thread in the reservation step
     __shared__ uint32_t cnt[NBMAX], soff[NBMAX + 1], wsum[NW];
@@ -794,6 +794,8 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // this call's ring entry: start on the chip's constant 100 MHz clock, the
     // samples, the call count (plain stores: one thread, and the previous
     // call's kernels have finished)
+    // the rows this call bins, for the accumulate's regime choice
+    if (rows_out && (blockIdx.x | blockIdx.y) == 0 && threadIdx.x == 0) *rows_out = rows_of(B, im);
     if (timing && (blockIdx.x | blockIdx.y) == 0 && threadIdx.x == 0) {
         const uint32_t c = timing[0];
         uint32_t* h = timing + kTimingHeads + (c % NGP_GRID_TIMING_RING) * 4;
@@ -1125,12 +1127,20 @@ constexpr bool kWaveBins = NGP_WAVE_BINS != 0;  // (0: the image path for every 
 #define NGP_ACC_IMAGE_WGS 128
 #endif
 constexpr uint32_t kAccImageWgs = NGP_ACC_IMAGE_WGS;  // workgroups of the image path beside the wave bins
+#ifndef NGP_WAVE_MAX
+#define NGP_WAVE_MAX 512
+#endif
+constexpr uint32_t kWaveMax = NGP_WAVE_MAX;  // mean items per hashed bin above which the image path takes every bin
+constexpr uint32_t kRowsWord = 32;           // word of the retire area (unused with external cursors): the binned rows
+static_assert(kRowsWord > kRetireGroups && kRowsWord < 64, "the rows word lies in the 256-byte retire area, past its counters");
 static_assert(kWaveWords == 128, "two bitmap words per lane");
 
 NGP_DEV void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-NGP_DEV void wave_bin(uint32_t gb, uint32_t level, uint32_t lbin, uint32_t cap, uint32_t item0, uint32_t off0,
-                      uint32_t off1, const uint32_t* __restrict__ cursor,
+// Returns false (having done nothing) in the dense regime: rows_seen (loaded
+// by the caller, waited for only after this bin's first loads) > rows_max.
+NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32_t level, uint32_t lbin, uint32_t cap, uint32_t item0,
+                      uint32_t off0, uint32_t off1, const uint32_t* __restrict__ cursor,
                       const BinItem* __restrict__ items, ngp_half* __restrict__ grad_grid,
                       int32_t* __restrict__ nonfinite, unsigned long long* __restrict__ spill,
                       uint32_t* __restrict__ spill_bad, uint32_t* bm, uint32_t* pre, unsigned long long* sums,
@@ -1144,8 +1154,9 @@ NGP_DEV void wave_bin(uint32_t gb, uint32_t level, uint32_t lbin, uint32_t cap, 
 #pragma unroll
     for (uint32_t q = 0; q < kWaveQ; ++q) it[q] = __builtin_nontemporal_load(src + min(q * 64 + lane, cap - 1u));
     const uint32_t raw = cursor[gb];
+    if (__builtin_amdgcn_readfirstlane(rows_seen) > rows_max) return false;  // (its wait after this bin's loads)
     STAMP(11, raw ? __builtin_amdgcn_s_memtime() : 0ull);
-    if (raw == 0) return;
+    if (raw == 0) return true;
     WSTAMP(0, (unsigned long long)min(raw, cap) | ((unsigned long long)level << 32) | ((unsigned long long)(raw > cap) << 40));
     WSTAMP(1, __builtin_amdgcn_s_memtime());
     const uint32_t n = min(raw, cap);
@@ -1320,6 +1331,7 @@ NGP_DEV void wave_bin(uint32_t gb, uint32_t level, uint32_t lbin, uint32_t cap, 
     if (nonfinite && (__ballot(inf_out) != 0 || unit_bad) && lane == 0) atomicOr(nonfinite, 1);
     WSTAMP(2, __builtin_amdgcn_s_memtime());
     WSTAMP(3, distinct);
+    return true;
 }
 
 // ZEROED (the fused step: NGP_GRID_GRAD_ZEROED) drops the read-back of owned
@@ -1333,7 +1345,8 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
                  bool external, unsigned long long* __restrict__ msums,
                  uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing,
                  int32_t* __restrict__ reset_counter, unsigned long long* __restrict__ spill,
-                 uint32_t* __restrict__ spill_bad, uint32_t wave_bins0, uint32_t nimg) {
+                 uint32_t* __restrict__ spill_bad, uint32_t wave_bins0, uint32_t nimg,
+                 const uint32_t* __restrict__ rows_in, uint32_t wave_rows_max) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     // [entry][channel]; a channel-planar image (8-byte lane stride for the
     // 64-bit atomics instead of 16) measured the same
@@ -1344,13 +1357,17 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     extern __shared__ uint32_t dyn[];
     // bins [wave_bins0, total) go one per wave (wave_bin) to the workgroups
     // from nimg on; the first nimg workgroups run the image path over the
-    // bins before wave_bins0 (wave_bins0 = total: every workgroup, every bin)
-    const uint32_t nbins = min(wave_bins0, bp.total_bins);
-    const bool wave_role = nbins < bp.total_bins && blockIdx.x >= nimg;
+    // bins before wave_bins0 (wave_bins0 = total: every workgroup, every bin).
+    // Dense regime: more rows than wave_rows_max (the rows this call's bin
+    // launch binned, *rows_in) put ~kWaveMax items or more in a hashed bin,
+    // where the image path is faster: every workgroup then runs it over every
+    // bin. The row count is loaded beside each role's first loads.
+    uint32_t nbins = min(wave_bins0, bp.total_bins);
+    const bool waves = nbins < bp.total_bins;
+    const uint32_t rows_seen = waves && rows_in ? *rows_in : 0u;
+    bool wave_role = waves && blockIdx.x >= nimg;
     STAMP(0, __builtin_amdgcn_s_memtime());
     RSTAMP(60);
-    uint32_t* upre = dyn;              // [nbins + 1] first unit of each bin
-    uint32_t* bn = dyn + nbins + 1;    // [nbins] items of each bin (clipped at its capacity)
     // the plan's per-level arrays, indexed per lane below: kernel arguments
     // indexed by a varying value are memory loads, so keep a copy in LDS
     __shared__ uint32_t s_bin0[kMaxLevels + 1], s_cap[kMaxLevels], s_item0[kMaxLevels], s_off[kMaxLevels + 1];
@@ -1361,6 +1378,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // the sample counter of the batch whose backward this is, once every
     // kernel that reads it has finished (the bin launch drew the next batch)
     if (reset_counter && blockIdx.x == 0 && t < 2) reset_counter[t] = 0;
+    uint32_t ngr_img = nimg;  // workgroups of the image path
     if (wave_role) {
         // no plan copy and no barrier: a wave's level and plan entries are
         // wave-uniform, read from the kernel arguments with scalar loads
@@ -1372,23 +1390,40 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         for (uint32_t gb = nbins + (blockIdx.x - nimg) * NW + wv; gb < bp.total_bins; gb += nw) {
             gb = __builtin_amdgcn_readfirstlane(gb);
             while (lv + 1 < nlev && gb >= bp.bin0[lv + 1]) ++lv;
-            wave_bin(gb, lv, gb - bp.bin0[lv], bp.cap[lv], bp.item0[lv], bp.off[lv], bp.off[lv + 1], cursor, items,
-                     grad_grid, nonfinite, spill, spill_bad, reinterpret_cast<uint32_t*>(wl),
-                     reinterpret_cast<uint32_t*>(wl) + kWaveWords, wl + kWaveWords, lane);
+            if (!wave_bin(rows_seen, wave_rows_max, gb, lv, gb - bp.bin0[lv], bp.cap[lv], bp.item0[lv], bp.off[lv], bp.off[lv + 1],
+                          cursor, items, grad_grid, nonfinite, spill, spill_bad, reinterpret_cast<uint32_t*>(wl),
+                          reinterpret_cast<uint32_t*>(wl) + kWaveWords, wl + kWaveWords, lane))
+                break;
         }
-        STAMP(14, __builtin_amdgcn_s_memtime());
-        __syncthreads();  // the workgroup's end below is its last wave's
-    } else {
+        if (__builtin_amdgcn_readfirstlane(rows_seen) > wave_rows_max) {  // every wave saw the same row count
+            wave_role = false;
+            nbins = bp.total_bins;
+            ngr_img = gridDim.x;
+        } else {
+            STAMP(14, __builtin_amdgcn_s_memtime());
+            __syncthreads();  // the workgroup's end below is its last wave's
+        }
+    }
+    if (!wave_role) {
     // the first group of this thread's bin counts (step 1 below) is loaded
     // before anything else: its round trip overlaps the plan's LDS copy
     constexpr uint32_t kStep1Loads = 4;
-    const uint32_t per = (nbins + kAccThreads - 1) / kAccThreads;
+    // (sized for every bin: the same ownership whichever bins this call takes)
+    const uint32_t per = (bp.total_bins + kAccThreads - 1) / kAccThreads;
     uint32_t cv0[kStep1Loads];
 #pragma unroll
     for (uint32_t j = 0; j < kStep1Loads; ++j) {
         const uint32_t b = t * per + j;
-        cv0[j] = !wave_role && j < per && b < nbins ? cursor[b] : 0u;
+        cv0[j] = j < per && b < bp.total_bins ? cursor[b] : 0u;
     }
+    if (waves && ngr_img == nimg && rows_seen > wave_rows_max) {  // dense regime (decided after the loads above are issued)
+        nbins = bp.total_bins;
+        ngr_img = gridDim.x;
+    }
+    // (after the regime is known: nbins is final here; the host sized the
+    // dynamic LDS for every bin whenever the dense regime can occur)
+    uint32_t* upre = dyn;              // [nbins + 1] first unit of each bin
+    uint32_t* bn = dyn + nbins + 1;    // [nbins] items of each bin (clipped at its capacity)
     if (t <= nlev) {
         s_bin0[t] = t < nlev ? bp.bin0[t] : bp.total_bins;
         s_off[t] = bp.off[t];  // (the plan's host copy: no global load ahead of the first barrier)
@@ -1555,7 +1590,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // units run in bin order, so round 0's first workgroups hold the coarse
     // levels' long units (up to 4x the items of a fine-level unit); dealt
     // forward they also got a round-2 unit and finished last.
-    const uint32_t ngr = nbins < bp.total_bins ? nimg : gridDim.x, full = total / ngr;
+    const uint32_t ngr = ngr_img, full = total / ngr;
     auto unit_at = [&](uint32_t k) {  // this workgroup's k-th unit, or total (none)
         const uint32_t uk = k < full ? k * ngr + blockIdx.x : full * ngr + (ngr - 1 - blockIdx.x);
         return k <= full && uk < total ? uk : total;
@@ -2289,11 +2324,11 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         if (nbmax <= kMaxBinsPerLevel)
             k_grid_bwd_bin<3, kMaxBinsPerLevel><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad);
+                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad, retire + kRowsWord);
         else
             k_grid_bwd_bin<3, kMaxBinsPerLevelBig><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
                 (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad);
+                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad, retire + kRowsWord);
         // the hashed levels' bins one per wave (wave_bin) when the grad is
         // cleared and the caller clears the cursors (the fused step): the
         // image path then covers only the dense levels' bins, on the first
@@ -2301,20 +2336,34 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
         const bool waves = zeroed && external && kWaveBins && bp.img_bins < bp.total_bins;
         const uint32_t img_bins = waves ? bp.img_bins : bp.total_bins;
         // two persistent workgroups per CU while both fit the CU's LDS (the
-        // 64 KiB image + two words per bin), else one
-        const size_t dyn = (2 * (size_t)img_bins + 1) * sizeof(uint32_t);
-        const uint32_t per_cu = 2 * (dyn + kAccStaticLds) <= 160 * 1024 ? 2u : 1u;
+        // 64 KiB image + two words per bin), else one. With the wave bins the
+        // image path may take every bin in the dense regime (more rows than
+        // wave_rows_max: ~kWaveMax items per hashed bin), when two workgroups
+        // per CU still fit that; else the wave bins take the hashed levels
+        // whatever the rows.
+        auto two_fit = [](size_t d) { return 2 * (d + kAccStaticLds) <= 160 * 1024; };
+        const size_t dyn_all = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
+        const bool dense_ok = waves && two_fit(dyn_all);
+        const size_t dyn = dense_ok || !waves ? dyn_all : (2 * (size_t)img_bins + 1) * sizeof(uint32_t);
+        const uint32_t per_cu = two_fit(dyn) ? 2u : 1u;
         const uint32_t grid_acc = per_cu * ngp_num_cus();
         const uint32_t nimg = waves ? (img_bins ? std::min(kAccImageWgs, grid_acc / 2) : 0u) : grid_acc;
+        uint32_t wave_rows_max = 0xffffffffu;
+        if (dense_ok) {
+            uint32_t hl = 0;  // the first level of the wave bins
+            while (hl + 1 < bp.nlev && bp.bin0[hl + 1] <= img_bins) ++hl;
+            wave_rows_max = (uint32_t)std::min<uint64_t>(0xfffffffeu, (uint64_t)kWaveMax * bp.nbins[hl] >> 3);
+        }
+        uint32_t* rows_word = retire + kRowsWord;  // written by the bin launch
         int32_t* reset = bl.nlego ? bl.out.counter : nullptr;
         if (zeroed)
             k_grid_bin_accum<true><<<grid_acc, kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
-                marrive, timing, reset, spill, spill_bad, img_bins, nimg);
+                marrive, timing, reset, spill, spill_bad, img_bins, nimg, waves ? rows_word : nullptr, wave_rows_max);
         else
             k_grid_bin_accum<false><<<grid_acc, kAccThreads, dyn, st>>>(
                 offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
-                marrive, timing, reset, spill, spill_bad, img_bins, nimg);
+                marrive, timing, reset, spill, spill_bad, img_bins, nimg, waves ? rows_word : nullptr, wave_rows_max);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
