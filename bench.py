@@ -397,6 +397,16 @@ def dp_path_probe(args, model, data, dev, headline):
                                              "zero1_reduce_scatter_plus_all_gather":
                                                  int(2 * 2 * ft4.total * 7 / 8)}}
         del ft4, m4
+        # ZeRO-1 with the gradient reduced in fp32 (options exact_reduce: DDP's
+        # arithmetic, twice the reduce-scatter's bytes)
+        m5, d5, _, _, _, _, _ = make_workload(args.workload, dev, 1, args.num_rays)
+        ft5, _ = make_trainer(args, m5, d5, 1, dev, dtg, distributed=True, options=dict(exact_reduce=True))
+        e5, g5, _ = timed_run(args, ft5, 1, dev, steps, 5, 300, args.graph_steps)
+        exact = {"ms_per_step": round(e5 / steps * 1e3, 4), "graphs": bool(g5),
+                 "whole_step_graph": ft5._dp_whole is not None,
+                 "per_rank_bytes_8_ranks": {"reduce_scatter_fp32": int(4 * ft5.total * 7 / 8),
+                                            "all_gather_fp16": int(2 * ft5.total * 7 / 8)}}
+        del ft5, m5
         grad_bytes = 2 * ft.total  # the flat fp16 gradient = the fp16 forward copy
         truck_bytes = 2 * _flat_total(22)
         W = 8
@@ -405,7 +415,7 @@ def dp_path_probe(args, model, data, dev, headline):
         out = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "graphs": used_graph,
                "whole_step_graph": whole_captured, "graph_steps": graph_steps,
                "ms_per_step": round(ms, 4), "rays_per_s": round(args.num_rays / (ms * 1e-3), 1),
-               "three_graphs": three, "sparse_exchange": sparse,
+               "three_graphs": three, "sparse_exchange": sparse, "exact_reduce": exact,
                "phases_ms": {k: round(v, 5) for k, v in phases.items()},
                "flat_grad_bytes": int(grad_bytes),
                "per_rank_bytes_8_ranks": {

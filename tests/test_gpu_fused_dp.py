@@ -100,7 +100,9 @@ def _equiv_worker(rank, world, port, q):
         with torch.no_grad():
             model.encoder.embeddings.normal_(0, 0.05)
         model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
-        return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, seed=seed, distributed=distributed)
+        opts = dict(exact_reduce=True) if distributed and os.environ.get("NGP_TEST_EXACT_REDUCE") else None
+        return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, seed=seed, distributed=distributed,
+                            options=opts)
 
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -110,7 +112,7 @@ def _equiv_worker(rank, world, port, q):
         shard = ft.grad_shard.cpu().numpy()
         ft.flush()
         torch.cuda.synchronize()
-        q.put((rank, ft.lo, shard, [p.detach().cpu().numpy() for p in ft.params], ft.total))
+        q.put((rank, ft.lo, shard, [p.detach().cpu().numpy() for p in ft.params], ft.total, ft._exact_reduce))
         dist.barrier()
         dist.destroy_process_group()
         return
@@ -123,10 +125,11 @@ def _equiv_worker(rank, world, port, q):
         grads.append(ft.flat_grad.clone())
     # the gradient of the mean loss over both batches, then the optimizer on it
     mean = ((grads[0].float() + grads[1].float()).half() / 2)
+    exact = ((grads[0].float() + grads[1].float()) / 2).half()  # DDP's arithmetic: fp32 sum, / world, one rounding
     ft.flat_grad.copy_(mean)
     ft._optimizer()
     torch.cuda.synchronize()
-    q.put((0, 0, mean.cpu().numpy(), [p.detach().cpu().numpy() for p in ft.params], ft.total))
+    q.put((0, 0, mean.cpu().numpy(), [p.detach().cpu().numpy() for p in ft.params], ft.total, exact.cpu().numpy()))
 
 
 def _run(world, target=_worker):
@@ -161,9 +164,9 @@ def test_zero1_step_equals_single_process_step_on_both_batches():
     (flush: Adam per shard + all-gather) equal a single-process Adam step on
     that mean."""
     two = sorted(_run(2, _equiv_worker), key=lambda t: t[0])
-    (_, _, want, p_ref, total), = _run(1, _equiv_worker)
+    (_, _, want, p_ref, total, _), = _run(1, _equiv_worker)
     got = np.zeros(total, np.float16)
-    for _, lo, shard, _, _ in two:
+    for _, lo, shard, _, _, _ in two:
         got[lo:lo + shard.size] = shard
     g, w = got.astype(np.float64), want.astype(np.float64)
     assert np.abs(w).max() > 0
@@ -173,6 +176,26 @@ def test_zero1_step_equals_single_process_step_on_both_batches():
         for a, b in zip(p, p_ref):
             assert np.abs(a - b).max() <= 2.5e-2  # Adam's first step is lr * sign(g)
             assert (a == b).mean() >= 0.999
+
+
+def test_zero1_exact_reduce_is_the_fp32_mean(parity_report, monkeypatch):
+    """options exact_reduce: the reduce-scatter runs in
+    fp32 (SUM, / world) and rounds each averaged value to fp16 once -- the
+    arithmetic of the reference's DDP all-reduce of fp32 gradients
+    (nerf/utils.py:325-327). The two ranks' shards equal fp16((g0 + g1) / 2)
+    from single-process trainers' gradients bit for bit."""
+    monkeypatch.setenv("NGP_TEST_EXACT_REDUCE", "1")
+    two = sorted(_run(2, _equiv_worker), key=lambda t: t[0])
+    assert all(t[5] for t in two)
+    (_, _, _, _, total, exact), = _run(1, _equiv_worker)
+    got = np.zeros(total, np.float16)
+    for _, lo, shard, _, _, _ in two:
+        got[lo:lo + shard.size] = shard
+    assert np.abs(exact.astype(np.float32)).max() > 0
+    ne = got.view(np.uint16) != exact.view(np.uint16)
+    assert not ne.any(), (int(ne.sum()), np.argwhere(ne)[:4].ravel().tolist())
+    parity_report(f"ZeRO-1 exact_reduce, 2 ranks: {total} averaged gradient values bit-identical to "
+                  f"fp16(fp32 sum / 2) of the single-process gradients")
 
 
 def _density_worker(rank, world, port, q):

@@ -44,7 +44,9 @@ def _trainer(dev, distributed, mode="whole_step_graph"):
     with torch.no_grad():
         model.encoder.embeddings.normal_(0, 0.05)
     model.density_bitfield.copy_(torch.from_numpy(lego_bitfield()).to(dev))
-    opts = dict(sparse_exchange=True) if mode == "sparse_exchange" else dict(dp_graph=mode == "whole_step_graph")
+    opts = dict(sparse_exchange=True) if mode == "sparse_exchange" else dict(dp_graph=mode != "three_graphs")
+    if mode == "exact_reduce":
+        opts["exact_reduce"] = True
     return FusedTrainer(model, SyntheticLego(dev, num_rays=1024), M=40000, distributed=distributed, options=opts)
 
 
@@ -102,7 +104,7 @@ def _worker(port, q, mode):
         q.put(("error", repr(e), traceback.format_exc(), None))
 
 
-@pytest.mark.parametrize("mode", ["three_graphs", "whole_step_graph", "sparse_exchange"])
+@pytest.mark.parametrize("mode", ["three_graphs", "whole_step_graph", "sparse_exchange", "exact_reduce"])
 def test_rccl_world1_data_parallel_step_equals_single_process(parity_report, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -117,7 +119,7 @@ def test_rccl_world1_data_parallel_step_equals_single_process(parity_report, mod
         assert dp["xchg"] and not dp["dp"]
     else:
         assert dp["dp"] and not dp["xchg"]
-        assert dp["whole"] == (mode == "whole_step_graph")  # the graph phase replayed the whole-step graph
+        assert dp["whole"] == (mode != "three_graphs")  # the graph phase replayed the whole-step graph
     assert dp["steps"] == single["steps"] >= 8 and dp["scale"] == single["scale"]
     assert np.isfinite(dp["loss"]) and dp["loss"] == single["loss"]
     for ph in dp["phases"]:  # first phase where the runs part, and by how much

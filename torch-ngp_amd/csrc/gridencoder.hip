@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include <cmath>
+#include <type_traits>
 
 namespace {
 
@@ -268,6 +269,11 @@ k_grid_fwd(const float* __restrict__ inputs, const E* __restrict__ grid,
 // 1-2M query points measured faster level-interleaved (r05ad: full update
 // 0.655-0.668 -> 0.600-0.609 ms, partial unchanged), hence the threshold.
 constexpr uint32_t kFwdLevelsPerBlock = 2;
+#ifndef NGP_FWD_LDS
+#define NGP_FWD_LDS 0
+#endif
+constexpr uint32_t kFwdLdsLevels = NGP_FWD_LDS;  // coarse levels served from LDS (k_grid_fwd_lds), 0: none
+constexpr uint32_t kFwdLdsMin = 1u << 18;         // points from which they are
 constexpr uint32_t kFwdGroupMajorMin = (1u << 22);
 // XCD balance of the level-interleaved forward for large batches (the
 // density queries; 16 levels: one level pair per XCD): the XCDs whose pair is
@@ -432,9 +438,90 @@ __global__ void __launch_bounds__(256)
 k_grid_fwd_pair(const float* __restrict__ inputs, const E* __restrict__ grid,
                 const int32_t* __restrict__ offsets, T* __restrict__ outputs, uint32_t B, uint32_t L,
                 GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
-                int32_t out_layout, InMap im) {
+                int32_t out_layout, InMap im, uint32_t lo = 0) {
     grid_fwd_pair_block<T, E, D, C, KL>(blockIdx.x, inputs, grid, offsets, outputs, B, L, lv, gridtype,
-                                        align_corners, interp, out_layout, im, LevelRange{0u, L});
+                                        align_corners, interp, out_layout, im, LevelRange{lo, L});
+}
+
+// north_star's "per-level features staged in LDS" (VERDICT r05 item 2): the
+// coarsest dense levels [0, S) of a large batch (the density queries: 1-2M
+// points) from a copy of their tables in LDS. Each persistent workgroup reads
+// the levels' tables once (fp16 half2 per entry, the value the gathers round
+// to: levels 0-1 are 4,920 + 12,168 entries, 67 KB) and then serves every
+// corner of its points from LDS instead of the L2 (4 line requests per point
+// and level with the lane-pair gathers). Same arithmetic as
+// grid_fwd_pair_block (corner order, weights, Acc::mac), so the encodings
+// are bit-identical; the pair kernel takes levels [S, L).
+template <typename E, uint32_t D, uint32_t S>
+__global__ void __launch_bounds__(512)
+k_grid_fwd_lds(const float* __restrict__ inputs, const E* __restrict__ grid, const int32_t* __restrict__ offsets,
+               ngp_half* __restrict__ outputs, uint32_t B, uint32_t L, GridLevels lv, uint32_t gridtype,
+               bool align_corners, uint32_t interp, int32_t out_layout, InMap im) {
+    using A = Acc<ngp_half>;
+    constexpr uint32_t C = 2;
+    extern __shared__ uint32_t tab[];  // half2 bits per entry, levels back to back
+    uint32_t lbase[S + 1];
+    lbase[0] = 0;
+#pragma unroll
+    for (uint32_t l = 0; l < S; ++l) {
+        const uint32_t off = (uint32_t)offsets[l], hs = (uint32_t)offsets[l + 1] - off;
+        for (uint32_t i = threadIdx.x; i < hs; i += blockDim.x) {
+            A::F v[C];
+            load_entry_as<ngp_half, E, C>(grid + (size_t)(off + i) * C, v);
+            const ngp_half2 h{(ngp_half)v[0], (ngp_half)v[1]};
+            tab[lbase[l] + i] = __builtin_bit_cast(uint32_t, h);
+        }
+        lbase[l + 1] = lbase[l] + hs;
+    }
+    __syncthreads();
+    const uint32_t rows = rows_of(B, im);
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < rows; b += gridDim.x * blockDim.x) {
+        float x[D];
+        bool oob = false;
+#pragma unroll
+        for (uint32_t d = 0; d < D; d++) {
+            x[d] = inputs[(size_t)b * D + d];
+            if (im.scale != 0.0f) x[d] = (x[d] + im.shift) * im.scale;
+            if (x[d] < 0 || x[d] > 1) oob = true;
+        }
+#pragma unroll
+        for (uint32_t level = 0; level < S; ++level) {
+            const uint32_t hs = lbase[level + 1] - lbase[level];
+            const uint32_t hs_mask = (hs & (hs - 1)) == 0 ? hs - 1 : 0;
+            const float scale = lv.scale[level];
+            const uint32_t resolution = lv.res[level];
+            float pos[D];
+            uint32_t pg[D];
+#pragma unroll
+            for (uint32_t d = 0; d < D; d++) {
+                pos[d] = fmaf(x[d], scale, align_corners ? 0.0f : 0.5f);
+                pg[d] = (uint32_t)floorf(pos[d]);
+                pos[d] -= (float)pg[d];
+                if (interp == 1) pos[d] = smoothstep(pos[d]);
+            }
+            uint32_t raw[1u << D];
+#pragma unroll
+            for (uint32_t idx = 0; idx < (1u << D); idx++) {  // every LDS read first
+                uint32_t pl[D];
+#pragma unroll
+                for (uint32_t d = 0; d < D; d++) pl[d] = (idx & (1u << d)) ? pg[d] + 1 : pg[d];
+                raw[idx] = tab[lbase[level] + grid_index<D>(gridtype, align_corners, hs, hs_mask, resolution, pl)];
+            }
+            A::S res[C] = {A::zero(), A::zero()};
+#pragma unroll
+            for (uint32_t idx = 0; idx < (1u << D); idx++) {
+                float w = 1;
+#pragma unroll
+                for (uint32_t d = 0; d < D; d++) w *= (idx & (1u << d)) ? pos[d] : 1 - pos[d];
+                const ngp_half2 h = __builtin_bit_cast(ngp_half2, raw[idx]);
+#pragma unroll
+                for (uint32_t c = 0; c < C; ++c) res[c] = A::mac(res[c], (A::F)w, oob ? 0.0f : (float)h[c]);
+            }
+            if (oob) res[0] = res[1] = A::zero();
+            ngp_half* out = out_layout == 0 ? outputs + ((size_t)level * B + b) * C : outputs + ((size_t)b * L + level) * C;
+            store_entry<ngp_half, C>(out, res);
+        }
+    }
 }
 
 // The fused step's grid forward with the step's tail (ngp_grid_encode_forward_fused_tail):
@@ -1972,6 +2059,28 @@ int fwd_c(const float* inputs, const void* emb, const int32_t* offsets, void* ou
     const E* e = (const E*)emb;
     T* o = (T*)out;
     T* dd = (T*)dy_dx;
+    if constexpr (std::is_same<T, ngp_half>::value && D == 3) {
+        // large batches: the coarsest dense levels from LDS (k_grid_fwd_lds),
+        // the pair kernel over the rest
+        if (!dd && kFwdLdsLevels && B >= kFwdLdsMin && C == 2 && L > kFwdLdsLevels) {
+            size_t ent = 0;
+            for (uint32_t l = 0; l < kFwdLdsLevels; ++l) {  // a level holds at most its dense grid, 8-aligned
+                const double side = ac ? lv.res[l] : lv.res[l] + 1.0;
+                ent += ((size_t)(side * side * side) + 7) / 8 * 8;
+            }
+            if (ent * 4 <= 80 * 1024) {  // two workgroups per CU
+                const uint32_t nb = std::min<uint32_t>(2 * ngp_num_cus(), ngp_div_up(B, 512));
+                k_grid_fwd_lds<E, 3, (kFwdLdsLevels ? kFwdLdsLevels : 1u)><<<nb, 512, ent * 4, st>>>(
+                    inputs, e, offsets, o, B, L, lv, gridtype, ac, interp, layout, im);
+                const uint32_t Lr = L - kFwdLdsLevels;
+                const uint32_t gpx = ((Lr + 7) / 8 + kFwdLevelsPerBlock - 1) / kFwdLevelsPerBlock;
+                const dim3 gp(8 * gpx * ngp_div_up(B, 128));
+                k_grid_fwd_pair<T, E, D, 2><<<gp, 256, 0, st>>>(inputs, e, offsets, o, B, L, lv, gridtype, ac, interp,
+                                                                layout, im, kFwdLdsLevels);
+                return ngp_check_launch("grid_encode_forward");
+            }
+        }
+    }
     if (!dd && (sizeof(T) <= 4)) {
         // XCD-aware 1-D grid (see the kernel): 8 XCDs x level groups x point chunks
         const bool gm = B >= kFwdGroupMajorMin;

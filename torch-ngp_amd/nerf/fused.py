@@ -79,9 +79,14 @@ def _vp_array(ptrs):
 #   sparse_exchange  data parallel: every rank runs the world-1 step with the
 #                 full Adam, the gradients meet in a touched-entry exchange
 #                 (nerf/exchange.py) instead of the ZeRO-1 collectives
+#   exact_reduce  ZeRO-1: reduce-scatter the gradient in fp32 (SUM, then / world
+#                 and one fp16 rounding into the shard), the arithmetic of the
+#                 reference's DDP all-reduce of fp32 grads (nerf/utils.py:325-327),
+#                 at twice the reduce-scatter's link bytes; default: an fp16 AVG
+#                 reduce-scatter, which rounds at every ring hop
 DEFAULT_OPTIONS = dict(table16=False, split_head=False, split_reduce=False, split_fwd=False, split_bwd=False,
                        march_adam=True, tail_in_fwd=True, emit_inline=True, draw_ahead=True, live_rows=True,
-                       dp_graph=True, density_sort=True, sparse_exchange=False)
+                       dp_graph=True, density_sort=True, sparse_exchange=False, exact_reduce=False)
 
 
 class FusedTrainer:
@@ -184,6 +189,10 @@ class FusedTrainer:
         self.exp_avg, self.exp_avg_sq = z(chunk), z(chunk)
         # the averaged gradient shard (reduce-scatter output); world 1: the flat grad itself
         self.grad_shard = z(chunk, dtype=h) if self.dp else self.flat_grad
+        # exact_reduce: the fp32 image of the flat gradient and of this rank's shard sum
+        self._exact_reduce = self.dp and opts["exact_reduce"]
+        self._grad32 = z(self.total) if self._exact_reduce else None
+        self._shard32 = z(chunk) if self._exact_reduce else None
         self._offsets_host = (ctypes.c_int32 * enc.offsets.numel())(*enc.offsets.cpu().tolist())
         gb = nat.lib().ngp_grid_encode_backward_fused_workspace_bytes(
             M, enc.input_dim, enc.level_dim, enc.num_levels, self.S, enc.base_resolution,
@@ -709,7 +718,20 @@ class FusedTrainer:
         optimizer launch that consumes the shard (`_optimizer`)."""
         if not self.dp:
             return
-        if self._nccl:
+        if self._exact_reduce:
+            # DDP's arithmetic: fp32 sum over the ranks, / world, then the one
+            # fp16 rounding the shard's storage needs (a NaN from the guard
+            # still reaches every owner)
+            self._grad32.copy_(self.flat_grad)
+            if self._nccl:
+                dist.reduce_scatter_tensor(self._shard32, self._grad32, op=dist.ReduceOp.SUM)
+            else:
+                out = torch.empty(self.chunk, dtype=torch.float32)
+                dist.reduce_scatter_tensor(out, self._grad32.cpu(), op=dist.ReduceOp.SUM)
+                self._shard32.copy_(out)
+            torch.div(self._shard32, float(self.world), out=self._shard32)
+            self.grad_shard.copy_(self._shard32)
+        elif self._nccl:
             dist.reduce_scatter_tensor(self.grad_shard, self.flat_grad, op=dist.ReduceOp.AVG)
         else:  # gloo (tests): host-staged
             out = torch.empty(self.chunk, dtype=self.flat_grad.dtype)
