@@ -1206,6 +1206,11 @@ constexpr uint32_t kWaveAcc = (kWaveLdsUll - kWaveWords) / 2;          // distin
 #define NGP_WAVE_Q 8
 #endif
 constexpr uint32_t kWaveQ = NGP_WAVE_Q;  // items per lane in flight (a bin of <= 64 kWaveQ items: one load round)
+#ifndef NGP_WAVE_SPEC
+#define NGP_WAVE_SPEC 0
+#endif
+constexpr uint32_t kWaveSpec = NGP_WAVE_SPEC;  // of them requested before the bin's count is known
+static_assert(kWaveSpec <= kWaveQ, "speculative items are a prefix of the first round");
 #ifndef NGP_WAVE_BINS
 #define NGP_WAVE_BINS 1
 #endif
@@ -1234,12 +1239,15 @@ NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32
                       uint32_t lane) {
     constexpr uint32_t C = 2;
     const uint64_t* src = reinterpret_cast<const uint64_t*>(items + item0 + (size_t)lbin * cap);
-    // the first kWaveQ x 64 item slots are requested beside the count (slots
-    // past the count hold stale items and are masked below; clamped to the
-    // bin's capacity, so every address is the bin's own)
+    // the first kWaveSpec x 64 item slots may be requested beside the count
+    // (slots past the count hold stale items and are masked below; clamped to
+    // the bin's capacity, so every address is the bin's own), the rest of the
+    // first round once the count is known. All kWaveQ x 64 up front read 2.9x
+    // the live items' bytes in the trained regime (PMC, r07ev); 0, 2 and 8
+    // measured the same time (r07r), so none are speculative by default.
     uint64_t it[kWaveQ];
 #pragma unroll
-    for (uint32_t q = 0; q < kWaveQ; ++q) it[q] = __builtin_nontemporal_load(src + min(q * 64 + lane, cap - 1u));
+    for (uint32_t q = 0; q < kWaveSpec; ++q) it[q] = __builtin_nontemporal_load(src + min(q * 64 + lane, cap - 1u));
     const uint32_t raw = cursor[gb];
     if (__builtin_amdgcn_readfirstlane(rows_seen) > rows_max) return false;  // (its wait after this bin's loads)
     STAMP(11, raw ? __builtin_amdgcn_s_memtime() : 0ull);
@@ -1248,6 +1256,11 @@ NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32
     WSTAMP(1, __builtin_amdgcn_s_memtime());
     const uint32_t n = min(raw, cap);
     const bool spilled = raw > cap;
+#pragma unroll
+    for (uint32_t q = kWaveSpec; q < kWaveQ; ++q) {
+        const uint32_t k = q * 64 + lane;
+        it[q] = k < n ? __builtin_nontemporal_load(src + k) : ~0ull;
+    }
     const uint32_t e0 = lbin * kBinEntries;
     const uint32_t ne = min(kBinEntries, off1 - off0 - e0);
     const size_t ebase = (size_t)off0 + e0;
