@@ -830,6 +830,25 @@ constexpr uint32_t kTimingHeads = 64, kTimingEnds = kTimingHeads + 4 * NGP_GRID_
 // wait for the wave's outstanding global loads, stores and atomics.
 NGP_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Loads of bytes another workgroup of the SAME launch stored (the one-launch
+// grid backward, k_grid_bwd_fused): `sc1` loads, L2-served, never a stale L1
+// line; the producer stores those bytes `sc1` too and signals after its waves'
+// vmcnt(0) waits and a workgroup barrier (MI355X_MICROARCH.md, inter-workgroup
+// visibility: the first hand-off row). Two launches need neither.
+template <bool SC1> NGP_DEV uint64_t ld_u64(const uint64_t* p) {
+    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return __builtin_nontemporal_load(p);
+}
+template <bool SC1> NGP_DEV uint32_t ld_u32(const uint32_t* p) {
+    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool SC1> NGP_DEV ulonglong2 ld_u64x2(const unsigned long long* p) {
+    if constexpr (SC1) return ulonglong2{ld_u64<true>(reinterpret_cast<const uint64_t*>(p)),
+                                         ld_u64<true>(reinterpret_cast<const uint64_t*>(p) + 1)};
+    else return *reinterpret_cast<const ulonglong2*>(p);
+}
+
 #ifdef NGP_STAMPS  // diagnostic build only (tools/accum_stamps.py): per-workgroup phase clocks
 __device__ unsigned long long* g_stamps;
 #define STAMP(slot, v) do { if (g_stamps && threadIdx.x == 0) g_stamps[blockIdx.x * 64 + (slot)] = (v); } while (0)
@@ -862,46 +881,58 @@ struct BinLego {
     uint32_t N, nlego;
 };
 
-template <uint32_t D, uint32_t NBMAX>
-__global__ void __launch_bounds__(kBinPts, kBinWavesPerSimd * 256 / kBinPts)  // kBinWavesPerSimd waves per SIMD
-k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
-               const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
-               uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
-               InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
-               int32_t grad_layout, int32_t* __restrict__ nonfinite, ngp_reduce::ReduceJobs rj, uint32_t nred,
-               uint32_t* __restrict__ timing, BinLego next_batch, unsigned long long* __restrict__ spill,
-               uint32_t* __restrict__ spill_bad, uint32_t* __restrict__ rows_out) {
+// The bin launch's LDS, carved from one region (the one-launch form reuses
+// the accumulate's image for it): counters, scan offsets, per-bin staging
+// info, then the staged items.
+template <uint32_t NBMAX> constexpr size_t bin_lds_words() {
+    return (2 * (size_t)NBMAX + 1 + kBinPts / 64 + 1 + 1) / 2 * 2 + 2 * (size_t)NBMAX + 2 + (size_t)kBinPts * 8 * 2;
+}
+
+template <uint32_t D, uint32_t NBMAX, bool SC1>
+NGP_DEV void bin_block(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
+                       const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
+                       uint32_t L, const GridLevels& lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+                       const InMap& im, const BinPlan& bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
+                       int32_t grad_layout, int32_t* __restrict__ nonfinite, const ngp_reduce::ReduceJobs& rj,
+                       uint32_t nred, uint32_t* __restrict__ timing, const BinLego& next_batch,
+                       unsigned long long* __restrict__ spill, uint32_t* __restrict__ spill_bad,
+                       uint32_t* __restrict__ rows_out, uint32_t bx, uint32_t by, uint32_t gy, uint32_t* lds) {
     constexpr uint32_t NC = 1u << D, NW = kBinPts / 64;
     constexpr uint32_t BPT = (NBMAX + kBinPts - 1) / kBinPts;  // bins per thread in the reservation step
-    __shared__ uint32_t cnt[NBMAX], soff[NBMAX + 1], wsum[NW];
-    __shared__ uint2 binfo[NBMAX];  // (slot - stage index, end of the bin's in-capacity stage run)
-    __shared__ uint32_t s_over;                // some bin of this workgroup ran past its capacity
-    extern __shared__ BinItem stage[];  // kBinPts * NC
+    uint32_t* cnt = lds;                 // [NBMAX]
+    uint32_t* soff = cnt + NBMAX;        // [NBMAX + 1]
+    uint32_t* wsum = soff + NBMAX + 1;   // [NW]
+    uint32_t& s_over = wsum[NW];         // some bin of this workgroup ran past its capacity
+    uint2* binfo = reinterpret_cast<uint2*>(lds + (2 * NBMAX + 1 + NW + 1 + 1) / 2 * 2);  // (slot - stage index, end of the bin's in-capacity stage run)
+    BinItem* stage = reinterpret_cast<BinItem*>(binfo + NBMAX + 1);  // kBinPts * NC
     // launch timing (NGP_GRID_TIMING): block (0, 0), dispatched first, opens
     // this call's ring entry: start on the chip's constant 100 MHz clock, the
     // samples, the call count (plain stores: one thread, and the previous
     // call's kernels have finished)
     // the rows this call bins, for the accumulate's regime choice
-    if (rows_out && (blockIdx.x | blockIdx.y) == 0 && threadIdx.x == 0) *rows_out = rows_of(B, im);
-    if (timing && (blockIdx.x | blockIdx.y) == 0 && threadIdx.x == 0) {
+    if (rows_out && (bx | by) == 0 && threadIdx.x == 0) *rows_out = rows_of(B, im);
+    if (timing && (bx | by) == 0 && threadIdx.x == 0) {
         const uint32_t c = timing[0];
         uint32_t* h = timing + kTimingHeads + (c % NGP_GRID_TIMING_RING) * 4;
         h[0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         h[1] = rows_of(B, im);
-        timing[0] = c + 1;
+        if constexpr (SC1)  // read by the same launch's accumulate workgroups
+            __hip_atomic_store(timing, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            timing[0] = c + 1;
     }
     // the extra column of blocks (x == nlev): the MLP dW slab reduce, which
     // neither needs nor feeds this kernel (one launch less per step; the same
     // fixed summation order as k_slab_reduce, ngp_reduce.h)
     // and the column after it (x == nlev + (nred != 0)): the next batch's
     // sampler blocks, when the launch carries it
-    if (blockIdx.x >= bp.nlev) {
-        if (nred && blockIdx.x == bp.nlev) {
-            if (blockIdx.y < nred)
-                ngp_reduce::slab_reduce_block<ngp_half, kBinPts>(rj, blockIdx.y, reinterpret_cast<float(*)[64]>(stage));
-        } else if (blockIdx.y < next_batch.nlego) {
+    if (bx >= bp.nlev) {
+        if (nred && bx == bp.nlev) {
+            if (by < nred)
+                ngp_reduce::slab_reduce_block<ngp_half, kBinPts>(rj, by, reinterpret_cast<float(*)[64]>(stage));
+        } else if (by < next_batch.nlego) {
             const BinLego& q = next_batch;
-            ngp_head::lego_rays_block(blockIdx.y, q.nlego, q.poses, q.sc, q.N, q.st, q.out);
+            ngp_head::lego_rays_block(by, q.nlego, q.poses, q.sc, q.N, q.st, q.out);
         }
         return;
     }
@@ -915,11 +946,11 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     // A workgroup takes point blocks blockIdx.y, blockIdx.y + gridDim.y, ...:
     // the host may cap the grid's height below the row capacity (most of a
     // capacity-sized grid exits at once in the live-row regime)
-    const uint32_t level = blockIdx.x;
+    const uint32_t level = bx;
     const uint32_t rows = rows_of(B, im);
-    for (uint32_t chunk = blockIdx.y; chunk * kBinPts < rows; chunk += gridDim.y) {
-    if (chunk != blockIdx.y) __syncthreads();  // the last block's write-out has read the LDS
-    [[maybe_unused]] const uint32_t stamp_id = level * gridDim.y + chunk;
+    for (uint32_t chunk = by; chunk * kBinPts < rows; chunk += gy) {
+    if (chunk != by) __syncthreads();  // the last block's write-out has read the LDS
+    [[maybe_unused]] const uint32_t stamp_id = level * gy + chunk;
     const uint32_t nb = bp.nbins[level];
     const bool merge = (bp.merge_mask >> level) & 1u;
     const int lane = (int)(threadIdx.x & 63);
@@ -1130,7 +1161,15 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     for (uint32_t k = threadIdx.x; k < total; k += kBinPts) {
         const BinItem it = stage[k];
         const uint2 bi = binfo[it.e >> 16];
-        if (k < bi.y) lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
+        if (k < bi.y) {
+            if constexpr (SC1)  // read by the same launch's accumulate workgroups
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(lvl_items + k + bi.x),
+                                   (unsigned long long)(it.e & 0xffffu) |
+                                       ((unsigned long long)__builtin_bit_cast(uint32_t, it.v) << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                lvl_items[k + bi.x] = BinItem{it.e & 0xffffu, it.v};
+        }
     }
     // Past a bin's capacity: the item's exact int64 counts go into the spill
     // image (integer atomics, so the sum does not depend on the arrival
@@ -1143,7 +1182,7 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
         if (k >= bi.y) {
             const uint32_t vb = __builtin_bit_cast(uint32_t, it.v);
             if (((vb >> 10) & 31u) == 31u || ((vb >> 26) & 31u) == 31u) {
-                spill_bad[bp.bin0[level] + bin] = 1u;  // benign race: every writer stores 1
+                atomicOr(spill_bad + bp.bin0[level] + bin, 1u);  // (an atomic: seen by the one-launch form's readers)
                 if (nonfinite) atomicOr(nonfinite, 1);
             } else {
                 const size_t e = (size_t)off0 + (size_t)bin * kBinEntries + (it.e & 0xffffu);
@@ -1155,6 +1194,21 @@ k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inpu
     BSTAMP(4);
     BRSTAMP(9);
     }
+}
+
+template <uint32_t D, uint32_t NBMAX>
+__global__ void __launch_bounds__(kBinPts, kBinWavesPerSimd * 256 / kBinPts)  // kBinWavesPerSimd waves per SIMD
+k_grid_bwd_bin(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
+               const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
+               uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+               InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
+               int32_t grad_layout, int32_t* __restrict__ nonfinite, ngp_reduce::ReduceJobs rj, uint32_t nred,
+               uint32_t* __restrict__ timing, BinLego next_batch, unsigned long long* __restrict__ spill,
+               uint32_t* __restrict__ spill_bad, uint32_t* __restrict__ rows_out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t bin_lds[];  // bin_lds_words<NBMAX>()
+    bin_block<D, NBMAX, false>(grad, inputs, offsets, grad_grid, B, L, lv, gridtype, align_corners, interp, im, bp,
+                               cursor, items, grad_layout, nonfinite, rj, nred, timing, next_batch, spill, spill_bad,
+                               rows_out, blockIdx.x, blockIdx.y, gridDim.y, bin_lds);
 }
 
 // Persistent accumulation: every workgroup reads all bins' counts, forms the
@@ -1223,6 +1277,17 @@ constexpr uint32_t kAccImageWgs = NGP_ACC_IMAGE_WGS;  // workgroups of the image
 #define NGP_WAVE_MAX 512
 #endif
 constexpr uint32_t kWaveMax = NGP_WAVE_MAX;  // mean items per hashed bin above which the image path takes every bin
+#ifndef NGP_FUSED_BWD
+#define NGP_FUSED_BWD 0
+#endif
+constexpr uint32_t kFusedBwd = NGP_FUSED_BWD;  // the one-launch grid backward (k_grid_bwd_fused): 1 tickets, 2 block roles
+constexpr uint32_t kFusedYCap = 64;            // its point blocks per level (each loops over more)
+// after the counters: the retire area (the accumulate's retire counters, the
+// binned rows word, the one-launch form's ticket / done counters), cleared
+// with the counters by a caller that clears them (NGP_GRID_CURSORS_EXTERNAL)
+constexpr size_t kRetireBytes = 512;
+constexpr uint32_t kFusedWords = 40;  // word of the retire area: ticket, finished count, error, -, done[level]
+static_assert(kFusedWords + 4 + kMaxLevels <= kRetireBytes / 4, "the one-launch counters fit the retire area");
 constexpr uint32_t kRowsWord = 32;           // word of the retire area (unused with external cursors): the binned rows
 static_assert(kRowsWord > kRetireGroups && kRowsWord < 64, "the rows word lies in the 256-byte retire area, past its counters");
 static_assert(kWaveWords == 128, "two bitmap words per lane");
@@ -1231,6 +1296,7 @@ NGP_DEV void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Returns false (having done nothing) in the dense regime: rows_seen (loaded
 // by the caller, waited for only after this bin's first loads) > rows_max.
+template <bool SC1>
 NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32_t level, uint32_t lbin, uint32_t cap, uint32_t item0,
                       uint32_t off0, uint32_t off1, const uint32_t* __restrict__ cursor,
                       const BinItem* __restrict__ items, ngp_half* __restrict__ grad_grid,
@@ -1247,8 +1313,8 @@ NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32
     // measured the same time (r07r), so none are speculative by default.
     uint64_t it[kWaveQ];
 #pragma unroll
-    for (uint32_t q = 0; q < kWaveSpec; ++q) it[q] = __builtin_nontemporal_load(src + min(q * 64 + lane, cap - 1u));
-    const uint32_t raw = cursor[gb];
+    for (uint32_t q = 0; q < kWaveSpec; ++q) it[q] = ld_u64<SC1>(src + min(q * 64 + lane, cap - 1u));
+    const uint32_t raw = ld_u32<SC1>(cursor + gb);
     if (__builtin_amdgcn_readfirstlane(rows_seen) > rows_max) return false;  // (its wait after this bin's loads)
     STAMP(11, raw ? __builtin_amdgcn_s_memtime() : 0ull);
     if (raw == 0) return true;
@@ -1259,7 +1325,7 @@ NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32
 #pragma unroll
     for (uint32_t q = kWaveSpec; q < kWaveQ; ++q) {
         const uint32_t k = q * 64 + lane;
-        it[q] = k < n ? __builtin_nontemporal_load(src + k) : ~0ull;
+        it[q] = k < n ? ld_u64<SC1>(src + k) : ~0ull;
     }
     const uint32_t e0 = lbin * kBinEntries;
     const uint32_t ne = min(kBinEntries, off1 - off0 - e0);
@@ -1273,7 +1339,7 @@ NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32
 #pragma unroll
         for (uint32_t q = 0; q < kWaveQ; ++q) {
             const uint32_t k = k0 + q * 64 + lane;
-            it[q] = k < n ? __builtin_nontemporal_load(src + k) : ~0ull;
+            it[q] = k < n ? ld_u64<SC1>(src + k) : ~0ull;
         }
     };
     auto mask = [&]() {
@@ -1296,10 +1362,10 @@ NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32
     }
     if (spilled) {  // entries past the bin's capacity went to the spill image (rare)
         for (uint32_t e = lane; e < ne; e += 64) {
-            const ulonglong2 x = reinterpret_cast<const ulonglong2*>(sp)[e];
+            const ulonglong2 x = ld_u64x2<SC1>(sp + 2 * e);
             if (x.x | x.y) atomicOr(&bm[e >> 5], 1u << (e & 31));
         }
-        if (lane == 0 && spill_bad[gb]) {
+        if (lane == 0 && ld_u32<SC1>(spill_bad + gb)) {
             bad = true;
             spill_bad[gb] = 0u;
         }
@@ -1376,7 +1442,7 @@ NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32
             }
             if (spilled) {
                 for (uint32_t e = lane; e < ne; e += 64) {
-                    const ulonglong2 x = reinterpret_cast<const ulonglong2*>(sp)[e];
+                    const ulonglong2 x = ld_u64x2<SC1>(sp + 2 * e);
                     if (!(x.x | x.y)) continue;
                     const uint32_t i = cidx(e) - r0;
                     if (i >= kWaveAcc) continue;
@@ -1437,24 +1503,40 @@ NGP_DEV bool wave_bin(uint32_t rows_seen, uint32_t rows_max, uint32_t gb, uint32
 // ZEROED (the fused step: NGP_GRID_GRAD_ZEROED) drops the read-back of owned
 // slices (non-fresh owners occur only with a grad that was not zeroed) and the
 // registers it holds.
-template <bool ZEROED>
-__global__ void __launch_bounds__(kAccThreads, 4)  // 2 workgroups per CU: <= 128 VGPRs
-k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
-                 uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
-                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
-                 bool external, unsigned long long* __restrict__ msums,
-                 uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing,
-                 int32_t* __restrict__ reset_counter, unsigned long long* __restrict__ spill,
-                 uint32_t* __restrict__ spill_bad, uint32_t wave_bins0, uint32_t nimg,
-                 const uint32_t* __restrict__ rows_in, uint32_t wave_rows_max) {
+// The one-launch form's synchronisation (k_grid_bwd_fused): each bin
+// workgroup adds 1 to done[level] once its items are stored; an accumulate
+// workgroup waits for the levels it reads. err: a wait that ran out (bounded).
+struct FusedSync {
+    uint32_t* done;        // [nlev] bin workgroups finished, per level (zero before the launch)
+    uint32_t per_level;    // bin workgroups per level
+    uint32_t* err;         // set to 1 when a bounded wait ran out
+    uint32_t* opened;      // 1 once the launch-timing ring entry is open (ticket 0's workgroup)
+};
+// Poll (one lane) until *p >= need; bounded (~0.1 s), then flags err.
+NGP_DEV void wait_at_least(const uint32_t* p, uint32_t need, uint32_t* err) {
+    for (uint32_t it = 0; it < (1u << 17); ++it) {
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) return;
+        __builtin_amdgcn_s_sleep(16);
+    }
+    if (err) atomicOr(err, 1u);
+}
+
+template <bool ZEROED, bool FUSED>
+NGP_DEV void accum_block(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, const BinPlan& bp,
+                         uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
+                         const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
+                         bool external, unsigned long long* __restrict__ msums,
+                         uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing,
+                         int32_t* __restrict__ reset_counter, unsigned long long* __restrict__ spill,
+                         uint32_t* __restrict__ spill_bad, uint32_t wave_bins0, uint32_t nimg,
+                         const uint32_t* __restrict__ rows_in, uint32_t wave_rows_max, uint32_t bid, uint32_t nblk,
+                         unsigned long long* acc, uint32_t* dyn, const FusedSync& fs) {
     constexpr uint32_t C = 2, NW = kAccThreads / 64;
     // [entry][channel]; a channel-planar image (8-byte lane stride for the
     // 64-bit atomics instead of 16) measured the same
-    __shared__ __attribute__((aligned(16))) unsigned long long acc[kBinEntries * C];
     auto acc_entry = [&](uint32_t e) { return reinterpret_cast<const ulonglong2*>(acc)[e]; };
     __shared__ uint32_t wsum[NW];
     __shared__ uint32_t s_last, s_bad;
-    extern __shared__ uint32_t dyn[];
     // bins [wave_bins0, total) go one per wave (wave_bin) to the workgroups
     // from nimg on; the first nimg workgroups run the image path over the
     // bins before wave_bins0 (wave_bins0 = total: every workgroup, every bin).
@@ -1465,7 +1547,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     uint32_t nbins = min(wave_bins0, bp.total_bins);
     const bool waves = nbins < bp.total_bins;
     const uint32_t rows_seen = waves && rows_in ? *rows_in : 0u;
-    bool wave_role = waves && blockIdx.x >= nimg;
+    bool wave_role = waves && bid >= nimg;
     STAMP(0, __builtin_amdgcn_s_memtime());
     RSTAMP(60);
     // the plan's per-level arrays, indexed per lane below: kernel arguments
@@ -1477,7 +1559,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     const uint32_t nlev = bp.nlev;
     // the sample counter of the batch whose backward this is, once every
     // kernel that reads it has finished (the bin launch drew the next batch)
-    if (reset_counter && blockIdx.x == 0 && t < 2) reset_counter[t] = 0;
+    if (reset_counter && bid == 0 && t < 2) reset_counter[t] = 0;
     uint32_t ngr_img = nimg;  // workgroups of the image path
     if (wave_role) {
         // no plan copy and no barrier: a wave's level and plan entries are
@@ -1485,12 +1567,18 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         unsigned long long* wl = acc + wv * kWaveLdsUll;  // this wave's 8 KB: bitmap, prefix, sums
         for (uint32_t i = lane; i < kWaveLdsUll / 2; i += 64) reinterpret_cast<ulonglong2*>(wl)[i] = ulonglong2{0ull, 0ull};
         STAMP(10, __builtin_amdgcn_s_memtime());
-        const uint32_t nw = (gridDim.x - nimg) * NW;
-        uint32_t lv = 0;
-        for (uint32_t gb = nbins + (blockIdx.x - nimg) * NW + wv; gb < bp.total_bins; gb += nw) {
+        const uint32_t nw = (nblk - nimg) * NW;
+        uint32_t lv = 0, lv_ready = 0xffffffffu;
+        for (uint32_t gb = nbins + (bid - nimg) * NW + wv; gb < bp.total_bins; gb += nw) {
             gb = __builtin_amdgcn_readfirstlane(gb);
             while (lv + 1 < nlev && gb >= bp.bin0[lv + 1]) ++lv;
-            if (!wave_bin(rows_seen, wave_rows_max, gb, lv, gb - bp.bin0[lv], bp.cap[lv], bp.item0[lv], bp.off[lv], bp.off[lv + 1],
+            if constexpr (FUSED) {  // this level's bin workgroups have stored their items
+                if (lv != lv_ready && __builtin_amdgcn_readfirstlane(rows_seen) <= wave_rows_max) {
+                    if (lane == 0) wait_at_least(fs.done + lv, fs.per_level, fs.err);
+                    lv_ready = lv;
+                }
+            }
+            if (!wave_bin<FUSED>(rows_seen, wave_rows_max, gb, lv, gb - bp.bin0[lv], bp.cap[lv], bp.item0[lv], bp.off[lv], bp.off[lv + 1],
                           cursor, items, grad_grid, nonfinite, spill, spill_bad, reinterpret_cast<uint32_t*>(wl),
                           reinterpret_cast<uint32_t*>(wl) + kWaveWords, wl + kWaveWords, lane))
                 break;
@@ -1498,7 +1586,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
         if (__builtin_amdgcn_readfirstlane(rows_seen) > wave_rows_max) {  // every wave saw the same row count
             wave_role = false;
             nbins = bp.total_bins;
-            ngr_img = gridDim.x;
+            ngr_img = nblk;
         } else {
             STAMP(14, __builtin_amdgcn_s_memtime());
             __syncthreads();  // the workgroup's end below is its last wave's
@@ -1514,11 +1602,27 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
     for (uint32_t j = 0; j < kStep1Loads; ++j) {
         const uint32_t b = t * per + j;
-        cv0[j] = j < per && b < bp.total_bins ? cursor[b] : 0u;
+        cv0[j] = !FUSED && j < per && b < bp.total_bins ? cursor[b] : 0u;
     }
     if (waves && ngr_img == nimg && rows_seen > wave_rows_max) {  // dense regime (decided after the loads above are issued)
         nbins = bp.total_bins;
-        ngr_img = gridDim.x;
+        ngr_img = nblk;
+    }
+    if constexpr (FUSED) {
+        // the levels of this role's bins have stored their items (the dense
+        // regime: every level), then the counts
+        if (t < 64) {
+            for (uint32_t l = 0; l < bp.nlev; ++l) {
+                if (bp.bin0[l] >= nbins) break;
+                if (t == 0) wait_at_least(fs.done + l, fs.per_level, fs.err);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kStep1Loads; ++j) {
+            const uint32_t b = t * per + j;
+            cv0[j] = j < per && b < bp.total_bins ? ld_u32<true>(cursor + b) : 0u;
+        }
     }
     // (after the regime is known: nbins is final here; the host sized the
     // dynamic LDS for every bin whenever the dense regime can occur)
@@ -1556,7 +1660,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
         for (uint32_t j = 0; j < kStep1Loads; ++j) {
             const uint32_t b = t * per + j0 + j;
-            cv[j] = j0 == 0 ? cv0[j] : j0 + j < per && b < nbins ? cursor[b] : 0u;
+            cv[j] = j0 == 0 ? cv0[j] : j0 + j < per && b < nbins ? ld_u32<FUSED>(cursor + b) : 0u;
         }
 #pragma unroll
         for (uint32_t j = 0; j < kStep1Loads; ++j) {
@@ -1597,12 +1701,12 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // kernel) skips it.
     if (!external && t == 0) {
         __threadfence();
-        const uint32_t grp = blockIdx.x % kRetireGroups;
-        const uint32_t members = gridDim.x / kRetireGroups + (grp < gridDim.x % kRetireGroups ? 1u : 0u);
+        const uint32_t grp = bid % kRetireGroups;
+        const uint32_t members = nblk / kRetireGroups + (grp < nblk % kRetireGroups ? 1u : 0u);
         s_last = 0;
         if (atomicAdd(&retire[1 + grp], 1u) == members - 1) {
             retire[1 + grp] = 0;
-            const uint32_t groups = min(gridDim.x, kRetireGroups);
+            const uint32_t groups = min(nblk, kRetireGroups);
             s_last = atomicAdd(&retire[0], 1u) == groups - 1;
         }
     }
@@ -1667,7 +1771,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
 #pragma unroll
         for (uint32_t q = 0; q < kAccBatch; ++q) {
             const uint32_t k = k0 + q * kAccThreads + t;
-            it[q] = k < w.s1 ? __builtin_nontemporal_load(w.src + k) : ~0ull;
+            it[q] = k < w.s1 ? ld_u64<FUSED>(w.src + k) : ~0ull;
         }
     };
     // Only a non-fresh owner reads its slice back. No select on the loaded
@@ -1692,7 +1796,7 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // forward they also got a round-2 unit and finished last.
     const uint32_t ngr = ngr_img, full = total / ngr;
     auto unit_at = [&](uint32_t k) {  // this workgroup's k-th unit, or total (none)
-        const uint32_t uk = k < full ? k * ngr + blockIdx.x : full * ngr + (ngr - 1 - blockIdx.x);
+        const uint32_t uk = k < full ? k * ngr + bid : full * ngr + (ngr - 1 - bid);
         return k <= full && uk < total ? uk : total;
     };
     uint32_t u = unit_at(0);
@@ -1746,14 +1850,14 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
             unsigned long long* sp = spill + 2 * ebase;
 #pragma unroll 1
             for (uint32_t e = t; e < cur.ne; e += kAccThreads) {
-                const ulonglong2 x = reinterpret_cast<const ulonglong2*>(sp)[e];
+                const ulonglong2 x = ld_u64x2<FUSED>(sp + 2 * e);
                 if (x.x | x.y) {
                     acc[e * C] += x.x;
                     acc[e * C + 1] += x.y;
                     reinterpret_cast<ulonglong2*>(sp)[e] = ulonglong2{0ull, 0ull};
                 }
             }
-            if (t == 0 && spill_bad[cur.gb]) {
+            if (t == 0 && ld_u32<FUSED>(spill_bad + cur.gb)) {
                 bad = true;
                 spill_bad[cur.gb] = 0u;
             }
@@ -1892,11 +1996,111 @@ k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ gra
     // call's ring entry (one vector store each, no atomics, so the timed
     // kernel keeps its critical path); the host takes the latest
     if (timing && t == 0) {
-        const uint32_t c = (timing[0] - 1) % NGP_GRID_TIMING_RING;
-        if (blockIdx.x == 0) timing[kTimingHeads + c * 4 + 2] = gridDim.x;
-        if (blockIdx.x < NGP_GRID_TIMING_MAX_WG)
-            timing[kTimingEnds + c * NGP_GRID_TIMING_MAX_WG + blockIdx.x] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        // (the one-launch form: level 0's first bin workgroup opened this
+        // call's entry; wait for it before reading the call count)
+        if constexpr (FUSED) wait_at_least(fs.opened, 1u, fs.err);
+        const uint32_t c = (ld_u32<FUSED>(timing) - 1) % NGP_GRID_TIMING_RING;
+        if (bid == 0) timing[kTimingHeads + c * 4 + 2] = nblk;
+        if (bid < NGP_GRID_TIMING_MAX_WG)
+            timing[kTimingEnds + c * NGP_GRID_TIMING_MAX_WG + bid] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     }}
+
+template <bool ZEROED>
+__global__ void __launch_bounds__(kAccThreads, 4)  // 2 workgroups per CU: <= 128 VGPRs
+k_grid_bin_accum(const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, BinPlan bp,
+                 uint32_t* __restrict__ cursor, uint32_t* __restrict__ retire,
+                 const BinItem* __restrict__ items, int32_t* __restrict__ nonfinite,
+                 bool external, unsigned long long* __restrict__ msums,
+                 uint32_t* __restrict__ marrive, uint32_t* __restrict__ timing,
+                 int32_t* __restrict__ reset_counter, unsigned long long* __restrict__ spill,
+                 uint32_t* __restrict__ spill_bad, uint32_t wave_bins0, uint32_t nimg,
+                 const uint32_t* __restrict__ rows_in, uint32_t wave_rows_max) {
+    // [entry][channel]; a channel-planar image (8-byte lane stride for the
+    // 64-bit atomics instead of 16) measured the same
+    __shared__ __attribute__((aligned(16))) unsigned long long acc[kBinEntries * 2];
+    extern __shared__ uint32_t dyn[];
+    accum_block<ZEROED, false>(offsets, grad_grid, bp, cursor, retire, items, nonfinite, external, msums, marrive,
+                               timing, reset_counter, spill, spill_bad, wave_bins0, nimg, rows_in, wave_rows_max,
+                               blockIdx.x, gridDim.x, acc, dyn, FusedSync{});
+}
+
+// The grid backward as ONE launch (round 7; the fused step's configuration:
+// cursors cleared by the caller, a zeroed grad, the wave bins). A workgroup
+// takes a ticket: the first nlev x ycap tickets bin (level, point block), the
+// next ones run the MLP dW reduce and the sampler columns, the rest
+// accumulate. Tickets are taken in order by running workgroups, so when an
+// accumulate workgroup waits on a level's done counter, every bin workgroup
+// of that level holds a ticket and is running or finished: no wait depends
+// on a workgroup that may not be resident (MI355X_MICROARCH.md: dispatch
+// order is not promised). A hashed bin's wave starts as soon as its level's
+// bin workgroups are done instead of after the whole bin launch and the
+// launch boundary; the dense levels' image units after theirs. Items are
+// stored and loaded `sc1`, the done counters are agent-scope atomics added
+// after every storing wave's vmcnt(0) wait and a workgroup barrier.
+template <uint32_t D, uint32_t NBMAX>
+__global__ void __launch_bounds__(kAccThreads, 4)
+k_grid_bwd_fused(const ngp_half* __restrict__ grad, const float* __restrict__ inputs,
+                 const int32_t* __restrict__ offsets, ngp_half* __restrict__ grad_grid, uint32_t B,
+                 uint32_t L, GridLevels lv, uint32_t gridtype, bool align_corners, uint32_t interp,
+                 InMap im, BinPlan bp, uint32_t* __restrict__ cursor, BinItem* __restrict__ items,
+                 int32_t grad_layout, int32_t* __restrict__ nonfinite, ngp_reduce::ReduceJobs rj, uint32_t nred,
+                 uint32_t* __restrict__ timing, BinLego next_batch, unsigned long long* __restrict__ spill,
+                 uint32_t* __restrict__ spill_bad, uint32_t* __restrict__ retire,
+                 unsigned long long* __restrict__ msums, uint32_t* __restrict__ marrive,
+                 int32_t* __restrict__ reset_counter, uint32_t wave_bins0, uint32_t nimg,
+                 const uint32_t* __restrict__ rows_in, uint32_t wave_rows_max, uint32_t ycap, uint32_t nacc) {
+    static_assert(kAccThreads == kBinPts, "one workgroup size for both roles");
+    static_assert(bin_lds_words<NBMAX>() * 4 <= kBinEntries * 2 * sizeof(unsigned long long),
+                  "the bin role's LDS fits the accumulate's image");
+    __shared__ __attribute__((aligned(16))) unsigned long long acc[kBinEntries * 2];
+    extern __shared__ uint32_t dyn[];
+    __shared__ uint32_t s_tk;
+    uint32_t* fw = retire + kFusedWords;  // ticket, finished, error, -, done[level]
+    if constexpr (kFusedBwd == 2) {
+        // the grid is one co-resident wave of workgroups (2 per CU): the
+        // block index is the role (no ticket: one returning atomic per
+        // workgroup on one word serialised ~1,550 of them, r07s)
+        if (threadIdx.x == 0) s_tk = blockIdx.x;
+    } else {
+        if (threadIdx.x == 0) s_tk = atomicAdd(fw, 1u);
+    }
+    __syncthreads();
+    const uint32_t tk = s_tk, nlev = bp.nlev;
+    const uint32_t nbin = nlev * ycap, nextra = nred + next_batch.nlego;
+    if (tk < nbin + nextra) {
+        uint32_t bx, by;
+        if (tk < nbin) {
+            bx = tk % nlev;
+            by = tk / nlev;
+        } else if (tk < nbin + nred) {
+            bx = nlev;  // the dW reduce column
+            by = tk - nbin;
+        } else {
+            bx = nlev + (nred ? 1u : 0u);  // the sampler column
+            by = tk - nbin - nred;
+        }
+        bin_block<D, NBMAX, true>(grad, inputs, offsets, grad_grid, B, L, lv, gridtype, align_corners, interp, im,
+                                  bp, cursor, items, grad_layout, nonfinite, rj, nred, timing, next_batch, spill,
+                                  spill_bad, nullptr, bx, by, ycap, reinterpret_cast<uint32_t*>(acc));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores and atomics have landed
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (tk == 0) atomicAdd(fw + 3, 1u);  // the timing entry is open (timing[0] stored atomically)
+            if (tk < nbin) atomicAdd(fw + 4 + bx, 1u);
+            // the last of the non-accumulate workgroups: every reader of this
+            // batch's sample counter (the bin and sampler workgroups) is done
+            if (atomicAdd(fw + 1, 1u) == nbin + nextra - 1 && reset_counter) {
+                reset_counter[0] = 0;
+                reset_counter[1] = 0;
+            }
+        }
+        return;
+    }
+    const FusedSync fs{fw + 4, ycap, fw + 2, fw + 3};
+    accum_block<true, true>(offsets, grad_grid, bp, cursor, retire, items, nonfinite, true, msums, marrive, timing,
+                            nullptr, spill, spill_bad, wave_bins0, nimg, rows_in, wave_rows_max, tk - nbin - nextra,
+                            nacc, acc, dyn, fs);
+}
 
 // GradScaler's inf/nan check over a grad range (levels the binned path does
 // not cover): sets *flag.
@@ -1955,7 +2159,7 @@ static size_t bin_items_bytes(const BinPlan& bp) {
     for (uint32_t l = 0; l < bp.nlev; ++l) slots += (size_t)bp.nbins[l] * bp.cap[l];
     return (slots * sizeof(BinItem) + 255) / 256 * 256;
 }
-static size_t bin_sums_offset(const BinPlan& bp) { return bin_counters_bytes(bp) + 256 + bin_items_bytes(bp); }
+static size_t bin_sums_offset(const BinPlan& bp) { return bin_counters_bytes(bp) + kRetireBytes + bin_items_bytes(bp); }
 static size_t bin_arrive_offset(const BinPlan& bp) {
     return bin_sums_offset(bp) + (size_t)bp.nmslots * kBinEntries * 2 * sizeof(unsigned long long);
 }
@@ -2383,7 +2587,7 @@ extern "C" size_t ngp_grid_encode_backward_fused_counter_bytes(uint32_t B, uint3
     GridLevels lv;
     make_levels(lv, L, S, H);
     const BinPlan bp = make_bin_plan(offsets_host, L, D, lv, align_corners != 0, B);
-    return bp.nlev ? bin_counters_bytes(bp) : 0;
+    return bp.nlev ? bin_counters_bytes(bp) + kRetireBytes : 0;
 }
 
 namespace {
@@ -2426,7 +2630,7 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
     if (bp.nlev) {  // the workspace's counters start zeroed and are left zeroed
         uint32_t* cursor = static_cast<uint32_t*>(workspace);
         uint32_t* retire = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + bin_counters_bytes(bp));
-        BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) + bin_counters_bytes(bp) + 256);
+        BinItem* items = reinterpret_cast<BinItem*>(static_cast<char*>(workspace) + bin_counters_bytes(bp) + kRetireBytes);
         unsigned long long* msums =
             reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) + bin_sums_offset(bp));
         uint32_t* timing =
@@ -2443,49 +2647,91 @@ int bwd_fused_impl(const void* grad, const float* xyz, float bound, const int32_
                         std::max(std::max(std::min(ngp_div_up(B, kBinPts), kBinYCap), nred), bl.nlego));
         uint32_t nbmax = 0;
         for (uint32_t l = 0; l < bp.nlev; ++l) nbmax = std::max(nbmax, bp.nbins[l]);
-        if (nbmax <= kMaxBinsPerLevel)
-            k_grid_bwd_bin<3, kMaxBinsPerLevel><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
-                (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad, retire + kRowsWord);
-        else
-            k_grid_bwd_bin<3, kMaxBinsPerLevelBig><<<grid, kBinPts, kBinPts * 8 * sizeof(BinItem), st>>>(
-                (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
-                im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad, retire + kRowsWord);
-        // the hashed levels' bins one per wave (wave_bin) when the grad is
-        // cleared and the caller clears the cursors (the fused step): the
-        // image path then covers only the dense levels' bins, on the first
-        // kAccImageWgs workgroups
-        const bool waves = zeroed && external && kWaveBins && bp.img_bins < bp.total_bins;
-        const uint32_t img_bins = waves ? bp.img_bins : bp.total_bins;
-        // two persistent workgroups per CU while both fit the CU's LDS (the
-        // 64 KiB image + two words per bin), else one. With the wave bins the
-        // image path may take every bin in the dense regime (more rows than
-        // wave_rows_max: ~kWaveMax items per hashed bin), when two workgroups
-        // per CU still fit that; else the wave bins take the hashed levels
-        // whatever the rows.
-        auto two_fit = [](size_t d) { return 2 * (d + kAccStaticLds) <= 160 * 1024; };
-        const size_t dyn_all = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
-        const bool dense_ok = waves && two_fit(dyn_all);
-        const size_t dyn = dense_ok || !waves ? dyn_all : (2 * (size_t)img_bins + 1) * sizeof(uint32_t);
-        const uint32_t per_cu = two_fit(dyn) ? 2u : 1u;
-        const uint32_t grid_acc = per_cu * ngp_num_cus();
-        const uint32_t nimg = waves ? (img_bins ? std::min(kAccImageWgs, grid_acc / 2) : 0u) : grid_acc;
-        uint32_t wave_rows_max = 0xffffffffu;
-        if (dense_ok) {
-            uint32_t hl = 0;  // the first level of the wave bins
-            while (hl + 1 < bp.nlev && bp.bin0[hl + 1] <= img_bins) ++hl;
-            wave_rows_max = (uint32_t)std::min<uint64_t>(0xfffffffeu, (uint64_t)kWaveMax * bp.nbins[hl] >> 3);
+        // the one-launch form (k_grid_bwd_fused) where the wave bins run: the
+        // same kernels' work, the accumulate's waits per level
+        const bool waves_cfg = zeroed && external && kWaveBins && bp.img_bins < bp.total_bins;
+        const bool fused_fits = kFusedBwd != 2 ||
+                                bp.nlev * std::min(ngp_div_up(B, kBinPts), 8u) + nred + bl.nlego + kAccImageWgs + 64 <=
+                                    2 * ngp_num_cus();
+        if (kFusedBwd && waves_cfg && fused_fits && B >= 1) {
+            const uint32_t img_bins = bp.img_bins;
+            auto two_fit = [](size_t d) { return 2 * (d + kAccStaticLds) <= 160 * 1024; };
+            const size_t dyn_all = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
+            const bool dense_ok = two_fit(dyn_all);
+            const size_t dyn = dense_ok ? dyn_all : (2 * (size_t)img_bins + 1) * sizeof(uint32_t);
+            const uint32_t per_cu = two_fit(dyn) ? 2u : 1u;
+            const uint32_t nacc = per_cu * ngp_num_cus();
+            const uint32_t nimg = img_bins ? std::min(kAccImageWgs, nacc / 2) : 0u;
+            uint32_t wave_rows_max = 0xffffffffu;
+            if (dense_ok) {
+                uint32_t hl = 0;
+                while (hl + 1 < bp.nlev && bp.bin0[hl + 1] <= img_bins) ++hl;
+                wave_rows_max = (uint32_t)std::min<uint64_t>(0xfffffffeu, (uint64_t)kWaveMax * bp.nbins[hl] >> 3);
+            }
+            const uint32_t ycap = std::min(ngp_div_up(B, kBinPts), kFusedBwd == 2 ? 8u : kFusedYCap);
+            uint32_t nacc_l = nacc;
+            if (kFusedBwd == 2) {  // one co-resident grid: the accumulate takes what the bin roles leave
+                const uint32_t used = bp.nlev * ycap + nred + bl.nlego;
+                nacc_l = used + nimg + 64 <= nacc ? nacc - used : 0u;
+            }
+            const uint32_t nblocks = bp.nlev * ycap + nred + bl.nlego + nacc_l;
+            int32_t* reset = bl.nlego ? bl.out.counter : nullptr;
+            const uint32_t* rows_in = reinterpret_cast<const uint32_t*>(count);
+            if (nbmax <= kMaxBinsPerLevel)
+                k_grid_bwd_fused<3, kMaxBinsPerLevel><<<nblocks, kAccThreads, dyn, st>>>(
+                    (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
+                    im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad, retire,
+                    msums, marrive, reset, img_bins, nimg, rows_in, wave_rows_max, ycap, nacc_l);
+            else
+                k_grid_bwd_fused<3, kMaxBinsPerLevelBig><<<nblocks, kAccThreads, dyn, st>>>(
+                    (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
+                    im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad, retire,
+                    msums, marrive, reset, img_bins, nimg, rows_in, wave_rows_max, ycap, nacc_l);
+        } else {
+            if (nbmax <= kMaxBinsPerLevel)
+                k_grid_bwd_bin<3, kMaxBinsPerLevel><<<grid, kBinPts, bin_lds_words<kMaxBinsPerLevel>() * 4, st>>>(
+                    (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
+                    im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad, retire + kRowsWord);
+            else
+                k_grid_bwd_bin<3, kMaxBinsPerLevelBig><<<grid, kBinPts, bin_lds_words<kMaxBinsPerLevelBig>() * 4, st>>>(
+                    (const ngp_half*)grad, xyz, offsets, (ngp_half*)grad_embeddings, B, L, lv, gridtype, ac, interp,
+                    im, bp, cursor, items, grad_layout, nonfinite, rjv, nred, timing, bl, spill, spill_bad, retire + kRowsWord);
+            // the hashed levels' bins one per wave (wave_bin) when the grad is
+            // cleared and the caller clears the cursors (the fused step): the
+            // image path then covers only the dense levels' bins, on the first
+            // kAccImageWgs workgroups
+            const bool waves = zeroed && external && kWaveBins && bp.img_bins < bp.total_bins;
+            const uint32_t img_bins = waves ? bp.img_bins : bp.total_bins;
+            // two persistent workgroups per CU while both fit the CU's LDS (the
+            // 64 KiB image + two words per bin), else one. With the wave bins the
+            // image path may take every bin in the dense regime (more rows than
+            // wave_rows_max: ~kWaveMax items per hashed bin), when two workgroups
+            // per CU still fit that; else the wave bins take the hashed levels
+            // whatever the rows.
+            auto two_fit = [](size_t d) { return 2 * (d + kAccStaticLds) <= 160 * 1024; };
+            const size_t dyn_all = (2 * (size_t)bp.total_bins + 1) * sizeof(uint32_t);
+            const bool dense_ok = waves && two_fit(dyn_all);
+            const size_t dyn = dense_ok || !waves ? dyn_all : (2 * (size_t)img_bins + 1) * sizeof(uint32_t);
+            const uint32_t per_cu = two_fit(dyn) ? 2u : 1u;
+            const uint32_t grid_acc = per_cu * ngp_num_cus();
+            const uint32_t nimg = waves ? (img_bins ? std::min(kAccImageWgs, grid_acc / 2) : 0u) : grid_acc;
+            uint32_t wave_rows_max = 0xffffffffu;
+            if (dense_ok) {
+                uint32_t hl = 0;  // the first level of the wave bins
+                while (hl + 1 < bp.nlev && bp.bin0[hl + 1] <= img_bins) ++hl;
+                wave_rows_max = (uint32_t)std::min<uint64_t>(0xfffffffeu, (uint64_t)kWaveMax * bp.nbins[hl] >> 3);
+            }
+            uint32_t* rows_word = retire + kRowsWord;  // written by the bin launch
+            int32_t* reset = bl.nlego ? bl.out.counter : nullptr;
+            if (zeroed)
+                k_grid_bin_accum<true><<<grid_acc, kAccThreads, dyn, st>>>(
+                    offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
+                    marrive, timing, reset, spill, spill_bad, img_bins, nimg, waves ? rows_word : nullptr, wave_rows_max);
+            else
+                k_grid_bin_accum<false><<<grid_acc, kAccThreads, dyn, st>>>(
+                    offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
+                    marrive, timing, reset, spill, spill_bad, img_bins, nimg, waves ? rows_word : nullptr, wave_rows_max);
         }
-        uint32_t* rows_word = retire + kRowsWord;  // written by the bin launch
-        int32_t* reset = bl.nlego ? bl.out.counter : nullptr;
-        if (zeroed)
-            k_grid_bin_accum<true><<<grid_acc, kAccThreads, dyn, st>>>(
-                offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
-                marrive, timing, reset, spill, spill_bad, img_bins, nimg, waves ? rows_word : nullptr, wave_rows_max);
-        else
-            k_grid_bin_accum<false><<<grid_acc, kAccThreads, dyn, st>>>(
-                offsets, (ngp_half*)grad_embeddings, bp, cursor, retire, items, nonfinite, external, msums,
-                marrive, timing, reset, spill, spill_bad, img_bins, nimg, waves ? rows_word : nullptr, wave_rows_max);
     }
     if (bp.nlev < L) {  // levels past the binned prefix: merged atomics
         if (D == 3 && C == 2) {
