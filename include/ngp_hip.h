@@ -354,9 +354,11 @@ size_t ngp_grid_encode_backward_fused_workspace_bytes(uint32_t B, uint32_t D, ui
  * their sums instead of reading the slice back first. */
 #define NGP_GRID_GRAD_ZEROED 0x10
 /* grad_layout | NGP_GRID_CURSORS_EXTERNAL: the caller zeroes the workspace's
- * first ngp_grid_encode_backward_fused_counter_bytes bytes (the bin cursors)
- * between calls (the fused step's head kernel does), so the call does not
- * leave them zeroed itself. */
+ * first ngp_grid_encode_backward_fused_counter_bytes bytes (the bin cursors and
+ * the 512-byte area after them) between calls (the fused step's march launch
+ * does), so the call does not leave them zeroed itself. With
+ * NGP_GRID_GRAD_ZEROED too, the hashed levels' bins are summed one per wave
+ * (same sums, same bits as the workgroup image path; round 7). */
 #define NGP_GRID_CURSORS_EXTERNAL 0x20
 /* grad_layout | NGP_GRID_TIMING: the binned launches time themselves on the
  * chip's 100 MHz constant clock (s_memrealtime) into a ring in the workspace

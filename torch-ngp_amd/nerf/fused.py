@@ -1111,6 +1111,7 @@ class FusedTrainer:
         for _ in range(warmup):
             self.step()
         torch.cuda.synchronize()
+        self._drain_watchdog()
         if ring and not self.dp:
             self._ring, self._ring_i = [], 0
             try:
@@ -1202,6 +1203,20 @@ class FusedTrainer:
             self.graph = graphs
         # capture recorded the launches without running them: the pending
         # update is still pending and the next step() replays it first
+
+    def _drain_watchdog(self):
+        """Before a capture over RCCL: wait until the process group's watchdog
+        has retired every eager collective. Its poll queries each work's end
+        event, and HIP answers a query of an event last recorded on a stream
+        that has since joined a capture with hipErrorCapturedEvent, which ends
+        the watchdog thread and aborts the process (seen once in a round-7
+        bench run: an eager collective's work still listed when the next
+        capture forked RCCL's stream)."""
+        if not self._nccl:
+            return
+        wait = getattr(dist.distributed_c10d._get_default_group(), "_wait_for_pending_works", None)
+        if wait is not None:
+            wait()
 
     def _capture_replicated(self, multi):
         """sparse_exchange over RCCL: the world-1 body graphs with the
