@@ -274,6 +274,37 @@ NGP_DEV void pack_act(const f32x4 (&acc)[NB][MT], ACT act, half8 (&out)[NB][KS])
         }
 }
 
+// ReLU policy: round each pair of accumulators to fp16 (RNE, one packed
+// conversion), then a packed signed 16-bit max with 0: every negative value,
+// -0 included, has the sign bit set and becomes +0. That is max(x, 0) rounded,
+// for every non-NaN x (a NaN with the sign bit clear stays NaN, as torch's
+// ReLU keeps it), at 2 VALU per 2 values; the fp32 compare/select before the
+// conversion was ~2 per value (a fifth of k_nerf_fwd's instructions).
+typedef short ngp_short2 __attribute__((ext_vector_type(2)));
+typedef float ngp_float2 __attribute__((ext_vector_type(2)));
+template <int MT, int KS, int NB>
+NGP_DEV void pack_act(const f32x4 (&acc)[NB][MT], ActReLU, half8 (&out)[NB][KS]) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            half8 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int mt = 2 * s + (j >> 1), r = 2 * (j & 1);
+                ngp_short2 q = ngp_short2{0, 0};
+                if (mt < MT) {
+                    const ngp_half2 h = __builtin_convertvector(ngp_float2{acc[nb][mt][r], acc[nb][mt][r + 1]}, ngp_half2);
+                    q = __builtin_elementwise_max(__builtin_bit_cast(ngp_short2, h), ngp_short2{0, 0});
+                }
+                const ngp_half2 h = __builtin_bit_cast(ngp_half2, q);
+                v[2 * j] = h[0];
+                v[2 * j + 1] = h[1];
+            }
+            out[nb][s] = v;
+        }
+}
+
 // load a [rows, width] fp16 row-major block as natural-K B operands
 template <int KS, int NB>
 NGP_DEV void load_rows(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t B,
@@ -330,6 +361,37 @@ struct InPairMajor {
                     v[2 * p + 1] = ok ? h[1] : (ngp_half)0.0f;
                 }
                 out[nb][s] = v;
+            }
+        }
+    }
+};
+
+// The forward kernels' pair-major loads (k_density_fwd, k_nerf_fwd): one
+// buffer descriptor over the [width / 2][ld] pairs, the lane's pair row in the
+// 32-bit voffset and each pair's distance (p ld 4 bytes) in an SGPR soffset:
+// no 64-bit address, clamp or select per load (InPairMajor spent ~30 VALU per
+// 32-row chunk on them). Rows are not masked: a forward's columns (samples)
+// are independent and its epilogues store rows < B only, so a row in [B, ld)
+// may hold anything, and a row past the allocation reads 0 (range check).
+struct InPairMajorFwd {
+    uint32_t ld;  // allocated rows
+    template <int KS, int NB>
+    NGP_DEV void operator()(const ngp_half* __restrict__ src, uint32_t width, uint32_t row0, uint32_t,
+                            half8 (&out)[NB][KS]) const {
+        const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<ngp_half*>(src), (short)0, (int)(width / 2 * ld * 4u), 0x00020000);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const uint32_t col = 32 * s + 8 * g;
+                const int voff = (int)(((col / 2) * ld + row0 + nb * 16 + c) * 4u);
+                uint32_t w[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) w[p] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (int)(p * ld * 4u), 0);
+                const half8 v = __builtin_bit_cast(half8, (uint4{w[0], w[1], w[2], w[3]}));
+                out[nb][s] = col < width ? v : half8{0, 0, 0, 0, 0, 0, 0, 0};
             }
         }
     }
@@ -548,50 +610,66 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
 
 
 // The density query's sigma network (update_extra_state, renderer.py:533-538)
-// on the pair-major encodings of the grid forward, from the prepacked image:
-// each wave requests its next chunk's encodings and cell indices before it
-// computes the current one, so the 1-2M-point batch streams at HBM rate
-// instead of one round trip per chunk. Same values as k_mlp_fwd<EpiDensity>.
+// on the pair-major encodings of the grid forward, from the prepacked image.
+// A 1-2M-point batch is a stream (64 B of encodings per point): the grid is
+// sized to the workgroups that are resident at once (the occupancy query in
+// launch_fwd_density) and each wave keeps its next kDensityPf chunks' encodings
+// and cell indices in flight while it computes the current one, so the bytes
+// in flight cover HBM's latency (one chunk ahead at 3 waves per SIMD left
+// ~6 MB in flight: 2.5 TB/s). Same values as k_mlp_fwd<EpiDensity>.
+#ifndef NGP_DENSITY_PF
+#define NGP_DENSITY_PF 1
+#endif
+constexpr int kDensityPf = NGP_DENSITY_PF;
 template <int W, int NH>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
 k_density_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img, uint32_t B, EpiDensity epi) {
     using N = Net<W, 1, NH>;
-    const InPairMajor xl{B};
+    const InPairMajorFwd xl{B};
     extern __shared__ half8 lds[];
     const ActReLU act;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB), stride = gridDim.x * kWaves;
     uint32_t chunk = blockIdx.x * kWaves + wave;
-    half8 xn[kNB][1];
-    int32_t in_[kNB];
-    xl.template operator()<1>(enc, 32u, chunk * 16 * kNB, B, xn);
-    epi.load_index(chunk * 16 * kNB, B, in_);
+    half8 xn[kDensityPf][kNB][1];
+    int32_t in_[kDensityPf][kNB];
+#pragma unroll
+    for (int s = 0; s < kDensityPf; ++s) {  // clamped rows past the batch: no branch
+        xl.template operator()<1>(enc, 32u, (chunk + s * stride) * 16 * kNB, B, xn[s]);
+        epi.load_index((chunk + s * stride) * 16 * kNB, B, in_[s]);
+    }
     copy_frags<N::FWD_FRAGS, kThreads>(lds, img);
     __syncthreads();
-    for (; chunk < nchunks; chunk += stride) {
-        const uint32_t row0 = chunk * 16 * kNB;
-        half8 x[kNB][1];
-        int32_t ix[kNB];
+    for (; chunk < nchunks; chunk += kDensityPf * stride) {
 #pragma unroll
-        for (int nb = 0; nb < kNB; ++nb) {
-            x[nb][0] = xn[nb][0];
-            ix[nb] = in_[nb];
-        }
-        // the next chunk's inputs (clamped rows: no branch), in flight during this one
-        xl.template operator()<1>(enc, 32u, row0 + stride * 16 * kNB, B, xn);
-        epi.load_index(row0 + stride * 16 * kNB, B, in_);
-        f32x4 acc[kNB][N::MTW];
-        half8 h[kNB][N::KSW];
-        dense<N::MTW, 1>(lds, fwd_desc<W, 1, NH>(0, 32u).frag0, x, acc);
-        pack_act<N::MTW, N::KSW>(acc, act, h);
+        for (int s = 0; s < kDensityPf; ++s) {
+            const uint32_t c = chunk + s * stride;
+            if (c >= nchunks) break;  // uniform in the wave
+            const uint32_t row0 = c * 16 * kNB;
+            half8 x[kNB][1];
+            int32_t ix[kNB];
 #pragma unroll
-        for (int q = 1; q <= NH; ++q) {
-            dense<N::MTW, N::KSW>(lds, fwd_desc<W, 1, NH>(q, 32u).frag0, h, acc);
+            for (int nb = 0; nb < kNB; ++nb) {
+                x[nb][0] = xn[s][nb][0];
+                ix[nb] = in_[s][nb];
+            }
+            // the chunk kDensityPf strides ahead into the freed slot
+            const uint32_t ahead = (c + kDensityPf * stride) * 16 * kNB;
+            xl.template operator()<1>(enc, 32u, ahead, B, xn[s]);
+            epi.load_index(ahead, B, in_[s]);
+            f32x4 acc[kNB][N::MTW];
+            half8 h[kNB][N::KSW];
+            dense<N::MTW, 1>(lds, fwd_desc<W, 1, NH>(0, 32u).frag0, x, acc);
             pack_act<N::MTW, N::KSW>(acc, act, h);
+#pragma unroll
+            for (int q = 1; q <= NH; ++q) {
+                dense<N::MTW, N::KSW>(lds, fwd_desc<W, 1, NH>(q, 32u).frag0, h, acc);
+                pack_act<N::MTW, N::KSW>(acc, act, h);
+            }
+            f32x4 o[kNB][1];
+            dense<1, N::KSW>(lds, fwd_desc<W, 1, NH>(NH + 1, 32u).frag0, h, o);
+            epi.run(row0, B, o, ActNone{}, ix);
         }
-        f32x4 o[kNB][1];
-        dense<1, N::KSW>(lds, fwd_desc<W, 1, NH>(NH + 1, 32u).frag0, h, o);
-        epi.run(row0, B, o, ActNone{}, ix);
     }
 }
 
@@ -603,12 +681,12 @@ k_density_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img, u
 // color_in read and its fragment copy and launch tail go away. Both networks
 // are W wide with 32 inputs; the images are the ngp_ffmlp_pack ones.
 template <int W, int NHS, int NHC>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
 k_nerf_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img_s, const half8* __restrict__ img_c,
            uint32_t B, const int32_t* __restrict__ count, EpiNerfSigma es, ngp_half* __restrict__ color_out) {
     using NS = Net<W, 1, NHS>;
     using NC = Net<W, 1, NHC>;
-    const InPairMajor xl{B};  // the encodings' allocated rows
+    const InPairMajorFwd xl{B};  // the encodings' allocated rows
     FRSTAMP(8);
     FSTAMPW(0);
     if (count) B = *count <= 0 ? 0u : min(B, (uint32_t)*count);
@@ -1311,11 +1389,26 @@ int launch_fwd_density(const void* in, const void* w, const void* image, uint32_
                        const EpiDensity& epi, hipStream_t st) {
     if (IN_KS == 1 && image) {  // the streaming kernel (prepacked image, 32 inputs)
         using N = Net<W, 1, NH>;
+        const size_t lds = (size_t)N::FWD_FRAGS * 64 * 16;
+        // the workgroups resident at once (occupancy x CUs, queried once per
+        // device and shape): each wave then streams its share of the chunks
+        static int resident[16] = {0};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16)
+            return ngp_set_error(NGP_ERR_HIP, "nerf_density_forward: no current device");
+        if (resident[dev] == 0) {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_density_fwd<W, NH>, kThreads, lds) !=
+                    hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                return ngp_set_error(NGP_ERR_HIP, "nerf_density_forward: occupancy query failed");
+            resident[dev] = std::max(1, per_cu) * std::max(1, cus);
+        }
         const uint32_t nchunks = ngp_div_up(B, 16 * kNB);
-        uint32_t blocks = ngp_div_up(nchunks, kWaves);
-        if (blocks > 2048) blocks = 2048;
-        hipLaunchKernelGGL((k_density_fwd<W, NH>), dim3(blocks), dim3(kThreads), (size_t)N::FWD_FRAGS * 64 * 16, st,
-                           (const ngp_half*)in, (const half8*)image, B, epi);
+        const uint32_t blocks = std::min<uint32_t>(ngp_div_up(nchunks, kWaves), (uint32_t)resident[dev]);
+        if (blocks == 0) return NGP_OK;
+        hipLaunchKernelGGL((k_density_fwd<W, NH>), dim3(blocks), dim3(kThreads), lds, st, (const ngp_half*)in,
+                           (const half8*)image, B, epi);
         return ngp_check_launch("nerf_density_forward");
     }
     return launch_fwd_t<W, IN_KS, NH>(in, w, image, B, in_dim, ActReLU{}, ActNone{}, nullptr, nullptr, epi, st,
