@@ -621,8 +621,11 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
 #define NGP_DENSITY_PF 1
 #endif
 constexpr int kDensityPf = NGP_DENSITY_PF;
+#ifndef NGP_DENSITY_WPE
+#define NGP_DENSITY_WPE 2
+#endif
 template <int W, int NH>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(NGP_DENSITY_WPE)))
 k_density_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img, uint32_t B, EpiDensity epi) {
     using N = Net<W, 1, NH>;
     const InPairMajorFwd xl{B};
@@ -829,6 +832,40 @@ NGP_DEV void pack_delta(const f32x4 (&acc)[NB][MT], const half8 (&h)[NB][KS], AC
                 v[j] = mt < MT ? (ngp_half)act.bwd(acc[nb][mt][j & 3], (float)h[nb][s][j]) : (ngp_half)0.0f;
             }
             out[nb][s] = v;
+        }
+}
+
+// ReLU policy: the delta pairs rounded to fp16 (one packed conversion), then
+// masked where the post-activation is 0. The recomputed activations come from
+// pack_act's ReLU, so they are +0 or positive (bits in (0, 0x7fff] as signed
+// 16-bit values): 0 - y is negative exactly where y > 0, and its sign spread
+// over the half (>> 15) is the mask. Equal to (y > 0 ? g : 0) rounded, at 4
+// VALU per 2 values against ~8 (an fp32 conversion of y, a compare and a
+// select per value, and single conversions).
+template <int MT, int KS, int NB>
+NGP_DEV void pack_delta(const f32x4 (&acc)[NB][MT], const half8 (&h)[NB][KS], ActReLU, half8 (&out)[NB][KS]) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const uint4 hv = __builtin_bit_cast(uint4, h[nb][s]);
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int mt = 2 * s + (j >> 1), r = 2 * (j & 1);
+                o[j] = 0u;
+                if (mt < MT) {
+                    const ngp_half2 g2 =
+                        __builtin_convertvector(ngp_float2{acc[nb][mt][r], acc[nb][mt][r + 1]}, ngp_half2);
+                    // (the compiler rewrites the C form into two compares and
+                    // selects; op_sel_hi:[0,1]: both halves shift by the
+                    // constant's low half)
+                    uint32_t m;
+                    asm("v_pk_sub_i16 %0, 0, %1\n\tv_pk_ashrrev_i16 %0, 15, %0 op_sel_hi:[0,1]" : "=&v"(m) : "v"(hv[j]));
+                    o[j] = __builtin_bit_cast(uint32_t, g2) & m;
+                }
+            }
+            out[nb][s] = __builtin_bit_cast(half8, (uint4{o[0], o[1], o[2], o[3]}));
         }
 }
 
