@@ -3,7 +3,8 @@ after 16 full ones) on the bench's Lego workload: run it under
 `rocprofv3 --kernel-trace --stats` and read the per-kernel stats; the script
 prints the mean wall time of `reps` updates each followed by a training step
 (the bench's cadence work between two updates is 16 steps).
-    rocprofv3 --kernel-trace --stats -d OUT -o run -- python3 tools/density_trace.py [reps]"""
+    rocprofv3 --kernel-trace --stats -d OUT -o run -- python3 tools/density_trace.py [reps] [options-json]"""
+import json
 import os
 import sys
 import time
@@ -17,12 +18,13 @@ import bench  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    opts = json.loads(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] else None
     argv, sys.argv = sys.argv, sys.argv[:1]
     args = bench.parse()
     sys.argv = argv
     dev = torch.device("cuda:0")
     model, data, bits, *_, dt_gamma = bench.make_workload("lego", dev, 1, args.num_rays)
-    ft, _ = bench.make_trainer(args, model, data, 1, dev, dt_gamma, grid_timing=False)
+    ft, _ = bench.make_trainer(args, model, data, 1, dev, dt_gamma, grid_timing=False, options=opts)
     ft.capture(multi=args.graph_steps)
     ft.run(200)
     while model.iter_density < 16:

@@ -86,7 +86,8 @@ def _vp_array(ptrs):
 #                 reduce-scatter, which rounds at every ring hop
 DEFAULT_OPTIONS = dict(table16=False, split_head=False, split_reduce=False, split_fwd=False, split_bwd=False,
                        march_adam=True, tail_in_fwd=True, emit_inline=True, draw_ahead=True, live_rows=True,
-                       dp_graph=True, density_sort=True, sparse_exchange=False, exact_reduce=False)
+                       dp_graph=True, density_sort=True, sparse_exchange=False, exact_reduce=False,
+                       density_run_max=True)
 
 
 class FusedTrainer:
@@ -437,11 +438,15 @@ class FusedTrainer:
         # step packs them again from the same weights)
         nat.check(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
         dens = (P_(d["enc"]), P_(self.mlp_img[0]), n, sn.hidden_dim, sn.num_layers, float(m.density_scale))
-        if sorted_:
+        if sorted_ and self.options["density_run_max"]:
             # densities per point, then each run of one cell's draws -> its max (no global atomics)
             nat.check(lib.ngp_nerf_density_forward_rows(*dens, P_(d["sigma"]), s), "nerf_density_forward_rows")
             nat.check(lib.ngp_density_grid_run_max(P_(d["sigma"]), P_(d["idx"]), C, H, lo0, hi, P_(d["tmp"]), s),
                       "density_grid_run_max")
+        elif sorted_:  # an integer atomic max per point from the MLP's epilogue (the draws at lo = 0)
+            nat.check(lib.ngp_nerf_density_forward(P_(d["enc"]), P_(self.w_half[1]), P_(self.mlp_img[0]), n,
+                                                   sn.input_dim, sn.hidden_dim, sn.num_layers, float(m.density_scale),
+                                                   P_(d["idx"]), P_(d["tmp"]), s), "nerf_density_forward")
         elif not partial and H & (H - 1) == 0:
             # the full update's point p is cell p (Morton order): densities straight into tmp_grid
             nat.check(lib.ngp_nerf_density_forward_rows(*dens, P_(d["tmp"]) + 4 * lo, s), "nerf_density_forward_rows")
