@@ -87,7 +87,7 @@ def _vp_array(ptrs):
 DEFAULT_OPTIONS = dict(table16=False, split_head=False, split_reduce=False, split_fwd=False, split_bwd=False,
                        march_adam=True, tail_in_fwd=True, emit_inline=True, draw_ahead=True, live_rows=True,
                        dp_graph=True, density_sort=True, sparse_exchange=False, exact_reduce=False,
-                       density_run_max=True)
+                       density_run_max=False)
 
 
 class FusedTrainer:
@@ -443,7 +443,10 @@ class FusedTrainer:
             nat.check(lib.ngp_nerf_density_forward_rows(*dens, P_(d["sigma"]), s), "nerf_density_forward_rows")
             nat.check(lib.ngp_density_grid_run_max(P_(d["sigma"]), P_(d["idx"]), C, H, lo0, hi, P_(d["tmp"]), s),
                       "density_grid_run_max")
-        elif sorted_:  # an integer atomic max per point from the MLP's epilogue (the draws at lo = 0)
+        elif sorted_:
+            # an integer atomic max per point from the MLP's epilogue (the draws at
+            # lo = 0): the epilogue's atomics cost the query ~4 us, the run-max
+            # launch 14 (partial update 0.428 -> 0.415 ms wall, r07zd)
             nat.check(lib.ngp_nerf_density_forward(P_(d["enc"]), P_(self.w_half[1]), P_(self.mlp_img[0]), n,
                                                    sn.input_dim, sn.hidden_dim, sn.num_layers, float(m.density_scale),
                                                    P_(d["idx"]), P_(d["tmp"]), s), "nerf_density_forward")
