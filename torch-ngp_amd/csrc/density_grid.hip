@@ -145,15 +145,31 @@ k_density_ema(float* __restrict__ grid, float* __restrict__ tmp, uint32_t n, flo
               double* __restrict__ partial) {
     __shared__ double wsum[kEmaThreads / 64];
     double acc = 0.0;
-    for (uint32_t i = blockIdx.x * kEmaThreads + threadIdx.x; i < n; i += gridDim.x * kEmaThreads) {
-        float g = grid[i];
-        const float t = tmp[i];
-        if (g >= 0 && t >= 0) {
-            g = torch_maximum(g * decay, t);
-            grid[i] = g;
+    // U cells' loads in flight per thread, then the cells in the original
+    // order (the fp64 sum's order is unchanged)
+    constexpr uint32_t U = 4;
+    const uint32_t stride = gridDim.x * kEmaThreads;
+    for (uint32_t i0 = blockIdx.x * kEmaThreads + threadIdx.x; i0 < n; i0 += U * stride) {
+        float gv[U], tv[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t i = min(i0 + u * stride, n - 1);
+            gv[u] = grid[i];
+            tv[u] = tmp[i];
         }
-        tmp[i] = -1.0f;
-        acc += g < 0 ? 0.0 : (double)g;  // clamp(min=0)
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t i = i0 + u * stride;
+            if (i >= n) break;
+            float g = gv[u];
+            const float t = tv[u];
+            if (g >= 0 && t >= 0) {
+                g = torch_maximum(g * decay, t);
+                grid[i] = g;
+            }
+            tmp[i] = -1.0f;
+            acc += g < 0 ? 0.0 : (double)g;  // clamp(min=0)
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
@@ -176,7 +192,17 @@ k_density_pack(const float* __restrict__ grid, uint32_t nbytes, uint32_t n, cons
     // every block adds the EMA's partial sums up in the same order
     __shared__ double s_sum[256];
     double acc = 0.0;
-    for (uint32_t i = threadIdx.x; i < nparts; i += 256) acc += partial[i];
+    {  // the loads in flight together, then the adds in the original order
+        constexpr uint32_t U = 4;
+        for (uint32_t i0 = threadIdx.x; i0 < nparts; i0 += 256 * U) {
+            double v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = partial[min(i0 + 256 * u, nparts - 1)];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
+                if (i0 + 256 * u < nparts) acc += v[u];
+        }
+    }
     s_sum[threadIdx.x] = acc;
     __syncthreads();
     for (uint32_t o = 128; o > 0; o >>= 1) {
@@ -537,10 +563,19 @@ k_ostat_points(Ostat o, uint32_t chunks, const unsigned long long* __restrict__ 
     __shared__ unsigned long long s_base, s_tot;
     if (threadIdx.x < 64) {  // the earlier chunks' sums and the segment's total, wave 0
         unsigned long long b = 0, t = 0;
-        for (uint32_t c = threadIdx.x; c < chunks; c += 64) {
-            const unsigned long long v = sums[g * chunks + c];
-            b += c < ch ? v : 0ull;
-            t += v;
+        constexpr uint32_t U = 8;  // loads in flight per lane (exact integer sums: any order)
+        for (uint32_t c0 = threadIdx.x; c0 < chunks; c0 += 64 * U) {
+            unsigned long long v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = sums[g * chunks + min(c0 + 64 * u, chunks - 1)];  // clamped
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = c0 + 64 * u < chunks ? v[u] : 0ull;
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t c = c0 + 64 * u;
+                b += c < ch ? v[u] : 0ull;
+                t += v[u];
+            }
         }
 #pragma unroll
         for (uint32_t off = 32; off > 0; off >>= 1) {

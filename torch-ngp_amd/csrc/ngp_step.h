@@ -72,8 +72,20 @@ NGP_DEV void step_end_block(StepState* __restrict__ st, const ScalerArgs& sa, co
                             int32_t* __restrict__ step_counter, const float* __restrict__ loss_ray, uint32_t n_rays) {
     __shared__ float part[256];
     float acc = 0.0f;
-    if (loss_ray)
-        for (uint32_t i = threadIdx.x; i < n_rays; i += 256) acc += loss_ray[i];
+    if (loss_ray && n_rays) {
+        // 16 loads in flight per thread, then the adds in the original order
+        // (one dependent round trip per load made the flush's standalone
+        // k_step_end ~8 us)
+        constexpr uint32_t U = 16;
+        for (uint32_t base = threadIdx.x; base < n_rays; base += 256 * U) {
+            float v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = loss_ray[min(base + u * 256, n_rays - 1)];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
+                if (base + u * 256 < n_rays) acc += v[u];
+        }
+    }
     part[threadIdx.x] = acc;
     __syncthreads();
     for (uint32_t o = 128; o > 0; o >>= 1) {
