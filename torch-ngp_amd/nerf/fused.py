@@ -403,7 +403,10 @@ class FusedTrainer:
         # the pending optimizer update first (the query reads the parameters);
         # its sweep writes the query's fp16 table copy as well
         fresh_table = d["table"] is not None and self._pending and not self.dp
-        self.flush(table_half=d["table"] if fresh_table else None)
+        # world 1: the update's bookkeeping rides in the query's grid-forward
+        # launch below (one block, beside the MLP fragment packs), not in a
+        # launch of its own after the sweep
+        self.flush(table_half=d["table"] if fresh_table else None, defer_end=not self.dp)
         partial = int(m.iter_density >= 16)
         ppc = 2 * (H3 // 4) if partial else H3
         P = C * ppc
@@ -428,15 +431,17 @@ class FusedTrainer:
         if d["table"] is not None and not fresh_table:  # world 1 keeps no fp16 table copy: make one for the query
             d["table"].copy_(self.params[0].detach())
         table = d["table"] if d["table"] is not None else self.w_half[0]
-        # the encodings are [L][n][2] (pair-major, row stride n) at the buffer's head
-        nat.check(lib.ngp_grid_encode_forward_fused(
+        # the encodings are [L][n][2] (pair-major, row stride n) at the buffer's
+        # head; the same launch packs the fragment images of the weights the
+        # flush left (the next step packs them again from the same weights)
+        # and, world 1, runs the flush's deferred bookkeeping (end_pending)
+        sn, pk = self.sig_net, self._pk
+        nat.check(lib.ngp_grid_encode_forward_fused_tail(
             P_(d["xyzs"]) + 12 * lo, float(m.bound), P_(table), _F16, P_(e.offsets), P_(d["enc"]), n, None,
             e.input_dim, e.level_dim, e.num_levels, self.S, e.base_resolution, e.gridtype_id, int(e.align_corners),
-            e.interp_id, 0, s), "grid_encode_fused")
-        sn, pk = self.sig_net, self._pk
-        # the fragment images of the weights the flush above left (the next
-        # step packs them again from the same weights)
-        nat.check(lib.ngp_ffmlp_pack(2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s), "ffmlp_pack")
+            e.interp_id, None if self.dp else P_(self.state), 2.0, 0.5, self.growth_interval, _PRECHECKED,
+            P_(self.loss_ray), self.N, 2, pk["w"], pk["ins"], pk["hid"], pk["nl"], pk["img"], s),
+            "grid_encode_forward_fused_tail")
         dens = (P_(d["enc"]), P_(self.mlp_img[0]), n, sn.hidden_dim, sn.num_layers, float(m.density_scale))
         if sorted_ and self.options["density_run_max"]:
             # densities per point, then each run of one cell's draws -> its max (no global atomics)
@@ -1089,14 +1094,16 @@ class FusedTrainer:
         for _ in range(k):
             self.step()
 
-    def flush(self, table_half=None):
+    def flush(self, table_half=None, defer_end=False):
         """Apply the pending optimizer step (before reading or saving the
         parameters, or evaluating); data parallel: every rank then holds the
-        full fp32 masters and fp16 forward copies."""
+        full fp32 masters and fp16 forward copies. defer_end (world 1): the
+        update's scaler / LR / loss bookkeeping is left pending for the
+        caller's next launch that carries it (update_density's query)."""
         if self._pending:
             # the pending grads are the last step's: its kernels (and the
             # exchange's reduce) set the found-inf flag
-            self._optimizer(prechecked=True, table_half=table_half)
+            self._optimizer(prechecked=True, table_half=table_half, defer=defer_end and not self.dp)
             self._gather_half(wait=True)
             self._gather_masters()
             self._pending = False
