@@ -356,11 +356,12 @@ NGP_DEV uint32_t nonzero_bytes(const uint32_t (&d)[8]) {
     return m;
 }
 
-// Two kernels build the image, 256 groups (32 KB of bitfield) per workgroup:
-//   k_occ_count    summary words + per-group counts (count scratch after the image)
-//   k_occ_compact  base = counts of all earlier groups (each workgroup sums
-//                  them itself: a few thousand L2 reads), in-workgroup scan ->
-//                  rank directory, then the non-zero bytes written in order
+// Two kernels build the image:
+//   k_occ_count    summary words + per-group counts (count scratch after the
+//                  image), 256 groups (32 KB of bitfield) per workgroup
+//   k_occ_compact  one wave per group: base = counts of all earlier groups
+//                  (each workgroup sums them itself: a few thousand L2 reads)
+//                  -> rank directory, then the non-zero bytes written in order
 constexpr uint32_t kBuildThreads = 256;
 __global__ void __launch_bounds__(kBuildThreads)
 k_occ_count(const uint8_t* __restrict__ grid, OccLayout L, uint8_t* __restrict__ img,
@@ -381,39 +382,59 @@ k_occ_count(const uint8_t* __restrict__ grid, OccLayout L, uint8_t* __restrict__
     cnt[g] = c;
 }
 
+// One wave per group (its 128 bitfield bytes, two per lane): the group's base
+// is the sum of every earlier group's count (the workgroup's 256 threads sum
+// them together, loads batched), each nonzero byte's rank inside the group
+// comes from two ballots and mbcnt. (One thread per group walked its 128
+// bytes serially: 8 workgroups for a 128^3 grid, ~14 us.)
+constexpr uint32_t kCompactGroups = kBuildThreads / 64;
 __global__ void __launch_bounds__(kBuildThreads)
 k_occ_compact(const uint8_t* __restrict__ grid, OccLayout L, uint8_t* __restrict__ img,
               const uint32_t* __restrict__ cnt) {
-    __shared__ uint32_t lds_waves[kBuildThreads / 64];
-    const uint32_t g0 = blockIdx.x * kBuildThreads;
+    __shared__ uint32_t s_w[kBuildThreads / 64];
+    __shared__ uint32_t s_cnt[kCompactGroups];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t g0 = blockIdx.x * kCompactGroups;
     uint32_t part = 0;
-    for (uint32_t g = threadIdx.x; g < g0; g += kBuildThreads) part += cnt[g];
-    uint32_t base;
-    block_exclusive_scan<kBuildThreads>(part, lds_waves, base);  // base = sum of all earlier groups
-    const uint32_t g = g0 + threadIdx.x;
-    const uint32_t c = g < L.ngroups ? cnt[g] : 0u;
-    uint32_t total;
-    uint32_t pos = base + block_exclusive_scan<kBuildThreads>(c, lds_waves, total);
+    constexpr uint32_t U = 8;  // loads in flight per thread (integer sum: any order)
+    for (uint32_t q0 = threadIdx.x; q0 < g0; q0 += kBuildThreads * U) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) v[u] = cnt[min(q0 + u * kBuildThreads, g0 - 1)];  // clamped: no branch
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) part += q0 + u * kBuildThreads < g0 ? v[u] : 0u;
+    }
+#pragma unroll
+    for (uint32_t o = 32; o > 0; o >>= 1) part += __shfl_down(part, o, 64);
+    if (lane == 0) s_w[wave] = part;
+    if (threadIdx.x < kCompactGroups) {
+        const uint32_t g = g0 + threadIdx.x;
+        s_cnt[threadIdx.x] = g < L.ngroups ? cnt[g] : 0u;
+    }
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kBuildThreads / 64; ++w) base += s_w[w];
+#pragma unroll
+    for (uint32_t w = 0; w < kCompactGroups; ++w) {
+        base += w < wave ? s_cnt[w] : 0u;
+        total += s_cnt[w];
+    }
+    const uint32_t g = g0 + wave;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+        reinterpret_cast<uint32_t*>(img)[0] = base + total;  // wave 0: base = the earlier blocks' sum
+    if (g >= L.ngroups) return;
     uint32_t* pre = occ_sum(img) + 4 * L.ngroups;
     uint8_t* bytes = reinterpret_cast<uint8_t*>(pre + L.ngroups);
-    if (g < L.ngroups) {
-        pre[g] = pos;
-        if (c) {
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i) {
-                uint32_t d[8];
-                load_word32(grid, 4 * g + i, L.nbytes, d);
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const uint32_t v = (d[q] >> (8 * j)) & 0xffu;
-                        if (v) bytes[pos++] = (uint8_t)v;
-                    }
-            }
-        }
-    }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) reinterpret_cast<uint32_t*>(img)[0] = base + total;
+    if (lane == 0) pre[g] = base;
+    const uint32_t o = 128 * g + 2 * lane, last = L.nbytes - 1;
+    const uint32_t v0 = grid[min(o, last)], v1 = grid[min(o + 1, last)];
+    const uint32_t b0 = o < L.nbytes ? v0 : 0u, b1 = o + 1 < L.nbytes ? v1 : 0u;
+    const uint64_t m0 = __ballot(b0 != 0u), m1 = __ballot(b1 != 0u);
+    const uint32_t r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u)) +
+                       __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+    if (b0) bytes[r] = (uint8_t)b0;
+    if (b1) bytes[r + (b0 ? 1u : 0u)] = (uint8_t)b1;
 }
 
 // Copies the global image into this workgroup's LDS when its bytes fit.
@@ -1454,7 +1475,7 @@ static int march_train_impl(const float* rays_o, const float* rays_d, const uint
         uint32_t* cnt = reinterpret_cast<uint32_t*>(img + occ_image_bytes(L));
         const uint32_t wg = ngp_div_up(L.ngroups, kBuildThreads);
         k_occ_count<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
-        k_occ_compact<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
+        k_occ_compact<<<ngp_div_up(L.ngroups, kCompactGroups), kBuildThreads, 0, st>>>(grid, L, img, cnt);
     }
     MarchEmit me{};
     if (ma && ma->st) {  // every CU gets a workgroup: the Adam waves sweep 1/gridDim of the parameters each
@@ -1507,7 +1528,7 @@ extern "C" int ngp_march_occupancy_build(const uint8_t* grid, uint32_t C, uint32
     uint32_t* cnt = reinterpret_cast<uint32_t*>(img + occ_image_bytes(L));
     const uint32_t wg = ngp_div_up(L.ngroups, kBuildThreads);
     k_occ_count<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
-    k_occ_compact<<<wg, kBuildThreads, 0, st>>>(grid, L, img, cnt);
+    k_occ_compact<<<ngp_div_up(L.ngroups, kCompactGroups), kBuildThreads, 0, st>>>(grid, L, img, cnt);
     return ngp_check_launch("march_occupancy_build");
 }
 
