@@ -611,12 +611,12 @@ k_mlp_fwd(const ngp_half* __restrict__ inputs, const ngp_half* __restrict__ weig
 
 // The density query's sigma network (update_extra_state, renderer.py:533-538)
 // on the pair-major encodings of the grid forward, from the prepacked image.
-// A 1-2M-point batch is a stream (64 B of encodings per point): the grid is
-// sized to the workgroups that are resident at once (the occupancy query in
-// launch_fwd_density) and each wave keeps its next kDensityPf chunks' encodings
-// and cell indices in flight while it computes the current one, so the bytes
-// in flight cover HBM's latency (one chunk ahead at 3 waves per SIMD left
-// ~6 MB in flight: 2.5 TB/s). Same values as k_mlp_fwd<EpiDensity>.
+// The grid is sized to the workgroups resident at once (the occupancy query in
+// launch_fwd_density); each wave keeps its next kDensityPf chunks' encodings
+// and cell indices in flight while it computes the current one. The kernel is
+// bound by vector-instruction issue, not by the bytes in flight (DESIGN.md §4:
+// 2-4 chunks ahead measured no faster than one, which keeps 4 waves per SIMD).
+// Same values as k_mlp_fwd<EpiDensity>.
 #ifndef NGP_DENSITY_PF
 #define NGP_DENSITY_PF 1
 #endif
