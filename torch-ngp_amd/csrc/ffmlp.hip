@@ -552,6 +552,27 @@ struct EpiDensity {
 #pragma unroll
         for (int nb = 0; nb < kNB; ++nb) ix[nb] = sigma_out ? 0 : index[clamp_row(row0 + nb * 16 + c, B)];
     }
+    // k_density_fwd's form: lanes 0..31 take one row each (row0 + lane; the
+    // second column block's log densities move from lane group 0 to lanes
+    // 16..31 with one permute), so the exp and the atomic run once per lane
+    // instead of twice in a quarter of the wave
+    NGP_DEV int32_t load_index1(uint32_t row0, uint32_t B) const {
+        const uint32_t lane = threadIdx.x & 63;
+        return sigma_out ? 0 : index[clamp_row(row0 + (lane & 31), B)];
+    }
+    NGP_DEV void run1(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], int32_t ix) const {
+        static_assert(kNB == 2, "two column blocks of 16 rows");
+        const int lane = threadIdx.x & 63;
+        const float v1 = __shfl(o[1][0][0], lane - 16, 64);  // lanes 16..31 <- lanes 0..15
+        const float v = lane < 16 ? o[0][0][0] : v1;
+        const uint32_t row = row0 + (uint32_t)lane;
+        if (lane >= 32 || row >= B) return;
+        const float s = expf((float)(ngp_half)v) * density_scale;
+        if (sigma_out)
+            sigma_out[row] = s;
+        else
+            atomicMax(reinterpret_cast<int*>(tmp_grid) + ix, __float_as_int(s));
+    }
     template <typename FO>
     NGP_DEV void run(uint32_t row0, uint32_t B, const f32x4 (&o)[kNB][1], FO out_act, const int32_t (&ix)[kNB]) const {
         const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
@@ -635,11 +656,11 @@ k_density_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img, u
     const uint32_t nchunks = ngp_div_up(B, 16 * kNB), stride = gridDim.x * kWaves;
     uint32_t chunk = blockIdx.x * kWaves + wave;
     half8 xn[kDensityPf][kNB][1];
-    int32_t in_[kDensityPf][kNB];
+    int32_t in_[kDensityPf];
 #pragma unroll
     for (int s = 0; s < kDensityPf; ++s) {  // clamped rows past the batch: no branch
         xl.template operator()<1>(enc, 32u, (chunk + s * stride) * 16 * kNB, B, xn[s]);
-        epi.load_index((chunk + s * stride) * 16 * kNB, B, in_[s]);
+        in_[s] = epi.load_index1((chunk + s * stride) * 16 * kNB, B);
     }
     copy_frags<N::FWD_FRAGS, kThreads>(lds, img);
     __syncthreads();
@@ -650,16 +671,13 @@ k_density_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img, u
             if (c >= nchunks) break;  // uniform in the wave
             const uint32_t row0 = c * 16 * kNB;
             half8 x[kNB][1];
-            int32_t ix[kNB];
 #pragma unroll
-            for (int nb = 0; nb < kNB; ++nb) {
-                x[nb][0] = xn[s][nb][0];
-                ix[nb] = in_[s][nb];
-            }
+            for (int nb = 0; nb < kNB; ++nb) x[nb][0] = xn[s][nb][0];
+            const int32_t ix = in_[s];
             // the chunk kDensityPf strides ahead into the freed slot
             const uint32_t ahead = (c + kDensityPf * stride) * 16 * kNB;
             xl.template operator()<1>(enc, 32u, ahead, B, xn[s]);
-            epi.load_index(ahead, B, in_[s]);
+            in_[s] = epi.load_index1(ahead, B);
             f32x4 acc[kNB][N::MTW];
             half8 h[kNB][N::KSW];
             dense<N::MTW, 1>(lds, fwd_desc<W, 1, NH>(0, 32u).frag0, x, acc);
@@ -671,7 +689,7 @@ k_density_fwd(const ngp_half* __restrict__ enc, const half8* __restrict__ img, u
             }
             f32x4 o[kNB][1];
             dense<1, N::KSW>(lds, fwd_desc<W, 1, NH>(NH + 1, 32u).frag0, h, o);
-            epi.run(row0, B, o, ActNone{}, ix);
+            epi.run1(row0, B, o, ix);
         }
     }
 }
