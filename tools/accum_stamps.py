@@ -144,6 +144,15 @@ if (b[:, 8] > 0).all() and (st_all[:, 60] > 0).all():
         for nm, sel in (("wave", wr_all), ("image", ~wr_all)):
             if sel.any():
                 tl[nm + "_end_us"] = [round((x - r0) / 100, 2) for x in np.percentile(st_all[sel, 61], [0, 50, 90, 100])]
+    # the bin launch's extra columns (XSTAMP: role 0 the MLP dW reduce, role 1
+    # the next batch's sampler): start / end per block
+    xs = stamps[200000:200000 + 2 * 4096 * 2].view(2, 4096, 2).cpu().numpy().astype(np.int64)
+    for role, nm in ((0, "reduce"), (1, "sampler")):
+        r = xs[role][xs[role][:, 0] > 0]
+        if len(r):
+            tl[nm + "_blocks"] = int(len(r))
+            tl[nm + "_start_us"] = [round((x - r0) / 100, 2) for x in np.percentile(r[:, 0], [0, 50, 100])]
+            tl[nm + "_end_us"] = [round((x - r0) / 100, 2) for x in np.percentile(r[:, 1], [0, 50, 90, 100])]
     print(json.dumps({"timeline": tl}))
 per = {}
 for lv in np.unique(blevel):

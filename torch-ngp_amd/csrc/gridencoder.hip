@@ -861,9 +861,11 @@ __device__ unsigned long long* g_stamps;
 #define WSTAMP(slot, v) do { if (g_stamps && (threadIdx.x & 63) == 0) g_stamps[131072 + (size_t)(blockIdx.x * (kAccThreads / 64) + (threadIdx.x >> 6)) * 4 + (slot)] = (v); } while (0)
 // after the wave's outstanding loads have arrived
 #define BSTAMPW(slot) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); BSTAMP(slot); } while (0)
+#define XSTAMP(role, by, k) do { if (g_stamps && threadIdx.x == 0 && (by) < 4096) g_stamps[200000 + ((size_t)(role) * 4096 + (by)) * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define BSTAMPW(slot) do { } while (0)
 #define WSTAMP(slot, v) do { } while (0)
+#define XSTAMP(role, by, k) do { } while (0)
 #define BRSTAMP(slot) do { } while (0)
 #define RSTAMP(slot) do { } while (0)
 #define STAMP(slot, v) do { } while (0)
@@ -927,6 +929,10 @@ NGP_DEV void bin_block(const ngp_half* __restrict__ grad, const float* __restric
     // and the column after it (x == nlev + (nred != 0)): the next batch's
     // sampler blocks, when the launch carries it
     if (bx >= bp.nlev) {
+        // (stamps build: each extra block's start / end on the constant clock,
+        // role 0 the dW reduce, role 1 the sampler)
+        [[maybe_unused]] const uint32_t xrole = nred && bx == bp.nlev ? 0u : 1u;
+        XSTAMP(xrole, by, 0);
         if (nred && bx == bp.nlev) {
             if (by < nred)
                 ngp_reduce::slab_reduce_block<ngp_half, kBinPts>(rj, by, reinterpret_cast<float(*)[64]>(stage));
@@ -934,6 +940,7 @@ NGP_DEV void bin_block(const ngp_half* __restrict__ grad, const float* __restric
             const BinLego& q = next_batch;
             ngp_head::lego_rays_block(by, q.nlego, q.poses, q.sc, q.N, q.st, q.out);
         }
+        XSTAMP(xrole, by, 1);
         return;
     }
     // the grid covers the row capacity; workgroups past the marched sample
