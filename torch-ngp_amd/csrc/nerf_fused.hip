@@ -305,6 +305,22 @@ k_composite_loss(const float* __restrict__ sigma, const ngp_half* __restrict__ c
     bool stopped = false;
     uint32_t nlive = 0;  // rows of this ray with a nonzero gradient so far (listed in ray_rows)
     for (uint32_t base = 0; base < num_steps; base += 64) {
+        if (stopped) {
+            // past the early stop every row's gradient is exactly zero and
+            // none is live (the chunk body gives +0 everywhere): the zeros
+            // are written without the chunk's loads and scans (a ray hitting
+            // the surface marches on behind it; those chunks were a load
+            // round trip and a scan chain each)
+            if (base + lane < num_steps) {
+                const uint32_t i = offset + base + lane;
+                const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+                half8* go = reinterpret_cast<half8*>(grad_color_out + (size_t)i * 16);
+                go[0] = z;
+                go[1] = z;
+                grad_h[(size_t)i * 16] = (ngp_half)0.0f;
+            }
+            continue;
+        }
         bool stop = false;
         Chunk c{};
         float h0 = 0.0f;
